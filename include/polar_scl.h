@@ -1,0 +1,177 @@
+/*
+ * polar_scl.h -- C ABI of libpolar_mi355x.so, the MI355X (gfx950) polar SC/SCL engine.
+ *
+ * This is the drop-in boundary for the reference's hot path (heimrih/polar_code,
+ * package dl_scl_polar).  The reference has no FFI of its own: it is pure Python/NumPy,
+ * so each entry point below replaces a Python function, and the binding a maintainer adds
+ * on the reference side is the ctypes stub shown in INTEGRATION.md.
+ *
+ *   pscl_create / pscl_destroy  <- the implicit per-call setup of decode_scl
+ *                                  (info mask scl.py:125-126, CRC poly crc.py:10-16)
+ *   pscl_decode                 <- decode_scl(llr, info_set, M, crc, force_info_bits=...)
+ *                                  dl_scl_polar/polar/scl.py:108-209, batched over B frames
+ *                                  (sc_decode polar.py:130-168 is the M=1 case)
+ *   pscl_decode_device          <- same, device-resident buffers, asynchronous; optionally
+ *                                  folds the FER/BER counting of run_fer_sweep.py:91-109
+ *   pscl_channel_device         <- the per-frame TX chain of run_fer_sweep.py:79-87
+ *                                  (payload, attach_crc crc.py:19-37, encode polar.py:106-119,
+ *                                  BPSK, AWGN, LLR) with a counter-based Philox stream
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; no torch/HIP types in signatures (streams are void*).
+ *   - Every function returns 0 on success or a negative PSCL_E* code; pscl_last_error()
+ *     returns a thread-local message for the last failure.  The Python host layer maps
+ *     PSCL_EINVAL to ValueError, PSCL_EPRUNED to RuntimeError (scl.py:171-172), the rest
+ *     to RuntimeError.
+ *   - Host-buffer calls are synchronous and never retain caller pointers.  Device-buffer
+ *     calls are enqueued on the handle's stream (pscl_set_stream) and return immediately.
+ *   - Bit vectors crossing the boundary as "words" are little-endian packed uint64:
+ *     bit j of a K-bit vector is bit (j & 63) of word (j >> 6); K-bit vectors use
+ *     PSCL_WORDS(K) words.
+ *   - Arithmetic is IEEE fp64 end to end, like the reference (scl.py:41, polar.py:167); the
+ *     path metric reproduces numpy's logaddexp (glibc exp/log1p) bit for bit.
+ */
+#ifndef POLAR_SCL_H
+#define POLAR_SCL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSCL_ABI_VERSION 1
+
+#define PSCL_OK 0
+#define PSCL_EINVAL -1   /* bad argument (shape, range, list size, force value, CRC length) */
+#define PSCL_EDEVICE -2  /* HIP runtime / device failure, or no GPU */
+#define PSCL_ENOMEM -3   /* device allocation failed */
+#define PSCL_EPRUNED -4  /* "All paths pruned during decoding" (cannot happen for valid input) */
+#define PSCL_EUNSUP -5   /* configuration outside what the kernels implement (N, L, CRC degree) */
+
+#define PSCL_MAX_N 128   /* code length N: power of two, 2..128 (every BASELINE config is N=128) */
+#define PSCL_MAX_L 32    /* list size M/L: 1..32 (2L candidates fit one 64-lane wavefront) */
+#define PSCL_MAX_CRC 32  /* CRC degree: 1..32 */
+#define PSCL_WORDS(K) (((K) + 63) / 64)
+
+/* decode flags bit layout (pscl_decode_device d_flags[b]) */
+#define PSCL_FLAG_CRC_PASS 0x80u  /* best candidate passes the CRC */
+#define PSCL_FLAG_IDX_MASK 0x3fu  /* index of the best candidate in the final list */
+
+/* counters accumulated by pscl_decode_device when d_ref_words != NULL (int64[PSCL_NCOUNT]) */
+#define PSCL_CNT_FRAMES 0      /* frames decoded */
+#define PSCL_CNT_FRAME_ERR 1   /* best candidate fails CRC (run_fer_sweep FER, :92-94) */
+#define PSCL_CNT_BIT_ERR 2     /* best bits != reference over all K bits (run_fer_sweep BER, :95-99) */
+#define PSCL_CNT_PAYLOAD_ERR 3 /* frames with >=1 error in the first k_payload bits (run_ber_sweep FER) */
+#define PSCL_CNT_PAYLOAD_BIT 4 /* payload bit errors (run_ber_sweep BER, :77-82) */
+#define PSCL_NCOUNT 8
+
+typedef struct pscl_handle pscl_handle;
+
+/* Last error message for the calling thread ("" if none). */
+const char* pscl_last_error(void);
+
+/* ABI version compiled into the library (PSCL_ABI_VERSION). */
+int pscl_abi_version(void);
+
+/* Number of visible HIP devices (0 when there is no GPU); negative on runtime failure. */
+int pscl_device_count(void);
+
+/*
+ * Create a decoder for one polar code on one device.
+ *   N        code length (power of two, 2..PSCL_MAX_N)
+ *   info_set K distinct indices in [0, N), any order; candidate bits follow this order
+ *            (u[info_set], scl.py:183)
+ *   L        list size M (1..PSCL_MAX_L)
+ *   crc_poly CRC generator as the integer value of the reference's hex string
+ *            (e.g. 0x1864CFB for CRC-24A); 0 = no CRC (decode_scl crc=None)
+ */
+int pscl_create(pscl_handle** out, int device, int N, const int32_t* info_set, int K, int L,
+                uint64_t crc_poly);
+int pscl_destroy(pscl_handle* h);
+
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL restores
+ * the handle's own stream. */
+int pscl_set_stream(pscl_handle* h, void* hip_stream);
+void* pscl_get_stream(pscl_handle* h);
+int pscl_sync(pscl_handle* h);
+
+/*
+ * Batched decode_scl on host buffers (synchronous).
+ *   llr        [B][N] float64 channel LLRs (not modified)
+ *   forced     NULL or [B][K] int8 in {-1,0,1}  (force_info_bits, scl.py:127-131,146-152)
+ * Outputs (any may be NULL except n_paths):
+ *   n_paths    [B] int32   number of paths in the final list (== min(L, 2^free_info_bits))
+ *   best_bits  [B][K] int8 best_path_bits (scl.py:190-201)
+ *   crc_pass   [B] uint8   check_crc(best_path_bits) (1 if crc_poly == 0)
+ *   best_idx   [B] int32   index of best_path_bits in the candidate list
+ *   metrics    [B][L] float64   path metrics in list order (rows >= n_paths untouched)
+ *   cands      [B][L][K] int8   candidates in list order
+ *   info_llrs  [B][L][K] float64 decision LLRs at info phases (scl.py:158,166)
+ */
+int pscl_decode(pscl_handle* h, const double* llr, int64_t B, const int8_t* forced, int32_t* n_paths,
+                int8_t* best_bits, uint8_t* crc_pass, int32_t* best_idx, double* metrics, int8_t* cands,
+                double* info_llrs);
+
+/*
+ * Batched sc_decode (dl_scl_polar/polar/polar.py:130-168): successive cancellation with hard
+ * decisions u = (llr < 0) at information leaves, on host buffers (synchronous).
+ *   bits [B][K] int8 out = u_hat[info_set]
+ * The handle's list size and CRC are ignored (one path, no list, no CRC selection).
+ */
+int pscl_sc_decode(pscl_handle* h, const double* llr, int64_t B, int8_t* bits);
+
+/*
+ * Batched decode on device buffers, enqueued on the handle's stream.
+ *   d_llr       [B][N] float64
+ *   d_force     NULL or [B][2][W] uint64 (W = PSCL_WORDS(K)): force mask words, then
+ *               forced-value words, indexed by info position j
+ *   d_best      [B][W] uint64 best_path_bits as words (may be NULL)
+ *   d_flags     [B] uint8 PSCL_FLAG_* (may be NULL)
+ *   d_metrics   NULL or [B][L] float64
+ *   d_cands     NULL or [B][L][W] uint64
+ *   d_info_llrs NULL or [B][L][K] float64
+ *   d_ref       NULL or [B][W] uint64 transmitted message words; when given, the kernel adds
+ *               this batch's error statistics into d_counters (int64[PSCL_NCOUNT], device)
+ *   k_payload   payload length for the PSCL_CNT_PAYLOAD_* counters (ignored if d_ref NULL)
+ */
+int pscl_decode_device(pscl_handle* h, const double* d_llr, int64_t B, const uint64_t* d_force,
+                       uint64_t* d_best, uint8_t* d_flags, double* d_metrics, uint64_t* d_cands,
+                       double* d_info_llrs, const uint64_t* d_ref, int k_payload, int64_t* d_counters);
+
+/*
+ * Generate B frames of the reference TX chain on the device (run_fer_sweep.py:79-87):
+ *   payload = k_payload uniform bits; msg = attach_crc(payload) (K bits, K = k_payload + deg);
+ *   u[info_set] = msg; x = polar transform(u); y = (1 - 2x) + sigma * n; llr = 2 y / sigma^2
+ *   with sigma^2 = 1 / (2 * rate * 10^(ebno_db/10)).
+ * Randomness: Philox4x32-10, key = (seed, stream_id), counter = (frame index, draw): frame f's
+ * samples depend only on (seed, stream_id, f), so sharding frames over GPUs is exact.
+ *   d_llr [B][N] float64 out;  d_msg NULL or [B][W] uint64 out (msg words)
+ */
+int pscl_channel_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate,
+                        int k_payload, int64_t frame0, int64_t B, double* d_llr, uint64_t* d_msg);
+
+/* Device scratch helpers so that non-torch callers can drive the device path. */
+int pscl_device_alloc(pscl_handle* h, void** d_ptr, int64_t bytes);
+int pscl_device_free(pscl_handle* h, void* d_ptr);
+int pscl_memcpy_htod(pscl_handle* h, void* d_dst, const void* src, int64_t bytes);
+int pscl_memcpy_dtoh(pscl_handle* h, void* dst, const void* d_src, int64_t bytes);
+int pscl_memset_device(pscl_handle* h, void* d_dst, int value, int64_t bytes);
+
+/*
+ * Kernel timing with HIP events recorded on the launch stream around every decode kernel
+ * launch (enable = 1 starts a fresh accumulation).  pscl_timing_read returns the number of
+ * timed launches and their summed duration in milliseconds (synchronizes the stream).
+ */
+int pscl_timing_enable(pscl_handle* h, int enable);
+int pscl_timing_read(pscl_handle* h, int64_t* launches, double* total_ms);
+
+/* Launch geometry used by the decode kernel (for roofline bookkeeping): waves per
+ * workgroup, workgroups per launch for B frames, LDS bytes per workgroup. */
+int pscl_launch_info(pscl_handle* h, int64_t B, int* waves_per_wg, int64_t* grid, int* lds_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* POLAR_SCL_H */

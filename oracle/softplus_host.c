@@ -1,0 +1,42 @@
+/*
+ * TEST INFRASTRUCTURE: host build of polar_code_amd/csrc/glibc_softplus.h (the device
+ * metric code) next to the platform libm, so tests/test_softplus_host.py can check the
+ * port bit for bit on the CPU.  Not linked into the product.
+ */
+#include <math.h>
+#include <stdint.h>
+
+#include "glibc_softplus.h"
+
+static const uint64_t kT[256] = {
+#include "exp_table.inc"
+};
+
+/* count mismatches of (port exp, port log1p, port logaddexp0) vs libm over v[0..n) */
+void softplus_compare(const double* v, int64_t n, int64_t* bad_exp, int64_t* bad_log1p, int64_t* bad_lae) {
+    int64_t be = 0, bl = 0, bs = 0;
+    for (int64_t i = 0; i < n; i++) {
+        double x = -fabs(v[i]);
+        double e1 = exp(x), e2 = pscl_exp(x, kT);
+        if (pscl_asu64(e1) != pscl_asu64(e2)) be++;
+        double l1 = log1p(e1), l2 = pscl_log1p(e1);
+        if (pscl_asu64(l1) != pscl_asu64(l2)) bl++;
+        /* npy_logaddexp(0, v) */
+        double ref;
+        if (v[i] == 0.0)
+            ref = 0.0 + 0.693147180559945309417232121458176568;
+        else if (0.0 - v[i] > 0)
+            ref = 0.0 + log1p(exp(-(0.0 - v[i])));
+        else
+            ref = v[i] + log1p(exp(0.0 - v[i]));
+        double got = pscl_logaddexp0(v[i], pscl_softplus_tail(v[i], kT));
+        if (pscl_asu64(ref) != pscl_asu64(got)) bs++;
+    }
+    *bad_exp = be;
+    *bad_log1p = bl;
+    *bad_lae = bs;
+}
+
+void softplus_port_batch(const double* v, int64_t n, double* out) {
+    for (int64_t i = 0; i < n; i++) out[i] = pscl_logaddexp0(v[i], pscl_softplus_tail(v[i], kT));
+}

@@ -1,0 +1,240 @@
+"""ctypes binding of libpolar_mi355x.so (include/polar_scl.h).
+
+There is deliberately no fallback: if the HIP library is missing or no GPU is visible,
+every decode raises.  Argument errors are mapped back to the reference's exception types
+(ValueError / RuntimeError, dl_scl_polar/polar/scl.py:117-131,171-172).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import functools
+import threading
+from pathlib import Path
+
+import numpy as np
+
+LIB_PATH = Path(__file__).resolve().parent / "libpolar_mi355x.so"
+
+PSCL_OK = 0
+PSCL_EINVAL = -1
+PSCL_EDEVICE = -2
+PSCL_ENOMEM = -3
+PSCL_EPRUNED = -4
+PSCL_EUNSUP = -5
+PSCL_MAX_N = 128
+PSCL_MAX_L = 32
+PSCL_FLAG_CRC_PASS = 0x80
+PSCL_FLAG_IDX_MASK = 0x3F
+PSCL_NCOUNT = 8
+CNT_FRAMES, CNT_FRAME_ERR, CNT_BIT_ERR, CNT_PAYLOAD_ERR, CNT_PAYLOAD_BIT = range(5)
+
+# every symbol the header declares (tests/test_capi_symbols.py checks the .so exports them)
+EXPORTS = (
+    "pscl_last_error", "pscl_abi_version", "pscl_device_count", "pscl_create", "pscl_destroy",
+    "pscl_set_stream", "pscl_get_stream", "pscl_sync", "pscl_decode", "pscl_sc_decode",
+    "pscl_decode_device", "pscl_channel_device", "pscl_device_alloc", "pscl_device_free",
+    "pscl_memcpy_htod", "pscl_memcpy_dtoh", "pscl_memset_device", "pscl_timing_enable",
+    "pscl_timing_read", "pscl_launch_info",
+)
+
+_vp, _i32, _i64, _u64, _dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
+
+
+class PolarNativeError(RuntimeError):
+    """Device/runtime failure inside libpolar_mi355x.so."""
+
+
+@functools.lru_cache(maxsize=1)
+def lib() -> C.CDLL:
+    if not LIB_PATH.exists():
+        raise PolarNativeError(
+            f"{LIB_PATH} not built: run `python -m polar_code_amd.build` (hipcc, gfx950). "
+            "There is no CPU fallback for the decoder.")
+    L = C.CDLL(str(LIB_PATH))
+    P = C.POINTER
+    sig = {
+        "pscl_last_error": (C.c_char_p, []),
+        "pscl_abi_version": (C.c_int, []),
+        "pscl_device_count": (C.c_int, []),
+        "pscl_create": (C.c_int, [P(_vp), C.c_int, C.c_int, P(_i32), C.c_int, C.c_int, _u64]),
+        "pscl_destroy": (C.c_int, [_vp]),
+        "pscl_set_stream": (C.c_int, [_vp, _vp]),
+        "pscl_get_stream": (_vp, [_vp]),
+        "pscl_sync": (C.c_int, [_vp]),
+        "pscl_decode": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+        "pscl_sc_decode": (C.c_int, [_vp, _vp, _i64, _vp]),
+        "pscl_decode_device": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int, _vp]),
+        "pscl_channel_device": (C.c_int, [_vp, _u64, C.c_uint32, _dbl, _dbl, C.c_int, _i64, _i64, _vp, _vp]),
+        "pscl_device_alloc": (C.c_int, [_vp, P(_vp), _i64]),
+        "pscl_device_free": (C.c_int, [_vp, _vp]),
+        "pscl_memcpy_htod": (C.c_int, [_vp, _vp, _vp, _i64]),
+        "pscl_memcpy_dtoh": (C.c_int, [_vp, _vp, _vp, _i64]),
+        "pscl_memset_device": (C.c_int, [_vp, _vp, C.c_int, _i64]),
+        "pscl_timing_enable": (C.c_int, [_vp, C.c_int]),
+        "pscl_timing_read": (C.c_int, [_vp, P(_i64), P(_dbl)]),
+        "pscl_launch_info": (C.c_int, [_vp, _i64, P(C.c_int), P(_i64), P(C.c_int)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
+def last_error() -> str:
+    return lib().pscl_last_error().decode(errors="replace")
+
+
+def check(rc: int) -> None:
+    if rc == PSCL_OK:
+        return
+    msg = last_error()
+    if rc == PSCL_EINVAL:
+        raise ValueError(msg)
+    if rc == PSCL_EPRUNED:
+        raise RuntimeError("All paths pruned during decoding")
+    if rc == PSCL_EUNSUP:
+        raise NotImplementedError(msg)
+    raise PolarNativeError(f"libpolar_mi355x error {rc}: {msg}")
+
+
+def device_count() -> int:
+    n = lib().pscl_device_count()
+    if n < 0:
+        raise PolarNativeError(last_error())
+    return n
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data
+
+
+def poly_value(crc) -> int:
+    """The reference's CRC polynomial hex string (crc.py:10-16) as an integer (0 = no CRC)."""
+    if crc is None:
+        return 0
+    if isinstance(crc, (int, np.integer)):
+        return int(crc)
+    if not crc:
+        raise ValueError("CRC polynomial string must be non-empty")
+    return int(str(crc), 16)
+
+
+class Decoder:
+    """One pscl_handle: a polar code (N, info set, list size, CRC) bound to one device."""
+
+    def __init__(self, N: int, info_set, L: int, crc=None, device: int = 0):
+        info = np.ascontiguousarray(np.asarray(info_set).astype(np.int32).ravel())
+        self.N, self.K, self.L = int(N), int(info.size), int(L)
+        self.info_set = info
+        self.crc_poly = poly_value(crc)
+        self.crc_deg = max(self.crc_poly.bit_length() - 1, 0)
+        self.W = (self.K + 63) // 64 if self.K else 1
+        self.device = int(device)
+        h = _vp()
+        check(lib().pscl_create(C.byref(h), self.device, self.N, info.ctypes.data_as(C.POINTER(_i32)), self.K,
+                                self.L, self.crc_poly))
+        self._h = h
+        self._lock = threading.Lock()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().pscl_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
+
+    # ---------------------------------------------------------------- host buffers
+    def decode(self, llr: np.ndarray, forced: np.ndarray | None = None, *, want_metrics=True,
+               want_cands=True, want_info_llrs=True):
+        """Batched decode_scl on host arrays.  llr: [B, N] float64."""
+        llr = np.ascontiguousarray(llr, dtype=np.float64)
+        if llr.ndim == 1:
+            llr = llr[None, :]
+        B = llr.shape[0]
+        if llr.shape[1] != self.N:
+            raise ValueError("Channel LLR length must be a power of two")
+        if forced is not None:
+            forced = np.ascontiguousarray(forced, dtype=np.int8).reshape(B, self.K)
+        out = {
+            "n_paths": np.zeros(B, np.int32),
+            "best_bits": np.zeros((B, self.K), np.int8),
+            "crc_pass": np.zeros(B, np.uint8),
+            "best_idx": np.zeros(B, np.int32),
+            "metrics": np.full((B, self.L), np.nan) if want_metrics else None,
+            "cands": np.zeros((B, self.L, self.K), np.int8) if want_cands else None,
+            "info_llrs": np.full((B, self.L, self.K), np.nan) if want_info_llrs else None,
+        }
+        with self._lock:
+            check(lib().pscl_decode(self._h, _ptr(llr), B, _ptr(forced), _ptr(out["n_paths"]),
+                                    _ptr(out["best_bits"]), _ptr(out["crc_pass"]), _ptr(out["best_idx"]),
+                                    _ptr(out["metrics"]), _ptr(out["cands"]), _ptr(out["info_llrs"])))
+        out["crc_pass"] = out["crc_pass"].astype(bool)
+        return out
+
+    def sc_decode(self, llr: np.ndarray) -> np.ndarray:
+        llr = np.ascontiguousarray(llr, dtype=np.float64)
+        if llr.ndim == 1:
+            llr = llr[None, :]
+        bits = np.zeros((llr.shape[0], self.K), np.int8)
+        with self._lock:
+            check(lib().pscl_sc_decode(self._h, _ptr(llr), llr.shape[0], _ptr(bits)))
+        return bits
+
+    # -------------------------------------------------------------- device buffers
+    def set_stream(self, stream_ptr: int | None) -> None:
+        check(lib().pscl_set_stream(self._h, stream_ptr))
+
+    def decode_device(self, d_llr: int, B: int, *, d_force=0, d_best=0, d_flags=0, d_metrics=0, d_cands=0,
+                      d_info_llrs=0, d_ref=0, k_payload=0, d_counters=0) -> None:
+        check(lib().pscl_decode_device(self._h, d_llr, B, d_force or None, d_best or None, d_flags or None,
+                                       d_metrics or None, d_cands or None, d_info_llrs or None, d_ref or None,
+                                       int(k_payload), d_counters or None))
+
+    def channel_device(self, seed: int, stream_id: int, ebno_db: float, rate: float, k_payload: int, frame0: int,
+                       B: int, d_llr: int, d_msg: int = 0) -> None:
+        check(lib().pscl_channel_device(self._h, int(seed) & (2**64 - 1), int(stream_id) & 0xFFFFFFFF,
+                                        float(ebno_db), float(rate), int(k_payload), int(frame0), int(B), d_llr,
+                                        d_msg or None))
+
+    def sync(self) -> None:
+        check(lib().pscl_sync(self._h))
+
+    def timing_enable(self, on: bool = True) -> None:
+        check(lib().pscl_timing_enable(self._h, 1 if on else 0))
+
+    def timing_read(self):
+        n, ms = _i64(), _dbl()
+        check(lib().pscl_timing_read(self._h, C.byref(n), C.byref(ms)))
+        return int(n.value), float(ms.value)
+
+    def launch_info(self, B: int):
+        w, g, lds = C.c_int(), _i64(), C.c_int()
+        check(lib().pscl_launch_info(self._h, int(B), C.byref(w), C.byref(g), C.byref(lds)))
+        return int(w.value), int(g.value), int(lds.value)
+
+
+_CACHE: dict = {}
+_CACHE_LOCK = threading.Lock()
+
+
+def get_decoder(N: int, info_set, L: int, crc=None, device: int = 0) -> Decoder:
+    """Cached Decoder per (N, info set, L, CRC, device): decode_scl is called per frame."""
+    info = np.asarray(info_set).astype(np.int64).ravel()
+    key = (int(N), info.tobytes(), int(L), poly_value(crc), int(device))
+    with _CACHE_LOCK:
+        dec = _CACHE.get(key)
+        if dec is None:
+            if len(_CACHE) > 64:
+                _CACHE.clear()
+            dec = Decoder(N, info, L, crc, device)
+            _CACHE[key] = dec
+        return dec

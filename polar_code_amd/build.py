@@ -1,0 +1,85 @@
+"""Build the native parts in-tree.
+
+  polar_code_amd/libpolar_mi355x.so   HIP kernels + C ABI for gfx950 (the product)
+  oracle/liboracle_scl.so             C restatement of the reference (test/baseline only)
+  oracle/libsoftplus_host.so          host build of csrc/glibc_softplus.h (parity test only)
+
+Run:  python -m polar_code_amd.build   (or __graft_entry__.build()).
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+INCLUDE = ROOT / "include"
+ORACLE = ROOT / "oracle"
+LIB = PKG / "libpolar_mi355x.so"
+ARCH = os.environ.get("PSCL_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+HIP_SOURCES = ["scl_kernels.hip", "capi.cpp"]
+HIP_DEPS = HIP_SOURCES + ["scl_kernels.h", "glibc_softplus.h", "exp_table.inc"]
+
+
+def _run(cmd: list[str]) -> None:
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        sys.stderr.write(res.stdout + res.stderr)
+        raise RuntimeError(f"build step failed: {' '.join(cmd)}")
+
+
+def _stale(target: Path, deps: list[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def build_hip(force: bool = False) -> Path:
+    deps = [CSRC / s for s in HIP_DEPS] + [INCLUDE / "polar_scl.h"]
+    if not force and not _stale(LIB, deps):
+        return LIB
+    objdir = PKG / "_build"
+    objdir.mkdir(exist_ok=True)
+    objs = []
+    for src in HIP_SOURCES:
+        obj = objdir / (Path(src).stem + ".o")
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+              "-Wno-unused-result", "-Wno-unused-value", f"-I{INCLUDE}", f"-I{CSRC}",
+              "-c", str(CSRC / src), "-o", str(obj)])
+        objs.append(str(obj))
+    tmp = LIB.with_suffix(".so.tmp")
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", str(tmp)])
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def build_oracle(force: bool = False) -> list[Path]:
+    out = []
+    lib = ORACLE / "liboracle_scl.so"
+    src = ORACLE / "scl_oracle.c"
+    if force or _stale(lib, [src]):
+        _run(["gcc", "-O2", "-fPIC", "-shared", "-fopenmp", "-ffp-contract=off", "-fno-builtin",
+              str(src), "-o", str(lib), "-lm"])
+    out.append(lib)
+    sp = ORACLE / "libsoftplus_host.so"
+    spsrc = ORACLE / "softplus_host.c"
+    if force or _stale(sp, [spsrc, CSRC / "glibc_softplus.h", CSRC / "exp_table.inc"]):
+        _run(["gcc", "-O2", "-fPIC", "-shared", "-ffp-contract=off", f"-I{CSRC}", str(spsrc), "-o", str(sp), "-lm"])
+    out.append(sp)
+    return out
+
+
+def build_all(force: bool = False) -> None:
+    build_hip(force)
+    build_oracle(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)
+    print(LIB)

@@ -1,0 +1,511 @@
+// capi.cpp -- C ABI of libpolar_mi355x.so (declared in include/polar_scl.h).
+//
+// Host side of the engine: validates arguments with the reference's error semantics
+// (scl.py:117-131, crc.py:40-49), precomputes the per-code constants (information mask,
+// CRC syndrome/remainder columns, glibc exp table), owns device scratch and the stream,
+// and launches the kernels in scl_kernels.hip.  There is no CPU decode path: every
+// decode runs on the GPU, and calls fail with PSCL_EDEVICE when no GPU is present.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "polar_scl.h"
+#include "scl_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t _e = (expr);                                                           \
+        if (_e != hipSuccess)                                                             \
+            return fail(_e == hipErrorOutOfMemory ? PSCL_ENOMEM : PSCL_EDEVICE, "%s: %s", \
+                        #expr, hipGetErrorString(_e));                                    \
+    } while (0)
+
+const uint64_t kExpTable[256] = {
+#include "exp_table.inc"
+};
+
+// MSB-first bits of the polynomial value (crc.py:10-16); returns degree
+int poly_degree(uint64_t poly) {
+    int len = 0;
+    for (uint64_t v = poly; v; v >>= 1) len++;
+    return len - 1;
+}
+
+// remainder of bits[0..len) after the long division of crc.py (positions 0..len-deg-1
+// are divided out); remainder bit i = buffer[len-deg+i]
+uint32_t crc_remainder(const std::vector<uint8_t>& in, uint64_t poly, int deg) {
+    std::vector<uint8_t> buf(in);
+    const int len = (int)buf.size();
+    for (int i = 0; i + deg < len; ++i) {
+        if (!buf[i]) continue;
+        for (int k = 0; k <= deg; ++k) buf[i + k] ^= (uint8_t)((poly >> (deg - k)) & 1);
+    }
+    uint32_t r = 0;
+    for (int i = 0; i < deg; ++i)
+        if (buf[len - deg + i]) r |= 1u << i;
+    return r;
+}
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+};
+
+}  // namespace
+
+struct pscl_handle {
+    int device = 0;
+    int N = 0, n = 0, K = 0, L = 0, W = 1, crc_deg = 0;
+    uint64_t crc_poly = 0;
+    uint64_t info_mask[2] = {0, 0};
+    std::vector<int32_t> info_set;
+    std::vector<uint32_t> check_cols;   // [K]
+    std::vector<uint32_t> attach_cols;  // [K - deg]
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    uint32_t* d_check_cols = nullptr;
+    uint32_t* d_attach_cols = nullptr;
+    int32_t* d_info_set = nullptr;
+    uint64_t* d_exp_table = nullptr;
+    DevBuf scratch[12];
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+};
+
+namespace {
+
+int ensure(pscl_handle* h, int slot, size_t bytes, void** out) {
+    DevBuf& b = h->scratch[slot];
+    if (b.n < bytes) {
+        if (b.p) hipFree(b.p);
+        b.p = nullptr;
+        b.n = 0;
+        size_t want = bytes < 4096 ? 4096 : bytes;
+        HIP_TRY(hipMalloc(&b.p, want));
+        b.n = want;
+    }
+    *out = b.p;
+    return PSCL_OK;
+}
+
+int set_device(pscl_handle* h) {
+    HIP_TRY(hipSetDevice(h->device));
+    return PSCL_OK;
+}
+
+void fill_decode_params(const pscl_handle* h, pscl_decode_params& P, int hist) {
+    memset(&P, 0, sizeof(P));
+    P.N = h->N;
+    P.n = h->n;
+    P.K = h->K;
+    P.L = h->L;
+    P.W = h->W;
+    P.info_mask[0] = h->info_mask[0];
+    P.info_mask[1] = h->info_mask[1];
+    P.crc_cols = h->d_check_cols;
+    P.has_crc = h->crc_poly != 0;
+    P.exp_table = h->d_exp_table;
+    const int a_bytes = h->N >= 4 ? h->L * (h->N - 2) * 8 : 0;
+    P.a_bytes = a_bytes;
+    int wb = a_bytes + 64 + (hist ? h->K * h->L * 9 : 0);
+    P.wave_bytes = (wb + 15) & ~15;
+}
+
+int launch_decode(pscl_handle* h, const pscl_decode_params& P, int hist) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (h->timing) {
+        while (h->ev_pool.size() < h->ev_used + 2) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreate(&e));
+            h->ev_pool.push_back(e);
+        }
+        e0 = h->ev_pool[h->ev_used];
+        e1 = h->ev_pool[h->ev_used + 1];
+        h->ev_used += 2;
+        HIP_TRY(hipEventRecord(e0, h->stream));
+    }
+    hipError_t err = pscl_launch_decode(P, hist, h->stream);
+    if (err != hipSuccess) return fail(PSCL_EDEVICE, "decode kernel launch: %s", hipGetErrorString(err));
+    if (h->timing) HIP_TRY(hipEventRecord(e1, h->stream));
+    return PSCL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* pscl_last_error(void) { return g_err.c_str(); }
+
+int pscl_abi_version(void) { return PSCL_ABI_VERSION; }
+
+int pscl_device_count(void) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e == hipErrorNoDevice) return 0;
+    if (e != hipSuccess) return fail(PSCL_EDEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    return n;
+}
+
+int pscl_create(pscl_handle** out, int device, int N, const int32_t* info_set, int K, int L, uint64_t crc_poly) {
+    if (!out) return fail(PSCL_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (N <= 1 || (N & (N - 1))) return fail(PSCL_EINVAL, "Channel LLR length must be a power of two");
+    if (N > PSCL_MAX_N) return fail(PSCL_EUNSUP, "N=%d exceeds PSCL_MAX_N=%d", N, PSCL_MAX_N);
+    if (L <= 0) return fail(PSCL_EINVAL, "List size M must be positive");
+    if (L > PSCL_MAX_L) return fail(PSCL_EUNSUP, "list size %d exceeds PSCL_MAX_L=%d", L, PSCL_MAX_L);
+    if (K < 0 || K > N || (K > 0 && !info_set)) return fail(PSCL_EINVAL, "info_set must hold 0..N indices");
+    pscl_handle tmp;
+    tmp.N = N;
+    while ((1 << tmp.n) < N) tmp.n++;
+    tmp.K = K;
+    tmp.L = L;
+    tmp.W = K > 64 ? 2 : 1;
+    tmp.crc_poly = crc_poly;
+    for (int i = 0; i < K; ++i) {
+        int p = info_set[i];
+        if (p < 0 || p >= N) return fail(PSCL_EINVAL, "info_set indices out of range");
+        uint64_t bit = 1ULL << (p & 63);
+        if (tmp.info_mask[p >> 6] & bit) return fail(PSCL_EUNSUP, "duplicate info_set index %d", p);
+        tmp.info_mask[p >> 6] |= bit;
+        tmp.info_set.push_back(p);
+    }
+    // The decoder visits info phases in increasing phase order; candidate bit j belongs to
+    // info_set[j] (u[info_set], scl.py:183).  Both orders agree only for sorted info sets.
+    for (int i = 1; i < K; ++i)
+        if (tmp.info_set[i] < tmp.info_set[i - 1]) return fail(PSCL_EUNSUP, "info_set must be sorted ascending");
+    tmp.check_cols.assign((size_t)(K > 0 ? K : 1), 0u);
+    if (crc_poly) {
+        tmp.crc_deg = poly_degree(crc_poly);
+        if (tmp.crc_deg <= 0) return fail(PSCL_EINVAL, "Polynomial degree must be positive");
+        if (tmp.crc_deg > PSCL_MAX_CRC) return fail(PSCL_EUNSUP, "CRC degree %d > %d", tmp.crc_deg, PSCL_MAX_CRC);
+        if (K <= tmp.crc_deg) return fail(PSCL_EINVAL, "Message too short for the provided CRC polynomial");
+        for (int jj = 0; jj < K; ++jj) {
+            std::vector<uint8_t> e((size_t)K, 0);
+            e[(size_t)jj] = 1;
+            tmp.check_cols[(size_t)jj] = crc_remainder(e, crc_poly, tmp.crc_deg);
+        }
+        const int kp = K - tmp.crc_deg;
+        tmp.attach_cols.assign((size_t)(kp > 0 ? kp : 1), 0u);
+        for (int jj = 0; jj < kp; ++jj) {
+            std::vector<uint8_t> e((size_t)(kp + tmp.crc_deg), 0);
+            e[(size_t)jj] = 1;
+            tmp.attach_cols[(size_t)jj] = crc_remainder(e, crc_poly, tmp.crc_deg);
+        }
+    } else {
+        tmp.attach_cols.assign((size_t)(K > 0 ? K : 1), 0u);
+    }
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0)
+        return fail(PSCL_EDEVICE, "no HIP device available (%s)", e == hipSuccess ? "0 devices" : hipGetErrorString(e));
+    if (device < 0 || device >= ndev) return fail(PSCL_EINVAL, "device %d out of range (%d devices)", device, ndev);
+    pscl_handle* h = new pscl_handle(tmp);
+    h->device = device;
+    int rc = set_device(h);
+    if (rc) {
+        delete h;
+        return rc;
+    }
+#define CREATE_TRY(expr)                                                         \
+    do {                                                                         \
+        hipError_t _e = (expr);                                                  \
+        if (_e != hipSuccess) {                                                  \
+            int _c = fail(PSCL_EDEVICE, "%s: %s", #expr, hipGetErrorString(_e)); \
+            pscl_destroy(h);                                                     \
+            return _c;                                                           \
+        }                                                                        \
+    } while (0)
+    CREATE_TRY(hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking));
+    h->stream = h->own_stream;
+    CREATE_TRY(hipMalloc(&h->d_check_cols, h->check_cols.size() * 4));
+    CREATE_TRY(hipMalloc(&h->d_attach_cols, h->attach_cols.size() * 4));
+    CREATE_TRY(hipMalloc(&h->d_info_set, (size_t)(K > 0 ? K : 1) * 4));
+    CREATE_TRY(hipMalloc(&h->d_exp_table, sizeof(kExpTable)));
+    CREATE_TRY(hipMemcpy(h->d_check_cols, h->check_cols.data(), h->check_cols.size() * 4, hipMemcpyHostToDevice));
+    CREATE_TRY(hipMemcpy(h->d_attach_cols, h->attach_cols.data(), h->attach_cols.size() * 4, hipMemcpyHostToDevice));
+    if (K > 0) CREATE_TRY(hipMemcpy(h->d_info_set, h->info_set.data(), (size_t)K * 4, hipMemcpyHostToDevice));
+    CREATE_TRY(hipMemcpy(h->d_exp_table, kExpTable, sizeof(kExpTable), hipMemcpyHostToDevice));
+#undef CREATE_TRY
+    *out = h;
+    return PSCL_OK;
+}
+
+int pscl_destroy(pscl_handle* h) {
+    if (!h) return PSCL_OK;
+    hipSetDevice(h->device);
+    if (h->own_stream) hipStreamSynchronize(h->own_stream);
+    for (auto& b : h->scratch)
+        if (b.p) hipFree(b.p);
+    for (auto e : h->ev_pool) hipEventDestroy(e);
+    if (h->d_check_cols) hipFree(h->d_check_cols);
+    if (h->d_attach_cols) hipFree(h->d_attach_cols);
+    if (h->d_info_set) hipFree(h->d_info_set);
+    if (h->d_exp_table) hipFree(h->d_exp_table);
+    if (h->own_stream) hipStreamDestroy(h->own_stream);
+    delete h;
+    return PSCL_OK;
+}
+
+int pscl_set_stream(pscl_handle* h, void* s) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    h->stream = s ? (hipStream_t)s : h->own_stream;
+    return PSCL_OK;
+}
+
+void* pscl_get_stream(pscl_handle* h) { return h ? (void*)h->stream : nullptr; }
+
+int pscl_sync(pscl_handle* h) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return PSCL_OK;
+}
+
+int pscl_decode_device(pscl_handle* h, const double* d_llr, int64_t B, const uint64_t* d_force, uint64_t* d_best,
+                       uint8_t* d_flags, double* d_metrics, uint64_t* d_cands, double* d_info_llrs,
+                       const uint64_t* d_ref, int k_payload, int64_t* d_counters) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    if (B < 0) return fail(PSCL_EINVAL, "B must be >= 0");
+    if (B == 0) return PSCL_OK;
+    if (!d_llr) return fail(PSCL_EINVAL, "d_llr is NULL");
+    if (d_ref && !d_counters) return fail(PSCL_EINVAL, "d_ref given without d_counters");
+    if (k_payload < 0 || k_payload > h->K) return fail(PSCL_EINVAL, "k_payload out of range");
+    int rc = set_device(h);
+    if (rc) return rc;
+    const int hist = d_info_llrs != nullptr;
+    pscl_decode_params P;
+    fill_decode_params(h, P, hist);
+    P.llr = d_llr;
+    P.B = B;
+    P.force = d_force;
+    P.best = d_best;
+    P.flags = d_flags;
+    P.metrics = d_metrics;
+    P.cands = d_cands;
+    P.info_llrs = d_info_llrs;
+    P.ref = d_ref;
+    P.k_payload = k_payload;
+    P.counters = d_counters;
+    if (pscl_decode_wpg(P) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
+    return launch_decode(h, P, hist);
+}
+
+static int decode_host(pscl_handle* h, const double* llr, int64_t B, const int8_t* forced, int32_t* n_paths,
+                       int8_t* best_bits, uint8_t* crc_pass, int32_t* best_idx, double* metrics, int8_t* cands,
+                       double* info_llrs, int sc_hard) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    if (B < 0) return fail(PSCL_EINVAL, "B must be >= 0");
+    if (B == 0) return PSCL_OK;
+    if (!llr || !n_paths) return fail(PSCL_EINVAL, "llr and n_paths are required");
+    const int K = h->K, L = h->L, W = h->W, N = h->N;
+    std::vector<uint64_t> hforce;
+    if (forced) {
+        hforce.assign((size_t)B * 2 * W, 0);
+        for (int64_t b = 0; b < B; ++b) {
+            uint64_t* fr = &hforce[(size_t)b * 2 * W];
+            for (int jj = 0; jj < K; ++jj) {
+                int v = forced[b * K + jj];
+                if (v == 0 || v == 1) {
+                    fr[jj >> 6] |= 1ULL << (jj & 63);
+                    if (v) fr[W + (jj >> 6)] |= 1ULL << (jj & 63);
+                } else if (v != -1) {
+                    return fail(PSCL_EINVAL, "force_info_bits entries must be -1, 0, or 1");
+                }
+            }
+        }
+    }
+    int rc = set_device(h);
+    if (rc) return rc;
+    void *d_llr, *d_force = nullptr, *d_np, *d_best, *d_flags, *d_met = nullptr, *d_cands = nullptr, *d_illr = nullptr;
+    const size_t sz_llr = (size_t)B * N * 8;
+    if ((rc = ensure(h, 0, sz_llr, &d_llr))) return rc;
+    if (forced && (rc = ensure(h, 1, hforce.size() * 8, &d_force))) return rc;
+    if ((rc = ensure(h, 2, (size_t)B * 4, &d_np))) return rc;
+    if ((rc = ensure(h, 3, (size_t)B * W * 8, &d_best))) return rc;
+    if ((rc = ensure(h, 4, (size_t)B, &d_flags))) return rc;
+    if (metrics && (rc = ensure(h, 5, (size_t)B * L * 8, &d_met))) return rc;
+    if (cands && (rc = ensure(h, 6, (size_t)B * L * W * 8, &d_cands))) return rc;
+    if (info_llrs && (rc = ensure(h, 7, (size_t)B * L * (K > 0 ? K : 1) * 8, &d_illr))) return rc;
+    HIP_TRY(hipMemcpyAsync(d_llr, llr, sz_llr, hipMemcpyHostToDevice, h->stream));
+    if (forced) HIP_TRY(hipMemcpyAsync(d_force, hforce.data(), hforce.size() * 8, hipMemcpyHostToDevice, h->stream));
+    const int hist = info_llrs != nullptr;
+    pscl_decode_params P;
+    fill_decode_params(h, P, hist);
+    P.llr = (const double*)d_llr;
+    P.B = B;
+    P.force = (const uint64_t*)d_force;
+    P.n_paths = (int32_t*)d_np;
+    P.best = (uint64_t*)d_best;
+    P.flags = (uint8_t*)d_flags;
+    P.metrics = (double*)d_met;
+    P.cands = (uint64_t*)d_cands;
+    P.info_llrs = (double*)d_illr;
+    P.sc_hard = sc_hard;
+    if (pscl_decode_wpg(P) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
+    if ((rc = launch_decode(h, P, hist))) return rc;
+    std::vector<int32_t> hnp((size_t)B);
+    std::vector<uint64_t> hbest((size_t)B * W);
+    std::vector<uint8_t> hflags((size_t)B);
+    HIP_TRY(hipMemcpyAsync(hnp.data(), d_np, (size_t)B * 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(hbest.data(), d_best, (size_t)B * W * 8, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(hflags.data(), d_flags, (size_t)B, hipMemcpyDeviceToHost, h->stream));
+    std::vector<uint64_t> hc;
+    if (cands) {
+        hc.resize((size_t)B * L * W);
+        HIP_TRY(hipMemcpyAsync(hc.data(), d_cands, hc.size() * 8, hipMemcpyDeviceToHost, h->stream));
+    }
+    if (metrics) HIP_TRY(hipMemcpyAsync(metrics, d_met, (size_t)B * L * 8, hipMemcpyDeviceToHost, h->stream));
+    if (info_llrs)
+        HIP_TRY(hipMemcpyAsync(info_llrs, d_illr, (size_t)B * L * K * 8, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    for (int64_t b = 0; b < B; ++b) {
+        n_paths[b] = hnp[(size_t)b];
+        if (best_bits)
+            for (int jj = 0; jj < K; ++jj)
+                best_bits[b * K + jj] = (int8_t)((hbest[(size_t)b * W + (jj >> 6)] >> (jj & 63)) & 1);
+        if (crc_pass) crc_pass[b] = (hflags[(size_t)b] & PSCL_FLAG_CRC_PASS) ? 1 : 0;
+        if (best_idx) best_idx[b] = (int32_t)(hflags[(size_t)b] & PSCL_FLAG_IDX_MASK);
+        if (cands)
+            for (int r = 0; r < L; ++r)
+                for (int jj = 0; jj < K; ++jj)
+                    cands[((size_t)b * L + r) * K + jj] =
+                        (int8_t)((hc[((size_t)b * L + r) * W + (jj >> 6)] >> (jj & 63)) & 1);
+    }
+    return PSCL_OK;
+}
+
+int pscl_decode(pscl_handle* h, const double* llr, int64_t B, const int8_t* forced, int32_t* n_paths,
+                int8_t* best_bits, uint8_t* crc_pass, int32_t* best_idx, double* metrics, int8_t* cands,
+                double* info_llrs) {
+    return decode_host(h, llr, B, forced, n_paths, best_bits, crc_pass, best_idx, metrics, cands, info_llrs, 0);
+}
+
+int pscl_sc_decode(pscl_handle* h, const double* llr, int64_t B, int8_t* bits) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    if (B <= 0) return B < 0 ? fail(PSCL_EINVAL, "B must be >= 0") : PSCL_OK;
+    std::vector<int32_t> np((size_t)B);
+    return decode_host(h, llr, B, nullptr, np.data(), bits, nullptr, nullptr, nullptr, nullptr, nullptr, 1);
+}
+
+int pscl_channel_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
+                        int64_t frame0, int64_t B, double* d_llr, uint64_t* d_msg) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    if (B < 0 || frame0 < 0) return fail(PSCL_EINVAL, "B and frame0 must be >= 0");
+    if (B == 0) return PSCL_OK;
+    if (!d_llr) return fail(PSCL_EINVAL, "d_llr is NULL");
+    if (!(rate > 0)) return fail(PSCL_EINVAL, "rate must be positive");
+    if (k_payload + h->crc_deg != h->K || k_payload < 0)
+        return fail(PSCL_EINVAL, "k_payload (%d) + crc degree (%d) must equal K (%d)", k_payload, h->crc_deg, h->K);
+    int rc = set_device(h);
+    if (rc) return rc;
+    pscl_channel_params P;
+    memset(&P, 0, sizeof(P));
+    P.seed = seed;
+    P.stream_id = stream_id;
+    P.N = h->N;
+    P.K = h->K;
+    P.W = h->W;
+    P.k_payload = k_payload;
+    P.crc_deg = h->crc_deg;
+    P.info_set = h->d_info_set;
+    P.attach_cols = h->d_attach_cols;
+    const double ebno = pow(10.0, ebno_db / 10.0);
+    P.noise_var = 1.0 / (2.0 * rate * ebno);
+    P.sigma = sqrt(P.noise_var);
+    P.frame0 = frame0;
+    P.B = B;
+    P.llr = d_llr;
+    P.msg = d_msg;
+    hipError_t e = pscl_launch_channel(P, h->stream);
+    if (e != hipSuccess) return fail(PSCL_EDEVICE, "channel kernel launch: %s", hipGetErrorString(e));
+    return PSCL_OK;
+}
+
+int pscl_device_alloc(pscl_handle* h, void** d_ptr, int64_t bytes) {
+    if (!h || !d_ptr || bytes < 0) return fail(PSCL_EINVAL, "bad arguments");
+    int rc = set_device(h);
+    if (rc) return rc;
+    HIP_TRY(hipMalloc(d_ptr, (size_t)(bytes > 0 ? bytes : 1)));
+    return PSCL_OK;
+}
+
+int pscl_device_free(pscl_handle* h, void* d_ptr) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    if (d_ptr) HIP_TRY(hipFree(d_ptr));
+    return PSCL_OK;
+}
+
+int pscl_memcpy_htod(pscl_handle* h, void* d_dst, const void* src, int64_t bytes) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    HIP_TRY(hipMemcpyAsync(d_dst, src, (size_t)bytes, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return PSCL_OK;
+}
+
+int pscl_memcpy_dtoh(pscl_handle* h, void* dst, const void* d_src, int64_t bytes) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    HIP_TRY(hipMemcpyAsync(dst, d_src, (size_t)bytes, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return PSCL_OK;
+}
+
+int pscl_memset_device(pscl_handle* h, void* d_dst, int value, int64_t bytes) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    HIP_TRY(hipMemsetAsync(d_dst, value, (size_t)bytes, h->stream));
+    return PSCL_OK;
+}
+
+int pscl_timing_enable(pscl_handle* h, int enable) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    h->timing = enable != 0;
+    h->ev_used = 0;
+    return PSCL_OK;
+}
+
+int pscl_timing_read(pscl_handle* h, int64_t* launches, double* total_ms) {
+    if (!h || !launches || !total_ms) return fail(PSCL_EINVAL, "bad arguments");
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    double tot = 0.0;
+    for (size_t i = 0; i + 1 < h->ev_used; i += 2) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, h->ev_pool[i], h->ev_pool[i + 1]));
+        tot += ms;
+    }
+    *launches = (int64_t)(h->ev_used / 2);
+    *total_ms = tot;
+    return PSCL_OK;
+}
+
+int pscl_launch_info(pscl_handle* h, int64_t B, int* waves_per_wg, int64_t* grid, int* lds_bytes) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    pscl_decode_params P;
+    fill_decode_params(h, P, 0);
+    P.B = B;
+    if (waves_per_wg) *waves_per_wg = pscl_decode_wpg(P);
+    if (grid) *grid = pscl_decode_grid(P);
+    if (lds_bytes) *lds_bytes = pscl_decode_lds(P, 0);
+    return PSCL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,215 @@
+/*
+ * Bit-exact softplus for the SCL path metric, usable from host C and gfx950 device code.
+ *
+ * The reference updates a path metric with
+ *     metric + float(np.logaddexp(0.0, v))          dl_scl_polar/polar/scl.py:102-105
+ * and numpy's scalar logaddexp (npy_logaddexp) is
+ *     x == y        -> x + LOGE2
+ *     tmp = x - y > 0 -> x + log1p(exp(-tmp))
+ *     else          -> y + log1p(exp(tmp))
+ * with exp/log1p taken from the platform libm (glibc 2.35 on this image).  The list
+ * decoder sorts on these metrics, so to make decisions bit-identical at ties and
+ * near-ties the device must reproduce glibc's exp and log1p *bit for bit*:
+ *
+ *   exp   : glibc 2.35 __exp_fma (the ifunc chosen on any FMA+AVX2 host, which is the
+ *           case for the survey container and the MI355X host). Table-driven, N=128,
+ *           degree-5 polynomial; the fused multiply-adds below follow that variant's
+ *           instruction sequence exactly, every other operation is unfused.
+ *   log1p : glibc 2.35 dbl-64 s_log1p.c (fdlibm algorithm with glibc's split
+ *           polynomial evaluation); no FMA in that build.
+ *
+ * The exp table is regenerated from mathematics by gen_exp_table.py.  Host parity of
+ * this header against libm is tested in tests/test_softplus_host.py; device parity in
+ * tests/test_gpu_parity.py.
+ *
+ * Contraction must stay OFF for this file (hipcc: the pragma below; gcc: -ffp-contract=off).
+ */
+#ifndef PSCL_GLIBC_SOFTPLUS_H
+#define PSCL_GLIBC_SOFTPLUS_H
+
+#include <stdint.h>
+#include <string.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define PSCL_HD __host__ __device__ __forceinline__
+#else
+#define PSCL_HD static inline
+#endif
+
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+
+#define PSCL_EXP_TABLE_WORDS 256
+
+/* constants from glibc's __exp_data (N = 128) */
+#define PSCL_EXP_INVLN2N 0x1.71547652b82fep0 * 128.0
+#define PSCL_EXP_SHIFT 0x1.8p52
+#define PSCL_EXP_NEGLN2HIN -0x1.62e42fefa0000p-8
+#define PSCL_EXP_NEGLN2LON -0x1.cf79abc9e3b3ap-47
+#define PSCL_EXP_C2 0x1.ffffffffffdbdp-2
+#define PSCL_EXP_C3 0x1.555555555543cp-3
+#define PSCL_EXP_C4 0x1.55555cf172b91p-5
+#define PSCL_EXP_C5 0x1.1111167a4d017p-7
+
+/* numpy's LOGE2 (npy_math.h NPY_LOGE2) */
+#define PSCL_LOGE2 0.693147180559945309417232121458176568
+
+PSCL_HD uint64_t pscl_asu64(double x) {
+    uint64_t u;
+    memcpy(&u, &x, 8);
+    return u;
+}
+
+PSCL_HD double pscl_asf64(uint64_t u) {
+    double x;
+    memcpy(&x, &u, 8);
+    return x;
+}
+
+PSCL_HD double pscl_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
+/* exp(x), bit-identical to glibc 2.35 __exp_fma.  T = the 256-word table (exp_table.inc). */
+PSCL_HD double pscl_exp(double x, const uint64_t* T) {
+    uint64_t ix = pscl_asu64(x);
+    uint32_t abstop = (uint32_t)(ix >> 52) & 0x7ff;
+    if (abstop - 0x3c9u >= 0x3fu) {
+        if ((int32_t)(abstop - 0x3c9u) < 0) return 1.0 + x; /* |x| < 2^-54, also +-0 */
+        if (abstop > 0x408u) {                               /* |x| >= 1024 */
+            if (ix == 0xfff0000000000000ULL) return 0.0;     /* -inf */
+            if (abstop == 0x7ffu) return 1.0 + x;            /* nan, +inf */
+            if (ix >> 63) return 0.0;                        /* __math_uflow(0) */
+            return pscl_asf64(0x7ff0000000000000ULL);        /* __math_oflow(0) */
+        }
+        abstop = 0; /* 512 <= |x| < 1024: handled by the special case below */
+    }
+    double kd = pscl_fma(x, PSCL_EXP_INVLN2N, PSCL_EXP_SHIFT);
+    uint64_t ki = pscl_asu64(kd);
+    kd = kd - PSCL_EXP_SHIFT;
+    double r = pscl_fma(kd, PSCL_EXP_NEGLN2HIN, x);
+    r = pscl_fma(kd, PSCL_EXP_NEGLN2LON, r);
+    uint64_t idx = 2 * (ki & 127);
+    uint64_t top = ki << 45;
+    double p1 = pscl_fma(r, PSCL_EXP_C3, PSCL_EXP_C2);
+    double tr = r + pscl_asf64(T[idx]); /* tail + r */
+    uint64_t sbits = T[idx + 1] + top;
+    double r2 = r * r;
+    double p2 = pscl_fma(r, PSCL_EXP_C5, PSCL_EXP_C4);
+    double t = pscl_fma(p1, r2, tr);
+    double r4 = r2 * r2;
+    double tmp = pscl_fma(r4, p2, t);
+    if (abstop == 0) {
+        if ((ki & 0x80000000ULL) == 0) {
+            /* k > 0: exponent of scale may have overflowed */
+            double scale = pscl_asf64(sbits - (1009ULL << 52));
+            double y = pscl_fma(scale, tmp, scale);
+            return y * 0x1p1009;
+        }
+        /* k < 0: subnormal range, rounded once (glibc specialcase) */
+        double scale = pscl_asf64(sbits + (1022ULL << 52));
+        double st = tmp * scale;
+        double y = scale + st;
+        if (y < 1.0) {
+            double hi = y + 1.0;
+            double lo = (scale - y) + st;
+            lo = ((1.0 - hi) + y) + lo;
+            y = (lo + hi) - 1.0;
+            if (y == 0.0) y = 0.0;
+        }
+        return y * 0x1p-1022;
+    }
+    double scale = pscl_asf64(sbits);
+    return pscl_fma(scale, tmp, scale);
+}
+
+/* log1p(x), bit-identical to glibc 2.35 (dbl-64 s_log1p.c, non-FMA build). */
+PSCL_HD double pscl_log1p(double x) {
+    const double ln2_hi = 6.93147180369123816490e-01;
+    const double ln2_lo = 1.90821492927058770002e-10;
+    const double Lp1 = 6.666666666666735130e-01, Lp2 = 3.999999999940941908e-01,
+                 Lp3 = 2.857142874366239149e-01, Lp4 = 2.222219843214978396e-01,
+                 Lp5 = 1.818357216161805012e-01, Lp6 = 1.531383769920937332e-01,
+                 Lp7 = 1.479819860511658591e-01;
+    uint64_t ix = pscl_asu64(x);
+    int32_t hx = (int32_t)(ix >> 32);
+    int32_t ax = hx & 0x7fffffff;
+    int32_t k = 1, hu = 0;
+    double f = 0.0, c = 0.0;
+    if (hx < 0x3FDA827A) {
+        if (ax >= 0x3ff00000) { /* x <= -1 */
+            if (x == -1.0) return -pscl_asf64(0x7ff0000000000000ULL);
+            return pscl_asf64(0x7ff8000000000000ULL);
+        }
+        if (ax < 0x3e200000) { /* |x| < 2^-29 */
+            if (ax < 0x3c900000) return x;
+            return x - (x * x) * 0.5;
+        }
+        if (hx > 0 || hx <= (int32_t)0xbfd2bec3) {
+            k = 0;
+            f = x;
+            hu = 1;
+        }
+    }
+    if (hx >= 0x7ff00000) return x + x;
+    if (k != 0) {
+        double u;
+        if (hx < 0x43400000) {
+            u = 1.0 + x;
+            hu = (int32_t)(pscl_asu64(u) >> 32);
+            k = (hu >> 20) - 1023;
+            c = (k > 0) ? 1.0 - (u - x) : x - (u - 1.0);
+            c = c / u;
+        } else {
+            u = x;
+            hu = (int32_t)(pscl_asu64(u) >> 32);
+            k = (hu >> 20) - 1023;
+            c = 0.0;
+        }
+        hu &= 0x000fffff;
+        uint64_t lo = pscl_asu64(u) & 0xffffffffULL;
+        if (hu < 0x6a09e) {
+            u = pscl_asf64(((uint64_t)(uint32_t)(hu | 0x3ff00000) << 32) | lo);
+        } else {
+            k += 1;
+            u = pscl_asf64(((uint64_t)(uint32_t)(hu | 0x3fe00000) << 32) | lo);
+            hu = (0x00100000 - hu) >> 2;
+        }
+        f = u - 1.0;
+    }
+    double hfsq = (0.5 * f) * f;
+    if (hu == 0) { /* |f| < 2^-20 */
+        if (f == 0.0) {
+            if (k == 0) return 0.0;
+            double kd = (double)k;
+            return (kd * ln2_lo + c) + kd * ln2_hi;
+        }
+        double R = (1.0 - 0.66666666666666666 * f) * hfsq;
+        if (k == 0) return f - R;
+        double kd = (double)k;
+        return kd * ln2_hi - ((R - (kd * ln2_lo + c)) - f);
+    }
+    double s = f / (2.0 + f);
+    double z = s * s;
+    double z2 = z * z;
+    double z4 = z2 * z2;
+    double z6 = z2 * z4;
+    double R = ((z * Lp1 + z2 * (z * Lp3 + Lp2)) + z4 * (z * Lp5 + Lp4)) + z6 * (z * Lp7 + Lp6);
+    double sR = (R + hfsq) * s;
+    if (k == 0) return f - (hfsq - sR);
+    double kd = (double)k;
+    return kd * ln2_hi - ((hfsq - ((kd * ln2_lo + c) + sR)) - f);
+}
+
+/* L = log1p(exp(-|v|)), the part of logaddexp(0, +-v) shared by both bit hypotheses. */
+PSCL_HD double pscl_softplus_tail(double v, const uint64_t* T) {
+    double a = v < 0 ? -v : v;
+    return pscl_log1p(pscl_exp(-a, T));
+}
+
+/* np.logaddexp(0.0, v) given the shared tail L (see above). */
+PSCL_HD double pscl_logaddexp0(double v, double L) {
+    if (v == 0.0) return PSCL_LOGE2; /* x == y branch: 0 + LOGE2 */
+    return v > 0.0 ? v + L : 0.0 + L;
+}
+
+#endif /* PSCL_GLIBC_SOFTPLUS_H */

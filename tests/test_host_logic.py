@@ -1,0 +1,70 @@
+"""Host-side logic of polar_code_amd against the reference's golden vectors (no GPU)."""
+import numpy as np
+import pytest
+
+from polar_code_amd import config
+from polar_code_amd.polar import crc as pcrc
+from polar_code_amd.polar import polar as ppolar
+from polar_code_amd.utils.seeding import seed_all
+
+
+def test_config_defaults():
+    cfg = config.get_config()
+    assert (cfg.N, cfg.K, cfg.crc_poly, cfg.crc_bits, cfg.retries) == (128, 64, "0x1864CFB", 24, 8)
+    assert cfg.list_sizes == [1, 2, 4, 8] and cfg.ebno_sweep == [4.0, 6.5, 0.5]
+
+
+def test_info_sets(golden):
+    g = golden("g1_info_sets.npz")
+    for key in g.files:
+        _, N, K = key.split("_")
+        np.testing.assert_array_equal(ppolar.construct_info_set(int(N), int(K)), g[key])
+    with pytest.raises(ValueError):
+        ppolar.construct_info_set(100, 10)
+    with pytest.raises(ValueError):
+        ppolar.construct_info_set(128, 0)
+
+
+def test_crc_attach_check(golden):
+    g = golden("g2_crc.npz")
+    np.testing.assert_array_equal(pcrc.attach_crc(g["payload"], "0x1864CFB"), g["attached"])
+    for p, a in zip(g["payload"][:16], g["attached"][:16]):
+        np.testing.assert_array_equal(pcrc.attach_crc(p, "0x1864CFB"), a)
+    np.testing.assert_array_equal(pcrc.attach_crc(g["payload8"], "0x17"), g["attached8_0x17"])
+    np.testing.assert_array_equal(pcrc.check_crc(g["attached"], "0x1864CFB"), g["check_ok"])
+    np.testing.assert_array_equal(pcrc.check_crc(g["corrupted"], "0x1864CFB"), g["check_bad"])
+    np.testing.assert_array_equal(pcrc.check_crc(g["random64"], "0x1864CFB"), g["check_random"])
+    assert pcrc.check_crc(g["attached"][0], "0x1864CFB") is True
+    with pytest.raises(ValueError):
+        pcrc.check_crc(np.zeros(24, np.int8), "0x1864CFB")
+    with pytest.raises(ValueError):
+        pcrc.attach_crc(np.zeros(4, np.int8), "")
+    with pytest.raises(ValueError):
+        pcrc.attach_crc(np.zeros(4, np.int8), "0x1")
+
+
+def test_crc_roundtrip_reference_case():
+    # tests/test_scl_crc.py:25-37 of the reference, restated
+    seed_all(7)
+    msg = np.random.randint(0, 2, size=40, dtype=np.int8)
+    msg_crc = pcrc.attach_crc(msg, "0x1864CFB")
+    assert msg_crc.shape[0] == 64 and pcrc.check_crc(msg_crc, "0x1864CFB")
+    corrupted = msg_crc.copy()
+    corrupted[3] ^= 1
+    assert not pcrc.check_crc(corrupted, "0x1864CFB")
+
+
+def test_encode(golden):
+    g = golden("g3_encode.npz")
+    np.testing.assert_array_equal(ppolar.encode(g["msg"]), g["code"])
+    np.testing.assert_array_equal(ppolar.encode(g["msg"][0]), g["code"][0])
+    np.testing.assert_array_equal(ppolar._polar_transform(g["u"]), g["transform"])
+    with pytest.raises(ValueError):
+        ppolar.encode(np.zeros(10, np.int8))
+
+
+def test_f_g_helpers():
+    a = np.array([1.0, -2.0, 0.0, -0.5])
+    b = np.array([-3.0, -1.0, 5.0, 0.25])
+    np.testing.assert_array_equal(ppolar._f(a, b), [-1.0, 1.0, 0.0, -0.25])
+    np.testing.assert_array_equal(ppolar._g(a, b, np.array([0, 1, 1, 0], np.int8)), [-2.0, 1.0, 5.0, -0.25])

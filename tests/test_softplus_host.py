@@ -1,0 +1,45 @@
+"""Host build of the device metric code (csrc/glibc_softplus.h) is bit-identical to the
+platform libm exp/log1p and to numpy's logaddexp(0, v) -- the reference's metric."""
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+LIB = Path(__file__).resolve().parent.parent / "oracle" / "libsoftplus_host.so"
+
+
+def _lib():
+    L = C.CDLL(str(LIB))
+    L.softplus_compare.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.softplus_port_batch.argtypes = [C.c_void_p, C.c_int64, C.c_void_p]
+    return L
+
+
+def _inputs(n, seed=0):
+    rng = np.random.default_rng(seed)
+    parts = [
+        rng.normal(0, 8, n),
+        rng.uniform(-1100, 1100, n),
+        rng.standard_normal(n) * 10.0 ** rng.uniform(-20, 3, n),
+        np.array([0.0, -0.0, 1e-300, -1e-300, 5e-324, 708.0, -708.4, 745.2, -745.2, 1e6, -1e6, 511.99, 512.0,
+                  1023.9, 1024.0, 2 ** -54, -(2 ** -54), 2 ** -29, 0.4142, np.log(2.0)]),
+    ]
+    u = rng.integers(0, 2 ** 63, n, dtype=np.int64).view(np.float64)
+    parts.append(u[np.isfinite(u)])
+    return np.ascontiguousarray(np.concatenate(parts))
+
+
+def test_port_matches_libm():
+    v = _inputs(400_000)
+    be, bl, bs = (np.zeros(1, np.int64) for _ in range(3))
+    _lib().softplus_compare(v.ctypes.data, v.size, be.ctypes.data, bl.ctypes.data, bs.ctypes.data)
+    assert (be[0], bl[0], bs[0]) == (0, 0, 0)
+
+
+def test_port_matches_numpy_logaddexp():
+    v = _inputs(50_000, seed=1)
+    v = v[np.abs(v) < 1e300]
+    out = np.empty_like(v)
+    _lib().softplus_port_batch(v.ctypes.data, v.size, out.ctypes.data)
+    ref = np.array([float(np.logaddexp(0.0, float(x))) for x in v])
+    np.testing.assert_array_equal(out.view(np.int64), ref.view(np.int64))
