@@ -1,0 +1,205 @@
+"""Headline benchmark: decoded frames/s, P(128,64)+CRC-24 SCL L=8 at Eb/N0 = 5 dB (BASELINE.json).
+
+    python bench.py [--gpus N --steps K --warmup W --frames B --list L --ebno 5.0]
+
+One step = one pass of the hot path over one batch of B frames per GPU that is already
+resident in HBM: SCL decode (fp64, bit-exact to the reference) + CRC selection + FER/BER
+counting, i.e. run_fer_sweep.py:79-109 without the TX chain.  The batches are generated
+on the device before the timed region by the Philox TX kernel (payload -> CRC-24 ->
+polar encode -> BPSK -> AWGN -> LLR), distinct frames per step and per rank.
+
+Multi-GPU: one process per GPU (torchrun), frames sharded by global frame index, no
+data-path collective; one RCCL all-reduce of the error counters and one of the timings.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+REF_FER_L8 = (26, 2000)  # results/fer_M8.csv:2, SCL L=8 @ 5 dB, CRC-fail FER
+POLY = "0x1864CFB"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--frames", type=int, default=1_000_000, help="frames per GPU per step")
+    ap.add_argument("--list", type=int, default=8)
+    ap.add_argument("--ebno", type=float, default=5.0)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def frame_bytes(N: int, W: int) -> int:
+    """Algorithmic HBM bytes per decoded frame: read N fp64 LLRs and W reference words,
+    write W best-candidate words and one flag byte."""
+    return N * 8 + W * 8 + W * 8 + 1
+
+
+def load_traffic(workload_key: str):
+    """HBM bytes per decode launch measured by rocprofv3 PMC passes (tools/pmc_traffic.py),
+    if a summary for this exact workload is committed under profiles/."""
+    p = ROOT / "profiles" / "pmc_traffic.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        e = d.get(workload_key)
+        return None if e is None else float(e["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def cpu_baseline(llr_host: np.ndarray, info, L: int, budget_s: float):
+    """The oracle (C restatement of the reference, OpenMP over frames) on host cores."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle  # test/baseline infrastructure only
+
+    t0 = time.perf_counter()
+    n0 = min(2000, llr_host.shape[0])
+    oracle.decode_batch(llr_host[:n0], info, L, POLY)
+    dt = time.perf_counter() - t0
+    n = int(min(llr_host.shape[0], max(n0, n0 * budget_s / max(dt, 1e-6))))
+    t0 = time.perf_counter()
+    oracle.decode_batch(llr_host[:n], info, L, POLY)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "frames/s", "cores": oracle.num_threads(), "kind": "port",
+            "sample": f"first {n} frames of the step-0 batch (same LLRs), oracle/scl_oracle.c decode_scl "
+                      f"L={L} + CRC select, OpenMP over frames, {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group(backend="nccl", device_id=dev)
+
+    from polar_code_amd import _native
+    from polar_code_amd.polar.polar import construct_info_set
+
+    N, K, L, B = 128, 64, args.list, args.frames
+    info = construct_info_set(N, K)
+    dec = _native.Decoder(N, info, L, POLY, device=local)
+    stream = torch.cuda.current_stream(dev)
+    dec.set_stream(stream.cuda_stream)
+    W = dec.W
+    kp = K - 24
+    rate = K / N
+
+    # ---- inputs resident in HBM: distinct frames per (rank, step), generated on device
+    nbuf = max(1, min(args.steps, int(48e9 // (B * N * 8))))
+    llr = [torch.empty((B, N), dtype=torch.float64, device=dev) for _ in range(nbuf)]
+    msg = [torch.empty((B, W), dtype=torch.int64, device=dev) for _ in range(nbuf)]
+    best = torch.empty((B, W), dtype=torch.int64, device=dev)
+    flags = torch.empty((B,), dtype=torch.uint8, device=dev)
+    counters = torch.zeros(8, dtype=torch.int64, device=dev)
+    snr_idx = int(round(args.ebno * 10))
+    for i in range(nbuf):
+        frame0 = (rank * nbuf + i) * B
+        dec.channel_device(args.seed, snr_idx, args.ebno, rate, kp, frame0, B, llr[i].data_ptr(), msg[i].data_ptr())
+    torch.cuda.synchronize(dev)
+
+    def step(i):
+        j = i % nbuf
+        dec.decode_device(llr[j].data_ptr(), B, d_best=best.data_ptr(), d_flags=flags.data_ptr(),
+                          d_ref=msg[j].data_ptr(), k_payload=kp, d_counters=counters.data_ptr())
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    counters.zero_()
+    dec.timing_enable(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    launches, kern_ms = dec.timing_read()
+    dec.timing_enable(False)
+
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(counters, op=dist.ReduceOp.SUM)
+    elapsed = float(tmax.item())
+    c = counters.cpu().numpy()
+    frames_total = B * args.steps * world
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        host = llr[0][: min(B, 400_000)].cpu().numpy()
+        cpu = cpu_baseline(host, info, L, args.cpu_seconds)
+
+    if rank == 0:
+        avg_ms = kern_ms / max(launches, 1)
+        fb = frame_bytes(N, W)
+        achieved = fb * B / (avg_ms * 1e-3) / 1e9
+        wkey = f"scl_L{L}_N{N}_K{K}_B{B}"
+        traffic = load_traffic(wkey)
+        fer = c[1] / max(c[0], 1)
+        p0 = REF_FER_L8[0] / REF_FER_L8[1]
+        pp = (c[1] + REF_FER_L8[0]) / (c[0] + REF_FER_L8[1])
+        se = math.sqrt(max(pp * (1 - pp) * (1 / max(c[0], 1) + 1 / REF_FER_L8[1]), 1e-30))
+        line = {
+            "metric": "decoded frames/sec, P(128,64)+CRC24 SCL L=8 @ Eb/N0=5 dB; FER match",
+            "value": frames_total / elapsed,
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: on-device Philox4x32 BPSK/AWGN frames (payload->CRC24->polar->LLR), resident in HBM",
+            "config": {"workload": f"SCL L={L} P({N},{K})+CRC24 (0x1864CFB) @ Eb/N0={args.ebno:g} dB, "
+                                   f"{B} frames/GPU/step, decode+CRC select+FER/BER count",
+                       "N": N, "K": K, "list_size": L, "ebno_db": args.ebno, "frames_per_gpu_per_step": B,
+                       "global_batch": B * world, "parallelism": f"frame-sharded x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBS,
+                         "traffic": traffic,
+                         "kernel": "scl_decode_kernel", "avg_launch_ms": avg_ms, "launches": launches,
+                         "bytes_per_frame": fb},
+            "cpu_baseline": cpu,
+            "fer": {"frames": int(c[0]), "frame_errors": int(c[1]), "fer": fer, "ber": c[2] / max(c[0] * K, 1),
+                    "reference_fer": p0, "z_vs_reference": (fer - p0) / se},
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

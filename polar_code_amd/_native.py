@@ -8,6 +8,9 @@ from __future__ import annotations
 
 import ctypes as C
 import functools
+import importlib.util
+import os
+import sys
 import threading
 from pathlib import Path
 
@@ -44,8 +47,24 @@ class PolarNativeError(RuntimeError):
     """Device/runtime failure inside libpolar_mi355x.so."""
 
 
+def _bind_hip_runtime() -> None:
+    """Keep ONE HIP runtime per process.  PyTorch-ROCm bundles its own libamdhip64.so.7; if
+    this library loaded /opt/rocm's copy first, torch would later load a second runtime and
+    see no GPU.  Preloading torch's copy (same soname) makes both bind to it.  Set
+    PSCL_HIP_RUNTIME=system to keep /opt/rocm's runtime (processes that never use torch)."""
+    if os.environ.get("PSCL_HIP_RUNTIME", "") == "system" or "torch" in sys.modules:
+        return
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    cand = Path(spec.origin).parent / "lib" / "libamdhip64.so"
+    if cand.exists():
+        C.CDLL(str(cand), mode=C.RTLD_GLOBAL)
+
+
 @functools.lru_cache(maxsize=1)
 def lib() -> C.CDLL:
+    _bind_hip_runtime()
     if not LIB_PATH.exists():
         raise PolarNativeError(
             f"{LIB_PATH} not built: run `python -m polar_code_amd.build` (hipcc, gfx950). "

@@ -150,7 +150,10 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
                     const uint64_t ti = shfl_u64(tab, isrc);
                     const uint64_t xi = is_g ? shfl_u64(xs, isrc) : 0;
                     if (tt < total) {
-                        const double* par = (d == 1) ? ch : A + off_in + slot_of(ti, d - 1) * (2 * w);
+                        // the first step reads the parent through the path's slot table; deeper
+                        // steps read the depth this phase just wrote into the path's own slot
+                        const int ps = (d == start) ? slot_of(ti, d - 1) : i;
+                        const double* par = (d == 1) ? ch : A + off_in + ps * (2 * w);
                         const double a = par[e], b = par[e + w];
                         A[off_out + i * w + e] = is_g ? g_node(a, b, (uint32_t)(xi >> e) & 1u) : f_minsum(a, b);
                     }
