@@ -16,7 +16,7 @@ from pathlib import Path
 
 import numpy as np
 
-LIB_PATH = Path(__file__).resolve().parent / "libpolar_mi355x.so"
+LIB_PATH = Path(os.environ.get("PSCL_LIB_PATH") or Path(__file__).resolve().parent / "libpolar_mi355x.so")
 
 PSCL_OK = 0
 PSCL_EINVAL = -1

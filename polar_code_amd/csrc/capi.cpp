@@ -126,9 +126,12 @@ void fill_decode_params(const pscl_handle* h, pscl_decode_params& P, int hist) {
     P.crc_cols = h->d_check_cols;
     P.has_crc = h->crc_poly != 0;
     P.exp_table = h->d_exp_table;
-    const int a_bytes = h->N >= 4 ? h->L * (h->N - 2) * 8 : 0;
+    // one wavefront decodes F = 32 / LMAX frames (2*LMAX lanes each)
+    const int F = 32 / pscl_decode_lmax(h->L);
+    const int fstride = h->N + (h->N >= 8 ? h->L * (h->N / 2 - 2) : 0);  // doubles per frame
+    const int a_bytes = F * fstride * 8;
     P.a_bytes = a_bytes;
-    int wb = a_bytes + 64 + (hist ? h->K * h->L * 9 : 0);
+    int wb = a_bytes + 64 + (hist ? F * (h->K * h->L * 8 + h->N * h->L) : 0);
     P.wave_bytes = (wb + 15) & ~15;
 }
 

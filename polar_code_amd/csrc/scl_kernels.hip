@@ -25,6 +25,11 @@
 #include "glibc_softplus.h"
 #include "scl_kernels.h"
 
+// Timing-only ablation switches for diagnostic builds (tools/ablate.py); 0 in the product.
+#ifndef PSCL_ABLATE
+#define PSCL_ABLATE 0
+#endif
+
 namespace {
 
 constexpr int kWave = 64;
@@ -78,12 +83,55 @@ __device__ __forceinline__ uint64_t polar_transform64(uint64_t x) {
 
 __device__ __forceinline__ uint64_t pick_word(uint64_t w0, uint64_t w1, int idx) { return idx ? w1 : w0; }
 
-// slot table: 5 bits per depth d in [1, n-1] at bit offset 5*d
-__device__ __forceinline__ int slot_of(uint64_t tab, int d) { return (int)((tab >> (5 * d)) & 31u); }
+
+// ---------------------------------------------------------------- lane-group helpers
+// A wavefront decodes F = 64/G frames at once; frame slot fl owns the G = 2*LMAX lanes
+// [fl*G, fl*G + G).  Lane g < L of a group holds list path g (list position == lane, so the
+// stable-sort tie key is the lane index itself); lanes [L, 2L) carry the bit-1 children
+// while the list is being extended.
+
+template <int G, int K>
+__device__ __forceinline__ uint32_t grot32c(uint32_t v, int lane) {
+    if constexpr (G == 16) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + K, 0xF, 0xF, false);  // row_ror:K
+    } else if constexpr (G == 8) {
+        const uint32_t a = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + K, 0xF, 0xF, false);
+        const uint32_t b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + K + 8, 0xF, 0xF, false);
+        return ((lane & 7) >= K) ? a : b;  // row_ror:K reads lane x-K; wrap inside the 8-lane group
+    } else if constexpr (G == 4) {
+        constexpr int q = ((0 + K) & 3) | (((1 + K) & 3) << 2) | (((2 + K) & 3) << 4) | (((3 + K) & 3) << 6);
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, q, 0xF, 0xF, false);  // quad_perm
+    } else if constexpr (G == 2) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    } else {
+        return bperm32(v, (lane & ~(G - 1)) | ((lane + K) & (G - 1)));
+    }
+}
+
+template <int G, int K>
+__device__ __forceinline__ double grot64c(double v, int lane) {
+    const uint64_t u = pscl_asu64(v);
+    const uint32_t lo = grot32c<G, K>((uint32_t)u, lane), hi = grot32c<G, K>((uint32_t)(u >> 32), lane);
+    return pscl_asf64(((uint64_t)hi << 32) | lo);
+}
+
+// stable rank of this lane's key (m, t) among the G keys of its group
+template <int G, int K>
+__device__ __forceinline__ void rank_step(double m, uint32_t t, int lane, int& r) {
+    if constexpr (K < G) {
+        const double my = grot64c<G, K>(m, lane);
+        const uint32_t ty = grot32c<G, K>(t, lane);
+        r += (my < m) || (my == m && ty < t);
+        rank_step<G, K + 1>(m, t, lane, r);
+    }
+}
 
 template <int LMAX, bool HIST>
 __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
     scl_decode_kernel(const pscl_decode_params P) {
+    constexpr int G = 2 * LMAX;      // lanes per frame
+    constexpr int F = kWave / G;     // frames per wavefront
+    constexpr int LOG_G = __builtin_ctz(G);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint64_t* T = reinterpret_cast<uint64_t*>(smem);  // exp table, 2 KB, shared by the WG
     for (int i = threadIdx.x; i < PSCL_EXP_TABLE_WORDS; i += blockDim.x) T[i] = P.exp_table[i];
@@ -91,20 +139,40 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
 
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    unsigned char* wbase = smem + PSCL_EXP_TABLE_WORDS * 8 + (size_t)wave * P.wave_bytes;
-    double* A = reinterpret_cast<double*>(wbase);                          // L*(N-2) LLRs
-    uint8_t* inv = wbase + P.a_bytes;                                       // 64 B selection map
-    double* hist_llr = reinterpret_cast<double*>(wbase + P.a_bytes + 64);   // [K][L]
-    uint8_t* hist_par = wbase + P.a_bytes + 64 + (size_t)P.K * P.L * 8;     // [K][L]
-
+    const int fl = lane >> LOG_G;        // frame slot of this lane
+    const int g = lane & (G - 1);        // lane within the frame group
+    const int gbase = lane & ~(G - 1);
     const int N = P.N, n = P.n, K = P.K, L = P.L, W = P.W;
-    const int wpg = (int)(blockDim.x >> 6);
-    const int64_t stride = (int64_t)gridDim.x * wpg;
+    // per frame in LDS: the N channel LLRs, then L slots for each stored depth 2..n-1
+    // (depth 1 is recomputed from the channel LLRs when depth 2 needs it)
+    const int fstride = N + (N >= 8 ? L * (N / 2 - 2) : 0);
+    const int half = N >> 1;
+    unsigned char* wbase = smem + PSCL_EXP_TABLE_WORDS * 8 + (size_t)wave * P.wave_bytes;
+    double* A = reinterpret_cast<double*>(wbase);                                     // [F][fstride]
+    uint8_t* inv = wbase + P.a_bytes;                                                  // [64]
+    double* hist_llr = reinterpret_cast<double*>(wbase + P.a_bytes + 64) + (size_t)fl * K * L;
+    uint8_t* hist_par = wbase + P.a_bytes + 64 + (size_t)F * K * L * 8 + (size_t)fl * N * L;  // [N][L]
+    double* Af = A + fl * fstride;       // this lane's frame
 
-    for (int64_t f = (int64_t)blockIdx.x * wpg + wave; f < P.B; f += stride) {
-        const double* ch = P.llr + f * N;
+    const int wpg = (int)(blockDim.x >> 6);
+    const int64_t wstride = (int64_t)gridDim.x * wpg * F;
+    const bool path_lane = g < L;
+    // candidate c = g: (path g, bit 0) for g < L, (path g-L, bit 1) for L <= g < 2L
+    const int cpath = g < L ? g : g - L;
+    const uint32_t cbit = g >= L ? 1u : 0u;
+    const bool cand_lane = g < 2 * L;
+
+    for (int64_t f0 = ((int64_t)blockIdx.x * wpg + wave) * F; f0 < P.B; f0 += wstride) {
+        const int64_t f = f0 + fl;
+        const bool fvalid = f < P.B;
+        {  // stage this frame's channel LLRs in LDS (coalesced; read at every depth-1 use)
+            const double* src = P.llr + (fvalid ? f : f0) * N;
+            for (int x = g; x < N; x += G) Af[x] = src[x];
+        }
+        wave_lds_fence();
+        const double* ch = Af;
         uint64_t fm0 = 0, fm1 = 0, fv0 = 0, fv1 = 0;
-        if (P.force) {
+        if (P.force && fvalid) {
             const uint64_t* fr = P.force + f * 2 * W;
             fm0 = fr[0];
             fv0 = fr[W];
@@ -113,193 +181,194 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
                 fv1 = fr[W + 1];
             }
         }
-        // per-path state (meaningful in lanes < cnt)
         double metric = 0.0;
-        int rank = 0;
         uint64_t u0 = 0, u1 = 0;    // decided bits u[phase]
         uint64_t ib0 = 0, ib1 = 0;  // candidate bits in info order
         uint32_t syn = 0;           // CRC syndrome of the candidate bits
-        uint64_t tab = 0;           // LDS slot per depth
-        int cnt = 1;                // live paths (wave-uniform)
+        uint32_t tab = 0;           // LDS slot per depth d (5 bits at 5*(d-1))
+        int cnt = 1;                // live paths of this frame (group-uniform)
+        int cu = 1;                 // wave-uniform bound: max live paths over the wave's frames
         int j = 0;                  // info index (wave-uniform)
 
         for (int phi = 0; phi < N; ++phi) {
             const int t = phi ? __builtin_ctz(phi) : n;
             const int start = phi ? n - t : 1;
-            // partial sums of the left sibling of the g node: transform of u[phi-w, phi)
-            uint64_t xs = 0;
+            uint64_t xs = 0;  // partial sums of the left sibling of the g node
             if (phi) {
                 const int w = 1 << t;
                 const int lo = phi - w;
-                uint64_t word = pick_word(u0, u1, lo >> 6);
-                uint64_t seg = (w == 64) ? word : (word >> (lo & 63)) & ((1ULL << w) - 1);
+                const uint64_t word = pick_word(u0, u1, lo >> 6);
+                const uint64_t seg = (w == 64) ? word : (word >> (lo & 63)) & ((1ULL << w) - 1);
                 xs = polar_transform64(seg);
             }
-            // ---- LLR tree: depths start .. n-1 into LDS slot = lane of the path
-            for (int d = start; d < n; ++d) {
+            // ---- LLR tree, depths start .. n-1: element (frame fl2, path i, index e)
+            const int lp = cu <= 1 ? 0 : 32 - __builtin_clz(cu - 1);  // log2 of pow2 >= cu
+            const bool right1 = phi >= half;  // depth-1 node on the path: right child of the root
+            // depth-1 value x of path data xp1 (transform of u[0, N/2)), recomputed from the channel
+            auto d1 = [&](const double* chf, int x, uint64_t xp1) -> double {
+                const double a = chf[x], b = chf[x + half];
+                return right1 ? g_node(a, b, (uint32_t)(xp1 >> x) & 1u) : f_minsum(a, b);
+            };
+            uint64_t xp1 = 0;
+            if (right1) xp1 = polar_transform64(half >= 64 ? u0 : (u0 & ((1ULL << half) - 1)));
+            for (int d = (start > 2 ? start : 2); d < n; ++d) {
                 const int lw = n - d, w = 1 << lw;
                 const bool is_g = (d == start) && phi;
-                const int total = cnt << lw;
-                const int off_out = L * (N - 2 * w);
-                const int off_in = L * (N - 4 * w);
+                const int total = F << (lp + lw);
+                const int off_out = N + L * (half - 2 * w);
+                const int off_in = N + L * (half - 4 * w);
                 for (int base = 0; base < total; base += kWave) {
                     const int tt = base + lane;
-                    const int i = tt >> lw;
+                    const int fl2 = tt >> (lp + lw);
+                    const int i = (tt >> lw) & ((1 << lp) - 1);
                     const int e = tt & (w - 1);
-                    const int isrc = i < kWave ? i : 0;
-                    const uint64_t ti = shfl_u64(tab, isrc);
-                    const uint64_t xi = is_g ? shfl_u64(xs, isrc) : 0;
-                    if (tt < total) {
-                        // the first step reads the parent through the path's slot table; deeper
-                        // steps read the depth this phase just wrote into the path's own slot
-                        const int ps = (d == start) ? slot_of(ti, d - 1) : i;
-                        const double* par = (d == 1) ? ch : A + off_in + ps * (2 * w);
-                        const double a = par[e], b = par[e + w];
-                        A[off_out + i * w + e] = is_g ? g_node(a, b, (uint32_t)(xi >> e) & 1u) : f_minsum(a, b);
+                    const int src = ((fl2 & (F - 1)) << LOG_G) | i;
+                    uint32_t ti = 0;
+                    uint64_t xi = 0, x1 = 0;
+                    if (d == 2) {
+                        if (right1) x1 = shfl_u64(xp1, src);
+                    } else if (d == start) {
+                        ti = bperm32(tab, src);
+                    }
+                    if (is_g) xi = shfl_u64(xs, src);
+                    if (tt < total && i < cu) {
+                        double* A2 = A + fl2 * fstride;
+                        double a, b;
+                        if (d == 2) {
+                            a = d1(A2, e, x1);
+                            b = d1(A2, e + w, x1);
+                        } else {
+                            const int ps = (d == start) ? (int)((ti >> (5 * (d - 3))) & 31u) : i;
+                            const double* par = A2 + off_in + ps * (2 * w);
+                            a = par[e];
+                            b = par[e + w];
+                        }
+                        A2[off_out + i * w + e] = is_g ? g_node(a, b, (uint32_t)(xi >> e) & 1u) : f_minsum(a, b);
                     }
                 }
                 wave_lds_fence();
             }
-            if (start < n) {
-                uint64_t mask = 0, val = 0;
-                for (int d = start; d < n; ++d) {
-                    mask |= 31ULL << (5 * d);
-                    val |= (uint64_t)lane << (5 * d);
+            if (start < n && n > 2) {
+                uint32_t mask = 0, val = 0;
+                for (int d = (start > 2 ? start : 2); d < n; ++d) {
+                    mask |= 31u << (5 * (d - 2));
+                    val |= (uint32_t)g << (5 * (d - 2));
                 }
                 tab = (tab & ~mask) | val;
             }
-            // ---- leaf LLR of each path
+            // ---- leaf LLR of each path (lanes g < L)
             double lam = 0.0;
-            if (lane < cnt) {
-                const double* par = (n == 1) ? ch : A + L * (N - 4) + slot_of(tab, n - 1) * 2;
-                const double a = par[0], b = par[1];
+            if (path_lane) {
+                double a, b;
+                if (n == 1) {
+                    a = ch[0];
+                    b = ch[1];
+                } else if (n == 2) {
+                    a = d1(ch, 0, xp1);
+                    b = d1(ch, 1, xp1);
+                } else {
+                    const double* par = Af + N + L * (half - 4) + ((tab >> (5 * (n - 3))) & 31u) * 2;
+                    a = par[0];
+                    b = par[1];
+                }
                 lam = (phi & 1) ? g_node(a, b, (uint32_t)xs & 1u) : f_minsum(a, b);
             }
-            // ---- path metric increments (scl.py:102-105), shared log1p(exp(-|llr|))
-            const double Lt = pscl_softplus_tail(lam, T);
+            // ---- metric increments (scl.py:102-105), shared log1p(exp(-|llr|))
+            const double Lt = (PSCL_ABLATE & 1) ? lam * 0.5 : pscl_softplus_tail(lam, T);
             const double m0 = metric + pscl_logaddexp0(-lam, Lt);
             const double m1 = metric + pscl_logaddexp0(lam, Lt);
             const uint64_t infow = pick_word(P.info_mask[0], P.info_mask[1], phi >> 6);
             const bool is_info = (infow >> (phi & 63)) & 1;
-            const uint64_t fmw = pick_word(fm0, fm1, j >> 6), fvw = pick_word(fv0, fv1, j >> 6);
-            // SC mode (sc_decode polar.py:149-153): every info bit is a hard decision llr < 0
-            const bool forced = is_info && (P.sc_hard || ((fmw >> (j & 63)) & 1));
-
-            if (!is_info || forced) {
-                // single child per path; stable re-sort (scl.py:173) = rank on (metric, rank)
-                uint32_t v = 0;
-                if (forced) v = P.sc_hard ? (uint32_t)(lam < 0.0) : (uint32_t)(fvw >> (j & 63)) & 1u;
-                metric = v ? m1 : m0;
-                if (v) {
-                    if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
-                    if (j < 64) ib0 |= 1ULL << j; else ib1 |= 1ULL << (j - 64);
-                    syn ^= P.crc_cols[j];
-                }
-                if (HIST && is_info && lane < cnt) {
-                    hist_llr[j * L + lane] = lam;
-                    hist_par[j * L + lane] = (uint8_t)lane;
-                }
-                if (cnt > 1) {
-                    int r = 0;
-#pragma unroll
-                    for (int k = 0; k < LMAX; ++k) {
-                        if (k < cnt) {
-                            const double mk = rdl_f64(metric, k);
-                            const int rk = (int)rdl_u32((uint32_t)rank, k);
-                            r += (mk < metric) || (mk == metric && rk < rank);
-                        }
-                    }
-                    rank = r;
-                }
+            // candidate key of this lane: (metric of child, 2 * list position + bit)
+            const int psrc = gbase + cpath;
+            const double pm1 = shfl_f64(m1, psrc);
+            const double plam = shfl_f64(lam, psrc);
+            double km = cbit ? pm1 : m0;
+            const uint32_t kt = 2u * (uint32_t)cpath + cbit;
+            bool kval = cand_lane && cpath < cnt;
+            int ncnt = cnt;
+            if (!is_info) {
+                kval = kval && cbit == 0;  // frozen: bit 0 (scl.py:149-153)
             } else {
-                // free info bit: children (bit0, bit1) of each path in list order,
-                // stable sort on (metric, 2*rank + bit), keep the first L (scl.py:163-174)
-                int r0 = 0, r1 = 0;
-                const int k0 = 2 * rank, k1 = 2 * rank + 1;
-#pragma unroll
-                for (int k = 0; k < LMAX; ++k) {
-                    if (k < cnt) {
-                        const double a0 = rdl_f64(m0, k), a1 = rdl_f64(m1, k);
-                        const int kk = 2 * (int)rdl_u32((uint32_t)rank, k);
-                        r0 += (a0 < m0) || (a0 == m0 && kk < k0);
-                        r0 += (a1 < m0) || (a1 == m0 && kk + 1 < k0);
-                        r1 += (a0 < m1) || (a0 == m1 && kk < k1);
-                        r1 += (a1 < m1) || (a1 == m1 && kk + 1 < k1);
-                    }
-                }
-                const int ncnt = (2 * cnt < L) ? 2 * cnt : L;
-                if (lane < cnt) {
-                    if (r0 < ncnt) inv[r0] = (uint8_t)(2 * lane);
-                    if (r1 < ncnt) inv[r1] = (uint8_t)(2 * lane + 1);
-                }
-                wave_lds_fence();
-                const int sel = (lane < ncnt) ? inv[lane] : 0;
-                const int p = sel >> 1;
-                const uint32_t b = (uint32_t)sel & 1u;
-                const double pm0 = shfl_f64(m0, p), pm1 = shfl_f64(m1, p);
-                const double plam = shfl_f64(lam, p);
-                const uint64_t pu0 = shfl_u64(u0, p), pu1 = shfl_u64(u1, p);
-                const uint64_t pib0 = shfl_u64(ib0, p), pib1 = shfl_u64(ib1, p);
-                const uint64_t ptab = shfl_u64(tab, p);
-                const uint32_t psyn = bperm32(syn, p);
-                wave_lds_fence();  // inv[] is rewritten at the next free phase
-                metric = b ? pm1 : pm0;
-                u0 = pu0;
-                u1 = pu1;
-                ib0 = pib0;
-                ib1 = pib1;
-                tab = ptab;
-                syn = psyn;
-                if (b) {
-                    if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
-                    if (j < 64) ib0 |= 1ULL << j; else ib1 |= 1ULL << (j - 64);
-                    syn ^= P.crc_cols[j];
-                }
-                rank = lane;
-                cnt = ncnt;
-                if (HIST && lane < cnt) {
-                    hist_llr[j * L + lane] = plam;
-                    hist_par[j * L + lane] = (uint8_t)p;
+                const uint64_t fmw = pick_word(fm0, fm1, j >> 6), fvw = pick_word(fv0, fv1, j >> 6);
+                if (P.sc_hard) {
+                    kval = kval && cbit == (uint32_t)(plam < 0.0);  // sc_decode polar.py:149-153
+                } else if ((fmw >> (j & 63)) & 1) {
+                    kval = kval && cbit == (uint32_t)((fvw >> (j & 63)) & 1);  // forced (scl.py:146-161)
+                } else {
+                    ncnt = 2 * cnt < L ? 2 * cnt : L;  // both children (scl.py:163-168)
                 }
             }
-            if (is_info) ++j;
+            if (!kval) km = __builtin_huge_val();
+            const uint32_t ktv = kval ? kt : 0x7fffffffu;
+            // stable sort of the children, keep the first L (scl.py:173-174): rank count
+            int r = 0;
+            if (!(PSCL_ABLATE & 2)) rank_step<G, 1>(km, ktv, lane, r);
+            else r = (int)kt;
+            if (kval && r < ncnt) inv[gbase + r] = (uint8_t)g;
+            wave_lds_fence();
+            const int c = (g < ncnt) ? inv[gbase + g] : g;
+            const int par_g = c < L ? c : c - L;
+            const uint32_t b = c >= L ? 1u : 0u;
+            const int ps2 = gbase + par_g;
+            const double nm = shfl_f64(km, gbase + c);
+            const double nlam = shfl_f64(lam, ps2);
+            const uint64_t nu0 = shfl_u64(u0, ps2), nu1 = shfl_u64(u1, ps2);
+            const uint64_t nib0 = shfl_u64(ib0, ps2), nib1 = shfl_u64(ib1, ps2);
+            const uint32_t ntab = bperm32(tab, ps2), nsyn = bperm32(syn, ps2);
+            wave_lds_fence();  // inv[] is rewritten next phase
+            metric = nm;
+            u0 = nu0;
+            u1 = nu1;
+            ib0 = nib0;
+            ib1 = nib1;
+            tab = ntab;
+            syn = nsyn;
+            if (b) {
+                if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
+                if (j < 64) ib0 |= 1ULL << j; else ib1 |= 1ULL << (j - 64);
+                syn ^= P.crc_cols[j];
+            }
+            if (HIST && g < ncnt) {
+                if (is_info) hist_llr[j * L + g] = nlam;  // decision LLR (scl.py:158,166)
+                hist_par[phi * L + g] = (uint8_t)par_g;   // list position before this phase
+            }
+            cnt = ncnt;
+            if (is_info) {
+                if (!P.sc_hard) cu = 2 * cu < L ? 2 * cu : L;
+                ++j;
+            }
         }
 
-        // ---- epilogue: list in rank order, best = first CRC-passing candidate (scl.py:190-201)
-        const bool active = lane < cnt;
-        const bool pass = active && P.has_crc && syn == 0;
-        int best_rank = 0;
-        if (P.has_crc) {
-            int cand = pass ? rank : 1 << 20;
-#pragma unroll
-            for (int k = 0; k < LMAX; ++k)
-                if (k < cnt) {
-                    const int ck = (int)rdl_u32((uint32_t)cand, k);
-                    best_rank = (k == 0 || ck < best_rank) ? ck : best_rank;
-                }
-            if (best_rank >= (1 << 20)) best_rank = 0;
-        }
+        // ---- epilogue: the list is in lane order; best = first CRC-passing candidate
+        const bool active = path_lane && g < cnt && fvalid;
+        const uint64_t passmask = __ballot(active && syn == 0);
+        const uint64_t gmask = (passmask >> gbase) & ((G == 64) ? ~0ULL : ((1ULL << G) - 1));
+        const int best = (P.has_crc && gmask) ? __builtin_ctzll(gmask) : 0;
         if (active) {
-            const int64_t row = f * L + rank;
+            const int64_t row = f * L + g;
             if (P.metrics) P.metrics[row] = metric;
             if (P.cands) {
                 P.cands[row * W] = ib0;
                 if (W > 1) P.cands[row * W + 1] = ib1;
             }
-            if (HIST && P.info_llrs) {
-                int cur = lane;
-                for (int jj = K - 1; jj >= 0; --jj) {
-                    P.info_llrs[row * K + jj] = hist_llr[jj * L + cur];
-                    cur = hist_par[jj * L + cur];
+            if (HIST && P.info_llrs) {  // trace the path's history back through every phase
+                int cur = g, jj = K - 1;
+                for (int ph = N - 1; ph >= 0; --ph) {
+                    if ((pick_word(P.info_mask[0], P.info_mask[1], ph >> 6) >> (ph & 63)) & 1) {
+                        P.info_llrs[row * K + jj] = hist_llr[jj * L + cur];
+                        --jj;
+                    }
+                    cur = hist_par[ph * L + cur];
                 }
             }
-            if (rank == best_rank) {
+            if (g == best) {
                 const bool bpass = P.has_crc ? (syn == 0) : true;
                 if (P.best) {
                     P.best[f * W] = ib0;
                     if (W > 1) P.best[f * W + 1] = ib1;
                 }
-                if (P.flags) P.flags[f] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best_rank);
+                if (P.flags) P.flags[f] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
                 if (P.n_paths) P.n_paths[f] = cnt;
                 if (P.ref) {
                     const uint64_t r0 = P.ref[f * W], r1 = (W > 1) ? P.ref[f * W + 1] : 0;
@@ -319,8 +388,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
                 }
             }
         }
-        // next frame reuses A/inv/hist: keep this frame's LDS reads ahead of its writes
-        wave_lds_fence();
+        wave_lds_fence();  // the next frames reuse this wave's LDS
     }
     if (P.ref && blockIdx.x == 0 && threadIdx.x == 0)
         atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
@@ -410,11 +478,22 @@ __global__ void __launch_bounds__(256) channel_kernel(const pscl_channel_params 
 
 // ------------------------------------------------------------------------- launchers
 
-// waves (frames) per workgroup: as many as fit 160 KB of LDS, at most PSCL_MAX_WAVES_PER_WG
+// wavefronts per workgroup: the choice that keeps the most wavefronts resident per CU
+// under the 160 KB LDS budget (each workgroup also holds the 2 KB exp table); 0 if none fits
 int pscl_decode_wpg(const pscl_decode_params& P) {
-    const int avail = 160 * 1024 - PSCL_EXP_TABLE_WORDS * 8;
-    int w = avail / (P.wave_bytes > 0 ? P.wave_bytes : 1);
-    return w > PSCL_MAX_WAVES_PER_WG ? PSCL_MAX_WAVES_PER_WG : w;
+    const int cu_lds = 160 * 1024, tbl = PSCL_EXP_TABLE_WORDS * 8;
+    int best = 0, best_res = 0;
+    for (int w = 1; w <= PSCL_MAX_WAVES_PER_WG; ++w) {
+        const int wg = tbl + w * P.wave_bytes;
+        if (wg > cu_lds) break;
+        int res = (cu_lds / wg) * w;
+        if (res > 32) res = 32;
+        if (res >= best_res) {
+            best_res = res;
+            best = w;
+        }
+    }
+    return best;
 }
 
 static int decode_lds_bytes(const pscl_decode_params& P, int hist) {
@@ -444,8 +523,8 @@ int pscl_decode_lmax(int L) {
 }
 
 int64_t pscl_decode_grid(const pscl_decode_params& P) {
-    const int wpg = pscl_decode_wpg(P);
-    int64_t g = (P.B + wpg - 1) / wpg;
+    const int per_wg = pscl_decode_wpg(P) * (32 / pscl_decode_lmax(P.L));  // frames per workgroup
+    int64_t g = (P.B + per_wg - 1) / per_wg;
     const int64_t cap = 1 << 20;
     return g < 1 ? 1 : (g > cap ? cap : g);
 }
