@@ -30,7 +30,10 @@ void softplus_compare(const double* v, int64_t n, int64_t* bad_exp, int64_t* bad
         else
             ref = v[i] + log1p(exp(0.0 - v[i]));
         double got = pscl_logaddexp0(v[i], pscl_softplus_tail(v[i], kT));
-        if (pscl_asu64(ref) != pscl_asu64(got)) bs++;
+        double got_bf = pscl_logaddexp0(v[i], pscl_softplus_tail_bf(v[i], kT));
+        if (pscl_asu64(ref) != pscl_asu64(got) || pscl_asu64(ref) != pscl_asu64(got_bf)) bs++;
+        if (pscl_asu64(pscl_exp_neg(x, kT)) != pscl_asu64(e1)) be++;
+        if (pscl_asu64(pscl_log1p_unit(e1)) != pscl_asu64(l1)) bl++;
     }
     *bad_exp = be;
     *bad_log1p = bl;
@@ -38,5 +41,13 @@ void softplus_compare(const double* v, int64_t n, int64_t* bad_exp, int64_t* bad
 }
 
 void softplus_port_batch(const double* v, int64_t n, double* out) {
-    for (int64_t i = 0; i < n; i++) out[i] = pscl_logaddexp0(v[i], pscl_softplus_tail(v[i], kT));
+    for (int64_t i = 0; i < n; i++) out[i] = pscl_logaddexp0(v[i], pscl_softplus_tail_bf(v[i], kT));
+}
+
+/* log1p on [0, 1]: branch-free form vs libm */
+int64_t log1p_unit_compare(const double* y, int64_t n) {
+    int64_t bad = 0;
+    for (int64_t i = 0; i < n; i++)
+        if (pscl_asu64(pscl_log1p_unit(y[i])) != pscl_asu64(log1p(y[i]))) bad++;
+    return bad;
 }

@@ -124,15 +124,10 @@ void fill_decode_params(const pscl_handle* h, pscl_decode_params& P, int hist) {
     P.info_mask[0] = h->info_mask[0];
     P.info_mask[1] = h->info_mask[1];
     P.crc_cols = h->d_check_cols;
+    P.info_set = h->d_info_set;
     P.has_crc = h->crc_poly != 0;
     P.exp_table = h->d_exp_table;
-    // one wavefront decodes F = 32 / LMAX frames (2*LMAX lanes each)
-    const int F = 32 / pscl_decode_lmax(h->L);
-    const int fstride = h->N + (h->N >= 8 ? h->L * (h->N / 2 - 2) : 0);  // doubles per frame
-    const int a_bytes = F * fstride * 8;
-    P.a_bytes = a_bytes;
-    int wb = a_bytes + 64 + (hist ? F * (h->K * h->L * 8 + h->N * h->L) : 0);
-    P.wave_bytes = (wb + 15) & ~15;
+    pscl_decode_layout(P, hist);
 }
 
 int launch_decode(pscl_handle* h, const pscl_decode_params& P, int hist) {

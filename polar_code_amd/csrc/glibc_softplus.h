@@ -29,6 +29,9 @@
 
 #include <stdint.h>
 #include <string.h>
+#ifndef __cplusplus
+#include <stdbool.h>
+#endif
 
 #if defined(__HIPCC__) || defined(__HIP__)
 #define PSCL_HD __host__ __device__ __forceinline__
@@ -198,6 +201,102 @@ PSCL_HD double pscl_log1p(double x) {
     if (k == 0) return f - (hfsq - sR);
     double kd = (double)k;
     return kd * ln2_hi - ((hfsq - ((kd * ln2_lo + c) + sR)) - f);
+}
+
+/*
+ * Branch-free forms for the decoder's domain: exp(x) for x <= 0 and log1p(y) for y in [0, 1].
+ * Every branch of the functions above is evaluated and the live one selected, so a wavefront
+ * runs one straight-line sequence instead of exec-masked divergent regions.  Results are
+ * identical to pscl_exp / pscl_log1p on that domain (tests/test_softplus_host.py).
+ */
+PSCL_HD double pscl_sel(bool c, double a, double b) { return c ? a : b; }
+
+PSCL_HD double pscl_exp_neg(double x, const uint64_t* T) {
+    const uint64_t ix = pscl_asu64(x);
+    const uint32_t abstop = (uint32_t)(ix >> 52) & 0x7ff;
+    const double kd0 = pscl_fma(x, PSCL_EXP_INVLN2N, PSCL_EXP_SHIFT);
+    const uint64_t ki = pscl_asu64(kd0);
+    const double kd = kd0 - PSCL_EXP_SHIFT;
+    double r = pscl_fma(kd, PSCL_EXP_NEGLN2HIN, x);
+    r = pscl_fma(kd, PSCL_EXP_NEGLN2LON, r);
+    const uint64_t idx = 2 * (ki & 127);
+    const double p1 = pscl_fma(r, PSCL_EXP_C3, PSCL_EXP_C2);
+    const double tr = r + pscl_asf64(T[idx]);
+    const uint64_t sbits = T[idx + 1] + (ki << 45);
+    const double r2 = r * r;
+    const double p2 = pscl_fma(r, PSCL_EXP_C5, PSCL_EXP_C4);
+    const double t = pscl_fma(p1, r2, tr);
+    const double tmp = pscl_fma(r2 * r2, p2, t);
+    /* main range */
+    const double sc = pscl_asf64(sbits);
+    const double ymain = pscl_fma(sc, tmp, sc);
+    /* 512 <= |x| < 1024, k < 0: glibc specialcase, rounded once into the subnormal range */
+    const double scale = pscl_asf64(sbits + (1022ULL << 52));
+    const double st = tmp * scale;
+    const double y0 = scale + st;
+    const double hi = y0 + 1.0;
+    const double lo = ((1.0 - hi) + y0) + ((scale - y0) + st);
+    double yr = (lo + hi) - 1.0;
+    yr = yr == 0.0 ? 0.0 : yr;
+    const double yspec = pscl_sel(y0 < 1.0, yr, y0) * 0x1p-1022;
+    double y = abstop == 0x408u ? yspec : ymain;
+    y = abstop > 0x408u ? 0.0 : y;          /* |x| >= 1024 and -inf: underflow to +0 */
+    y = abstop < 0x3c9u ? 1.0 + x : y;      /* |x| < 2^-54 and -0 */
+    return y;
+}
+
+PSCL_HD double pscl_log1p_unit(double y) {
+    const double ln2_hi = 6.93147180369123816490e-01;
+    const double ln2_lo = 1.90821492927058770002e-10;
+    const double Lp1 = 6.666666666666735130e-01, Lp2 = 3.999999999940941908e-01,
+                 Lp3 = 2.857142874366239149e-01, Lp4 = 2.222219843214978396e-01,
+                 Lp5 = 1.818357216161805012e-01, Lp6 = 1.531383769920937332e-01,
+                 Lp7 = 1.479819860511658591e-01;
+    const int32_t hx = (int32_t)(pscl_asu64(y) >> 32);
+    const bool kp = hx >= 0x3FDA827A;  /* 1 + y >= sqrt(2): reduce through u = 1 + y */
+    /* u = 1 + y path (k in {0, 1} before normalisation) */
+    const double u = 1.0 + y;
+    const int32_t hu0 = (int32_t)(pscl_asu64(u) >> 32);
+    int32_t ku = (hu0 >> 20) - 1023;
+    double cu = (ku > 0) ? 1.0 - (u - y) : y - (u - 1.0);
+    cu = cu / u;
+    int32_t hum = hu0 & 0x000fffff;
+    const uint64_t ulo = pscl_asu64(u) & 0xffffffffULL;
+    const bool big = hum >= 0x6a09e;
+    const double un = pscl_asf64(((uint64_t)(uint32_t)(hum | (big ? 0x3fe00000 : 0x3ff00000)) << 32) | ulo);
+    ku += big ? 1 : 0;
+    hum = big ? ((0x00100000 - hum) >> 2) : hum;
+    /* select the reduction */
+    const int32_t k = kp ? ku : 0;
+    const double c = kp ? cu : 0.0;
+    const int32_t hu = kp ? hum : 1;
+    const double f = kp ? un - 1.0 : y;
+    const double kd = (double)k;
+    const double hfsq = (0.5 * f) * f;
+    /* |f| < 2^-20 (hu == 0) */
+    const double R0 = (1.0 - 0.66666666666666666 * f) * hfsq;
+    const double a_f0 = k == 0 ? 0.0 : (kd * ln2_lo + c) + kd * ln2_hi;
+    const double a_nz = k == 0 ? f - R0 : kd * ln2_hi - ((R0 - (kd * ln2_lo + c)) - f);
+    const double a = f == 0.0 ? a_f0 : a_nz;
+    /* general case */
+    const double s = f / (2.0 + f);
+    const double z = s * s;
+    const double z2 = z * z;
+    const double z4 = z2 * z2;
+    const double z6 = z2 * z4;
+    const double R = ((z * Lp1 + z2 * (z * Lp3 + Lp2)) + z4 * (z * Lp5 + Lp4)) + z6 * (z * Lp7 + Lp6);
+    const double sR = (R + hfsq) * s;
+    const double bres = k == 0 ? f - (hfsq - sR) : kd * ln2_hi - ((hfsq - ((kd * ln2_lo + c) + sR)) - f);
+    double res = hu == 0 ? a : bres;
+    res = hx < 0x3e200000 ? y - (y * y) * 0.5 : res; /* y < 2^-29 */
+    res = hx < 0x3c900000 ? y : res;                 /* y < 2^-54, subnormals, 0 */
+    return res;
+}
+
+/* branch-free L = log1p(exp(-|v|)) (identical to pscl_softplus_tail for finite v and +-inf) */
+PSCL_HD double pscl_softplus_tail_bf(double v, const uint64_t* T) {
+    const double a = v < 0 ? -v : v;
+    return pscl_log1p_unit(pscl_exp_neg(-a, T));
 }
 
 /* L = log1p(exp(-|v|)), the part of logaddexp(0, +-v) shared by both bit hypotheses. */

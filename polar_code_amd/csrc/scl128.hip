@@ -1,0 +1,364 @@
+// scl128.hip -- specialised list decoder for N = 128 and list sizes L <= 8 (every BASELINE
+// configuration).  Same contract and bit-exact results as the generic kernel in
+// scl_kernels.hip (decode_scl, dl_scl_polar/polar/scl.py:108-209); the N = 128 shape is
+// compiled in so the tree walk is straight-line code.
+//
+// Wavefront layout: F = 64/G frames per wavefront, G = 2*LMAX lanes per frame.  Lane g < L
+// of a frame group holds list path g (metric, list position `rank`, decided bits u, and the
+// LDS slot of each stored depth); lane g + LMAX is that path's bit-1 child while the list is
+// extended, and otherwise evaluates the sibling leaf's metric tail (below).
+//
+// LLR tree, per frame in LDS: the 128 channel LLRs and, per path slot, depths 3..6
+// (16 + 8 + 4 + 2 values).  Depths 1 and 2 are never stored: every 16th phase the lanes
+// recompute the 16 depth-3 values of each path directly from 8 channel LLRs each (f/g through
+// depths 1-3), which halves the LDS footprint per frame and with it raises occupancy.
+//
+// List update per phase:
+//   frozen  (all paths take bit 0, scl.py:149-153): metrics advance and the stable order is
+//           re-ranked in place (rank on (metric, rank)); no path state moves.
+//   info    (free, forced or SC-hard): 2L children ranked on (metric, 2*rank + bit) with a
+//           rotation count (python's stable sort, scl.py:173), survivors gathered into lanes
+//           0..L-1 in list order (scl.py:174).
+// Metric tail: at a frozen even leaf the right sibling's LLR for the known left bit is
+// already fixed, so lanes g >= LMAX evaluate its log1p(exp(-|llr|)) in the same pass; the
+// next phase reuses it (48 of 128 evaluations per frame for the (128,64) code).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "glibc_softplus.h"
+#include "scl_device.h"
+#include "scl_kernels.h"
+
+namespace {
+
+using namespace pscl;
+
+constexpr int kN = 128;
+constexpr int kn = 7;
+
+template <int LMAX>
+struct Layout128 {
+    static constexpr int G = 2 * LMAX;
+    static constexpr int F = 64 / G;
+    static constexpr int LOG_G = __builtin_ctz(G);
+    static constexpr int LOG_LM = __builtin_ctz(LMAX);
+    static constexpr int OFF3 = kN;                 // [LMAX][16]
+    static constexpr int OFF4 = OFF3 + 16 * LMAX;   // [LMAX][8]
+    static constexpr int OFF5 = OFF4 + 8 * LMAX;    // [LMAX][4]
+    static constexpr int OFF6 = OFF5 + 4 * LMAX;    // [LMAX][2]
+    static constexpr int FSTRIDE = OFF6 + 2 * LMAX;  // doubles per frame
+};
+
+__device__ __forceinline__ int slot_at(uint32_t tab, int d) { return (int)((tab >> (4 * (d - 3))) & 15u); }
+
+// Arikan transform of the w-bit segment u[lo, lo+w), w <= 64, lo a multiple of w
+__device__ __forceinline__ uint64_t seg_transform(uint64_t u0, uint64_t u1, int lo, int w) {
+    const uint64_t word = lo >= 64 ? u1 : u0;
+    const uint64_t seg = (w == 64) ? word : (word >> (lo & 63)) & ((1ULL << w) - 1);
+    return polar_transform64(seg);
+}
+
+// depth-d step (d = 4, 5, 6) of the tree walk for all frames and path slots of the wave
+template <int LMAX, int D>
+__device__ __forceinline__ void step_depth(double* A, int lane, uint32_t tab, uint32_t xs, bool first, bool is_g) {
+    using Ly = Layout128<LMAX>;
+    constexpr int LW = kn - D, W = 1 << LW;
+    constexpr int OFF_OUT = D == 4 ? Ly::OFF4 : (D == 5 ? Ly::OFF5 : Ly::OFF6);
+    constexpr int OFF_IN = D == 4 ? Ly::OFF3 : (D == 5 ? Ly::OFF4 : Ly::OFF5);
+    constexpr int CHUNKS = W / 2;  // F * LMAX * W / 64
+#pragma unroll
+    for (int c = 0; c < CHUNKS; ++c) {
+        const int tt = c * 64 + lane;
+        const int fl2 = tt >> (Ly::LOG_LM + LW);
+        const int i = (tt >> LW) & (LMAX - 1);
+        const int e = tt & (W - 1);
+        const int src = (fl2 << Ly::LOG_G) | i;
+        int ps = i;
+        uint32_t xi = 0;
+        if (first) ps = slot_at(bperm32(tab, src), D - 1);
+        if (is_g) xi = bperm32(xs, src);
+        double* A2 = A + fl2 * Ly::FSTRIDE;
+        const double* par = A2 + OFF_IN + ps * (2 * W);
+        const double a = par[e], b = par[e + W];
+        A2[OFF_OUT + i * W + e] = is_g ? g_node(a, b, (xi >> e) & 1u) : f_minsum(a, b);
+    }
+    wave_lds_fence();
+}
+
+template <int LMAX, bool HIST>
+__global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64) scl128_kernel(const pscl_decode_params P) {
+    using Ly = Layout128<LMAX>;
+    constexpr int G = Ly::G, F = Ly::F, LOG_G = Ly::LOG_G;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t* T = reinterpret_cast<uint64_t*>(smem);
+    for (int i = threadIdx.x; i < PSCL_EXP_TABLE_WORDS; i += blockDim.x) T[i] = P.exp_table[i];
+    __syncthreads();
+
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int fl = lane >> LOG_G;
+    const int g = lane & (G - 1);
+    const int gbase = lane & ~(G - 1);
+    const int K = P.K, L = P.L;
+    unsigned char* wbase = smem + PSCL_EXP_TABLE_WORDS * 8 + (size_t)wave * P.wave_bytes;
+    double* A = reinterpret_cast<double*>(wbase);
+    double* Af = A + fl * Ly::FSTRIDE;
+    double* hist_llr = reinterpret_cast<double*>(wbase + P.a_bytes) + (size_t)fl * K * L;
+    uint8_t* hist_par = wbase + P.a_bytes + (size_t)F * K * L * 8 + (size_t)fl * K * L;
+
+    const int wpg = (int)(blockDim.x >> 6);
+    const int64_t wstride = (int64_t)gridDim.x * wpg * F;
+    const bool path_lane = g < LMAX;
+    const int cpath = g & (LMAX - 1);
+    const uint32_t cbit = g >= LMAX ? 1u : 0u;
+    const uint64_t info0 = P.info_mask[0], info1 = P.info_mask[1];
+
+    for (int64_t f0 = ((int64_t)blockIdx.x * wpg + wave) * F; f0 < P.B; f0 += wstride) {
+        const int64_t f = f0 + fl;
+        const bool fvalid = f < P.B;
+        {
+            const double* src = P.llr + (fvalid ? f : f0) * kN;
+#pragma unroll
+            for (int x = 0; x < kN / G; ++x) Af[g + x * G] = src[g + x * G];
+        }
+        uint64_t fm0 = 0, fm1 = 0, fv0 = 0, fv1 = 0;
+        if (P.force && fvalid) {
+            const uint64_t* fr = P.force + f * 2 * P.W;
+            fm0 = fr[0];
+            fv0 = fr[P.W];
+            if (P.W > 1) {
+                fm1 = fr[1];
+                fv1 = fr[P.W + 1];
+            }
+        }
+        wave_lds_fence();
+        double metric = 0.0;
+        uint32_t rank = 0;          // list position of this path
+        uint64_t u0 = 0, u1 = 0;    // decided bits
+        uint32_t tab = 0;           // LDS slot of depths 3..6 (4 bits each)
+        int cnt = 1;                // live paths of this frame (group-uniform)
+        int j = 0;                  // info index (wave-uniform)
+        bool pre_ok = false;        // Lpre holds the tail of this phase's leaf (wave-uniform)
+        double Lpre = 0.0;
+
+        for (int phi = 0; phi < kN; ++phi) {
+            const int start = phi ? kn - __builtin_ctz(phi) : 1;
+            const uint64_t infow = phi < 64 ? info0 : info1;
+            const bool is_info = (infow >> (phi & 63)) & 1;
+            // ---- depths 1-3 recomputed from the channel (phi % 16 == 0)
+            if (start <= 3) {
+                const bool r1 = phi >= 64, r2 = (phi >> 5) & 1, r3 = (phi >> 4) & 1;
+                // path lanes: partial sums of the left siblings at depths 1, 2, 3
+                const uint64_t X1 = r1 ? polar_transform64(u0) : 0;
+                const uint32_t X2 = r2 ? (uint32_t)seg_transform(u0, u1, phi - (phi & 31) - 32, 32) : 0u;
+                const uint32_t X3 = r3 ? (uint32_t)seg_transform(u0, u1, phi - 16, 16) : 0u;
+#pragma unroll
+                for (int q = 0; q < 16 / G + (G > 16); ++q) {
+                    const int e = g + G * q;
+                    double c[8];
+#pragma unroll
+                    for (int m = 0; m < 8; ++m) c[m] = Af[e + 16 * m];
+                    double d1l[4];
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) d1l[m] = f_minsum(c[m], c[m + 4]);
+#pragma unroll
+                    for (int p = 0; p < LMAX; ++p) {
+                        const int src = gbase + p;
+                        uint64_t x1 = 0;
+                        uint32_t x2 = 0, x3 = 0;
+                        if (r1) x1 = shfl_u64(X1, src);
+                        if (r2) x2 = bperm32(X2, src);
+                        if (r3) x3 = bperm32(X3, src);
+                        double d1[4];
+#pragma unroll
+                        for (int m = 0; m < 4; ++m)
+                            d1[m] = r1 ? g_node(c[m], c[m + 4], (uint32_t)(x1 >> (e + 16 * m)) & 1u) : d1l[m];
+                        double d2[2];
+#pragma unroll
+                        for (int s2 = 0; s2 < 2; ++s2)
+                            d2[s2] = r2 ? g_node(d1[s2], d1[s2 + 2], (x2 >> (e + 16 * s2)) & 1u) : f_minsum(d1[s2], d1[s2 + 2]);
+                        const double d3 = r3 ? g_node(d2[0], d2[1], (x3 >> e) & 1u) : f_minsum(d2[0], d2[1]);
+                        Af[Ly::OFF3 + p * 16 + e] = d3;
+                    }
+                }
+                wave_lds_fence();
+            }
+            // ---- depths 4..6 (partial sums of the g node's left sibling: xs, <= 8 bits)
+            uint32_t xs = 0;
+            if (phi && start >= 4 && start <= 6) xs = (uint32_t)seg_transform(u0, u1, phi - (1 << (kn - start)), 1 << (kn - start));
+            if (start <= 4) step_depth<LMAX, 4>(A, lane, tab, xs, start == 4, start == 4 && phi);
+            if (start <= 5) step_depth<LMAX, 5>(A, lane, tab, xs, start == 5, start == 5);
+            if (start <= 6) step_depth<LMAX, 6>(A, lane, tab, xs, start == 6, start == 6);
+            if (start <= 6) {
+                const int s0 = start < 3 ? 3 : start;
+                uint32_t mask = 0, val = 0;
+                for (int d = s0; d <= 6; ++d) {
+                    mask |= 15u << (4 * (d - 3));
+                    val |= (uint32_t)cpath << (4 * (d - 3));
+                }
+                tab = (tab & ~mask) | val;
+            }
+            // ---- leaf LLRs.  Lanes >= LMAX: the sibling leaf (phi+1) given bit 0 here.
+            const uint32_t tab_lo = from_lower_half<G, LMAX>(tab, lane);
+            const uint32_t ptab = path_lane ? tab : tab_lo;
+            const double* par = Af + Ly::OFF6 + slot_at(ptab, 6) * 2;
+            const double la = par[0], lb = par[1];
+            const uint32_t xleaf = phi ? (uint32_t)((phi - 1 < 64 ? u0 >> (phi - 1) : u1 >> (phi - 65)) & 1u) : 0u;
+            const double lam = path_lane ? ((phi & 1) ? g_node(la, lb, xleaf) : f_minsum(la, lb)) : lb + la;
+            // ---- metric tail log1p(exp(-|llr|)) (scl.py:102-105)
+            double Lt;
+            const uint64_t lpre_up = from_upper_half64<G, LMAX>(pscl_asu64(Lpre), lane);
+            if (pre_ok) {
+                Lt = pscl_asf64(lpre_up);
+            } else {
+                Lt = (PSCL_ABLATE & 1) ? lam * 0.5 : pscl_softplus_tail_bf(lam, T);
+            }
+            const bool frozen_even = !is_info && !(phi & 1);
+            Lpre = Lt;
+            pre_ok = frozen_even;
+            const double m0 = metric + pscl_logaddexp0(-lam, Lt);
+            const double m1 = metric + pscl_logaddexp0(lam, Lt);
+
+            if (!is_info) {
+                // frozen: bit 0, metrics advance, stable re-rank in place (lanes do not move)
+                metric = m0;
+                const bool kv = path_lane && g < cnt;
+                uint64_t km = kv ? pscl_asu64(m0) : 0x7ff0000000000000ULL;
+                uint32_t kt = kv ? rank : 0x7fffffffu;
+                // duplicate the path keys into the upper half: LMAX-1 rotations then see every path
+                const uint64_t km_lo = from_lower_half64<G, LMAX>(km, lane);
+                const uint32_t kt_lo = from_lower_half<G, LMAX>(kt, lane);
+                if (!path_lane) {
+                    km = km_lo;
+                    kt = kt_lo;
+                }
+                uint32_t r = 0;
+                if (!(PSCL_ABLATE & 2)) rank_step_n<G, 1, LMAX>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
+                if (path_lane) rank = r;
+            } else {
+                // info: children (bit 0 in lane g, bit 1 in lane g + LMAX) of every path
+                const uint64_t pm1 = from_lower_half64<G, LMAX>(pscl_asu64(m1), lane);
+                const uint32_t prank = from_lower_half<G, LMAX>(rank, lane);
+                const double plam = pscl_asf64(from_lower_half64<G, LMAX>(pscl_asu64(lam), lane));
+                uint64_t km = cbit ? pm1 : pscl_asu64(m0);
+                const uint32_t myrank = cbit ? prank : rank;
+                const double mylam = cbit ? plam : lam;
+                bool kval = cpath < cnt;
+                int ncnt = cnt;
+                const uint64_t fmw = j < 64 ? fm0 : fm1, fvw = j < 64 ? fv0 : fv1;
+                if (P.sc_hard) {
+                    kval = kval && cbit == (uint32_t)(mylam < 0.0);  // sc_decode polar.py:149-153
+                } else if ((fmw >> (j & 63)) & 1) {
+                    kval = kval && cbit == (uint32_t)((fvw >> (j & 63)) & 1);  // forced (scl.py:146-161)
+                } else {
+                    ncnt = 2 * cnt < L ? 2 * cnt : L;  // both children (scl.py:163-168)
+                }
+                if (!kval) km = 0x7ff0000000000000ULL;
+                const uint32_t kt = kval ? 2u * myrank + cbit : 0x7fffffffu;
+                uint32_t r = 0;
+                if (!(PSCL_ABLATE & 2)) rank_step<G, 1>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
+                else r = kt & 15u;
+                // survivor with list position r -> lane r of the group (push), scl.py:174
+                const int c = __builtin_amdgcn_ds_permute((gbase + (int)(r & (G - 1))) << 2, g);
+                const int cc = (g < ncnt) ? c : g;
+                const int par_g = cc & (LMAX - 1);
+                const uint32_t b = cc >= LMAX ? 1u : 0u;
+                const int ps2 = gbase + par_g;
+                const uint64_t nm = shfl_u64(km, gbase + cc);
+                const uint64_t nu0 = shfl_u64(u0, ps2), nu1 = shfl_u64(u1, ps2);
+                const uint32_t ntab = bperm32(tab, ps2);
+                if (HIST) {
+                    const uint64_t plam_h = shfl_u64(pscl_asu64(lam), ps2);
+                    if (g < ncnt && path_lane) {
+                        hist_llr[j * L + g] = pscl_asf64(plam_h);  // decision LLR (scl.py:158,166)
+                        hist_par[j * L + g] = (uint8_t)par_g;
+                    }
+                }
+                metric = pscl_asf64(nm);
+                u0 = nu0;
+                u1 = nu1;
+                tab = ntab;
+                if (b) {
+                    if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
+                }
+                rank = (uint32_t)g;
+                cnt = ncnt;
+                ++j;
+            }
+        }
+
+        // ---- epilogue: u[info_set] and its CRC syndrome, best = lowest-ranked CRC pass
+        uint64_t ib0 = 0, ib1 = 0;
+        uint32_t syn = 0;
+        for (int jj = 0; jj < K; ++jj) {
+            const int ph = P.info_set[jj];
+            const uint64_t bit = ((ph < 64 ? u0 : u1) >> (ph & 63)) & 1ULL;
+            if (jj < 64) ib0 |= bit << jj; else ib1 |= bit << (jj - 64);
+            syn ^= bit ? P.crc_cols[jj] : 0u;
+        }
+        const bool active = path_lane && g < cnt && fvalid;
+        uint32_t pm = (active && syn == 0) ? (1u << rank) : 0u;
+        pm = or_reduce_group<G>(pm, lane);
+        const int best = (P.has_crc && pm) ? __builtin_ctz(pm) : 0;
+        if (active) {
+            const int64_t row = f * L + rank;
+            if (P.metrics) P.metrics[row] = metric;
+            if (P.cands) {
+                P.cands[row * P.W] = ib0;
+                if (P.W > 1) P.cands[row * P.W + 1] = ib1;
+            }
+            if (HIST && P.info_llrs) {
+                int cur = g;
+                for (int jj = K - 1; jj >= 0; --jj) {
+                    P.info_llrs[row * K + jj] = hist_llr[jj * L + cur];
+                    cur = hist_par[jj * L + cur];
+                }
+            }
+            if ((int)rank == best) {
+                const bool bpass = P.has_crc ? (syn == 0) : true;
+                if (P.best) {
+                    P.best[f * P.W] = ib0;
+                    if (P.W > 1) P.best[f * P.W + 1] = ib1;
+                }
+                if (P.flags) P.flags[f] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
+                if (P.n_paths) P.n_paths[f] = cnt;
+                if (P.ref)
+                    count_errors(P.counters, ib0, ib1, P.ref[f * P.W], P.W > 1 ? P.ref[f * P.W + 1] : 0, P.k_payload,
+                                 bpass);
+            }
+        }
+        wave_lds_fence();
+    }
+    if (P.ref && blockIdx.x == 0 && threadIdx.x == 0)
+        atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
+}
+
+template <int LMAX>
+hipError_t launch128(const pscl_decode_params& P, int hist, int wpg, int64_t grid, int lds, hipStream_t s) {
+    if (hist)
+        hipLaunchKernelGGL((scl128_kernel<LMAX, true>), dim3((unsigned)grid), dim3(wpg * 64), lds, s, P);
+    else
+        hipLaunchKernelGGL((scl128_kernel<LMAX, false>), dim3((unsigned)grid), dim3(wpg * 64), lds, s, P);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+int pscl_fast128_fstride(int L) {
+    switch (pscl_decode_lmax(L)) {
+        case 1: return Layout128<1>::FSTRIDE;
+        case 2: return Layout128<2>::FSTRIDE;
+        case 4: return Layout128<4>::FSTRIDE;
+        default: return Layout128<8>::FSTRIDE;
+    }
+}
+
+hipError_t pscl_launch_decode128(const pscl_decode_params& P, int hist, int wpg, int64_t grid, int lds, hipStream_t s) {
+    switch (pscl_decode_lmax(P.L)) {
+        case 1: return launch128<1>(P, hist, wpg, grid, lds, s);
+        case 2: return launch128<2>(P, hist, wpg, grid, lds, s);
+        case 4: return launch128<4>(P, hist, wpg, grid, lds, s);
+        case 8: return launch128<8>(P, hist, wpg, grid, lds, s);
+        default: return hipErrorInvalidValue;
+    }
+}

@@ -1,0 +1,202 @@
+// scl_device.h -- device helpers shared by the decode kernels (wavefront = 64 lanes).
+#ifndef PSCL_SCL_DEVICE_H
+#define PSCL_SCL_DEVICE_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "glibc_softplus.h"
+#include "polar_scl.h"
+
+// Timing-only ablation switches for diagnostic builds (tools/ablate.py); 0 in the product.
+#ifndef PSCL_ABLATE
+#define PSCL_ABLATE 0
+#endif
+
+namespace pscl {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ uint32_t bperm32(uint32_t v, int src) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+    uint32_t lo = bperm32((uint32_t)v, src), hi = bperm32((uint32_t)(v >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ double shfl_f64(double v, int src) {
+    return pscl_asf64(shfl_u64(pscl_asu64(v), src));
+}
+__device__ __forceinline__ uint32_t rdl_u32(uint32_t v, int l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ double rdl_f64(double v, int l) {
+    uint64_t u = pscl_asu64(v);
+    uint32_t lo = rdl_u32((uint32_t)u, l), hi = rdl_u32((uint32_t)(u >> 32), l);
+    return pscl_asf64(((uint64_t)hi << 32) | lo);
+}
+
+// Orders the wave's LDS traffic: hardware executes one wave's LDS instructions in order;
+// this keeps the compiler from moving loads above the stores they depend on.
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// f(a,b) = sign(a) sign(b) min(|a|,|b|)  (polar.py:122-123; exact, sign(0)=0 gives +-0)
+__device__ __forceinline__ double f_minsum(double a, double b) {
+    double m = fmin(fabs(a), fabs(b));
+    return ((a < 0.0) != (b < 0.0)) ? -m : m;
+}
+// g(a,b,c) = b + (1-2c) a  (polar.py:126-127; one rounding)
+__device__ __forceinline__ double g_node(double a, double b, uint32_t c) { return c ? b - a : b + a; }
+
+// Arikan transform of the low w bits of x (in-word, w <= 64): bit j ^= bit j+s for bit s of j
+// clear, for every stage s (stages commute).  Bits >= w must be zero.
+__device__ __forceinline__ uint64_t polar_transform64(uint64_t x) {
+    x ^= (x >> 1) & 0x5555555555555555ULL;
+    x ^= (x >> 2) & 0x3333333333333333ULL;
+    x ^= (x >> 4) & 0x0f0f0f0f0f0f0f0fULL;
+    x ^= (x >> 8) & 0x00ff00ff00ff00ffULL;
+    x ^= (x >> 16) & 0x0000ffff0000ffffULL;
+    x ^= (x >> 32) & 0x00000000ffffffffULL;
+    return x;
+}
+
+__device__ __forceinline__ uint64_t pick_word(uint64_t w0, uint64_t w1, int idx) { return idx ? w1 : w0; }
+
+
+// ---------------------------------------------------------------- lane-group helpers
+// A wavefront decodes F = 64/G frames at once; frame slot fl owns the G = 2*LMAX lanes
+// [fl*G, fl*G + G).  Lane g < L of a group holds list path g (list position == lane, so the
+// stable-sort tie key is the lane index itself); lanes [L, 2L) carry the bit-1 children
+// while the list is being extended.
+
+template <int G, int K>
+__device__ __forceinline__ uint32_t grot32c(uint32_t v, int lane) {
+    if constexpr (G == 16) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + K, 0xF, 0xF, false);  // row_ror:K
+    } else if constexpr (G == 8) {
+        const uint32_t a = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + K, 0xF, 0xF, false);
+        const uint32_t b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + K + 8, 0xF, 0xF, false);
+        return ((lane & 7) >= K) ? a : b;  // row_ror:K reads lane x-K; wrap inside the 8-lane group
+    } else if constexpr (G == 4) {
+        constexpr int q = ((0 + K) & 3) | (((1 + K) & 3) << 2) | (((2 + K) & 3) << 4) | (((3 + K) & 3) << 6);
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, q, 0xF, 0xF, false);  // quad_perm
+    } else if constexpr (G == 2) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    } else {
+        return bperm32(v, (lane & ~(G - 1)) | ((lane + K) & (G - 1)));
+    }
+}
+
+template <int G, int K>
+__device__ __forceinline__ double grot64c(double v, int lane) {
+    const uint64_t u = pscl_asu64(v);
+    const uint32_t lo = grot32c<G, K>((uint32_t)u, lane), hi = grot32c<G, K>((uint32_t)(u >> 32), lane);
+    return pscl_asf64(((uint64_t)hi << 32) | lo);
+}
+
+// Stable rank of this lane's key among the G keys of its group.  The key is (metric, t):
+// metrics are sums of non-negative increments, never -0 or NaN, and +inf marks an empty
+// candidate, so their IEEE bit patterns order like unsigned integers and the whole key
+// compares as one 96-bit unsigned number (hi word, lo word, t) with a borrow chain.
+template <int G, int K>
+__device__ __forceinline__ void rank_step(uint32_t mh, uint32_t ml, uint32_t t, int lane, uint32_t& r) {
+    if constexpr (K < G) {
+        const uint32_t th = grot32c<G, K>(t, lane);
+        const uint32_t lh = grot32c<G, K>(ml, lane);
+        const uint32_t hh = grot32c<G, K>(mh, lane);
+        unsigned c0, c1, c2;
+        (void)__builtin_subc(th, t, 0u, &c0);
+        (void)__builtin_subc(lh, ml, c0, &c1);
+        (void)__builtin_subc(hh, mh, c1, &c2);
+        r += c2;  // 1 iff key of lane (g-K) < my key
+        rank_step<G, K + 1>(mh, ml, t, lane, r);
+    }
+}
+
+// rank over rotations K = K0 .. KEND-1 only (keys duplicated so that fewer rotations cover
+// every other key of interest)
+template <int G, int K, int KEND>
+__device__ __forceinline__ void rank_step_n(uint32_t mh, uint32_t ml, uint32_t t, int lane, uint32_t& r) {
+    if constexpr (K < KEND) {
+        const uint32_t th = grot32c<G, K>(t, lane);
+        const uint32_t lh = grot32c<G, K>(ml, lane);
+        const uint32_t hh = grot32c<G, K>(mh, lane);
+        unsigned c0, c1, c2;
+        (void)__builtin_subc(th, t, 0u, &c0);
+        (void)__builtin_subc(lh, ml, c0, &c1);
+        (void)__builtin_subc(hh, mh, c1, &c2);
+        r += c2;
+        rank_step_n<G, K + 1, KEND>(mh, ml, t, lane, r);
+    }
+}
+
+// OR of v over the G lanes of the group
+template <int G, int K = 1>
+__device__ __forceinline__ uint32_t or_reduce_group(uint32_t v, int lane, uint32_t acc = 0) {
+    if constexpr (K == 1) acc = v;
+    if constexpr (K < G) {
+        acc |= grot32c<G, K>(v, lane);
+        return or_reduce_group<G, K + 1>(v, lane, acc);
+    } else {
+        return acc;
+    }
+}
+
+// value from lane g - LMAX of the group (the bit-0 sibling of a bit-1 candidate lane)
+template <int G, int LMAX>
+__device__ __forceinline__ uint32_t from_lower_half(uint32_t v, int lane) {
+    if constexpr (G <= 16) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + LMAX, 0xF, 0xF, false);  // row_ror:LMAX
+    } else {
+        return bperm32(v, lane - LMAX);
+    }
+}
+
+
+// value from lane g + LMAX of the group (the bit-1 half), G = 2*LMAX <= 16
+template <int G, int LMAX>
+__device__ __forceinline__ uint32_t from_upper_half(uint32_t v, int lane) {
+    if constexpr (G <= 16) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + ((16 - LMAX) & 15), 0xF, 0xF, false);
+    } else {
+        return bperm32(v, lane + LMAX);
+    }
+}
+
+template <int G, int LMAX>
+__device__ __forceinline__ uint64_t from_lower_half64(uint64_t v, int lane) {
+    return ((uint64_t)from_lower_half<G, LMAX>((uint32_t)(v >> 32), lane) << 32) |
+           from_lower_half<G, LMAX>((uint32_t)v, lane);
+}
+
+template <int G, int LMAX>
+__device__ __forceinline__ uint64_t from_upper_half64(uint64_t v, int lane) {
+    return ((uint64_t)from_upper_half<G, LMAX>((uint32_t)(v >> 32), lane) << 32) |
+           from_upper_half<G, LMAX>((uint32_t)v, lane);
+}
+
+// error counters of one decoded frame (run_fer_sweep.py:91-109, run_ber_sweep.py:77-82,156)
+__device__ __forceinline__ void count_errors(int64_t* counters, uint64_t ib0, uint64_t ib1, uint64_t r0, uint64_t r1,
+                                             int k_payload, bool pass) {
+    const uint64_t d0 = ib0 ^ r0, d1 = ib1 ^ r1;
+    const int bit_err = __popcll(d0) + __popcll(d1);
+    const int kp = k_payload;
+    const uint64_t pm0 = kp >= 64 ? ~0ULL : ((1ULL << kp) - 1);
+    const uint64_t pm1 = kp >= 128 ? ~0ULL : (kp > 64 ? ((1ULL << (kp - 64)) - 1) : 0ULL);
+    const int pay_err = __popcll(d0 & pm0) + __popcll(d1 & pm1);
+    unsigned long long* C = reinterpret_cast<unsigned long long*>(counters);
+    if (!pass) atomicAdd(C + PSCL_CNT_FRAME_ERR, 1ULL);
+    if (bit_err) atomicAdd(C + PSCL_CNT_BIT_ERR, (unsigned long long)bit_err);
+    if (pay_err) {
+        atomicAdd(C + PSCL_CNT_PAYLOAD_ERR, 1ULL);
+        atomicAdd(C + PSCL_CNT_PAYLOAD_BIT, (unsigned long long)pay_err);
+    }
+}
+
+}  // namespace pscl
+
+#endif

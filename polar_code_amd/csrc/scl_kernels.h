@@ -15,6 +15,7 @@ struct pscl_decode_params {
     int N, n, K, L, W;
     uint64_t info_mask[2];       // bit phi set <=> phase phi is an information bit
     const uint32_t* crc_cols;    // [K] check syndrome columns (zeros when no CRC)
+    const int32_t* info_set;     // [K] information positions, ascending (device)
     int has_crc;
     int sc_hard;                 // 1: successive cancellation, hard decisions (L = 1 path)
     const uint64_t* exp_table;   // [256] glibc exp table (device)
@@ -28,6 +29,7 @@ struct pscl_decode_params {
     const uint64_t* ref;         // [B][W] or null
     int k_payload;
     int64_t* counters;           // [PSCL_NCOUNT] (device)
+    int fast;                    // 1: the specialised N = 128, L <= 8 kernel (scl128.hip)
     int wave_bytes;              // LDS bytes per wavefront
     int a_bytes;                 // LDS bytes of the LLR slots per wavefront
 };
@@ -45,6 +47,10 @@ struct pscl_channel_params {
 };
 
 int pscl_decode_lmax(int L);
+// fills P.a_bytes / P.wave_bytes / P.fast for the kernel that will decode this shape
+void pscl_decode_layout(pscl_decode_params& P, int hist);
+int pscl_fast128_fstride(int L);
+hipError_t pscl_launch_decode128(const pscl_decode_params& P, int hist, int wpg, int64_t grid, int lds, hipStream_t s);
 int64_t pscl_decode_grid(const pscl_decode_params& P);
 int pscl_decode_wpg(const pscl_decode_params& P);
 int pscl_decode_lds(const pscl_decode_params& P, int hist);

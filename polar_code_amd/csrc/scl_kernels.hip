@@ -23,108 +23,12 @@
 #include <stdint.h>
 
 #include "glibc_softplus.h"
+#include "scl_device.h"
 #include "scl_kernels.h"
-
-// Timing-only ablation switches for diagnostic builds (tools/ablate.py); 0 in the product.
-#ifndef PSCL_ABLATE
-#define PSCL_ABLATE 0
-#endif
 
 namespace {
 
-constexpr int kWave = 64;
-
-__device__ __forceinline__ uint32_t bperm32(uint32_t v, int src) {
-    return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
-}
-__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
-    uint32_t lo = bperm32((uint32_t)v, src), hi = bperm32((uint32_t)(v >> 32), src);
-    return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ double shfl_f64(double v, int src) {
-    return pscl_asf64(shfl_u64(pscl_asu64(v), src));
-}
-__device__ __forceinline__ uint32_t rdl_u32(uint32_t v, int l) {
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
-}
-__device__ __forceinline__ double rdl_f64(double v, int l) {
-    uint64_t u = pscl_asu64(v);
-    uint32_t lo = rdl_u32((uint32_t)u, l), hi = rdl_u32((uint32_t)(u >> 32), l);
-    return pscl_asf64(((uint64_t)hi << 32) | lo);
-}
-
-// Orders the wave's LDS traffic: hardware executes one wave's LDS instructions in order;
-// this keeps the compiler from moving loads above the stores they depend on.
-__device__ __forceinline__ void wave_lds_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// f(a,b) = sign(a) sign(b) min(|a|,|b|)  (polar.py:122-123; exact, sign(0)=0 gives +-0)
-__device__ __forceinline__ double f_minsum(double a, double b) {
-    double m = fmin(fabs(a), fabs(b));
-    return ((a < 0.0) != (b < 0.0)) ? -m : m;
-}
-// g(a,b,c) = b + (1-2c) a  (polar.py:126-127; one rounding)
-__device__ __forceinline__ double g_node(double a, double b, uint32_t c) { return c ? b - a : b + a; }
-
-// Arikan transform of the low w bits of x (in-word, w <= 64): bit j ^= bit j+s for bit s of j
-// clear, for every stage s (stages commute).  Bits >= w must be zero.
-__device__ __forceinline__ uint64_t polar_transform64(uint64_t x) {
-    x ^= (x >> 1) & 0x5555555555555555ULL;
-    x ^= (x >> 2) & 0x3333333333333333ULL;
-    x ^= (x >> 4) & 0x0f0f0f0f0f0f0f0fULL;
-    x ^= (x >> 8) & 0x00ff00ff00ff00ffULL;
-    x ^= (x >> 16) & 0x0000ffff0000ffffULL;
-    x ^= (x >> 32) & 0x00000000ffffffffULL;
-    return x;
-}
-
-__device__ __forceinline__ uint64_t pick_word(uint64_t w0, uint64_t w1, int idx) { return idx ? w1 : w0; }
-
-
-// ---------------------------------------------------------------- lane-group helpers
-// A wavefront decodes F = 64/G frames at once; frame slot fl owns the G = 2*LMAX lanes
-// [fl*G, fl*G + G).  Lane g < L of a group holds list path g (list position == lane, so the
-// stable-sort tie key is the lane index itself); lanes [L, 2L) carry the bit-1 children
-// while the list is being extended.
-
-template <int G, int K>
-__device__ __forceinline__ uint32_t grot32c(uint32_t v, int lane) {
-    if constexpr (G == 16) {
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + K, 0xF, 0xF, false);  // row_ror:K
-    } else if constexpr (G == 8) {
-        const uint32_t a = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + K, 0xF, 0xF, false);
-        const uint32_t b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + K + 8, 0xF, 0xF, false);
-        return ((lane & 7) >= K) ? a : b;  // row_ror:K reads lane x-K; wrap inside the 8-lane group
-    } else if constexpr (G == 4) {
-        constexpr int q = ((0 + K) & 3) | (((1 + K) & 3) << 2) | (((2 + K) & 3) << 4) | (((3 + K) & 3) << 6);
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, q, 0xF, 0xF, false);  // quad_perm
-    } else if constexpr (G == 2) {
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-    } else {
-        return bperm32(v, (lane & ~(G - 1)) | ((lane + K) & (G - 1)));
-    }
-}
-
-template <int G, int K>
-__device__ __forceinline__ double grot64c(double v, int lane) {
-    const uint64_t u = pscl_asu64(v);
-    const uint32_t lo = grot32c<G, K>((uint32_t)u, lane), hi = grot32c<G, K>((uint32_t)(u >> 32), lane);
-    return pscl_asf64(((uint64_t)hi << 32) | lo);
-}
-
-// stable rank of this lane's key (m, t) among the G keys of its group
-template <int G, int K>
-__device__ __forceinline__ void rank_step(double m, uint32_t t, int lane, int& r) {
-    if constexpr (K < G) {
-        const double my = grot64c<G, K>(m, lane);
-        const uint32_t ty = grot32c<G, K>(t, lane);
-        r += (my < m) || (my == m && ty < t);
-        rank_step<G, K + 1>(m, t, lane, r);
-    }
-}
+using namespace pscl;
 
 template <int LMAX, bool HIST>
 __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
@@ -157,10 +61,9 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
     const int wpg = (int)(blockDim.x >> 6);
     const int64_t wstride = (int64_t)gridDim.x * wpg * F;
     const bool path_lane = g < L;
-    // candidate c = g: (path g, bit 0) for g < L, (path g-L, bit 1) for L <= g < 2L
-    const int cpath = g < L ? g : g - L;
-    const uint32_t cbit = g >= L ? 1u : 0u;
-    const bool cand_lane = g < 2 * L;
+    // candidate c = g: (path g, bit 0) for g < LMAX, (path g-LMAX, bit 1) for g >= LMAX
+    const int cpath = g & (LMAX - 1);
+    const uint32_t cbit = g >= LMAX ? 1u : 0u;
 
     for (int64_t f0 = ((int64_t)blockIdx.x * wpg + wave) * F; f0 < P.B; f0 += wstride) {
         const int64_t f = f0 + fl;
@@ -183,8 +86,6 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
         }
         double metric = 0.0;
         uint64_t u0 = 0, u1 = 0;    // decided bits u[phase]
-        uint64_t ib0 = 0, ib1 = 0;  // candidate bits in info order
-        uint32_t syn = 0;           // CRC syndrome of the candidate bits
         uint32_t tab = 0;           // LDS slot per depth d (5 bits at 5*(d-1))
         int cnt = 1;                // live paths of this frame (group-uniform)
         int cu = 1;                 // wave-uniform bound: max live paths over the wave's frames
@@ -211,7 +112,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
             };
             uint64_t xp1 = 0;
             if (right1) xp1 = polar_transform64(half >= 64 ? u0 : (u0 & ((1ULL << half) - 1)));
-            for (int d = (start > 2 ? start : 2); d < n; ++d) {
+            for (int d = (start > 2 ? start : 2); d < ((PSCL_ABLATE & 4) ? 0 : n); ++d) {
                 const int lw = n - d, w = 1 << lw;
                 const bool is_g = (d == start) && phi;
                 const int total = F << (lp + lw);
@@ -274,24 +175,24 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
                 lam = (phi & 1) ? g_node(a, b, (uint32_t)xs & 1u) : f_minsum(a, b);
             }
             // ---- metric increments (scl.py:102-105), shared log1p(exp(-|llr|))
-            const double Lt = (PSCL_ABLATE & 1) ? lam * 0.5 : pscl_softplus_tail(lam, T);
+            const double Lt = (PSCL_ABLATE & 1) ? lam * 0.5 : pscl_softplus_tail_bf(lam, T);
             const double m0 = metric + pscl_logaddexp0(-lam, Lt);
             const double m1 = metric + pscl_logaddexp0(lam, Lt);
             const uint64_t infow = pick_word(P.info_mask[0], P.info_mask[1], phi >> 6);
             const bool is_info = (infow >> (phi & 63)) & 1;
             // candidate key of this lane: (metric of child, 2 * list position + bit)
-            const int psrc = gbase + cpath;
-            const double pm1 = shfl_f64(m1, psrc);
-            const double plam = shfl_f64(lam, psrc);
-            double km = cbit ? pm1 : m0;
-            const uint32_t kt = 2u * (uint32_t)cpath + cbit;
-            bool kval = cand_lane && cpath < cnt;
+            const uint64_t m1b = pscl_asu64(m1);
+            const uint64_t pm1 = ((uint64_t)from_lower_half<G, LMAX>((uint32_t)(m1b >> 32), lane) << 32) |
+                                 from_lower_half<G, LMAX>((uint32_t)m1b, lane);
+            uint64_t km = cbit ? pm1 : pscl_asu64(m0);
+            bool kval = cpath < cnt;
             int ncnt = cnt;
             if (!is_info) {
                 kval = kval && cbit == 0;  // frozen: bit 0 (scl.py:149-153)
             } else {
                 const uint64_t fmw = pick_word(fm0, fm1, j >> 6), fvw = pick_word(fv0, fv1, j >> 6);
                 if (P.sc_hard) {
+                    const double plam = shfl_f64(lam, gbase + cpath);
                     kval = kval && cbit == (uint32_t)(plam < 0.0);  // sc_decode polar.py:149-153
                 } else if ((fmw >> (j & 63)) & 1) {
                     kval = kval && cbit == (uint32_t)((fvw >> (j & 63)) & 1);  // forced (scl.py:146-161)
@@ -299,35 +200,31 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
                     ncnt = 2 * cnt < L ? 2 * cnt : L;  // both children (scl.py:163-168)
                 }
             }
-            if (!kval) km = __builtin_huge_val();
-            const uint32_t ktv = kval ? kt : 0x7fffffffu;
+            if (!kval) km = 0x7ff0000000000000ULL;  // +inf: never ranks ahead of a live child
+            const uint32_t kt = kval ? 2u * (uint32_t)cpath + cbit : 0x7fffffffu;
             // stable sort of the children, keep the first L (scl.py:173-174): rank count
-            int r = 0;
-            if (!(PSCL_ABLATE & 2)) rank_step<G, 1>(km, ktv, lane, r);
-            else r = (int)kt;
-            if (kval && r < ncnt) inv[gbase + r] = (uint8_t)g;
+            uint32_t r = 0;
+            if (!(PSCL_ABLATE & 2)) rank_step<G, 1>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
+            else r = kt;
+            if (kval && r < (uint32_t)ncnt) inv[gbase + r] = (uint8_t)g;
             wave_lds_fence();
             const int c = (g < ncnt) ? inv[gbase + g] : g;
-            const int par_g = c < L ? c : c - L;
-            const uint32_t b = c >= L ? 1u : 0u;
+            const int par_g = c & (LMAX - 1);
+            const uint32_t b = c >= LMAX ? 1u : 0u;
             const int ps2 = gbase + par_g;
-            const double nm = shfl_f64(km, gbase + c);
-            const double nlam = shfl_f64(lam, ps2);
-            const uint64_t nu0 = shfl_u64(u0, ps2), nu1 = shfl_u64(u1, ps2);
-            const uint64_t nib0 = shfl_u64(ib0, ps2), nib1 = shfl_u64(ib1, ps2);
-            const uint32_t ntab = bperm32(tab, ps2), nsyn = bperm32(syn, ps2);
+            const uint64_t nm = shfl_u64(km, gbase + c);
+            const uint64_t nu0 = shfl_u64(u0, ps2);
+            const uint64_t nu1 = (N > 64) ? shfl_u64(u1, ps2) : 0;
+            const uint32_t ntab = bperm32(tab, ps2);
+            double nlam = 0.0;
+            if (HIST) nlam = shfl_f64(lam, ps2);
             wave_lds_fence();  // inv[] is rewritten next phase
-            metric = nm;
+            metric = pscl_asf64(nm);
             u0 = nu0;
             u1 = nu1;
-            ib0 = nib0;
-            ib1 = nib1;
             tab = ntab;
-            syn = nsyn;
             if (b) {
                 if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
-                if (j < 64) ib0 |= 1ULL << j; else ib1 |= 1ULL << (j - 64);
-                syn ^= P.crc_cols[j];
             }
             if (HIST && g < ncnt) {
                 if (is_info) hist_llr[j * L + g] = nlam;  // decision LLR (scl.py:158,166)
@@ -340,7 +237,16 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
             }
         }
 
-        // ---- epilogue: the list is in lane order; best = first CRC-passing candidate
+        // ---- epilogue: candidate bits u[info_set] and their CRC syndrome, rebuilt once from u
+        uint64_t ib0 = 0, ib1 = 0;
+        uint32_t syn = 0;
+        for (int jj = 0; jj < K; ++jj) {
+            const int ph = P.info_set[jj];
+            const uint64_t bit = (pick_word(u0, u1, ph >> 6) >> (ph & 63)) & 1ULL;
+            if (jj < 64) ib0 |= bit << jj; else ib1 |= bit << (jj - 64);
+            syn ^= bit ? P.crc_cols[jj] : 0u;
+        }
+        // the list is in lane order; best = first CRC-passing candidate (scl.py:190-201)
         const bool active = path_lane && g < cnt && fvalid;
         const uint64_t passmask = __ballot(active && syn == 0);
         const uint64_t gmask = (passmask >> gbase) & ((G == 64) ? ~0ULL : ((1ULL << G) - 1));
@@ -529,9 +435,26 @@ int64_t pscl_decode_grid(const pscl_decode_params& P) {
     return g < 1 ? 1 : (g > cap ? cap : g);
 }
 
+void pscl_decode_layout(pscl_decode_params& P, int hist) {
+    const int lmax = pscl_decode_lmax(P.L);
+    const int F = 32 / lmax;  // frames per wavefront
+    P.fast = (P.N == 128 && P.L <= 8) ? 1 : 0;
+    if (P.fast) {
+        P.a_bytes = F * pscl_fast128_fstride(P.L) * 8;
+        const int wb = P.a_bytes + (hist ? F * P.K * P.L * 9 : 0);
+        P.wave_bytes = (wb + 15) & ~15;
+    } else {
+        const int fstride = P.N + (P.N >= 8 ? P.L * (P.N / 2 - 2) : 0);  // doubles per frame
+        P.a_bytes = F * fstride * 8;
+        const int wb = P.a_bytes + 64 + (hist ? F * (P.K * P.L * 8 + P.N * P.L) : 0);
+        P.wave_bytes = (wb + 15) & ~15;
+    }
+}
+
 hipError_t pscl_launch_decode(const pscl_decode_params& P, int hist, hipStream_t s) {
     if (pscl_decode_wpg(P) < 1) return hipErrorInvalidValue;
     const int64_t grid = pscl_decode_grid(P);
+    if (P.fast) return pscl_launch_decode128(P, hist, pscl_decode_wpg(P), grid, decode_lds_bytes(P, hist), s);
     switch (pscl_decode_lmax(P.L)) {
         case 1: return launch_l<1>(P, hist, grid, s);
         case 2: return launch_l<2>(P, hist, grid, s);

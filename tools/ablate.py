@@ -20,7 +20,7 @@ def build():
     csrc, inc = ROOT / "polar_code_amd" / "csrc", ROOT / "include"
     for m in MASKS:
         objs = []
-        for src in ("scl_kernels.hip", "capi.cpp"):
+        for src in ("scl_kernels.hip", "scl128.hip", "capi.cpp"):
             o = OUT / f"{Path(src).stem}_{m}.o"
             subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
                                    "-ffp-contract=off", f"-DPSCL_ABLATE={m}", "-Wno-unused-result", "-Wno-unused-value",

@@ -1,0 +1,52 @@
+"""Summarise rocprofv3 PMC passes (tools/profile_pmc.sh output) for the decode kernel.
+
+    python tools/pmc_summary.py gpurun_out/pmc_<tag> [frames_per_launch]
+
+Prints per-launch averages and derived figures, and (with --json) the HBM traffic entry
+bench.py reads from profiles/pmc_traffic.json.  Corrections follow MI355X_MICROARCH.md
+(HBM section): FETCH_SIZE/WRITE_SIZE are in KiB; gfx950 FETCH_SIZE reports half the bytes of
+wide coalesced reads, so it is doubled; WRITE_SIZE is taken as reported.
+"""
+import collections
+import csv
+import json
+import sys
+from pathlib import Path
+
+
+def load(d):
+    agg = collections.defaultdict(list)
+    for f in sorted(Path(d).glob("p*/pmc_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if "scl_decode_kernel" in r["Kernel_Name"]:
+                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main():
+    d = sys.argv[1]
+    frames = float(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2].isdigit() else 1e6
+    c = load(d)
+    for k in sorted(c):
+        print(f"{k:28s} {c[k]:.6g}")
+    out = {}
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        fetch = 2 * c["FETCH_SIZE"] * 1024
+        write = c["WRITE_SIZE"] * 1024
+        out["hbm_bytes_per_launch"] = fetch + write
+        out["fetch_bytes_corrected"] = fetch
+        out["write_bytes"] = write
+        print(f"HBM bytes/launch (2*FETCH+WRITE) = {fetch + write:.4g}  ({(fetch + write) / frames:.1f} B/frame)")
+    if "SQ_WAVES" in c:
+        w = c["SQ_WAVES"]
+        for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"):
+            if k in c:
+                print(f"{k} per wave = {c[k] / w:.0f}")
+    if "GRBM_GUI_ACTIVE" in c:
+        print(f"GRBM_GUI_ACTIVE = {c['GRBM_GUI_ACTIVE']:.4g}")
+    if "--json" in sys.argv:
+        print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
