@@ -257,3 +257,39 @@ def get_decoder(N: int, info_set, L: int, crc=None, device: int = 0) -> Decoder:
             dec = Decoder(N, info, L, crc, device)
             _CACHE[key] = dec
         return dec
+
+
+class DeviceArena:
+    """Device buffers owned through the C ABI (pscl_device_alloc), freed on exit.  Lets the
+    host layer drive the device path without PyTorch."""
+
+    def __init__(self, dec: Decoder):
+        self.dec = dec
+        self.ptrs: list[int] = []
+
+    def __enter__(self) -> "DeviceArena":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.dec.sync()
+        for p in self.ptrs:
+            lib().pscl_device_free(self.dec.handle, p)
+        self.ptrs.clear()
+
+    def alloc(self, nbytes: int) -> int:
+        p = _vp()
+        check(lib().pscl_device_alloc(self.dec.handle, C.byref(p), int(nbytes)))
+        self.ptrs.append(p.value)
+        return p.value
+
+    def memset(self, d_ptr: int, value: int, nbytes: int) -> None:
+        check(lib().pscl_memset_device(self.dec.handle, d_ptr, int(value), int(nbytes)))
+
+    def upload(self, d_ptr: int, arr: np.ndarray) -> None:
+        arr = np.ascontiguousarray(arr)
+        check(lib().pscl_memcpy_htod(self.dec.handle, d_ptr, arr.ctypes.data, arr.nbytes))
+
+    def download(self, d_ptr: int, nbytes: int, dtype) -> np.ndarray:
+        out = np.empty(int(nbytes) // np.dtype(dtype).itemsize, dtype=dtype)
+        check(lib().pscl_memcpy_dtoh(self.dec.handle, out.ctypes.data, d_ptr, out.nbytes))
+        return out

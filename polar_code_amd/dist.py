@@ -1,0 +1,108 @@
+"""One process per GPU: frame sharding and the error-counter all-reduce.
+
+The Monte-Carlo frame loop (run_fer_sweep.py:79-121) has no cross-frame state except the
+RNG stream and the counters, so frames are split into contiguous global index ranges per
+rank and decoded independently; the only collective is one SUM all-reduce of an int64
+counter vector per SNR point (RCCL over xGMI under backend "nccl", gloo on CPU).
+The reference is single-process; this module has no reference counterpart.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+
+@dataclass
+class Context:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    backend: str = ""
+
+    @property
+    def is_root(self) -> bool:
+        return self.rank == 0
+
+
+_CTX: Context | None = None
+
+
+def init(backend: str | None = None) -> Context:
+    """Initialise torch.distributed from torchrun's environment (WORLD_SIZE > 1), else a
+    single-process context.  backend: "nccl" (RCCL) when the ranks own GPUs, else "gloo"."""
+    global _CTX
+    if _CTX is not None:
+        return _CTX
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if not dist.is_initialized():
+            if backend == "nccl":
+                torch.cuda.set_device(local)
+                dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group(backend=backend)
+    _CTX = Context(rank=rank, world=world, local_rank=local, backend=backend or "")
+    return _CTX
+
+
+def shard(total: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous global frame range [start, stop) of `rank`; ranks differ by at most one frame."""
+    base, extra = divmod(int(total), int(world))
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def allreduce_sum(vec: np.ndarray, ctx: Context | None = None) -> np.ndarray:
+    """SUM of an int64/float64 vector over all ranks (identity when world == 1)."""
+    ctx = ctx or _CTX or Context()
+    if ctx.world <= 1:
+        return np.asarray(vec)
+    import torch
+    import torch.distributed as dist
+
+    t = torch.as_tensor(np.ascontiguousarray(vec))
+    if ctx.backend == "nccl":
+        t = t.cuda()
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.cpu().numpy()
+
+
+def allreduce_max(x: float, ctx: Context | None = None) -> float:
+    ctx = ctx or _CTX or Context()
+    if ctx.world <= 1:
+        return float(x)
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    if ctx.backend == "nccl":
+        t = t.cuda()
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(ctx: Context | None = None) -> None:
+    ctx = ctx or _CTX or Context()
+    if ctx.world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def finalize() -> None:
+    global _CTX
+    if _CTX is not None and _CTX.world > 1:
+        import torch.distributed as dist
+
+        if dist.is_initialized():
+            dist.destroy_process_group()
+    _CTX = None

@@ -1,0 +1,282 @@
+"""FER sweep: SCL vs DL-SCL (mirror of dl_scl_polar/eval/run_fer_sweep.py, same flags,
+console lines, CSV schema and plot).
+
+    python -m polar_code_amd.eval.run_fer_sweep --M 8 --frames 2000 --snr_lo 5 --snr_hi 5 \
+        --snr_step 0 --retries 8 --beta tests/golden/beta_M8.npy --seed 0 --include_uncoded
+
+Every decode runs on the GPU (libpolar_mi355x.so).  Two channel modes:
+  --rng replay  (default) the reference's own NumPy PCG64 stream, frame by frame in its draw
+                order (run_fer_sweep.py:61,79-87,111-113): reproduces results/fer_M{4,8}.csv
+                exactly.  Frames are generated on the host and decoded in batches.
+  --rng philox  frames generated on the GPU by a counter-based Philox stream keyed by
+                (seed, SNR, global frame index): results independent of GPU count,
+                statistically equivalent to the reference (same channel model).
+Multi-GPU: launch with torchrun; frames are sharded by global index and the counters are
+summed with one all-reduce per SNR point (polar_code_amd/dist.py).
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import time
+from pathlib import Path
+from typing import Dict, List, Tuple
+
+import numpy as np
+
+from .. import _native, config, dist
+from ..dlscl.flip import decode_with_retries, decode_with_retries_batch
+from ..polar.crc import attach_crc
+from ..polar.polar import construct_info_set, encode
+from ..polar.scl import decode_scl
+from ..utils.seeding import seed_all
+
+# counter vector, summed across ranks
+C_FRAMES, C_SCL_ERR, C_DL_ERR, C_SCL_BIT, C_DL_BIT, C_UNC_ERR, C_UNC_BIT, C_BITS, C_BITS_UNC, C_DL_WORK = range(10)
+NCOUNT = 10
+
+
+def _bpsk(bits: np.ndarray) -> np.ndarray:
+    return 1.0 - 2.0 * bits
+
+
+def simulate_frame(llr, info_set, M, crc_poly, retries, beta) -> Tuple[Dict, Dict]:
+    """Baseline SCL and DL-SCL of one frame (run_fer_sweep.py:28-38)."""
+    base = decode_scl(llr, info_set, M, crc=crc_poly)
+    dl = decode_with_retries(llr, info_set, M, retries, crc=crc_poly, beta=beta)
+    return base, dl
+
+
+def noise_params(snr_db: float, rate: float) -> Tuple[float, float, float, float]:
+    ebno = 10 ** (snr_db / 10.0)
+    var_c = 1.0 / (2.0 * rate * ebno)
+    var_u = 1.0 / (2.0 * ebno)
+    return var_c, math.sqrt(var_c), var_u, math.sqrt(var_u)
+
+
+def replay_stream(seed: int, snr_db: float, start: int, stop: int, payload_bits: int, crc_poly: str,
+                  include_uncoded: bool):
+    """Frames [start, stop) of the reference's per-SNR stream default_rng(seed + int(snr*10)),
+    drawn in its order: integers(0,2,payload) -> normal(0,sigma,N) -> [normal(0,sigma_u,payload)]."""
+    cfg = config.get_config()
+    rng = np.random.default_rng(seed + int(snr_db * 10))
+    var_c, sig_c, var_u, sig_u = noise_params(snr_db, cfg.K / cfg.N)
+    n = stop - start
+    payload = np.empty((n, payload_bits), np.int8)
+    noise = np.empty((n, cfg.N))
+    unc = np.empty((n, payload_bits)) if include_uncoded else None
+    for fr in range(stop):
+        p = rng.integers(0, 2, size=payload_bits, dtype=np.int8)
+        z = rng.normal(0.0, sig_c, size=cfg.N)
+        zu = rng.normal(0.0, sig_u, size=payload_bits) if include_uncoded else None
+        if fr >= start:
+            payload[fr - start], noise[fr - start] = p, z
+            if include_uncoded:
+                unc[fr - start] = zu
+    msg = attach_crc(payload, crc_poly)
+    code = encode(msg)
+    llr = 2.0 * (_bpsk(code) + noise) / var_c
+    llr_unc = None
+    if include_uncoded:
+        llr_unc = 2.0 * (_bpsk(payload) + unc) / var_u
+    return payload, msg, llr, llr_unc
+
+
+def _count_block(c, msg, llr, payload, llr_unc, info_set, M, crc, retries, beta, device):
+    dec = _native.get_decoder(llr.shape[1], info_set, M, crc, device)
+    base = dec.decode(llr, want_metrics=False, want_cands=False, want_info_llrs=False)
+    c[C_FRAMES] += llr.shape[0]
+    c[C_SCL_ERR] += int(np.count_nonzero(~base["crc_pass"]))
+    c[C_SCL_BIT] += int(np.count_nonzero(base["best_bits"] != msg))
+    dl = decode_with_retries_batch(llr, info_set, M, retries, crc=crc, beta=beta, device=device, baseline=base)
+    c[C_DL_ERR] += int(np.count_nonzero(~dl["success"]))
+    c[C_DL_BIT] += int(np.count_nonzero(dl["best_bits"] != msg))
+    c[C_DL_WORK] += int((dl["attempts"] - 1).sum())
+    c[C_BITS] += msg.size
+    if llr_unc is not None:
+        errs = np.count_nonzero((llr_unc < 0).astype(np.int8) != payload, axis=1)
+        c[C_UNC_ERR] += int(np.count_nonzero(errs))
+        c[C_UNC_BIT] += int(errs.sum())
+        c[C_BITS_UNC] += payload.size
+
+
+def _philox_block(c, seed, snr_db, frame0, n, info_set, M, crc, retries, beta, device, include_uncoded,
+                  payload_bits):
+    """n frames generated on the device; SCL counted in-kernel, failing frames retried."""
+    cfg = config.get_config()
+    dec = _native.get_decoder(cfg.N, info_set, M, crc, device)
+    W = dec.W
+    with _native.DeviceArena(dec) as mem:
+        d_llr = mem.alloc(n * cfg.N * 8)
+        d_msg = mem.alloc(n * W * 8)
+        d_best = mem.alloc(n * W * 8)
+        d_flags = mem.alloc(n)
+        d_cnt = mem.alloc(8 * 8)
+        mem.memset(d_cnt, 0, 64)
+        dec.channel_device(seed, int(round(snr_db * 10)), snr_db, cfg.K / cfg.N, payload_bits, frame0, n, d_llr, d_msg)
+        dec.decode_device(d_llr, n, d_best=d_best, d_flags=d_flags, d_ref=d_msg, k_payload=payload_bits,
+                          d_counters=d_cnt)
+        cnt = mem.download(d_cnt, 64, np.int64)
+        flags = mem.download(d_flags, n, np.uint8)
+        c[C_FRAMES] += n
+        c[C_SCL_ERR] += int(cnt[_native.CNT_FRAME_ERR])
+        c[C_SCL_BIT] += int(cnt[_native.CNT_BIT_ERR])
+        c[C_BITS] += n * cfg.K
+        fail = np.flatnonzero((flags & _native.PSCL_FLAG_CRC_PASS) == 0)
+        dl_bit = int(cnt[_native.CNT_BIT_ERR])
+        if fail.size and retries > 0:
+            llr_all = mem.download(d_llr, n * cfg.N * 8, np.float64).reshape(n, cfg.N)
+            msg_w = mem.download(d_msg, n * W * 8, np.uint64).reshape(n, W)
+            best_w = mem.download(d_best, n * W * 8, np.uint64).reshape(n, W)
+            bits_of = lambda w: ((w[:, :, None] >> np.arange(64, dtype=np.uint64)) & 1).reshape(w.shape[0], -1)[:, :cfg.K]
+            msg_f = bits_of(msg_w[fail]).astype(np.int8)
+            base_f = bits_of(best_w[fail]).astype(np.int8)
+            dl = decode_with_retries_batch(llr_all[fail], info_set, M, retries, crc=crc, beta=beta, device=device,
+                                           baseline={"best_bits": base_f, "crc_pass": np.zeros(fail.size, bool)})
+            c[C_DL_ERR] += int(np.count_nonzero(~dl["success"]))
+            dl_bit += int(np.count_nonzero(dl["best_bits"] != msg_f)) - int(np.count_nonzero(base_f != msg_f))
+            c[C_DL_WORK] += int((dl["attempts"] - 1).sum())
+        else:
+            c[C_DL_ERR] += int(fail.size)
+        c[C_DL_BIT] += dl_bit
+    if include_uncoded:
+        rng = np.random.default_rng([seed, int(round(snr_db * 10)), frame0])
+        _, _, var_u, sig_u = noise_params(snr_db, cfg.K / cfg.N)
+        pay = rng.integers(0, 2, size=(n, payload_bits), dtype=np.int8)
+        y = _bpsk(pay) + rng.normal(0.0, sig_u, size=pay.shape)
+        errs = np.count_nonzero(((2.0 * y / var_u) < 0).astype(np.int8) != pay, axis=1)
+        c[C_UNC_ERR] += int(np.count_nonzero(errs))
+        c[C_UNC_BIT] += int(errs.sum())
+        c[C_BITS_UNC] += pay.size
+
+
+def run_sweep(args: argparse.Namespace) -> List[Dict[str, float]]:
+    cfg = config.get_config()
+    seed_all(args.seed)
+    ctx = dist.init()
+    device = ctx.local_rank
+    info_set = construct_info_set(cfg.N, cfg.K)
+    payload_bits = cfg.K - cfg.crc_bits
+    snr_points = (np.arange(args.snr_lo, args.snr_hi + 1e-9, args.snr_step) if args.snr_step > 0
+                  else np.array([args.snr_lo]))
+    beta = np.load(args.beta) if args.beta else None
+    results: List[Dict[str, float]] = []
+    t0 = time.perf_counter()
+    for snr_db in snr_points:
+        c = np.zeros(NCOUNT, np.int64)
+        start, stop = dist.shard(args.frames, ctx.rank, ctx.world)
+        for b0 in range(start, stop, args.batch):
+            b1 = min(stop, b0 + args.batch)
+            if args.rng == "replay":
+                payload, msg, llr, llr_unc = replay_stream(args.seed, float(snr_db), b0, b1, payload_bits,
+                                                           cfg.crc_poly, args.include_uncoded)
+                _count_block(c, msg, llr, payload, llr_unc, info_set, args.M, cfg.crc_poly, args.retries, beta, device)
+            else:
+                _philox_block(c, args.seed, float(snr_db), b0, b1 - b0, info_set, args.M, cfg.crc_poly, args.retries,
+                              beta, device, args.include_uncoded, payload_bits)
+        c = dist.allreduce_sum(c, ctx)
+        total_frames = args.frames
+        scl_fer = c[C_SCL_ERR] / total_frames
+        dl_fer = c[C_DL_ERR] / total_frames
+        row = {"snr_db": float(snr_db), "fer_scl": scl_fer, "fer_dl": dl_fer}
+        row["ber_scl"] = c[C_SCL_BIT] / c[C_BITS] if c[C_BITS] > 0 else float("nan")
+        row["ber_dl"] = c[C_DL_BIT] / c[C_BITS] if c[C_BITS] > 0 else float("nan")
+        row["avg_retries"] = c[C_DL_WORK] / max(total_frames, 1)
+        if args.include_uncoded:
+            row["fer_uncoded"] = c[C_UNC_ERR] / total_frames if total_frames > 0 else float("nan")
+            row["ber_uncoded"] = c[C_UNC_BIT] / c[C_BITS_UNC] if c[C_BITS_UNC] > 0 else float("nan")
+            msg_line = (f"SNR={snr_db:.2f} dB -> Uncoded FER={row['fer_uncoded']:.3e}, BER={row['ber_uncoded']:.3e}; "
+                        f"SCL FER={scl_fer:.3e}, BER={row['ber_scl']:.3e}; DL FER={dl_fer:.3e}, BER={row['ber_dl']:.3e}")
+        else:
+            msg_line = (f"SNR={snr_db:.2f} dB -> SCL FER={scl_fer:.3e}, BER={row['ber_scl']:.3e}; "
+                        f"DL FER={dl_fer:.3e}, BER={row['ber_dl']:.3e}")
+        if ctx.is_root:
+            print(msg_line, flush=True)
+        results.append(row)
+    elapsed = dist.allreduce_max(time.perf_counter() - t0, ctx)
+    if ctx.is_root:
+        write_outputs(results, args)
+        if args.verbose:
+            print(f"decoded {args.frames * len(snr_points)} frames x2 (SCL + DL-SCL) on {ctx.world} GPU(s) in "
+                  f"{elapsed:.2f} s ({args.rng} channel)")
+    return results
+
+
+def write_outputs(results: List[Dict[str, float]], args: argparse.Namespace) -> None:
+    """CSV (run_fer_sweep.py:150-173) and semilogy plot (:175-191)."""
+    output_dir = Path(args.out_dir)
+    output_dir.mkdir(parents=True, exist_ok=True)
+    csv_path = output_dir / f"fer_M{args.M}.csv"
+    with csv_path.open("w") as f:
+        headers = ["snr_db"]
+        if args.include_uncoded:
+            headers.extend(["fer_uncoded", "ber_uncoded"])
+        headers.extend(["fer_scl", "ber_scl", "fer_dl", "ber_dl"])
+        f.write(",".join(headers) + "\n")
+        for row in results:
+            values = [f"{row['snr_db']:.3f}"]
+            if args.include_uncoded:
+                values.extend([f"{row['fer_uncoded']:.6e}", f"{row['ber_uncoded']:.6e}"])
+            values.extend([f"{row['fer_scl']:.6e}", f"{row['ber_scl']:.6e}", f"{row['fer_dl']:.6e}",
+                           f"{row['ber_dl']:.6e}"])
+            f.write(",".join(values) + "\n")
+    print(f"Saved FER table to {csv_path}")
+    if args.no_plot:
+        return
+    try:
+        import matplotlib
+
+        matplotlib.use("Agg")
+        import matplotlib.pyplot as plt
+    except ImportError:
+        print("matplotlib not available; skipping plot")
+        return
+    plot_dir = Path(args.plot_dir)
+    plot_dir.mkdir(parents=True, exist_ok=True)
+    plot_path = plot_dir / f"fer_M{args.M}.png"
+    plt.figure(figsize=(6, 4))
+    snrs = [row["snr_db"] for row in results]
+    if args.include_uncoded:
+        plt.semilogy(snrs, [row["fer_uncoded"] for row in results], "^-", label="Uncoded")
+    plt.semilogy(snrs, [row["fer_scl"] for row in results], "o-", label="SCL")
+    plt.semilogy(snrs, [row["fer_dl"] for row in results], "s-", label="DL-SCL")
+    plt.xlabel("Eb/N0 (dB)")
+    plt.ylabel("Frame Error Rate")
+    plt.grid(True, which="both", ls="--", alpha=0.4)
+    plt.legend()
+    plt.tight_layout()
+    plt.savefig(plot_path, dpi=200)
+    plt.close()
+    print(f"Saved FER plot to {plot_path}")
+
+
+def build_argparser() -> argparse.ArgumentParser:
+    parser = argparse.ArgumentParser(description="Run FER sweep for DL-SCL")
+    parser.add_argument("--M", type=int, required=True, help="List size")
+    parser.add_argument("--frames", type=int, default=10000, help="Frames per SNR point")
+    parser.add_argument("--snr_lo", type=float, default=4.0)
+    parser.add_argument("--snr_hi", type=float, default=6.5)
+    parser.add_argument("--snr_step", type=float, default=0.5)
+    parser.add_argument("--retries", type=int, default=8)
+    parser.add_argument("--beta", type=str, help="Path to trained beta matrix (.npy)")
+    parser.add_argument("--seed", type=int, default=0)
+    parser.add_argument("--out_dir", type=str, default="results")
+    parser.add_argument("--plot_dir", type=str, default="plots")
+    parser.add_argument("--include_uncoded", action="store_true", help="Also simulate an uncoded BPSK baseline")
+    # engine options (not in the reference)
+    parser.add_argument("--rng", choices=["replay", "philox"], default="replay",
+                        help="replay: reference NumPy stream (exact); philox: on-device generation")
+    parser.add_argument("--batch", type=int, default=1 << 16, help="frames per GPU batch")
+    parser.add_argument("--no_plot", action="store_true")
+    parser.add_argument("--verbose", action="store_true")
+    return parser
+
+
+def main(argv: List[str] | None = None) -> None:
+    args = build_argparser().parse_args(argv)
+    run_sweep(args)
+    dist.finalize()
+
+
+if __name__ == "__main__":
+    main()
