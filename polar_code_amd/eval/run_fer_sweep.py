@@ -82,13 +82,21 @@ def replay_stream(seed: int, snr_db: float, start: int, stop: int, payload_bits:
     return payload, msg, llr, llr_unc
 
 
-def _count_block(c, msg, llr, payload, llr_unc, info_set, M, crc, retries, beta, device):
+def scl_batch(llr, info_set, M, crc, device):
+    """Batched decode_scl on the GPU: best_path_bits [B, K] and CRC pass [B]."""
     dec = _native.get_decoder(llr.shape[1], info_set, M, crc, device)
-    base = dec.decode(llr, want_metrics=False, want_cands=False, want_info_llrs=False)
+    return dec.decode(llr, want_metrics=False, want_cands=False, want_info_llrs=False)
+
+
+dl_batch = decode_with_retries_batch
+
+
+def _count_block(c, msg, llr, payload, llr_unc, info_set, M, crc, retries, beta, device):
+    base = scl_batch(llr, info_set, M, crc, device)
     c[C_FRAMES] += llr.shape[0]
     c[C_SCL_ERR] += int(np.count_nonzero(~base["crc_pass"]))
     c[C_SCL_BIT] += int(np.count_nonzero(base["best_bits"] != msg))
-    dl = decode_with_retries_batch(llr, info_set, M, retries, crc=crc, beta=beta, device=device, baseline=base)
+    dl = dl_batch(llr, info_set, M, retries, crc=crc, beta=beta, device=device, baseline=base)
     c[C_DL_ERR] += int(np.count_nonzero(~dl["success"]))
     c[C_DL_BIT] += int(np.count_nonzero(dl["best_bits"] != msg))
     c[C_DL_WORK] += int((dl["attempts"] - 1).sum())
