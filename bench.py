@@ -71,17 +71,21 @@ def cpu_baseline(llr_host: np.ndarray, info, L: int, budget_s: float):
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle  # test/baseline infrastructure only
 
+    n0 = min(4000, llr_host.shape[0])
     t0 = time.perf_counter()
-    n0 = min(2000, llr_host.shape[0])
-    oracle.decode_batch(llr_host[:n0], info, L, POLY)
-    dt = time.perf_counter() - t0
-    n = int(min(llr_host.shape[0], max(n0, n0 * budget_s / max(dt, 1e-6))))
+    oracle.decode_batch(llr_host[:n0], info, L, POLY)  # warm-up / calibration
+    rate = n0 / max(time.perf_counter() - t0, 1e-6)
+    n = int(min(llr_host.shape[0], max(n0, rate * budget_s)))
+    done, dt = 0, 0.0
     t0 = time.perf_counter()
-    oracle.decode_batch(llr_host[:n], info, L, POLY)
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "frames/s", "cores": oracle.num_threads(), "kind": "port",
-            "sample": f"first {n} frames of the step-0 batch (same LLRs), oracle/scl_oracle.c decode_scl "
-                      f"L={L} + CRC select, OpenMP over frames, {dt:.1f} s"}
+    while dt < budget_s * 0.8 or done == 0:  # repeat the sample until the budget is spent
+        oracle.decode_batch(llr_host[:n], info, L, POLY)
+        done += n
+        dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "frames/s", "cores": oracle.num_threads(), "kind": "port",
+            "sample": f"{done} frame decodes ({n} distinct frames of the step-0 batch, same LLRs as the GPU) by "
+                      f"oracle/scl_oracle.c (C restatement of decode_scl) L={L} + CRC select, OpenMP over frames, "
+                      f"{dt:.1f} s"}
 
 
 def main():
@@ -157,7 +161,7 @@ def main():
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
-        host = llr[0][: min(B, 400_000)].cpu().numpy()
+        host = llr[0][: min(B, 1_000_000)].cpu().numpy()
         cpu = cpu_baseline(host, info, L, args.cpu_seconds)
 
     if rank == 0:
@@ -190,7 +194,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS,
                          "traffic": traffic,
-                         "kernel": "scl_decode_kernel", "avg_launch_ms": avg_ms, "launches": launches,
+                         "kernel": "scl128_kernel" if N == 128 and L <= 8 else "scl_decode_kernel", "avg_launch_ms": avg_ms, "launches": launches,
                          "bytes_per_frame": fb},
             "cpu_baseline": cpu,
             "fer": {"frames": int(c[0]), "frame_errors": int(c[1]), "fer": fer, "ber": c[2] / max(c[0] * K, 1),

@@ -45,6 +45,14 @@
 
 #define PSCL_EXP_TABLE_WORDS 256
 
+/* PSCL_ANY(c): true if c holds in any lane of the wavefront (wave-uniform branch on the
+ * device; plain c on the host).  Used to skip rarely needed branch-free sections. */
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PSCL_ANY(c) __any(c)
+#else
+#define PSCL_ANY(c) (c)
+#endif
+
 /* constants from glibc's __exp_data (N = 128) */
 #define PSCL_EXP_INVLN2N 0x1.71547652b82fep0 * 128.0
 #define PSCL_EXP_SHIFT 0x1.8p52
@@ -230,16 +238,19 @@ PSCL_HD double pscl_exp_neg(double x, const uint64_t* T) {
     /* main range */
     const double sc = pscl_asf64(sbits);
     const double ymain = pscl_fma(sc, tmp, sc);
-    /* 512 <= |x| < 1024, k < 0: glibc specialcase, rounded once into the subnormal range */
-    const double scale = pscl_asf64(sbits + (1022ULL << 52));
-    const double st = tmp * scale;
-    const double y0 = scale + st;
-    const double hi = y0 + 1.0;
-    const double lo = ((1.0 - hi) + y0) + ((scale - y0) + st);
-    double yr = (lo + hi) - 1.0;
-    yr = yr == 0.0 ? 0.0 : yr;
-    const double yspec = pscl_sel(y0 < 1.0, yr, y0) * 0x1p-1022;
-    double y = abstop == 0x408u ? yspec : ymain;
+    double y = ymain;
+    if (PSCL_ANY(abstop == 0x408u)) {
+        /* 512 <= |x| < 1024, k < 0: glibc specialcase, rounded once into the subnormal range */
+        const double scale = pscl_asf64(sbits + (1022ULL << 52));
+        const double st = tmp * scale;
+        const double y0 = scale + st;
+        const double hi = y0 + 1.0;
+        const double lo = ((1.0 - hi) + y0) + ((scale - y0) + st);
+        double yr = (lo + hi) - 1.0;
+        yr = yr == 0.0 ? 0.0 : yr;
+        const double yspec = pscl_sel(y0 < 1.0, yr, y0) * 0x1p-1022;
+        y = abstop == 0x408u ? yspec : ymain;
+    }
     y = abstop > 0x408u ? 0.0 : y;          /* |x| >= 1024 and -inf: underflow to +0 */
     y = abstop < 0x3c9u ? 1.0 + x : y;      /* |x| < 2^-54 and -0 */
     return y;

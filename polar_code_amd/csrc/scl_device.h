@@ -44,13 +44,21 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// f(a,b) = sign(a) sign(b) min(|a|,|b|)  (polar.py:122-123; exact, sign(0)=0 gives +-0)
+// f(a,b) = sign(a) sign(b) min(|a|,|b|)  (polar.py:122-123).  Exact: the result is one of the
+// inputs' magnitudes with the XOR of the signs (sign(0) = 0 makes a +-0 result either way, and
+// the sign of a zero never reaches a decision or a metric).  v_min_f64 + v_xor + v_bfi.
 __device__ __forceinline__ double f_minsum(double a, double b) {
-    double m = fmin(fabs(a), fabs(b));
-    return ((a < 0.0) != (b < 0.0)) ? -m : m;
+    const double m = fmin(fabs(a), fabs(b));
+    const uint64_t ab = pscl_asu64(a), bb = pscl_asu64(b), mb = pscl_asu64(m);
+    const uint32_t hi = (uint32_t)(mb >> 32) | (((uint32_t)(ab >> 32) ^ (uint32_t)(bb >> 32)) & 0x80000000u);
+    return pscl_asf64(((uint64_t)hi << 32) | (uint32_t)mb);
 }
-// g(a,b,c) = b + (1-2c) a  (polar.py:126-127; one rounding)
-__device__ __forceinline__ double g_node(double a, double b, uint32_t c) { return c ? b - a : b + a; }
+// g(a,b,c) = b + (1-2c) a  (polar.py:126-127): b + (+-a), one rounding, sign of a flipped by c
+__device__ __forceinline__ double g_node(double a, double b, uint32_t c) {
+    const uint64_t ab = pscl_asu64(a);
+    const uint32_t hi = (uint32_t)(ab >> 32) ^ (c << 31);
+    return b + pscl_asf64(((uint64_t)hi << 32) | (uint32_t)ab);
+}
 
 // Arikan transform of the low w bits of x (in-word, w <= 64): bit j ^= bit j+s for bit s of j
 // clear, for every stage s (stages commute).  Bits >= w must be zero.
@@ -76,7 +84,7 @@ __device__ __forceinline__ uint64_t pick_word(uint64_t w0, uint64_t w1, int idx)
 template <int G, int K>
 __device__ __forceinline__ uint32_t grot32c(uint32_t v, int lane) {
     if constexpr (G == 16) {
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + K, 0xF, 0xF, false);  // row_ror:K
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x120 + K, 0xF, 0xF, true);  // row_ror:K
     } else if constexpr (G == 8) {
         const uint32_t a = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + K, 0xF, 0xF, false);
         const uint32_t b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + K + 8, 0xF, 0xF, false);
@@ -102,9 +110,30 @@ __device__ __forceinline__ double grot64c(double v, int lane) {
 // metrics are sums of non-negative increments, never -0 or NaN, and +inf marks an empty
 // candidate, so their IEEE bit patterns order like unsigned integers and the whole key
 // compares as one 96-bit unsigned number (hi word, lo word, t) with a borrow chain.
+// One rank rotation for 16-lane groups, hand-scheduled: the 96-bit subtract (lane g-K minus
+// lane g) runs as three DPP-fused VOP2 subtracts chained through VCC, and the final borrow
+// (= "that key is smaller") is added into r.  4 VALU, no SGPR masks.  The leading s_nop covers
+// the VALU-write -> DPP-read hazard on the key registers (inline asm is not hazard-checked).
+template <int K>
+__device__ __forceinline__ void rank_rot16(uint32_t mh, uint32_t ml, uint32_t t, uint32_t& r) {
+    uint32_t tmp;
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_sub_co_u32_dpp %0, vcc, %2, %2 row_ror:%5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_subb_co_u32_dpp %0, vcc, %3, %3, vcc row_ror:%5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_subb_co_u32_dpp %0, vcc, %4, %4, vcc row_ror:%5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_addc_co_u32 %1, vcc, 0, %1, vcc"
+        : "=&v"(tmp), "+v"(r)
+        : "v"(t), "v"(ml), "v"(mh), "i"(K)
+        : "vcc");
+}
+
 template <int G, int K>
 __device__ __forceinline__ void rank_step(uint32_t mh, uint32_t ml, uint32_t t, int lane, uint32_t& r) {
-    if constexpr (K < G) {
+    if constexpr (G == 16 && K < G) {
+        rank_rot16<K>(mh, ml, t, r);
+        rank_step<G, K + 1>(mh, ml, t, lane, r);
+    } else if constexpr (K < G) {
         const uint32_t th = grot32c<G, K>(t, lane);
         const uint32_t lh = grot32c<G, K>(ml, lane);
         const uint32_t hh = grot32c<G, K>(mh, lane);
@@ -121,7 +150,10 @@ __device__ __forceinline__ void rank_step(uint32_t mh, uint32_t ml, uint32_t t, 
 // every other key of interest)
 template <int G, int K, int KEND>
 __device__ __forceinline__ void rank_step_n(uint32_t mh, uint32_t ml, uint32_t t, int lane, uint32_t& r) {
-    if constexpr (K < KEND) {
+    if constexpr (G == 16 && K < KEND) {
+        rank_rot16<K>(mh, ml, t, r);
+        rank_step_n<G, K + 1, KEND>(mh, ml, t, lane, r);
+    } else if constexpr (K < KEND) {
         const uint32_t th = grot32c<G, K>(t, lane);
         const uint32_t lh = grot32c<G, K>(ml, lane);
         const uint32_t hh = grot32c<G, K>(mh, lane);

@@ -18,7 +18,7 @@ def load(d):
     agg = collections.defaultdict(list)
     for f in sorted(Path(d).glob("p*/pmc_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if "scl_decode_kernel" in r["Kernel_Name"]:
+            if "scl_decode_kernel" in r["Kernel_Name"] or "scl128_kernel" in r["Kernel_Name"]:
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
