@@ -151,6 +151,16 @@ int pscl_decode_device(pscl_handle* h, const double* d_llr, int64_t B, const uin
 int pscl_channel_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate,
                         int k_payload, int64_t frame0, int64_t B, double* d_llr, uint64_t* d_msg);
 
+/*
+ * NR rate matching (dl_scl_polar/nr/polar/*): after this call the handle's decode entry
+ * points take E received LLRs per frame ([B][E]) and run decode_rate_matched_scl's front end
+ * (scl_nr.py:38-57) inside the decode kernel: de-rate-match (rate_match.py:19-39, repeats
+ * averaged; E <= N pads with -1.0) then sub-block de-interleave (interleaver.py:26-37).
+ * pscl_channel_device then transmits the interleaved, repeated codeword (scl_nr.py:23-35).
+ * E = 0 switches rate matching off.  Repetition (E > N) needs N >= 32.
+ */
+int pscl_set_rate_match(pscl_handle* h, int E);
+
 /* Device scratch helpers so that non-torch callers can drive the device path. */
 int pscl_device_alloc(pscl_handle* h, void** d_ptr, int64_t bytes);
 int pscl_device_free(pscl_handle* h, void* d_ptr);

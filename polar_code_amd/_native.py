@@ -37,7 +37,7 @@ EXPORTS = (
     "pscl_set_stream", "pscl_get_stream", "pscl_sync", "pscl_decode", "pscl_sc_decode",
     "pscl_decode_device", "pscl_channel_device", "pscl_device_alloc", "pscl_device_free",
     "pscl_memcpy_htod", "pscl_memcpy_dtoh", "pscl_memset_device", "pscl_timing_enable",
-    "pscl_timing_read", "pscl_launch_info",
+    "pscl_timing_read", "pscl_launch_info", "pscl_set_rate_match",
 )
 
 _vp, _i32, _i64, _u64, _dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
@@ -92,6 +92,7 @@ def lib() -> C.CDLL:
         "pscl_timing_enable": (C.c_int, [_vp, C.c_int]),
         "pscl_timing_read": (C.c_int, [_vp, P(_i64), P(_dbl)]),
         "pscl_launch_info": (C.c_int, [_vp, _i64, P(C.c_int), P(_i64), P(C.c_int)]),
+        "pscl_set_rate_match": (C.c_int, [_vp, C.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -155,6 +156,12 @@ class Decoder:
                                 self.L, self.crc_poly))
         self._h = h
         self._lock = threading.Lock()
+        self.E = 0
+
+    def set_rate_match(self, E: int) -> None:
+        """NR: decode inputs become [B, E] received LLRs (de-rate-match + de-interleave on GPU)."""
+        check(lib().pscl_set_rate_match(self._h, int(E)))
+        self.E = int(E)
 
     @property
     def handle(self):
@@ -179,8 +186,9 @@ class Decoder:
         if llr.ndim == 1:
             llr = llr[None, :]
         B = llr.shape[0]
-        if llr.shape[1] != self.N:
-            raise ValueError("Channel LLR length must be a power of two")
+        if llr.shape[1] != (self.E or self.N):
+            raise ValueError("Channel LLR length must be a power of two" if not self.E
+                             else f"expected {self.E} rate-matched LLRs per frame")
         if forced is not None:
             forced = np.ascontiguousarray(forced, dtype=np.int8).reshape(B, self.K)
         out = {
@@ -245,16 +253,18 @@ _CACHE: dict = {}
 _CACHE_LOCK = threading.Lock()
 
 
-def get_decoder(N: int, info_set, L: int, crc=None, device: int = 0) -> Decoder:
-    """Cached Decoder per (N, info set, L, CRC, device): decode_scl is called per frame."""
+def get_decoder(N: int, info_set, L: int, crc=None, device: int = 0, E: int = 0) -> Decoder:
+    """Cached Decoder per (N, info set, L, CRC, device, rate-matched length E)."""
     info = np.asarray(info_set).astype(np.int64).ravel()
-    key = (int(N), info.tobytes(), int(L), poly_value(crc), int(device))
+    key = (int(N), info.tobytes(), int(L), poly_value(crc), int(device), int(E))
     with _CACHE_LOCK:
         dec = _CACHE.get(key)
         if dec is None:
             if len(_CACHE) > 64:
                 _CACHE.clear()
             dec = Decoder(N, info, L, crc, device)
+            if E:
+                dec.set_rate_match(E)
             _CACHE[key] = dec
         return dec
 

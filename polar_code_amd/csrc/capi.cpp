@@ -87,6 +87,9 @@ struct pscl_handle {
     uint32_t* d_attach_cols = nullptr;
     int32_t* d_info_set = nullptr;
     uint64_t* d_exp_table = nullptr;
+    int rm_E = 0;                     // NR rate matching (0 = off)
+    int32_t* d_rm_src = nullptr;      // [N] de-interleave gather index
+    int32_t* d_rm_order = nullptr;    // [N] interleaver order
     DevBuf scratch[12];
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
@@ -127,6 +130,8 @@ void fill_decode_params(const pscl_handle* h, pscl_decode_params& P, int hist) {
     P.info_set = h->d_info_set;
     P.has_crc = h->crc_poly != 0;
     P.exp_table = h->d_exp_table;
+    P.rm_E = h->rm_E;
+    P.rm_src = h->d_rm_src;
     pscl_decode_layout(P, hist);
 }
 
@@ -260,6 +265,8 @@ int pscl_destroy(pscl_handle* h) {
     if (h->d_attach_cols) hipFree(h->d_attach_cols);
     if (h->d_info_set) hipFree(h->d_info_set);
     if (h->d_exp_table) hipFree(h->d_exp_table);
+    if (h->d_rm_src) hipFree(h->d_rm_src);
+    if (h->d_rm_order) hipFree(h->d_rm_order);
     if (h->own_stream) hipStreamDestroy(h->own_stream);
     delete h;
     return PSCL_OK;
@@ -336,7 +343,7 @@ static int decode_host(pscl_handle* h, const double* llr, int64_t B, const int8_
     int rc = set_device(h);
     if (rc) return rc;
     void *d_llr, *d_force = nullptr, *d_np, *d_best, *d_flags, *d_met = nullptr, *d_cands = nullptr, *d_illr = nullptr;
-    const size_t sz_llr = (size_t)B * N * 8;
+    const size_t sz_llr = (size_t)B * (h->rm_E ? h->rm_E : N) * 8;
     if ((rc = ensure(h, 0, sz_llr, &d_llr))) return rc;
     if (forced && (rc = ensure(h, 1, hforce.size() * 8, &d_force))) return rc;
     if ((rc = ensure(h, 2, (size_t)B * 4, &d_np))) return rc;
@@ -435,8 +442,35 @@ int pscl_channel_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, doubl
     P.B = B;
     P.llr = d_llr;
     P.msg = d_msg;
+    P.rm_E = h->rm_E;
+    P.rm_order = h->d_rm_order;
     hipError_t e = pscl_launch_channel(P, h->stream);
     if (e != hipSuccess) return fail(PSCL_EDEVICE, "channel kernel launch: %s", hipGetErrorString(e));
+    return PSCL_OK;
+}
+
+int pscl_set_rate_match(pscl_handle* h, int E) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    if (E < 0) return fail(PSCL_EINVAL, "E must be >= 0");
+    if (E == 0) {
+        h->rm_E = 0;
+        return PSCL_OK;
+    }
+    const int N = h->N;
+    if (E > N && N < 32)
+        return fail(PSCL_EUNSUP, "repetition (E > N) needs N >= 32 (sub-block interleaver without padding)");
+    // interleaver.py:10-37: order[k] = (k % 32) * nb + k / 32 over nb*32 positions (identity when N < 32)
+    std::vector<int32_t> order((size_t)N), src((size_t)N);
+    const int nb = (N + 31) / 32;
+    for (int k = 0; k < N; ++k) order[(size_t)k] = N >= 32 ? (k % 32) * nb + k / 32 : k;
+    for (int k = 0; k < N; ++k) src[(size_t)order[(size_t)k]] = k;
+    int rc = set_device(h);
+    if (rc) return rc;
+    if (!h->d_rm_src) HIP_TRY(hipMalloc(&h->d_rm_src, (size_t)N * 4));
+    if (!h->d_rm_order) HIP_TRY(hipMalloc(&h->d_rm_order, (size_t)N * 4));
+    HIP_TRY(hipMemcpy(h->d_rm_src, src.data(), (size_t)N * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(h->d_rm_order, order.data(), (size_t)N * 4, hipMemcpyHostToDevice));
+    h->rm_E = E;
     return PSCL_OK;
 }
 

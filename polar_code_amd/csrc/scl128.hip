@@ -116,10 +116,13 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64) scl128_kernel(cons
     for (int64_t f0 = ((int64_t)blockIdx.x * wpg + wave) * F; f0 < P.B; f0 += wstride) {
         const int64_t f = f0 + fl;
         const bool fvalid = f < P.B;
-        {
+        if (P.rm_E == 0) {
             const double* src = P.llr + (fvalid ? f : f0) * kN;
 #pragma unroll
             for (int x = 0; x < kN / G; ++x) Af[g + x * G] = src[g + x * G];
+        } else {  // NR: de-rate-match + de-interleave while staging
+            const double* src = P.llr + (fvalid ? f : f0) * P.rm_E;
+            for (int x = 0; x < kN / G; ++x) Af[g + x * G] = nr_stage(src, P.rm_src[g + x * G], P.rm_E, kN);
         }
         uint64_t fm0 = 0, fm1 = 0, fv0 = 0, fv1 = 0;
         if (P.force && fvalid) {

@@ -211,6 +211,23 @@ __device__ __forceinline__ uint64_t from_upper_half64(uint64_t v, int lane) {
            from_upper_half<G, LMAX>((uint32_t)v, lane);
 }
 
+// Internal LLR i of an NR rate-matched frame (nr/polar/scl_nr.py:47-48): de-rate-match
+// (rate_match.py:19-39: repeats averaged in numpy's order, E <= N padded with -1.0) then
+// sub-block de-interleave (interleaver.py:26-37), as one gather from the E received LLRs.
+__device__ __forceinline__ double nr_stage(const double* src, int k, int E, int N) {
+    if (E <= N) return k < E ? src[k] : -1.0;
+    const int reps = E / N, rem = E - reps * N;
+    double s = src[k];
+    for (int r = 1; r < reps; ++r) s = s + src[k + r * N];
+    s = 0.0 + s;
+    int cnt = reps;
+    if (k < rem) {
+        s = s + src[reps * N + k];
+        ++cnt;
+    }
+    return s / (double)cnt;
+}
+
 // error counters of one decoded frame (run_fer_sweep.py:91-109, run_ber_sweep.py:77-82,156)
 __device__ __forceinline__ void count_errors(int64_t* counters, uint64_t ib0, uint64_t ib1, uint64_t r0, uint64_t r1,
                                              int k_payload, bool pass) {

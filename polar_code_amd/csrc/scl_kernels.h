@@ -26,6 +26,8 @@ struct pscl_decode_params {
     double* metrics;             // [B][L] or null
     uint64_t* cands;             // [B][L][W] or null
     double* info_llrs;           // [B][L][K] or null (needs the HIST kernel)
+    int rm_E;                    // NR rate matching: received length E (0 = none; llr is [B][E])
+    const int32_t* rm_src;       // [N] de-interleave source index k(i) into the de-rate-matched vector
     const uint64_t* ref;         // [B][W] or null
     int k_payload;
     int64_t* counters;           // [PSCL_NCOUNT] (device)
@@ -42,8 +44,10 @@ struct pscl_channel_params {
     const uint32_t* attach_cols; // [k_payload] CRC remainder columns (device)
     double sigma, noise_var;
     int64_t frame0, B;
-    double* llr;                 // [B][N]
+    double* llr;                 // [B][N] (or [B][E] with rate matching)
     uint64_t* msg;               // [B][W] or null
+    int rm_E;                    // NR: transmit E symbols, symbol p = x[rm_order[p % N]]
+    const int32_t* rm_order;     // [N] sub-block interleaver order
 };
 
 int pscl_decode_lmax(int L);

@@ -68,9 +68,12 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
     for (int64_t f0 = ((int64_t)blockIdx.x * wpg + wave) * F; f0 < P.B; f0 += wstride) {
         const int64_t f = f0 + fl;
         const bool fvalid = f < P.B;
-        {  // stage this frame's channel LLRs in LDS (coalesced; read at every depth-1 use)
+        if (P.rm_E == 0) {  // stage this frame's channel LLRs in LDS (read at every depth-1 use)
             const double* src = P.llr + (fvalid ? f : f0) * N;
             for (int x = g; x < N; x += G) Af[x] = src[x];
+        } else {  // NR: de-rate-match + de-interleave while staging
+            const double* src = P.llr + (fvalid ? f : f0) * P.rm_E;
+            for (int x = g; x < N; x += G) Af[x] = nr_stage(src, P.rm_src[x], P.rm_E, N);
         }
         wave_lds_fence();
         const double* ch = Af;
@@ -358,23 +361,28 @@ __global__ void __launch_bounds__(256) channel_kernel(const pscl_channel_params 
             P.msg[idx * P.W] = m0;
             if (P.W > 1) P.msg[idx * P.W + 1] = m1;
         }
-        // AWGN: lane handles positions lane and lane+64 with one Box-Muller pair
-        const u32x4 rn = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), (uint32_t)lane, 0u}, k0, k1);
-        const uint64_t a = ((uint64_t)rn.y << 32) | rn.x, bb = ((uint64_t)rn.w << 32) | rn.z;
-        const double uu1 = ((double)(a >> 11) + 1.0) * 0x1p-53;  // (0, 1]
-        const double uu2 = (double)(bb >> 11) * 0x1p-53;         // [0, 1)
-        const double rad = sqrt(-2.0 * log(uu1));
-        double sn, cs;
-        sincospi(2.0 * uu2, &sn, &cs);
-        const double z[2] = {rad * cs, rad * sn};
+        // AWGN: each lane handles symbols (lane + 128 q) and (lane + 64 + 128 q) with one
+        // Box-Muller pair per q; NR transmits E symbols, symbol p = x[order[p % N]]
+        const int E = P.rm_E ? P.rm_E : P.N;
+        for (int q = 0; q * 128 < E; ++q) {
+            const u32x4 rn = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), (uint32_t)(lane + 64 * q), 0u}, k0, k1);
+            const uint64_t a = ((uint64_t)rn.y << 32) | rn.x, bb = ((uint64_t)rn.w << 32) | rn.z;
+            const double uu1 = ((double)(a >> 11) + 1.0) * 0x1p-53;  // (0, 1]
+            const double uu2 = (double)(bb >> 11) * 0x1p-53;         // [0, 1)
+            const double rad = sqrt(-2.0 * log(uu1));
+            double sn, cs;
+            sincospi(2.0 * uu2, &sn, &cs);
+            const double z[2] = {rad * cs, rad * sn};
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int pos = lane + 64 * h;
-            if (pos < P.N) {
-                const uint64_t xw = pos < 64 ? x0 : x1;
-                const double sym = ((xw >> (pos & 63)) & 1) ? -1.0 : 1.0;
-                const double received = sym + P.sigma * z[h];
-                P.llr[idx * P.N + pos] = 2.0 * received / P.noise_var;
+            for (int h = 0; h < 2; ++h) {
+                const int p = lane + 64 * h + 128 * q;
+                if (p < E) {
+                    const int pos = P.rm_E ? P.rm_order[p % P.N] : p;
+                    const uint64_t xw = pos < 64 ? x0 : x1;
+                    const double sym = ((xw >> (pos & 63)) & 1) ? -1.0 : 1.0;
+                    const double received = sym + P.sigma * z[h];
+                    P.llr[idx * E + p] = 2.0 * received / P.noise_var;
+                }
             }
         }
     }

@@ -243,7 +243,47 @@ def g9():
     np.savez_compressed(OUT / "g9_sc.npz", info=info, llr=llr, bits=out)
 
 
+BER_CONFIGS = {
+    "ber_polar_small": ["--scheme", "polar_scl", "--K_payload", "8", "--K_crc", "4", "--E", "16", "--crc_poly", "0x17",
+                        "--M", "2", "--EbN0_lo", "6.0", "--EbN0_hi", "6.0", "--EbN0_step", "0.5", "--bits_cap", "64",
+                        "--err_cap", "2"],
+    "ber_polar_128": ["--scheme", "polar_scl", "--K_payload", "40", "--K_crc", "24", "--E", "128", "--M", "4",
+                      "--EbN0_lo", "6.0", "--EbN0_hi", "7.0", "--EbN0_step", "0.5", "--bits_cap", "24000",
+                      "--err_cap", "100", "--seed", "3"],
+    "ber_dl_128": ["--scheme", "dl_scl", "--K_payload", "40", "--K_crc", "24", "--E", "128", "--M", "4",
+                   "--retries", "8", "--beta", "BETA4", "--EbN0_lo", "6.0", "--EbN0_hi", "6.0", "--bits_cap", "8000",
+                   "--err_cap", "60", "--seed", "4"],
+    "ber_nr_256": ["--scheme", "nr_polar_scl", "--K_payload", "64", "--K_crc", "24", "--E", "256", "--N", "128",
+                   "--M", "8", "--EbN0_lo", "4.0", "--EbN0_hi", "4.5", "--EbN0_step", "0.5", "--bits_cap", "9600",
+                   "--err_cap", "100", "--seed", "5"],
+    "ber_nr_small": ["--scheme", "nr_polar_scl", "--K_payload", "8", "--K_crc", "4", "--E", "16", "--N", "16",
+                     "--M", "2", "--EbN0_lo", "5.0", "--EbN0_hi", "5.0", "--bits_cap", "64", "--err_cap", "2",
+                     "--crc_poly", "0x17"],
+}
+
+
+def g11():
+    """run_ber_sweep rows (CSV text) for several configurations (stop rule, shared stream)."""
+    from dl_scl_polar.eval import run_ber_sweep as rb
+    import tempfile
+
+    d = {}
+    for name, argv in BER_CONFIGS.items():
+        argv = [str(REF / "checkpoints" / "beta_M4.npy") if a == "BETA4" else a for a in argv]
+        with tempfile.TemporaryDirectory() as td:
+            out = Path(td) / "x.csv"
+            rows = rb.run(rb.parse_args(argv + ["--out", str(out)]))
+            rb.write_csv(rows, out)
+            d[name] = np.array(out.read_text())
+        d[name + "_argv"] = np.array(" ".join(BER_CONFIGS[name]))
+    np.savez_compressed(OUT / "g11_ber.npz", **d)
+
+
 def main():
+    if len(sys.argv) > 1:
+        for name in sys.argv[1:]:
+            globals()[name]()
+        return
     g1()
     g2()
     g3()
@@ -261,6 +301,7 @@ def main():
     decode_set("g10_n8", 8, 6, [2, 4], [2.0], 12, seed=15, crc="0x5")
     decode_set("g10_n4", 4, 3, [1, 2, 3], [1.0], 12, seed=16, crc=None)
     decode_set("g10_n2", 2, 1, [1, 2], [0.0], 12, seed=17, crc=None)
+    g11()
     for p in sorted(OUT.glob("*.npz")):
         print(p.name, p.stat().st_size)
 
