@@ -95,20 +95,27 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one process per GPU; PSCL_SHARE_GPU=1 lets a rehearsal put several ranks on fewer GPUs
+    ndev = torch.cuda.device_count()
+    device_index = local % ndev if os.environ.get("PSCL_SHARE_GPU") == "1" else local
+    torch.cuda.set_device(device_index)
+    dev = torch.device("cuda", device_index)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group(backend="nccl", device_id=dev)
+        backend = os.environ.get("PSCL_DIST_BACKEND", "nccl")  # nccl == RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend=backend)
 
     from polar_code_amd import _native
     from polar_code_amd.polar.polar import construct_info_set
 
     N, K, L, B = 128, 64, args.list, args.frames
     info = construct_info_set(N, K)
-    dec = _native.Decoder(N, info, L, POLY, device=local)
+    dec = _native.Decoder(N, info, L, POLY, device=device_index)
     stream = torch.cuda.current_stream(dev)
     dec.set_stream(stream.cuda_stream)
     W = dec.W
@@ -151,8 +158,10 @@ def main():
     launches, kern_ms = dec.timing_read()
     dec.timing_enable(False)
 
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    red_dev = dev if (dist is None or dist.get_backend() == "nccl") else torch.device("cpu")
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
     if dist:
+        counters = counters.to(red_dev)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(counters, op=dist.ReduceOp.SUM)
     elapsed = float(tmax.item())
