@@ -66,6 +66,24 @@ def load_traffic(workload_key: str):
         return None
 
 
+def load_valu_profile(workload_key: str):
+    """(VALU wave-instructions per frame, VALU-active fraction) of the decode kernel for this
+    workload, from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json)."""
+    p = ROOT / "profiles" / "pmc_traffic.json"
+    if not p.exists():
+        return None
+    try:
+        e = json.loads(p.read_text()).get(workload_key) or {}
+        return (float(e["valu_instr_per_frame"]), e.get("valu_active_frac")) if "valu_instr_per_frame" in e else None
+    except Exception:
+        return None
+
+
+# VALU issue peak of MI355X: 256 CUs x 4 SIMDs x 2.4 GHz; a wave64 f32/int VALU instruction
+# takes 2 cycles on a SIMD-32, an fp64 add/mul/fma 4 (MI355X_MICROARCH.md constants table)
+SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
+
+
 def cpu_baseline(llr_host: np.ndarray, info, L: int, budget_s: float):
     """The oracle (C restatement of the reference, OpenMP over frames) on host cores."""
     sys.path.insert(0, str(ROOT / "oracle"))
@@ -179,6 +197,17 @@ def main():
         achieved = fb * B / (avg_ms * 1e-3) / 1e9
         wkey = f"scl_L{L}_N{N}_K{K}_B{B}"
         traffic = load_traffic(wkey)
+        vp = load_valu_profile(wkey)
+        compute = None
+        if vp is not None:
+            rate = vp[0] * B / (avg_ms * 1e-3)
+            peak32, peak64 = SIMDS * CLOCK_HZ / 2, SIMDS * CLOCK_HZ / 4
+            compute = {"bound": "valu-issue", "unit": "wave-instr/s", "instr_per_frame": vp[0],
+                       "achieved": rate, "peak_f32_issue": peak32, "peak_f64_issue": peak64,
+                       "frac_of_f32_issue": rate / peak32, "frac_of_f64_issue": rate / peak64,
+                       "valu_active_frac_pmc": vp[1],
+                       "note": "instr/frame from SQ_INSTS_VALU (profiles/pmc_traffic.json) x live frames/s; the "
+                               "mix is fp64 (4 cyc) and int/f32 (2 cyc) ops, so the true issue peak lies between"}
         fer = c[1] / max(c[0], 1)
         p0 = REF_FER_L8[0] / REF_FER_L8[1]
         pp = (c[1] + REF_FER_L8[0]) / (c[0] + REF_FER_L8[1])
@@ -204,7 +233,7 @@ def main():
                          "frac": achieved / PEAK_HBM_GBS,
                          "traffic": traffic,
                          "kernel": "scl128_kernel" if N == 128 and L <= 8 else "scl_decode_kernel", "avg_launch_ms": avg_ms, "launches": launches,
-                         "bytes_per_frame": fb},
+                         "bytes_per_frame": fb, "compute": compute},
             "cpu_baseline": cpu,
             "fer": {"frames": int(c[0]), "frame_errors": int(c[1]), "fer": fer, "ber": c[2] / max(c[0] * K, 1),
                     "reference_fer": p0, "z_vs_reference": (fer - p0) / se},

@@ -264,31 +264,30 @@ PSCL_HD double pscl_log1p_unit(double y) {
                  Lp5 = 1.818357216161805012e-01, Lp6 = 1.531383769920937332e-01,
                  Lp7 = 1.479819860511658591e-01;
     const int32_t hx = (int32_t)(pscl_asu64(y) >> 32);
-    const bool kp = hx >= 0x3FDA827A;  /* 1 + y >= sqrt(2): reduce through u = 1 + y */
-    /* u = 1 + y path (k in {0, 1} before normalisation) */
-    const double u = 1.0 + y;
-    const int32_t hu0 = (int32_t)(pscl_asu64(u) >> 32);
-    int32_t ku = (hu0 >> 20) - 1023;
-    double cu = (ku > 0) ? 1.0 - (u - y) : y - (u - 1.0);
-    cu = cu / u;
-    int32_t hum = hu0 & 0x000fffff;
-    const uint64_t ulo = pscl_asu64(u) & 0xffffffffULL;
-    const bool big = hum >= 0x6a09e;
-    const double un = pscl_asf64(((uint64_t)(uint32_t)(hum | (big ? 0x3fe00000 : 0x3ff00000)) << 32) | ulo);
-    ku += big ? 1 : 0;
-    hum = big ? ((0x00100000 - hum) >> 2) : hum;
-    /* select the reduction */
-    const int32_t k = kp ? ku : 0;
-    const double c = kp ? cu : 0.0;
-    const int32_t hu = kp ? hum : 1;
-    const double f = kp ? un - 1.0 : y;
-    const double kd = (double)k;
+    /* y < 2^-29 (tiny metric tails, |llr| > ~20): x - x*x/2, or x below 2^-54 */
+    const double tiny = hx < 0x3c900000 ? y : y - (y * y) * 0.5;
+    if (!PSCL_ANY(hx >= 0x3e200000)) return tiny;
+    const bool kp = hx >= 0x3FDA827A; /* 1 + y >= sqrt(2): reduce through u = 1 + y */
+    int32_t k = 0, hu = 1;
+    double c = 0.0, f = y;
+    if (PSCL_ANY(kp)) {
+        const double u = 1.0 + y;
+        const int32_t hu0 = (int32_t)(pscl_asu64(u) >> 32);
+        int32_t ku = (hu0 >> 20) - 1023;
+        double cu = (ku > 0) ? 1.0 - (u - y) : y - (u - 1.0);
+        cu = cu / u;
+        int32_t hum = hu0 & 0x000fffff;
+        const uint64_t ulo = pscl_asu64(u) & 0xffffffffULL;
+        const bool big = hum >= 0x6a09e;
+        const double un = pscl_asf64(((uint64_t)(uint32_t)(hum | (big ? 0x3fe00000 : 0x3ff00000)) << 32) | ulo);
+        ku += big ? 1 : 0;
+        hum = big ? ((0x00100000 - hum) >> 2) : hum;
+        k = kp ? ku : 0;
+        c = kp ? cu : 0.0;
+        hu = kp ? hum : 1;
+        f = kp ? un - 1.0 : y;
+    }
     const double hfsq = (0.5 * f) * f;
-    /* |f| < 2^-20 (hu == 0) */
-    const double R0 = (1.0 - 0.66666666666666666 * f) * hfsq;
-    const double a_f0 = k == 0 ? 0.0 : (kd * ln2_lo + c) + kd * ln2_hi;
-    const double a_nz = k == 0 ? f - R0 : kd * ln2_hi - ((R0 - (kd * ln2_lo + c)) - f);
-    const double a = f == 0.0 ? a_f0 : a_nz;
     /* general case */
     const double s = f / (2.0 + f);
     const double z = s * s;
@@ -297,11 +296,22 @@ PSCL_HD double pscl_log1p_unit(double y) {
     const double z6 = z2 * z4;
     const double R = ((z * Lp1 + z2 * (z * Lp3 + Lp2)) + z4 * (z * Lp5 + Lp4)) + z6 * (z * Lp7 + Lp6);
     const double sR = (R + hfsq) * s;
-    const double bres = k == 0 ? f - (hfsq - sR) : kd * ln2_hi - ((hfsq - ((kd * ln2_lo + c) + sR)) - f);
-    double res = hu == 0 ? a : bres;
-    res = hx < 0x3e200000 ? y - (y * y) * 0.5 : res; /* y < 2^-29 */
-    res = hx < 0x3c900000 ? y : res;                 /* y < 2^-54, subnormals, 0 */
-    return res;
+    double res = f - (hfsq - sR);
+    if (PSCL_ANY(k != 0)) {
+        const double kd = (double)k;
+        const double bk = kd * ln2_hi - ((hfsq - ((kd * ln2_lo + c) + sR)) - f);
+        res = k == 0 ? res : bk;
+        if (PSCL_ANY(hu == 0)) { /* |f| < 2^-20 */
+            const double R0 = (1.0 - 0.66666666666666666 * f) * hfsq;
+            const double a_f0 = k == 0 ? 0.0 : (kd * ln2_lo + c) + kd * ln2_hi;
+            const double a_nz = k == 0 ? f - R0 : kd * ln2_hi - ((R0 - (kd * ln2_lo + c)) - f);
+            res = hu == 0 ? (f == 0.0 ? a_f0 : a_nz) : res;
+        }
+    } else if (PSCL_ANY(hu == 0)) { /* k == 0 with |f| < 2^-20 */
+        const double R0 = (1.0 - 0.66666666666666666 * f) * hfsq;
+        res = hu == 0 ? (f == 0.0 ? 0.0 : f - R0) : res;
+    }
+    return hx < 0x3e200000 ? tiny : res;
 }
 
 /* branch-free L = log1p(exp(-|v|)) (identical to pscl_softplus_tail for finite v and +-inf) */

@@ -86,7 +86,7 @@ __device__ __forceinline__ void step_depth(double* A, int lane, uint32_t tab, ui
 }
 
 template <int LMAX, bool HIST>
-__global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64) scl128_kernel(const pscl_decode_params P) {
+__global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(const pscl_decode_params P) {
     using Ly = Layout128<LMAX>;
     constexpr int G = Ly::G, F = Ly::F, LOG_G = Ly::LOG_G;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -149,12 +149,20 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64) scl128_kernel(cons
             const uint64_t infow = phi < 64 ? info0 : info1;
             const bool is_info = (infow >> (phi & 63)) & 1;
             // ---- depths 1-3 recomputed from the channel (phi % 16 == 0)
-            if (start <= 3) {
+            if (start <= 3 && !(PSCL_ABLATE & 4)) {
                 const bool r1 = phi >= 64, r2 = (phi >> 5) & 1, r3 = (phi >> 4) & 1;
                 // path lanes: partial sums of the left siblings at depths 1, 2, 3
-                const uint64_t X1 = r1 ? polar_transform64(u0) : 0;
-                const uint32_t X2 = r2 ? (uint32_t)seg_transform(u0, u1, phi - (phi & 31) - 32, 32) : 0u;
-                const uint32_t X3 = r3 ? (uint32_t)seg_transform(u0, u1, phi - 16, 16) : 0u;
+                uint64_t X1 = 0;
+                uint32_t X2 = 0, X3 = 0;
+                if (r1) X1 = polar_transform64(u0);
+                if (r2) {  // u[32(k2-1), 32 k2), k2 = phi >> 5 odd
+                    const int lo = phi - (phi & 31) - 32;
+                    X2 = polar_transform32((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)));
+                }
+                if (r3) {  // u[phi-16, phi)
+                    const int lo = phi - 16;
+                    X3 = polar_transform16((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)) & 0xffffu);
+                }
 #pragma unroll
                 for (int q = 0; q < 16 / G + (G > 16); ++q) {
                     const int e = g + G * q;
@@ -188,10 +196,15 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64) scl128_kernel(cons
             }
             // ---- depths 4..6 (partial sums of the g node's left sibling: xs, <= 8 bits)
             uint32_t xs = 0;
-            if (phi && start >= 4 && start <= 6) xs = (uint32_t)seg_transform(u0, u1, phi - (1 << (kn - start)), 1 << (kn - start));
-            if (start <= 4) step_depth<LMAX, 4>(A, lane, tab, xs, start == 4, start == 4 && phi);
-            if (start <= 5) step_depth<LMAX, 5>(A, lane, tab, xs, start == 5, start == 5);
-            if (start <= 6) step_depth<LMAX, 6>(A, lane, tab, xs, start == 6, start == 6);
+            if (phi && start >= 4 && start <= 6) {  // u[phi-w, phi), w = 8, 4, 2
+                const int w = 1 << (kn - start), lo = phi - w;
+                xs = polar_transform8((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)) & ((1u << w) - 1u));
+            }
+            if (!(PSCL_ABLATE & 4)) {
+                if (start <= 4) step_depth<LMAX, 4>(A, lane, tab, xs, start == 4, start == 4 && phi);
+                if (start <= 5) step_depth<LMAX, 5>(A, lane, tab, xs, start == 5, start == 5);
+                if (start <= 6) step_depth<LMAX, 6>(A, lane, tab, xs, start == 6, start == 6);
+            }
             if (start <= 6) {
                 const int s0 = start < 3 ? 3 : start;
                 uint32_t mask = 0, val = 0;
@@ -219,8 +232,10 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64) scl128_kernel(cons
             const bool frozen_even = !is_info && !(phi & 1);
             Lpre = Lt;
             pre_ok = frozen_even;
-            const double m0 = metric + pscl_logaddexp0(-lam, Lt);
-            const double m1 = metric + pscl_logaddexp0(lam, Lt);
+            double i0, i1;
+            metric_incr(lam, Lt, i0, i1);
+            const double m0 = metric + i0;
+            const double m1 = metric + i1;
 
             if (!is_info) {
                 // frozen: bit 0, metrics advance, stable re-rank in place (lanes do not move)
@@ -242,19 +257,20 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64) scl128_kernel(cons
                 // info: children (bit 0 in lane g, bit 1 in lane g + LMAX) of every path
                 const uint64_t pm1 = from_lower_half64<G, LMAX>(pscl_asu64(m1), lane);
                 const uint32_t prank = from_lower_half<G, LMAX>(rank, lane);
-                const double plam = pscl_asf64(from_lower_half64<G, LMAX>(pscl_asu64(lam), lane));
                 uint64_t km = cbit ? pm1 : pscl_asu64(m0);
                 const uint32_t myrank = cbit ? prank : rank;
-                const double mylam = cbit ? plam : lam;
                 bool kval = cpath < cnt;
-                int ncnt = cnt;
-                const uint64_t fmw = j < 64 ? fm0 : fm1, fvw = j < 64 ? fv0 : fv1;
-                if (P.sc_hard) {
-                    kval = kval && cbit == (uint32_t)(mylam < 0.0);  // sc_decode polar.py:149-153
-                } else if ((fmw >> (j & 63)) & 1) {
-                    kval = kval && cbit == (uint32_t)((fvw >> (j & 63)) & 1);  // forced (scl.py:146-161)
-                } else {
-                    ncnt = 2 * cnt < L ? 2 * cnt : L;  // both children (scl.py:163-168)
+                int ncnt = 2 * cnt < L ? 2 * cnt : L;  // both children (scl.py:163-168)
+                if (P.sc_hard) {                      // sc_decode polar.py:149-153
+                    const double plam = pscl_asf64(from_lower_half64<G, LMAX>(pscl_asu64(lam), lane));
+                    kval = kval && cbit == (uint32_t)((cbit ? plam : lam) < 0.0);
+                    ncnt = cnt;
+                } else if (P.force) {                 // forced bits (scl.py:146-161), per frame
+                    const uint64_t fmw = j < 64 ? fm0 : fm1, fvw = j < 64 ? fv0 : fv1;
+                    if ((fmw >> (j & 63)) & 1) {
+                        kval = kval && cbit == (uint32_t)((fvw >> (j & 63)) & 1);
+                        ncnt = cnt;
+                    }
                 }
                 if (!kval) km = 0x7ff0000000000000ULL;
                 const uint32_t kt = kval ? 2u * myrank + cbit : 0x7fffffffu;

@@ -72,6 +72,39 @@ __device__ __forceinline__ uint64_t polar_transform64(uint64_t x) {
     return x;
 }
 
+// transform of a segment of at most 32 (resp. 16, 8) bits held in a 32-bit word
+__device__ __forceinline__ uint32_t polar_transform32(uint32_t x) {
+    x ^= (x >> 1) & 0x55555555u;
+    x ^= (x >> 2) & 0x33333333u;
+    x ^= (x >> 4) & 0x0f0f0f0fu;
+    x ^= (x >> 8) & 0x00ff00ffu;
+    x ^= (x >> 16) & 0x0000ffffu;
+    return x;
+}
+__device__ __forceinline__ uint32_t polar_transform16(uint32_t x) {
+    x ^= (x >> 1) & 0x5555u;
+    x ^= (x >> 2) & 0x3333u;
+    x ^= (x >> 4) & 0x0f0fu;
+    x ^= (x >> 8) & 0x00ffu;
+    return x;
+}
+__device__ __forceinline__ uint32_t polar_transform8(uint32_t x) {
+    x ^= (x >> 1) & 0x55u;
+    x ^= (x >> 2) & 0x33u;
+    x ^= (x >> 4) & 0x0fu;
+    return x;
+}
+
+// metric increments of both bit hypotheses, np.logaddexp(0, -+llr) (scl.py:102-105):
+// max(0,v) + L with v = -llr (bit 0) / +llr (bit 1); L = log1p(exp(-|llr|)); llr == 0 -> LOGE2.
+// The "bad" child pays |llr| + L (|llr| = -v exactly), the "good" one 0.0 + L = L.
+__device__ __forceinline__ void metric_incr(double lam, double L, double& i0, double& i1) {
+    const double t = fabs(lam) + L;
+    const bool z = lam == 0.0;
+    i0 = z ? PSCL_LOGE2 : (lam < 0.0 ? t : L);
+    i1 = z ? PSCL_LOGE2 : (lam > 0.0 ? t : L);
+}
+
 __device__ __forceinline__ uint64_t pick_word(uint64_t w0, uint64_t w1, int idx) { return idx ? w1 : w0; }
 
 
