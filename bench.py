@@ -43,6 +43,10 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--retries", type=int, default=0,
+                    help="DL-SCL flip retries per CRC-failing frame (BASELINE config 4: --list 4 --retries 8)")
+    ap.add_argument("--beta", type=str, default="auto",
+                    help="flip metric .npy ('auto': tests/golden/beta_M{L}.npy, the reference checkpoint; 'none')")
     return ap.parse_args()
 
 
@@ -84,26 +88,31 @@ def load_valu_profile(workload_key: str):
 SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
 
 
-def cpu_baseline(llr_host: np.ndarray, info, L: int, budget_s: float):
+def cpu_baseline(llr_host: np.ndarray, info, L: int, budget_s: float, retries: int = 0, beta=None):
     """The oracle (C restatement of the reference, OpenMP over frames) on host cores."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle  # test/baseline infrastructure only
 
+    if retries > 0:
+        run = lambda x: oracle.dl_batch(x, info, L, retries, POLY, beta)  # noqa: E731
+        what = f"decode_with_retries (SCL L={L} + up to {retries} flips, beta)"
+    else:
+        run = lambda x: oracle.decode_batch(x, info, L, POLY)  # noqa: E731
+        what = f"decode_scl L={L} + CRC select"
     n0 = min(4000, llr_host.shape[0])
     t0 = time.perf_counter()
-    oracle.decode_batch(llr_host[:n0], info, L, POLY)  # warm-up / calibration
+    run(llr_host[:n0])  # warm-up / calibration
     rate = n0 / max(time.perf_counter() - t0, 1e-6)
     n = int(min(llr_host.shape[0], max(n0, rate * budget_s)))
     done, dt = 0, 0.0
     t0 = time.perf_counter()
     while dt < budget_s * 0.8 or done == 0:  # repeat the sample until the budget is spent
-        oracle.decode_batch(llr_host[:n], info, L, POLY)
+        run(llr_host[:n])
         done += n
         dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "frames/s", "cores": oracle.num_threads(), "kind": "port",
-            "sample": f"{done} frame decodes ({n} distinct frames of the step-0 batch, same LLRs as the GPU) by "
-                      f"oracle/scl_oracle.c (C restatement of decode_scl) L={L} + CRC select, OpenMP over frames, "
-                      f"{dt:.1f} s"}
+            "sample": f"{done} frames ({n} distinct frames of the step-0 batch, same LLRs as the GPU) through "
+                      f"oracle/scl_oracle.c (C restatement of {what}), OpenMP over frames, {dt:.1f} s"}
 
 
 def main():
@@ -153,15 +162,27 @@ def main():
         dec.channel_device(args.seed, snr_idx, args.ebno, rate, kp, frame0, B, llr[i].data_ptr(), msg[i].data_ptr())
     torch.cuda.synchronize(dev)
 
+    beta = None
+    if args.retries > 0 and args.beta != "none":
+        bp = ROOT / "tests" / "golden" / f"beta_M{L}.npy" if args.beta == "auto" else Path(args.beta)
+        beta = np.load(bp) if bp.exists() else None
+    counters_dl = torch.zeros(8, dtype=torch.int64, device=dev)
+
     def step(i):
         j = i % nbuf
-        dec.decode_device(llr[j].data_ptr(), B, d_best=best.data_ptr(), d_flags=flags.data_ptr(),
-                          d_ref=msg[j].data_ptr(), k_payload=kp, d_counters=counters.data_ptr())
+        if args.retries > 0:  # SCL + DL-SCL retry rounds, all on the device
+            dec.dlscl_device(llr[j].data_ptr(), B, args.retries, beta=beta, d_best=best.data_ptr(),
+                             d_flags=flags.data_ptr(), d_ref=msg[j].data_ptr(), k_payload=kp,
+                             d_counters_scl=counters.data_ptr(), d_counters_dl=counters_dl.data_ptr())
+        else:
+            dec.decode_device(llr[j].data_ptr(), B, d_best=best.data_ptr(), d_flags=flags.data_ptr(),
+                              d_ref=msg[j].data_ptr(), k_payload=kp, d_counters=counters.data_ptr())
 
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize(dev)
     counters.zero_()
+    counters_dl.zero_()
     dec.timing_enable(True)
     if dist:
         dist.barrier()
@@ -181,26 +202,32 @@ def main():
     if dist:
         counters = counters.to(red_dev)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        counters_dl = counters_dl.to(red_dev)
         dist.all_reduce(counters, op=dist.ReduceOp.SUM)
+        dist.all_reduce(counters_dl, op=dist.ReduceOp.SUM)
     elapsed = float(tmax.item())
     c = counters.cpu().numpy()
+    cdl = counters_dl.cpu().numpy()
     frames_total = B * args.steps * world
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         host = llr[0][: min(B, 1_000_000)].cpu().numpy()
-        cpu = cpu_baseline(host, info, L, args.cpu_seconds)
+        cpu = cpu_baseline(host, info, L, args.cpu_seconds, args.retries, beta)
 
     if rank == 0:
         avg_ms = kern_ms / max(launches, 1)
         fb = frame_bytes(N, W)
-        achieved = fb * B / (avg_ms * 1e-3) / 1e9
-        wkey = f"scl_L{L}_N{N}_K{K}_B{B}"
+        # DL mode: the step's decode launches (baseline + retry rounds) priced as one pass
+        # over the batch; otherwise one launch = one batch
+        per_batch_ms = kern_ms / args.steps if args.retries > 0 else avg_ms
+        achieved = fb * B / (per_batch_ms * 1e-3) / 1e9
+        wkey = f"scl_L{L}_N{N}_K{K}_B{B}" + (f"_dl{args.retries}" if args.retries > 0 else "")
         traffic = load_traffic(wkey)
         vp = load_valu_profile(wkey)
         compute = None
         if vp is not None:
-            rate = vp[0] * B / (avg_ms * 1e-3)
+            rate = vp[0] * B / (per_batch_ms * 1e-3)
             peak32, peak64 = SIMDS * CLOCK_HZ / 2, SIMDS * CLOCK_HZ / 4
             compute = {"bound": "valu-issue", "unit": "wave-instr/s", "instr_per_frame": vp[0],
                        "achieved": rate, "peak_f32_issue": peak32, "peak_f64_issue": peak64,
@@ -212,8 +239,20 @@ def main():
         p0 = REF_FER_L8[0] / REF_FER_L8[1]
         pp = (c[1] + REF_FER_L8[0]) / (c[0] + REF_FER_L8[1])
         se = math.sqrt(max(pp * (1 - pp) * (1 / max(c[0], 1) + 1 / REF_FER_L8[1]), 1e-30))
+        dl = None
+        if args.retries > 0:
+            dl = {"retries": args.retries, "beta": None if beta is None else "tests/golden/beta_M%d.npy" % L,
+                  "frame_errors": int(cdl[1]), "fer": cdl[1] / max(cdl[0], 1), "ber": cdl[2] / max(cdl[0] * K, 1),
+                  "redecodes": int(cdl[5]), "redecodes_per_frame": cdl[5] / max(cdl[0], 1)}
+        metric = "decoded frames/sec, P(128,64)+CRC24 SCL L=8 @ Eb/N0=5 dB; FER match"
+        workload = (f"SCL L={L} P({N},{K})+CRC24 (0x1864CFB) @ Eb/N0={args.ebno:g} dB, "
+                    f"{B} frames/GPU/step, decode+CRC select+FER/BER count")
+        if args.retries > 0:
+            metric = f"decoded frames/sec, P(128,64)+CRC24 DL-SCL L={L} + {args.retries} flip retries"
+            workload = (f"DL-SCL L={L} + {args.retries} flips (beta) P({N},{K})+CRC24 @ Eb/N0={args.ebno:g} dB, "
+                        f"{B} frames/GPU/step, SCL + retry rounds + FER/BER count")
         line = {
-            "metric": "decoded frames/sec, P(128,64)+CRC24 SCL L=8 @ Eb/N0=5 dB; FER match",
+            "metric": metric,
             "value": frames_total / elapsed,
             "unit": "frames/s",
             "n_gpus": world,
@@ -225,18 +264,20 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: on-device Philox4x32 BPSK/AWGN frames (payload->CRC24->polar->LLR), resident in HBM",
-            "config": {"workload": f"SCL L={L} P({N},{K})+CRC24 (0x1864CFB) @ Eb/N0={args.ebno:g} dB, "
-                                   f"{B} frames/GPU/step, decode+CRC select+FER/BER count",
+            "config": {"workload": workload, "retries": args.retries,
                        "N": N, "K": K, "list_size": L, "ebno_db": args.ebno, "frames_per_gpu_per_step": B,
                        "global_batch": B * world, "parallelism": f"frame-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS,
                          "traffic": traffic,
-                         "kernel": "scl128_kernel" if N == 128 and L <= 8 else "scl_decode_kernel", "avg_launch_ms": avg_ms, "launches": launches,
+                         "kernel": "scl128_kernel" if N == 128 and L <= 8 else "scl_decode_kernel",
+                         "avg_launch_ms": avg_ms, "launches": launches, "decode_ms_per_step": kern_ms / args.steps,
                          "bytes_per_frame": fb, "compute": compute},
             "cpu_baseline": cpu,
             "fer": {"frames": int(c[0]), "frame_errors": int(c[1]), "fer": fer, "ber": c[2] / max(c[0] * K, 1),
-                    "reference_fer": p0, "z_vs_reference": (fer - p0) / se},
+                    "reference_fer": p0 if L == 8 else None,
+                    "z_vs_reference": (fer - p0) / se if (L == 8 and args.ebno == 5.0) else None},
+            "dl_scl": dl,
         }
         print(json.dumps(line), flush=True)
     if dist:

@@ -64,6 +64,7 @@ extern "C" {
 #define PSCL_CNT_BIT_ERR 2     /* best bits != reference over all K bits (run_fer_sweep BER, :95-99) */
 #define PSCL_CNT_PAYLOAD_ERR 3 /* frames with >=1 error in the first k_payload bits (run_ber_sweep FER) */
 #define PSCL_CNT_PAYLOAD_BIT 4 /* payload bit errors (run_ber_sweep BER, :77-82) */
+#define PSCL_CNT_RETRIES 5     /* flip re-decodes run by pscl_dlscl_device */
 #define PSCL_NCOUNT 8
 
 typedef struct pscl_handle pscl_handle;
@@ -160,6 +161,45 @@ int pscl_channel_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, doubl
  * E = 0 switches rate matching off.  Repetition (E > N) needs N >= 32.
  */
 int pscl_set_rate_match(pscl_handle* h, int E);
+
+/*
+ * Decision LLRs of given paths (scl.py:158,166 info_llrs of a path whose bits are known):
+ * for frame b with information bits d_bits[b] (frozen bits 0), the leaf LLR at every
+ * information phase, recomputed top-down through the same f/g operations as the decoder
+ * (bit-identical to the decoder's info_llrs for that path).  Device buffers, handle stream.
+ *   d_llr [B][N] (or [B][E] with rate matching);  d_bits [B][W] uint64;  d_out [B][K] float64
+ */
+int pscl_path_llrs_device(pscl_handle* h, const double* d_llr, int64_t B, const uint64_t* d_bits, double* d_out);
+
+/*
+ * DL-SCL flip metric matrix (dl_scl_polar/dlscl/flip.py:104-106, checkpoints/beta_M*.npy):
+ * beta [K][K] row-major float64 on the host (the reference's float32 checkpoint widened
+ * exactly), or NULL to rank by |L0| alone (flip.py:107).  Applies to pscl_dlscl_device.
+ */
+int pscl_set_beta(pscl_handle* h, const double* beta);
+
+/*
+ * SCL + DL-SCL retries over a device batch: decode_with_retries (flip.py:65-141) for every
+ * frame, as run_fer_sweep.py:89-109 uses it (baseline SCL counted, then DL-SCL counted).
+ * Baseline SCL decode of all B frames; the frames whose best candidate fails the CRC are
+ * retried up to min(retries, K) times, each retry flipping the untried information index
+ * with the smallest q = |L0| @ beta (q = |L0| without beta; ties -> lower index), forcing
+ * the reference prefix, and re-decoding; the loop stops at the first CRC pass.  L0 and the
+ * reference bits follow the latest attempt's best path.  Enqueued on the handle's stream;
+ * the call synchronizes once (to size the retry state by the number of failing frames) and
+ * returns with the retry rounds queued behind it.
+ *   d_best       [B][W] uint64 out: final attempt's best bits (flip.py:126,137)
+ *   d_flags      [B] uint8 out: PSCL_FLAG_* of the final attempt
+ *   d_attempts   NULL or [B] int32 out: 1 + flips tried
+ *   d_tried      NULL or [B][tried_stride] int32 out: flip indices in order, -1 padded
+ *   d_ref        NULL or [B][W] transmitted words: baseline statistics are added into
+ *                d_counters_scl, final ones into d_counters_dl (both int64[PSCL_NCOUNT],
+ *                required with d_ref); PSCL_CNT_RETRIES of d_counters_dl counts re-decodes
+ * Requires a CRC (without one every baseline "passes", flip.py:84-86: results = baseline).
+ */
+int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retries, uint64_t* d_best,
+                      uint8_t* d_flags, int32_t* d_attempts, int32_t* d_tried, int tried_stride,
+                      const uint64_t* d_ref, int k_payload, int64_t* d_counters_scl, int64_t* d_counters_dl);
 
 /* Device scratch helpers so that non-torch callers can drive the device path. */
 int pscl_device_alloc(pscl_handle* h, void** d_ptr, int64_t bytes);

@@ -33,6 +33,8 @@ def lib() -> C.CDLL:
                                                  C.POINTER(C.c_float), bp, ip, ip, ip, ip]
         L.oracle_decode_batch.argtypes = [dp, C.c_int64, C.c_int, ip, C.c_int, C.c_int, C.c_uint64, bp,
                                           C.POINTER(C.c_uint8)]
+        L.oracle_dl_batch.argtypes = [dp, C.c_int64, C.c_int, ip, C.c_int, C.c_int, C.c_int, C.c_uint64,
+                                      C.POINTER(C.c_float), bp, ip, ip]
         L.oracle_num_threads.restype = C.c_int
         L.oracle_logaddexp0_batch.argtypes = [dp, C.c_int64, dp]
         _LIB = L
@@ -138,6 +140,25 @@ def decode_batch(llr, info, M, crc=None):
                                  _p(bits, C.c_int8), _p(ok, C.c_uint8)):
         raise ValueError("oracle_decode_batch failed")
     return bits, ok.astype(bool)
+
+
+def dl_batch(llr, info, M, retries, crc=None, beta=None):
+    """Parallel (OpenMP) decode_with_retries: returns (bits[B,K], success[B], attempts[B])."""
+    llr = np.ascontiguousarray(llr, np.float64)
+    info = np.ascontiguousarray(info, np.int32)
+    B, N = llr.shape
+    K = info.size
+    bits = np.zeros((B, K), np.int8)
+    succ = np.zeros(B, np.int32)
+    att = np.zeros(B, np.int32)
+    bp = None
+    if beta is not None:
+        beta = np.ascontiguousarray(beta, np.float32)
+        bp = _p(beta, C.c_float)
+    if lib().oracle_dl_batch(_p(llr, C.c_double), B, N, _p(info, C.c_int32), K, M, retries, poly_int(crc), bp,
+                             _p(bits, C.c_int8), _p(succ, C.c_int32), _p(att, C.c_int32)):
+        raise ValueError("oracle_dl_batch failed")
+    return bits, succ.astype(bool), att
 
 
 def num_threads() -> int:

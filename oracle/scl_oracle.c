@@ -527,6 +527,24 @@ int oracle_decode_batch(const double* llr, int64_t B, int N, const int32_t* info
     return err ? -1 : 0;
 }
 
+/*
+ * decode_with_retries over B frames (OpenMP over frames): final best bits [B][K], success
+ * [B], attempts [B].  beta: NULL or K*K float32.  Returns 0 or -1.
+ */
+int oracle_dl_batch(const double* llr, int64_t B, int N, const int32_t* info, int K, int M, int retries,
+                    uint64_t crc_poly, const float* beta, int8_t* best_bits, int32_t* success, int32_t* attempts) {
+    int err = 0;
+#pragma omp parallel for schedule(dynamic, 4) reduction(| : err)
+    for (int64_t b = 0; b < B; b++) {
+        int32_t tried[OR_MAXN];
+        int32_t nt;
+        if (oracle_decode_with_retries(llr + b * N, N, info, K, M, retries > K ? K : retries, crc_poly, beta,
+                                       best_bits + b * K, success + b, attempts + b, tried, &nt))
+            err |= 1;
+    }
+    return err ? -1 : 0;
+}
+
 int oracle_num_threads(void) {
 #ifdef _OPENMP
     extern int omp_get_max_threads(void);

@@ -29,7 +29,7 @@ PSCL_MAX_L = 32
 PSCL_FLAG_CRC_PASS = 0x80
 PSCL_FLAG_IDX_MASK = 0x3F
 PSCL_NCOUNT = 8
-CNT_FRAMES, CNT_FRAME_ERR, CNT_BIT_ERR, CNT_PAYLOAD_ERR, CNT_PAYLOAD_BIT = range(5)
+CNT_FRAMES, CNT_FRAME_ERR, CNT_BIT_ERR, CNT_PAYLOAD_ERR, CNT_PAYLOAD_BIT, CNT_RETRIES = range(6)
 
 # every symbol the header declares (tests/test_capi_symbols.py checks the .so exports them)
 EXPORTS = (
@@ -37,7 +37,8 @@ EXPORTS = (
     "pscl_set_stream", "pscl_get_stream", "pscl_sync", "pscl_decode", "pscl_sc_decode",
     "pscl_decode_device", "pscl_channel_device", "pscl_device_alloc", "pscl_device_free",
     "pscl_memcpy_htod", "pscl_memcpy_dtoh", "pscl_memset_device", "pscl_timing_enable",
-    "pscl_timing_read", "pscl_launch_info", "pscl_set_rate_match",
+    "pscl_timing_read", "pscl_launch_info", "pscl_set_rate_match", "pscl_set_beta", "pscl_dlscl_device",
+    "pscl_path_llrs_device",
 )
 
 _vp, _i32, _i64, _u64, _dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
@@ -93,6 +94,10 @@ def lib() -> C.CDLL:
         "pscl_timing_read": (C.c_int, [_vp, P(_i64), P(_dbl)]),
         "pscl_launch_info": (C.c_int, [_vp, _i64, P(C.c_int), P(_i64), P(C.c_int)]),
         "pscl_set_rate_match": (C.c_int, [_vp, C.c_int]),
+        "pscl_set_beta": (C.c_int, [_vp, _vp]),
+        "pscl_path_llrs_device": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
+        "pscl_dlscl_device": (C.c_int, [_vp, _vp, _i64, C.c_int, _vp, _vp, _vp, _vp, C.c_int, _vp, C.c_int, _vp,
+                                        _vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -157,6 +162,7 @@ class Decoder:
         self._h = h
         self._lock = threading.Lock()
         self.E = 0
+        self._beta = None
 
     def set_rate_match(self, E: int) -> None:
         """NR: decode inputs become [B, E] received LLRs (de-rate-match + de-interleave on GPU)."""
@@ -231,6 +237,56 @@ class Decoder:
         check(lib().pscl_channel_device(self._h, int(seed) & (2**64 - 1), int(stream_id) & 0xFFFFFFFF,
                                         float(ebno_db), float(rate), int(k_payload), int(frame0), int(B), d_llr,
                                         d_msg or None))
+
+    def path_llrs_device(self, d_llr: int, B: int, d_bits: int, d_out: int) -> None:
+        """Decision LLRs [B, K] of the paths with information bits d_bits [B, W] (replay)."""
+        with self._lock:
+            check(lib().pscl_path_llrs_device(self._h, d_llr, int(B), d_bits, d_out))
+
+    def path_llrs(self, llr: np.ndarray, bits: np.ndarray) -> np.ndarray:
+        """Host form of path_llrs_device: llr [B, N] (or [B, E]), bits [B, K] 0/1."""
+        llr = np.ascontiguousarray(llr, dtype=np.float64)
+        if llr.ndim == 1:
+            llr = llr[None, :]
+        B = llr.shape[0]
+        words = np.zeros((B, self.W), np.uint64)
+        bits = np.asarray(bits, dtype=np.uint64).reshape(B, self.K)
+        for j in range(self.K):
+            words[:, j >> 6] |= bits[:, j] << np.uint64(j & 63)
+        with DeviceArena(self) as mem:
+            d_llr = mem.alloc(llr.nbytes)
+            d_bits = mem.alloc(words.nbytes)
+            d_out = mem.alloc(max(B * self.K * 8, 8))
+            mem.upload(d_llr, llr)
+            mem.upload(d_bits, words)
+            self.path_llrs_device(d_llr, B, d_bits, d_out)
+            return mem.download(d_out, B * self.K * 8, np.float64).reshape(B, self.K)
+
+    def set_beta(self, beta: np.ndarray | None) -> None:
+        """DL-SCL flip metric matrix [K, K] (None: rank by |L0|); widened to float64 exactly."""
+        if beta is None:
+            if self._beta is not None:
+                check(lib().pscl_set_beta(self._h, None))
+            self._beta = None
+            return
+        b = np.asarray(beta)
+        if b.ndim != 2 or b.shape[0] != b.shape[1] or b.shape[0] != self.K:
+            raise ValueError("beta must be a square matrix matching abs_l0 length")
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        if self._beta is not None and np.array_equal(self._beta, b):
+            return
+        check(lib().pscl_set_beta(self._h, _ptr(b)))
+        self._beta = b.copy()
+
+    def dlscl_device(self, d_llr: int, B: int, retries: int, *, beta=None, d_best: int, d_flags: int,
+                     d_attempts=0, d_tried=0, tried_stride=0, d_ref=0, k_payload=0, d_counters_scl=0,
+                     d_counters_dl=0) -> None:
+        """SCL + DL-SCL retries of B device-resident frames (pscl_dlscl_device)."""
+        self.set_beta(beta)
+        with self._lock:
+            check(lib().pscl_dlscl_device(self._h, d_llr, int(B), int(retries), d_best, d_flags, d_attempts or None,
+                                          d_tried or None, int(tried_stride), d_ref or None, int(k_payload),
+                                          d_counters_scl or None, d_counters_dl or None))
 
     def sync(self) -> None:
         check(lib().pscl_sync(self._h))

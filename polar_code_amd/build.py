@@ -22,7 +22,7 @@ LIB = PKG / "libpolar_mi355x.so"
 ARCH = os.environ.get("PSCL_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-HIP_SOURCES = ["scl_kernels.hip", "scl128.hip", "capi.cpp"]
+HIP_SOURCES = ["scl_kernels.hip", "scl128.hip", "dlscl.hip", "capi.cpp"]
 HIP_DEPS = HIP_SOURCES + ["scl_kernels.h", "scl_device.h", "glibc_softplus.h", "exp_table.inc"]
 
 

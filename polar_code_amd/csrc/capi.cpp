@@ -90,7 +90,8 @@ struct pscl_handle {
     int rm_E = 0;                     // NR rate matching (0 = off)
     int32_t* d_rm_src = nullptr;      // [N] de-interleave gather index
     int32_t* d_rm_order = nullptr;    // [N] interleaver order
-    DevBuf scratch[12];
+    DevBuf scratch[28];
+    double* d_beta = nullptr;         // [K][K] DL-SCL flip metric (null = |L0|)
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
@@ -104,7 +105,8 @@ int ensure(pscl_handle* h, int slot, size_t bytes, void** out) {
         if (b.p) hipFree(b.p);
         b.p = nullptr;
         b.n = 0;
-        size_t want = bytes < 4096 ? 4096 : bytes;
+        size_t want = bytes + bytes / 2;  // geometric growth: varying batch sizes settle quickly
+        if (want < 4096) want = 4096;
         HIP_TRY(hipMalloc(&b.p, want));
         b.n = want;
     }
@@ -267,6 +269,7 @@ int pscl_destroy(pscl_handle* h) {
     if (h->d_exp_table) hipFree(h->d_exp_table);
     if (h->d_rm_src) hipFree(h->d_rm_src);
     if (h->d_rm_order) hipFree(h->d_rm_order);
+    if (h->d_beta) hipFree(h->d_beta);
     if (h->own_stream) hipStreamDestroy(h->own_stream);
     delete h;
     return PSCL_OK;
@@ -314,6 +317,198 @@ int pscl_decode_device(pscl_handle* h, const double* d_llr, int64_t B, const uin
     P.counters = d_counters;
     if (pscl_decode_wpg(P) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
     return launch_decode(h, P, hist);
+}
+
+int pscl_path_llrs_device(pscl_handle* h, const double* d_llr, int64_t B, const uint64_t* d_bits, double* d_out) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    if (B < 0) return fail(PSCL_EINVAL, "B must be >= 0");
+    if (B == 0) return PSCL_OK;
+    if (!d_llr || !d_bits || !d_out) return fail(PSCL_EINVAL, "d_llr, d_bits and d_out are required");
+    if (B > INT32_MAX) return fail(PSCL_EUNSUP, "B exceeds 2^31-1");
+    int rc = set_device(h);
+    if (rc) return rc;
+    void *d_cnt, *d_rows;
+    if ((rc = ensure(h, 25, 8, &d_cnt))) return rc;
+    if ((rc = ensure(h, 26, (size_t)B * 8, &d_rows))) return rc;
+    const int32_t nb = (int32_t)B;
+    HIP_TRY(hipMemcpyAsync(d_cnt, &nb, 4, hipMemcpyHostToDevice, h->stream));
+    hipError_t e = pscl_launch_iota64((int64_t*)d_rows, B, h->stream);
+    if (e != hipSuccess) return fail(PSCL_EDEVICE, "iota launch: %s", hipGetErrorString(e));
+    pscl_replay_params Rp;
+    memset(&Rp, 0, sizeof(Rp));
+    Rp.llr = d_llr;
+    Rp.N = h->N;
+    Rp.n = h->n;
+    Rp.K = h->K;
+    Rp.W = h->W;
+    Rp.rm_E = h->rm_E;
+    Rp.rm_src = h->d_rm_src;
+    Rp.info_mask[0] = h->info_mask[0];
+    Rp.info_mask[1] = h->info_mask[1];
+    Rp.count = (const int32_t*)d_cnt;
+    Rp.act = (const int64_t*)d_rows;
+    Rp.bits = d_bits;
+    Rp.bits_by_row = 1;
+    Rp.out = d_out;
+    if ((e = pscl_launch_replay(Rp, B, h->stream)) != hipSuccess)
+        return fail(PSCL_EDEVICE, "replay launch: %s", hipGetErrorString(e));
+    HIP_TRY(hipStreamSynchronize(h->stream));  // d_cnt is a host-staged value
+    return PSCL_OK;
+}
+
+int pscl_set_beta(pscl_handle* h, const double* beta) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    int rc = set_device(h);
+    if (rc) return rc;
+    if (!beta) {
+        if (h->d_beta) HIP_TRY(hipFree(h->d_beta));
+        h->d_beta = nullptr;
+        return PSCL_OK;
+    }
+    if (h->K == 0) return fail(PSCL_EINVAL, "beta must be a square matrix matching abs_l0 length");
+    const size_t bytes = (size_t)h->K * h->K * 8;
+    if (!h->d_beta) HIP_TRY(hipMalloc(&h->d_beta, bytes));
+    HIP_TRY(hipStreamSynchronize(h->stream));  // a previous round may still read the old matrix
+    HIP_TRY(hipMemcpy(h->d_beta, beta, bytes, hipMemcpyHostToDevice));
+    return PSCL_OK;
+}
+
+int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retries, uint64_t* d_best, uint8_t* d_flags,
+                      int32_t* d_attempts, int32_t* d_tried, int tried_stride, const uint64_t* d_ref, int k_payload,
+                      int64_t* d_counters_scl, int64_t* d_counters_dl) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    if (B < 0) return fail(PSCL_EINVAL, "B must be >= 0");
+    if (B == 0) return PSCL_OK;
+    if (!d_llr || !d_best || !d_flags) return fail(PSCL_EINVAL, "d_llr, d_best and d_flags are required");
+    if (d_ref && (!d_counters_scl || !d_counters_dl)) return fail(PSCL_EINVAL, "d_ref given without both counters");
+    if (k_payload < 0 || k_payload > h->K) return fail(PSCL_EINVAL, "k_payload out of range");
+    const int rounds = h->crc_poly && retries > 0 ? (retries < h->K ? retries : h->K) : 0;
+    if (d_tried && tried_stride < rounds) return fail(PSCL_EINVAL, "tried_stride < min(retries, K)");
+    int rc = set_device(h);
+    if (rc) return rc;
+    const int K = h->K, W = h->W;
+    hipStream_t s = h->stream;
+    // baseline SCL (flip.py:79-80)
+    pscl_decode_params P;
+    fill_decode_params(h, P, 0);
+    P.llr = d_llr;
+    P.B = B;
+    P.best = d_best;
+    P.flags = d_flags;
+    P.ref = d_ref;
+    P.k_payload = k_payload;
+    P.counters = d_counters_scl;
+    if (pscl_decode_wpg(P) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
+    if ((rc = launch_decode(h, P, 0))) return rc;
+    if (d_attempts) HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)d_attempts, 1, (size_t)B, s));
+    if (d_tried) HIP_TRY(hipMemsetAsync(d_tried, 0xff, (size_t)B * tried_stride * 4, s));
+    if (rounds > 0) {
+        void *d_cnt, *d_act, *d_list0, *d_list1;
+        // cnt[0] = failing frames, cnt[r + 1] = entries still live after round r
+        if ((rc = ensure(h, 12, (size_t)(rounds + 2) * 4, &d_cnt))) return rc;
+        if ((rc = ensure(h, 13, (size_t)B * 8, &d_act))) return rc;
+        if ((rc = ensure(h, 14, (size_t)B * 4, &d_list0))) return rc;
+        int32_t* cnt = (int32_t*)d_cnt;
+        HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)(rounds + 2) * 4, s));
+        hipError_t e = pscl_launch_dl_compact(d_flags, B, (int64_t*)d_act, (int32_t*)d_list0, cnt, s);
+        if (e != hipSuccess) return fail(PSCL_EDEVICE, "dl_compact launch: %s", hipGetErrorString(e));
+        int32_t A = 0;  // the one host read: sizes the entry state
+        HIP_TRY(hipMemcpyAsync(&A, cnt, 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (A > 0) {
+            void *d_al0, *d_refw, *d_tried_set, *d_nt, *d_force, *d_fidx, *d_ob, *d_of;
+            const size_t a = (size_t)A;
+            if ((rc = ensure(h, 15, a * 4, &d_list1))) return rc;
+            if ((rc = ensure(h, 16, a * K * 8, &d_al0))) return rc;
+            if ((rc = ensure(h, 17, a * W * 8, &d_refw))) return rc;
+            if ((rc = ensure(h, 18, a * 16, &d_tried_set))) return rc;
+            if ((rc = ensure(h, 19, a * 4, &d_nt))) return rc;
+            if ((rc = ensure(h, 20, a * 2 * W * 8, &d_force))) return rc;
+            if ((rc = ensure(h, 21, a * 8, &d_fidx))) return rc;
+            if ((rc = ensure(h, 22, a * W * 8, &d_ob))) return rc;
+            if ((rc = ensure(h, 23, a, &d_of))) return rc;
+            HIP_TRY(hipMemsetAsync(d_tried_set, 0, a * 16, s));
+            HIP_TRY(hipMemsetAsync(d_nt, 0, a * 4, s));
+            // L0 of the baseline's best path for the failing frames (flip.py:97-102),
+            // replayed from its bits; the reference bits are the baseline's best bits
+            pscl_replay_params Rp;
+            memset(&Rp, 0, sizeof(Rp));
+            Rp.llr = d_llr;
+            Rp.N = h->N;
+            Rp.n = h->n;
+            Rp.K = K;
+            Rp.W = W;
+            Rp.rm_E = h->rm_E;
+            Rp.rm_src = h->d_rm_src;
+            Rp.info_mask[0] = h->info_mask[0];
+            Rp.info_mask[1] = h->info_mask[1];
+            Rp.count = cnt;
+            Rp.list = nullptr;
+            Rp.act = (const int64_t*)d_act;
+            Rp.bits = d_best;
+            Rp.bits_by_row = 1;
+            Rp.out = (double*)d_al0;
+            if ((e = pscl_launch_replay(Rp, A, s)) != hipSuccess)
+                return fail(PSCL_EDEVICE, "replay launch: %s", hipGetErrorString(e));
+            if ((e = pscl_launch_dl_gather(d_best, (const int64_t*)d_act, cnt, A, W, (uint64_t*)d_refw, s)) != hipSuccess)
+                return fail(PSCL_EDEVICE, "dl_gather launch: %s", hipGetErrorString(e));
+            pscl_dl_params D;
+            memset(&D, 0, sizeof(D));
+            D.K = K;
+            D.W = W;
+            D.rounds = rounds;
+            D.act = (const int64_t*)d_act;
+            D.al0 = (double*)d_al0;
+            D.ref = (uint64_t*)d_refw;
+            D.tried = (uint64_t*)d_tried_set;
+            D.ntried = (int32_t*)d_nt;
+            D.beta = h->d_beta;
+            D.force = (uint64_t*)d_force;
+            D.fidx = (int64_t*)d_fidx;
+            D.ob = (const uint64_t*)d_ob;
+            D.oflags = (const uint8_t*)d_of;
+            D.best = d_best;
+            D.flags = d_flags;
+            D.attempts = d_attempts;
+            D.tried_out = d_tried;
+            D.tried_stride = tried_stride;
+            D.counters = d_ref ? d_counters_dl : nullptr;
+            int32_t* lists[2] = {(int32_t*)d_list0, (int32_t*)d_list1};
+            // the retry decodes: plain kernel, LLR rows by indirection, forced prefixes
+            pscl_decode_params H;
+            fill_decode_params(h, H, 0);
+            H.llr = d_llr;
+            H.B = A;
+            H.fidx = D.fidx;
+            H.force = D.force;
+            H.best = (uint64_t*)d_ob;
+            H.flags = (uint8_t*)d_of;
+            if (pscl_decode_wpg(H) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
+            Rp.bits = (const uint64_t*)d_ob;  // this round's best bits, by list position
+            Rp.bits_by_row = 0;
+            for (int r = 0; r < rounds; ++r) {  // no host round trips: counts stay on the device
+                D.n = cnt + r;
+                D.list = lists[r & 1];
+                D.next_list = lists[(r + 1) & 1];
+                D.next_count = cnt + r + 1;
+                if ((e = pscl_launch_dl_select(D, A, s)) != hipSuccess)
+                    return fail(PSCL_EDEVICE, "dl_select launch: %s", hipGetErrorString(e));
+                H.d_count = D.n;
+                if ((rc = launch_decode(h, H, 0))) return rc;
+                Rp.count = D.n;
+                Rp.list = D.list;
+                if ((e = pscl_launch_replay(Rp, A, s)) != hipSuccess)
+                    return fail(PSCL_EDEVICE, "replay launch: %s", hipGetErrorString(e));
+                if ((e = pscl_launch_dl_update(D, A, s)) != hipSuccess)
+                    return fail(PSCL_EDEVICE, "dl_update launch: %s", hipGetErrorString(e));
+            }
+        }
+    }
+    if (d_ref) {
+        hipError_t e = pscl_launch_dl_count(d_best, d_flags, d_ref, B, W, k_payload, d_counters_dl, s);
+        if (e != hipSuccess) return fail(PSCL_EDEVICE, "dl_count launch: %s", hipGetErrorString(e));
+    }
+    return PSCL_OK;
 }
 
 static int decode_host(pscl_handle* h, const double* llr, int64_t B, const int8_t* forced, int32_t* n_paths,

@@ -113,15 +113,18 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
     const uint32_t cbit = g >= LMAX ? 1u : 0u;
     const uint64_t info0 = P.info_mask[0], info1 = P.info_mask[1];
 
-    for (int64_t f0 = ((int64_t)blockIdx.x * wpg + wave) * F; f0 < P.B; f0 += wstride) {
+    // live batch size: P.B, or a device-side count bounded by P.B (DL-SCL retry rounds)
+    const int64_t Bn = P.d_count ? (*P.d_count < P.B ? (int64_t)*P.d_count : P.B) : P.B;
+    for (int64_t f0 = ((int64_t)blockIdx.x * wpg + wave) * F; f0 < Bn; f0 += wstride) {
         const int64_t f = f0 + fl;
-        const bool fvalid = f < P.B;
+        const bool fvalid = f < Bn;
+        const int64_t frow = P.fidx ? P.fidx[fvalid ? f : f0] : (fvalid ? f : f0);
         if (P.rm_E == 0) {
-            const double* src = P.llr + (fvalid ? f : f0) * kN;
+            const double* src = P.llr + frow * kN;
 #pragma unroll
             for (int x = 0; x < kN / G; ++x) Af[g + x * G] = src[g + x * G];
         } else {  // NR: de-rate-match + de-interleave while staging
-            const double* src = P.llr + (fvalid ? f : f0) * P.rm_E;
+            const double* src = P.llr + frow * P.rm_E;
             for (int x = 0; x < kN / G; ++x) Af[g + x * G] = nr_stage(src, P.rm_src[g + x * G], P.rm_E, kN);
         }
         uint64_t fm0 = 0, fm1 = 0, fv0 = 0, fv1 = 0;
@@ -335,6 +338,13 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
             }
             if ((int)rank == best) {
                 const bool bpass = P.has_crc ? (syn == 0) : true;
+                if (HIST && P.best_info_llrs) {
+                    int cur = g;
+                    for (int jj = K - 1; jj >= 0; --jj) {
+                        P.best_info_llrs[f * K + jj] = hist_llr[jj * L + cur];
+                        cur = hist_par[jj * L + cur];
+                    }
+                }
                 if (P.best) {
                     P.best[f * P.W] = ib0;
                     if (P.W > 1) P.best[f * P.W + 1] = ib1;

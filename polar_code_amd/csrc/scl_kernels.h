@@ -26,6 +26,9 @@ struct pscl_decode_params {
     double* metrics;             // [B][L] or null
     uint64_t* cands;             // [B][L][W] or null
     double* info_llrs;           // [B][L][K] or null (needs the HIST kernel)
+    double* best_info_llrs;      // [B][K] or null: the best path's decision LLRs (HIST kernel)
+    const int64_t* fidx;         // [B] or null: frame b reads LLR row fidx[b] (outputs stay at b)
+    const int32_t* d_count;      // or null: decode min(B, *d_count) frames (grid sized for B)
     int rm_E;                    // NR rate matching: received length E (0 = none; llr is [B][E])
     const int32_t* rm_src;       // [N] de-interleave source index k(i) into the de-rate-matched vector
     const uint64_t* ref;         // [B][W] or null
@@ -34,6 +37,46 @@ struct pscl_decode_params {
     int fast;                    // 1: the specialised N = 128, L <= 8 kernel (scl128.hip)
     int wave_bytes;              // LDS bytes per wavefront
     int a_bytes;                 // LDS bytes of the LLR slots per wavefront
+};
+
+// Decision-LLR replay (dlscl.hip): leaf LLRs of a known path, recomputed top-down
+struct pscl_replay_params {
+    const double* llr;           // channel LLRs [.][N] (or [.][E] with rate matching)
+    int N, n, K, W, rm_E;
+    const int32_t* rm_src;
+    uint64_t info_mask[2];
+    const int32_t* count;        // live entries (device)
+    const int32_t* list;         // [count] entry ids, or null (entry = position)
+    const int64_t* act;          // [entries] LLR row of each entry
+    const uint64_t* bits;        // info bits, [.][W] words
+    int bits_by_row;             // 1: bits row = act[entry]; 0: bits row = list position
+    double* out;                 // [entries][K] decision LLRs (signed), row = entry
+};
+
+// DL-SCL retry rounds (dlscl.hip): entry e = one failing frame's retry state
+struct pscl_dl_params {
+    int K, W;
+    int rounds;                  // min(retries, K): attempt budget per frame (flip.py:111)
+    const int32_t* n;            // live entries this round (device count)
+    const int32_t* list;         // [n] live entry ids
+    int32_t* next_list;          // [A] survivors of this round (dl_update)
+    int32_t* next_count;         // device counter of next_list
+    const int64_t* act;          // [A] frame index of each entry
+    double* al0;                 // [A][K] decision LLRs of the entry's reference path
+    uint64_t* ref;               // [A][W] reference bits
+    uint64_t* tried;             // [A][2] tried-index bit sets
+    int32_t* ntried;             // [A]
+    const double* beta;          // [K][K] fp64 or null (flip.py:104-108)
+    uint64_t* force;             // [n][2][W] force words of this round's decode
+    int64_t* fidx;               // [n] LLR row of this round's decode
+    const uint64_t* ob;          // [n][W] this round's best bits
+    const uint8_t* oflags;       // [n]
+    uint64_t* best;              // [B][W] final best bits (per frame)
+    uint8_t* flags;              // [B]
+    int32_t* attempts;           // [B] or null: 1 + flips tried
+    int32_t* tried_out;          // [B][tried_stride] or null: flip indices in order
+    int tried_stride;
+    int64_t* counters;           // or null: PSCL_CNT_RETRIES += decodes
 };
 
 struct pscl_channel_params {
@@ -60,5 +103,15 @@ int pscl_decode_wpg(const pscl_decode_params& P);
 int pscl_decode_lds(const pscl_decode_params& P, int hist);
 hipError_t pscl_launch_decode(const pscl_decode_params& P, int hist, hipStream_t s);
 hipError_t pscl_launch_channel(const pscl_channel_params& P, hipStream_t s);
+hipError_t pscl_launch_dl_compact(const uint8_t* flags, int64_t B, int64_t* act, int32_t* list, int32_t* count,
+                                  hipStream_t s);
+hipError_t pscl_launch_dl_select(const pscl_dl_params& D, int64_t cap, hipStream_t s);
+hipError_t pscl_launch_dl_update(const pscl_dl_params& D, int64_t cap, hipStream_t s);
+hipError_t pscl_launch_dl_gather(const uint64_t* best, const int64_t* act, const int32_t* count, int64_t cap, int W,
+                                 uint64_t* ref, hipStream_t s);
+hipError_t pscl_launch_iota64(int64_t* out, int64_t n, hipStream_t s);
+hipError_t pscl_launch_replay(const pscl_replay_params& R, int64_t cap, hipStream_t s);
+hipError_t pscl_launch_dl_count(const uint64_t* best, const uint8_t* flags, const uint64_t* ref, int64_t B, int W,
+                                int k_payload, int64_t* counters, hipStream_t s);
 
 #endif

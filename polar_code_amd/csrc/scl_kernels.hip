@@ -65,14 +65,17 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
     const int cpath = g & (LMAX - 1);
     const uint32_t cbit = g >= LMAX ? 1u : 0u;
 
-    for (int64_t f0 = ((int64_t)blockIdx.x * wpg + wave) * F; f0 < P.B; f0 += wstride) {
+    // live batch size: P.B, or a device-side count bounded by P.B (DL-SCL retry rounds)
+    const int64_t Bn = P.d_count ? (*P.d_count < P.B ? (int64_t)*P.d_count : P.B) : P.B;
+    for (int64_t f0 = ((int64_t)blockIdx.x * wpg + wave) * F; f0 < Bn; f0 += wstride) {
         const int64_t f = f0 + fl;
-        const bool fvalid = f < P.B;
+        const bool fvalid = f < Bn;
+        const int64_t frow = P.fidx ? P.fidx[fvalid ? f : f0] : (fvalid ? f : f0);
         if (P.rm_E == 0) {  // stage this frame's channel LLRs in LDS (read at every depth-1 use)
-            const double* src = P.llr + (fvalid ? f : f0) * N;
+            const double* src = P.llr + frow * N;
             for (int x = g; x < N; x += G) Af[x] = src[x];
         } else {  // NR: de-rate-match + de-interleave while staging
-            const double* src = P.llr + (fvalid ? f : f0) * P.rm_E;
+            const double* src = P.llr + frow * P.rm_E;
             for (int x = g; x < N; x += G) Af[x] = nr_stage(src, P.rm_src[x], P.rm_E, N);
         }
         wave_lds_fence();
@@ -273,6 +276,16 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
             }
             if (g == best) {
                 const bool bpass = P.has_crc ? (syn == 0) : true;
+                if (HIST && P.best_info_llrs) {
+                    int cur = g, jj = K - 1;
+                    for (int ph = N - 1; ph >= 0; --ph) {
+                        if ((pick_word(P.info_mask[0], P.info_mask[1], ph >> 6) >> (ph & 63)) & 1) {
+                            P.best_info_llrs[f * K + jj] = hist_llr[jj * L + cur];
+                            --jj;
+                        }
+                        cur = hist_par[ph * L + cur];
+                    }
+                }
                 if (P.best) {
                     P.best[f * W] = ib0;
                     if (W > 1) P.best[f * W + 1] = ib1;

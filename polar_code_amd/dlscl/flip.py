@@ -1,10 +1,13 @@
 """DL-SCL bit-flip retries (mirror of dl_scl_polar/dlscl/flip.py:13-141).
 
-Every decode runs on the GPU.  The flip ranking (q = |L0| @ beta, argsort, first untried
-index) stays on the host with exactly the reference's numpy calls -- per frame, on the
-same shapes -- so the ranking (including its tie order and BLAS summation order) is the
-reference's own.  `decode_with_retries_batch` is the throughput form used by the FER
-sweep: one batched GPU decode per retry round over the frames that still fail.
+Every decode runs on the GPU.  Two batch forms:
+  decode_with_retries_device  the whole retry loop on the device (pscl_dlscl_device):
+                              flip choice q = |L0| @ beta summed in index order, argmin over
+                              untried indices (ties -> lower index), compaction per round.
+  decode_with_retries_batch   GPU decodes, flip ranking on the host with exactly the
+                              reference's numpy calls (argsort, BLAS order) per frame.
+The two agree except where two q values of a frame tie within BLAS rounding (numpy's own
+argsort/BLAS order is machine-dependent there); tests hold both to the golden traces.
 """
 from __future__ import annotations
 
@@ -151,4 +154,75 @@ def decode_with_retries_batch(llr: np.ndarray, info_set, M: int, retries: int, *
     return {"best_bits": bits, "success": ok, "attempts": attempts, "tried": tried}
 
 
-__all__ = ["choose_flip_index", "retry_with_flip", "decode_with_retries", "decode_with_retries_batch"]
+def bits_to_words(bits: np.ndarray) -> np.ndarray:
+    """[B, K] 0/1 -> [B, W] uint64, bit j of word j // 64 = bits[:, j]."""
+    bits = np.asarray(bits, dtype=np.uint64)
+    B, K = bits.shape
+    W = (K + 63) // 64 if K else 1
+    out = np.zeros((B, W), np.uint64)
+    for j in range(K):
+        out[:, j >> 6] |= bits[:, j] << np.uint64(j & 63)
+    return out
+
+
+def words_to_bits(words: np.ndarray, K: int) -> np.ndarray:
+    w = np.asarray(words, dtype=np.uint64)
+    sh = np.arange(64, dtype=np.uint64)
+    return ((w[:, :, None] >> sh) & np.uint64(1)).reshape(w.shape[0], -1)[:, :K].astype(np.int8)
+
+
+def decode_with_retries_device(llr: np.ndarray, info_set, M: int, retries: int, *, crc=None, beta=None,
+                               device: int = 0, msg: Optional[np.ndarray] = None) -> dict:
+    """decode_with_retries for a batch [B, N] with the retry loop on the GPU.
+
+    Returns best_bits [B, K] (final attempt), success [B], attempts [B], tried [B, R]
+    (R = max(retries, 0), -1 padded), base_bits / base_pass (the baseline SCL), and with
+    `msg` [B, K] the in-kernel counters {"scl": [...], "dl": [...]} (PSCL_CNT_* order).
+    """
+    llr = np.ascontiguousarray(llr, dtype=np.float64)
+    B, N = llr.shape
+    info_set = np.asarray(info_set)
+    K = info_set.size
+    dec = _native.get_decoder(N, info_set, M, crc, device)
+    W = dec.W
+    R = max(int(retries), 0)
+    out = {}
+    with _native.DeviceArena(dec) as mem:
+        d_llr = mem.alloc(llr.nbytes)
+        mem.upload(d_llr, llr)
+        d_best = mem.alloc(B * W * 8)
+        d_flags = mem.alloc(B)
+        d_att = mem.alloc(B * 4)
+        d_tried = mem.alloc(max(B * R * 4, 4))
+        d_ref = d_cs = d_cd = 0
+        if msg is not None:
+            d_ref = mem.alloc(B * W * 8)
+            mem.upload(d_ref, bits_to_words(msg))
+            d_cs = mem.alloc(_native.PSCL_NCOUNT * 8)
+            d_cd = mem.alloc(_native.PSCL_NCOUNT * 8)
+            mem.memset(d_cs, 0, _native.PSCL_NCOUNT * 8)
+            mem.memset(d_cd, 0, _native.PSCL_NCOUNT * 8)
+        d_bbest = mem.alloc(B * W * 8)
+        d_bflags = mem.alloc(B)
+        dec.decode_device(d_llr, B, d_best=d_bbest, d_flags=d_bflags)
+        dec.dlscl_device(d_llr, B, retries, beta=beta, d_best=d_best, d_flags=d_flags, d_attempts=d_att,
+                         d_tried=d_tried if R else 0, tried_stride=R, d_ref=d_ref, k_payload=K - dec.crc_deg,
+                         d_counters_scl=d_cs, d_counters_dl=d_cd)
+        dec.sync()
+        flags = mem.download(d_flags, B, np.uint8)
+        bflags = mem.download(d_bflags, B, np.uint8)
+        out["best_bits"] = words_to_bits(mem.download(d_best, B * W * 8, np.uint64).reshape(B, W), K)
+        out["success"] = (flags & _native.PSCL_FLAG_CRC_PASS) != 0 if crc is not None else np.ones(B, bool)
+        out["attempts"] = mem.download(d_att, B * 4, np.int32)
+        out["tried"] = (mem.download(d_tried, B * R * 4, np.int32).reshape(B, R) if R
+                        else np.zeros((B, 0), np.int32))
+        out["base_bits"] = words_to_bits(mem.download(d_bbest, B * W * 8, np.uint64).reshape(B, W), K)
+        out["base_pass"] = (bflags & _native.PSCL_FLAG_CRC_PASS) != 0 if crc is not None else np.ones(B, bool)
+        if msg is not None:
+            out["counters"] = {"scl": mem.download(d_cs, _native.PSCL_NCOUNT * 8, np.int64),
+                               "dl": mem.download(d_cd, _native.PSCL_NCOUNT * 8, np.int64)}
+    return out
+
+
+__all__ = ["choose_flip_index", "retry_with_flip", "decode_with_retries", "decode_with_retries_batch",
+           "decode_with_retries_device", "bits_to_words", "words_to_bits"]

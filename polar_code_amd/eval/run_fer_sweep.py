@@ -4,7 +4,9 @@ console lines, CSV schema and plot).
     python -m polar_code_amd.eval.run_fer_sweep --M 8 --frames 2000 --snr_lo 5 --snr_hi 5 \
         --snr_step 0 --retries 8 --beta tests/golden/beta_M8.npy --seed 0 --include_uncoded
 
-Every decode runs on the GPU (libpolar_mi355x.so).  Two channel modes:
+Every decode runs on the GPU (libpolar_mi355x.so); by default the DL-SCL retry loop too
+(--dl_engine device; --dl_engine host ranks flips with the reference's numpy calls).
+Two channel modes:
   --rng replay  (default) the reference's own NumPy PCG64 stream, frame by frame in its draw
                 order (run_fer_sweep.py:61,79-87,111-113): reproduces results/fer_M{4,8}.csv
                 exactly.  Frames are generated on the host and decoded in batches.
@@ -25,7 +27,7 @@ from typing import Dict, List, Tuple
 import numpy as np
 
 from .. import _native, config, dist
-from ..dlscl.flip import decode_with_retries, decode_with_retries_batch
+from ..dlscl.flip import decode_with_retries, decode_with_retries_batch, decode_with_retries_device, words_to_bits
 from ..polar.crc import attach_crc
 from ..polar.polar import construct_info_set, encode
 from ..polar.scl import decode_scl
@@ -91,15 +93,25 @@ def scl_batch(llr, info_set, M, crc, device):
 dl_batch = decode_with_retries_batch
 
 
-def _count_block(c, msg, llr, payload, llr_unc, info_set, M, crc, retries, beta, device):
-    base = scl_batch(llr, info_set, M, crc, device)
-    c[C_FRAMES] += llr.shape[0]
-    c[C_SCL_ERR] += int(np.count_nonzero(~base["crc_pass"]))
-    c[C_SCL_BIT] += int(np.count_nonzero(base["best_bits"] != msg))
-    dl = dl_batch(llr, info_set, M, retries, crc=crc, beta=beta, device=device, baseline=base)
-    c[C_DL_ERR] += int(np.count_nonzero(~dl["success"]))
-    c[C_DL_BIT] += int(np.count_nonzero(dl["best_bits"] != msg))
-    c[C_DL_WORK] += int((dl["attempts"] - 1).sum())
+def _count_block(c, msg, llr, payload, llr_unc, info_set, M, crc, retries, beta, device, engine="device"):
+    if engine == "device":  # SCL + the whole DL-SCL retry loop on the GPU
+        out = decode_with_retries_device(llr, info_set, M, retries, crc=crc, beta=beta, device=device, msg=msg)
+        cs, cd = out["counters"]["scl"], out["counters"]["dl"]
+        c[C_FRAMES] += llr.shape[0]
+        c[C_SCL_ERR] += int(cs[_native.CNT_FRAME_ERR])
+        c[C_SCL_BIT] += int(cs[_native.CNT_BIT_ERR])
+        c[C_DL_ERR] += int(cd[_native.CNT_FRAME_ERR])
+        c[C_DL_BIT] += int(cd[_native.CNT_BIT_ERR])
+        c[C_DL_WORK] += int(cd[_native.CNT_RETRIES])
+    else:  # GPU decodes, flip ranking with the reference's numpy calls on the host
+        base = scl_batch(llr, info_set, M, crc, device)
+        c[C_FRAMES] += llr.shape[0]
+        c[C_SCL_ERR] += int(np.count_nonzero(~base["crc_pass"]))
+        c[C_SCL_BIT] += int(np.count_nonzero(base["best_bits"] != msg))
+        dl = dl_batch(llr, info_set, M, retries, crc=crc, beta=beta, device=device, baseline=base)
+        c[C_DL_ERR] += int(np.count_nonzero(~dl["success"]))
+        c[C_DL_BIT] += int(np.count_nonzero(dl["best_bits"] != msg))
+        c[C_DL_WORK] += int((dl["attempts"] - 1).sum())
     c[C_BITS] += msg.size
     if llr_unc is not None:
         errs = np.count_nonzero((llr_unc < 0).astype(np.int8) != payload, axis=1)
@@ -109,8 +121,8 @@ def _count_block(c, msg, llr, payload, llr_unc, info_set, M, crc, retries, beta,
 
 
 def _philox_block(c, seed, snr_db, frame0, n, info_set, M, crc, retries, beta, device, include_uncoded,
-                  payload_bits):
-    """n frames generated on the device; SCL counted in-kernel, failing frames retried."""
+                  payload_bits, engine="device"):
+    """n frames generated on the device; SCL and DL-SCL counted on the device."""
     cfg = config.get_config()
     dec = _native.get_decoder(cfg.N, info_set, M, crc, device)
     W = dec.W
@@ -119,34 +131,42 @@ def _philox_block(c, seed, snr_db, frame0, n, info_set, M, crc, retries, beta, d
         d_msg = mem.alloc(n * W * 8)
         d_best = mem.alloc(n * W * 8)
         d_flags = mem.alloc(n)
-        d_cnt = mem.alloc(8 * 8)
-        mem.memset(d_cnt, 0, 64)
+        d_cs = mem.alloc(_native.PSCL_NCOUNT * 8)
+        d_cd = mem.alloc(_native.PSCL_NCOUNT * 8)
+        mem.memset(d_cs, 0, _native.PSCL_NCOUNT * 8)
+        mem.memset(d_cd, 0, _native.PSCL_NCOUNT * 8)
         dec.channel_device(seed, int(round(snr_db * 10)), snr_db, cfg.K / cfg.N, payload_bits, frame0, n, d_llr, d_msg)
-        dec.decode_device(d_llr, n, d_best=d_best, d_flags=d_flags, d_ref=d_msg, k_payload=payload_bits,
-                          d_counters=d_cnt)
-        cnt = mem.download(d_cnt, 64, np.int64)
-        flags = mem.download(d_flags, n, np.uint8)
-        c[C_FRAMES] += n
-        c[C_SCL_ERR] += int(cnt[_native.CNT_FRAME_ERR])
-        c[C_SCL_BIT] += int(cnt[_native.CNT_BIT_ERR])
-        c[C_BITS] += n * cfg.K
-        fail = np.flatnonzero((flags & _native.PSCL_FLAG_CRC_PASS) == 0)
-        dl_bit = int(cnt[_native.CNT_BIT_ERR])
-        if fail.size and retries > 0:
-            llr_all = mem.download(d_llr, n * cfg.N * 8, np.float64).reshape(n, cfg.N)
-            msg_w = mem.download(d_msg, n * W * 8, np.uint64).reshape(n, W)
-            best_w = mem.download(d_best, n * W * 8, np.uint64).reshape(n, W)
-            bits_of = lambda w: ((w[:, :, None] >> np.arange(64, dtype=np.uint64)) & 1).reshape(w.shape[0], -1)[:, :cfg.K]
-            msg_f = bits_of(msg_w[fail]).astype(np.int8)
-            base_f = bits_of(best_w[fail]).astype(np.int8)
-            dl = decode_with_retries_batch(llr_all[fail], info_set, M, retries, crc=crc, beta=beta, device=device,
-                                           baseline={"best_bits": base_f, "crc_pass": np.zeros(fail.size, bool)})
-            c[C_DL_ERR] += int(np.count_nonzero(~dl["success"]))
-            dl_bit += int(np.count_nonzero(dl["best_bits"] != msg_f)) - int(np.count_nonzero(base_f != msg_f))
-            c[C_DL_WORK] += int((dl["attempts"] - 1).sum())
+        if engine == "device":
+            dec.dlscl_device(d_llr, n, retries, beta=beta, d_best=d_best, d_flags=d_flags, d_ref=d_msg,
+                             k_payload=payload_bits, d_counters_scl=d_cs, d_counters_dl=d_cd)
+            cs = mem.download(d_cs, 64, np.int64)
+            cd = mem.download(d_cd, 64, np.int64)
+            c[C_DL_ERR] += int(cd[_native.CNT_FRAME_ERR])
+            c[C_DL_BIT] += int(cd[_native.CNT_BIT_ERR])
+            c[C_DL_WORK] += int(cd[_native.CNT_RETRIES])
         else:
-            c[C_DL_ERR] += int(fail.size)
-        c[C_DL_BIT] += dl_bit
+            dec.decode_device(d_llr, n, d_best=d_best, d_flags=d_flags, d_ref=d_msg, k_payload=payload_bits,
+                              d_counters=d_cs)
+            cs = mem.download(d_cs, 64, np.int64)
+            flags = mem.download(d_flags, n, np.uint8)
+            fail = np.flatnonzero((flags & _native.PSCL_FLAG_CRC_PASS) == 0)
+            dl_bit = int(cs[_native.CNT_BIT_ERR])
+            if fail.size and retries > 0:
+                llr_all = mem.download(d_llr, n * cfg.N * 8, np.float64).reshape(n, cfg.N)
+                msg_f = words_to_bits(mem.download(d_msg, n * W * 8, np.uint64).reshape(n, W)[fail], cfg.K)
+                base_f = words_to_bits(mem.download(d_best, n * W * 8, np.uint64).reshape(n, W)[fail], cfg.K)
+                dl = decode_with_retries_batch(llr_all[fail], info_set, M, retries, crc=crc, beta=beta, device=device,
+                                               baseline={"best_bits": base_f, "crc_pass": np.zeros(fail.size, bool)})
+                c[C_DL_ERR] += int(np.count_nonzero(~dl["success"]))
+                dl_bit += int(np.count_nonzero(dl["best_bits"] != msg_f)) - int(np.count_nonzero(base_f != msg_f))
+                c[C_DL_WORK] += int((dl["attempts"] - 1).sum())
+            else:
+                c[C_DL_ERR] += int(fail.size)
+            c[C_DL_BIT] += dl_bit
+        c[C_FRAMES] += n
+        c[C_SCL_ERR] += int(cs[_native.CNT_FRAME_ERR])
+        c[C_SCL_BIT] += int(cs[_native.CNT_BIT_ERR])
+        c[C_BITS] += n * cfg.K
     if include_uncoded:
         rng = np.random.default_rng([seed, int(round(snr_db * 10)), frame0])
         _, _, var_u, sig_u = noise_params(snr_db, cfg.K / cfg.N)
@@ -178,10 +198,11 @@ def run_sweep(args: argparse.Namespace) -> List[Dict[str, float]]:
             if args.rng == "replay":
                 payload, msg, llr, llr_unc = replay_stream(args.seed, float(snr_db), b0, b1, payload_bits,
                                                            cfg.crc_poly, args.include_uncoded)
-                _count_block(c, msg, llr, payload, llr_unc, info_set, args.M, cfg.crc_poly, args.retries, beta, device)
+                _count_block(c, msg, llr, payload, llr_unc, info_set, args.M, cfg.crc_poly, args.retries, beta, device,
+                             args.dl_engine)
             else:
                 _philox_block(c, args.seed, float(snr_db), b0, b1 - b0, info_set, args.M, cfg.crc_poly, args.retries,
-                              beta, device, args.include_uncoded, payload_bits)
+                              beta, device, args.include_uncoded, payload_bits, args.dl_engine)
         c = dist.allreduce_sum(c, ctx)
         total_frames = args.frames
         scl_fer = c[C_SCL_ERR] / total_frames
@@ -275,6 +296,8 @@ def build_argparser() -> argparse.ArgumentParser:
     parser.add_argument("--rng", choices=["replay", "philox"], default="replay",
                         help="replay: reference NumPy stream (exact); philox: on-device generation")
     parser.add_argument("--batch", type=int, default=1 << 16, help="frames per GPU batch")
+    parser.add_argument("--dl_engine", choices=["device", "host"], default="device",
+                        help="device: DL-SCL retry loop on the GPU; host: numpy flip ranking (reference calls)")
     parser.add_argument("--no_plot", action="store_true")
     parser.add_argument("--verbose", action="store_true")
     return parser

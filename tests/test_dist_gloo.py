@@ -75,7 +75,7 @@ def test_shard_ranges_cover_exactly():
 
 def test_two_rank_sweep_equals_one_rank(tmp_path):
     argv = ["--M", "4", "--frames", "601", "--snr_lo", "4.5", "--snr_hi", "5", "--snr_step", "0.5", "--retries", "8",
-            "--beta", str(ROOT / "tests" / "golden" / "beta_M4.npy"), "--include_uncoded", "--batch", "128"]
+            "--beta", str(ROOT / "tests" / "golden" / "beta_M4.npy"), "--include_uncoded", "--batch", "128", "--dl_engine", "host"]
     (tmp_path / "w1").mkdir()
     (tmp_path / "w2").mkdir()
     _run(1, tmp_path / "w1", argv)

@@ -2,8 +2,9 @@
 
 * run_fer_sweep --rng replay (the reference's own NumPy stream, HIP decoder) writes a CSV
   byte-identical to the reference's results/fer_M{8,4}.csv.
-* DL-SCL retries (decode_with_retries and the batched form) match the reference's golden
-  retry traces.
+* DL-SCL retries (decode_with_retries, the host-ranked batch form and the on-device retry
+  loop) match the reference's golden retry traces; the device loop equals the host-ranked
+  form frame for frame on larger sets.
 * --rng philox (on-device channel): FER within Monte-Carlo error of the reference.
 """
 import math
@@ -11,7 +12,7 @@ import math
 import numpy as np
 import pytest
 
-from polar_code_amd.dlscl.flip import decode_with_retries, decode_with_retries_batch
+from polar_code_amd.dlscl.flip import decode_with_retries, decode_with_retries_batch, decode_with_retries_device
 from polar_code_amd.eval import run_fer_sweep
 
 from conftest import GOLDEN
@@ -19,11 +20,13 @@ from conftest import GOLDEN
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("engine", ["device", "host"])
 @pytest.mark.parametrize("M", [8, 4])
-def test_cli_replay_reproduces_reference_csv(tmp_path, M):
+def test_cli_replay_reproduces_reference_csv(tmp_path, M, engine):
     run_fer_sweep.main(["--M", str(M), "--frames", "2000", "--snr_lo", "5", "--snr_hi", "5", "--snr_step", "0",
                         "--retries", "8", "--beta", str(GOLDEN / f"beta_M{M}.npy"), "--seed", "0",
-                        "--include_uncoded", "--out_dir", str(tmp_path), "--plot_dir", str(tmp_path), "--no_plot"])
+                        "--include_uncoded", "--out_dir", str(tmp_path), "--plot_dir", str(tmp_path), "--no_plot",
+                        "--dl_engine", engine])
     got = (tmp_path / f"fer_M{M}.csv").read_text()
     assert got == (GOLDEN / f"ref_fer_M{M}.csv").read_text()
 
@@ -43,6 +46,52 @@ def test_flip_retries_golden(golden):
         np.testing.assert_array_equal(batch["success"], g[f"{tag}_success"])
         np.testing.assert_array_equal(batch["attempts"], g[f"{tag}_attempts"])
         np.testing.assert_array_equal(batch["tried"], g[f"{tag}_tried"])
+
+
+def test_device_retry_loop_golden(golden):
+    g = golden("g7_flip.npz")
+    for tag, beta in (("beta", g["beta"]), ("none", None)):
+        out = decode_with_retries_device(g["llr"], g["info"], 4, 8, crc="0x1864CFB", beta=beta, msg=g["msg"])
+        np.testing.assert_array_equal(out["best_bits"], g[f"{tag}_bits"])
+        np.testing.assert_array_equal(out["success"], g[f"{tag}_success"])
+        np.testing.assert_array_equal(out["attempts"], g[f"{tag}_attempts"])
+        np.testing.assert_array_equal(out["tried"], g[f"{tag}_tried"])
+        cd = out["counters"]["dl"]
+        assert cd[0] == len(g["llr"]) and cd[1] == int((~g[f"{tag}_success"].astype(bool)).sum())
+        assert cd[5] == int((g[f"{tag}_attempts"] - 1).sum())
+
+
+@pytest.mark.parametrize("M,retries,ebno", [(4, 8, 3.0), (8, 8, 3.5), (2, 3, 3.0), (1, 70, 4.0)])
+def test_device_retry_loop_equals_host_ranking(M, retries, ebno):
+    """Device retry loop == numpy-ranked retries, frame by frame (3000 frames, ~30% failing)."""
+    from polar_code_amd.polar.polar import construct_info_set, encode
+    from polar_code_amd.polar.crc import attach_crc
+
+    rng = np.random.default_rng(M * 100 + retries)
+    info = construct_info_set(128, 64)
+    msg = attach_crc(rng.integers(0, 2, size=(3000, 40), dtype=np.int8), "0x1864CFB")
+    var = 1.0 / (2.0 * 0.5 * 10 ** (ebno / 10))
+    llr = 2.0 * ((1.0 - 2.0 * encode(msg)) + rng.normal(0, math.sqrt(var), size=(3000, 128))) / var
+    beta = np.load(GOLDEN / "beta_M4.npy")
+    for b in (beta, None):
+        dev = decode_with_retries_device(llr, info, M, retries, crc="0x1864CFB", beta=b)
+        host = decode_with_retries_batch(llr, info, M, retries, crc="0x1864CFB", beta=b)
+        assert 0.05 < (~dev["base_pass"]).mean() < 0.9
+        np.testing.assert_array_equal(dev["tried"], host["tried"])
+        np.testing.assert_array_equal(dev["attempts"], host["attempts"])
+        np.testing.assert_array_equal(dev["best_bits"], host["best_bits"])
+        np.testing.assert_array_equal(dev["success"], host["success"])
+
+
+def test_philox_device_and_host_dl_engines_agree(tmp_path):
+    rows = {}
+    for engine in ("device", "host"):
+        rows[engine] = run_fer_sweep.run_sweep(run_fer_sweep.build_argparser().parse_args(
+            ["--M", "4", "--frames", "60000", "--snr_lo", "3.5", "--snr_hi", "4", "--snr_step", "0.5", "--retries",
+             "8", "--beta", str(GOLDEN / "beta_M4.npy"), "--rng", "philox", "--batch", "30000", "--out_dir",
+             str(tmp_path), "--plot_dir", str(tmp_path), "--no_plot", "--dl_engine", engine]))
+    assert rows["device"] == rows["host"]
+    assert rows["device"][0]["fer_dl"] < rows["device"][0]["fer_scl"]
 
 
 def test_philox_fer_matches_reference_statistically(tmp_path):

@@ -158,3 +158,23 @@ def test_scl_decoder_batch_and_device_api():
     dev_bits = ((w[:, None] >> np.arange(64, dtype=np.uint64)) & 1).astype(np.int8)
     np.testing.assert_array_equal(dev_bits, bits)
     np.testing.assert_array_equal((flags.cpu().numpy() & 0x80) != 0, ok)
+
+
+@pytest.mark.parametrize("N,K,L,E", [(128, 64, 8, 0), (128, 64, 4, 0), (64, 40, 4, 0), (32, 20, 2, 0),
+                                     (128, 88, 2, 0), (16, 8, 16, 0), (128, 64, 8, 200), (128, 64, 2, 300)])
+def test_path_llr_replay_equals_decoder_history(N, K, L, E):
+    """pscl_path_llrs_device (replay from a path's bits) == the decoder's info_llrs, bit for bit."""
+    rng = np.random.default_rng(N * 1000 + K + L + E)
+    info = construct_info_set(N, K)
+    B = 600
+    llr = rng.normal(1.0, 2.5, size=(B, E or N)) * rng.choice([1.0, -1.0], size=(B, E or N))
+    dec = _native.Decoder(N, info, L, "0x1864CFB" if K > 24 else None)
+    if E:
+        dec.set_rate_match(E)
+    out = dec.decode(llr, want_metrics=False)
+    rows = np.repeat(np.arange(B), L)
+    valid = (np.arange(L)[None, :] < out["n_paths"][:, None]).ravel()
+    cands = out["cands"].reshape(B * L, K)[valid]
+    got = dec.path_llrs(llr[rows[valid]], cands)
+    want = out["info_llrs"].reshape(B * L, K)[valid]
+    np.testing.assert_array_equal(got.view(np.uint64), want.view(np.uint64))
