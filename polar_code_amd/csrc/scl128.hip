@@ -8,7 +8,7 @@
 // LDS slot of each stored depth); lane g + LMAX is that path's bit-1 child while the list is
 // extended, and otherwise evaluates the sibling leaf's metric tail (below).
 //
-// LLR tree, per frame in LDS: the 128 channel LLRs and, per path slot, depths 3..6
+// LLR tree, per frame in LDS: (with rate matching) the 128 channel LLRs and, per path slot, depths 3..6
 // (16 + 8 + 4 + 2 values).  Depths 1 and 2 are never stored: every 16th phase the lanes
 // recompute the 16 depth-3 values of each path directly from 8 channel LLRs each (f/g through
 // depths 1-3), which halves the LDS footprint per frame and with it raises occupancy.
@@ -36,13 +36,17 @@ using namespace pscl;
 constexpr int kN = 128;
 constexpr int kn = 7;
 
-template <int LMAX>
+// CH: the frame's channel LLRs are staged in LDS (needed when the decode input is rate
+// matched: the de-rate-matched values exist nowhere else); otherwise the depth-1..3
+// recomputes read them straight from the (L2/MALL-resident) input row, which halves the
+// LDS per frame and lets the wave count reach the register limit.
+template <int LMAX, bool CH>
 struct Layout128 {
     static constexpr int G = 2 * LMAX;
     static constexpr int F = 64 / G;
     static constexpr int LOG_G = __builtin_ctz(G);
     static constexpr int LOG_LM = __builtin_ctz(LMAX);
-    static constexpr int OFF3 = kN;                 // [LMAX][16]
+    static constexpr int OFF3 = CH ? kN : 0;        // [LMAX][16]
     static constexpr int OFF4 = OFF3 + 16 * LMAX;   // [LMAX][8]
     static constexpr int OFF5 = OFF4 + 8 * LMAX;    // [LMAX][4]
     static constexpr int OFF6 = OFF5 + 4 * LMAX;    // [LMAX][2]
@@ -59,9 +63,9 @@ __device__ __forceinline__ uint64_t seg_transform(uint64_t u0, uint64_t u1, int 
 }
 
 // depth-d step (d = 4, 5, 6) of the tree walk for all frames and path slots of the wave
-template <int LMAX, int D>
+template <int LMAX, bool CH, int D>
 __device__ __forceinline__ void step_depth(double* A, int lane, uint32_t tab, uint32_t xs, bool first, bool is_g) {
-    using Ly = Layout128<LMAX>;
+    using Ly = Layout128<LMAX, CH>;
     constexpr int LW = kn - D, W = 1 << LW;
     constexpr int OFF_OUT = D == 4 ? Ly::OFF4 : (D == 5 ? Ly::OFF5 : Ly::OFF6);
     constexpr int OFF_IN = D == 4 ? Ly::OFF3 : (D == 5 ? Ly::OFF4 : Ly::OFF5);
@@ -85,9 +89,9 @@ __device__ __forceinline__ void step_depth(double* A, int lane, uint32_t tab, ui
     wave_lds_fence();
 }
 
-template <int LMAX, bool HIST>
+template <int LMAX, bool HIST, bool CH>
 __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(const pscl_decode_params P) {
-    using Ly = Layout128<LMAX>;
+    using Ly = Layout128<LMAX, CH>;
     constexpr int G = Ly::G, F = Ly::F, LOG_G = Ly::LOG_G;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint64_t* T = reinterpret_cast<uint64_t*>(smem);
@@ -119,13 +123,15 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
         const int64_t f = f0 + fl;
         const bool fvalid = f < Bn;
         const int64_t frow = P.fidx ? P.fidx[fvalid ? f : f0] : (fvalid ? f : f0);
-        if (P.rm_E == 0) {
-            const double* src = P.llr + frow * kN;
+        const double* chan = P.llr + frow * kN;  // !CH: channel LLRs read in place
+        if (CH) {
+            if (P.rm_E == 0) {
 #pragma unroll
-            for (int x = 0; x < kN / G; ++x) Af[g + x * G] = src[g + x * G];
-        } else {  // NR: de-rate-match + de-interleave while staging
-            const double* src = P.llr + frow * P.rm_E;
-            for (int x = 0; x < kN / G; ++x) Af[g + x * G] = nr_stage(src, P.rm_src[g + x * G], P.rm_E, kN);
+                for (int x = 0; x < kN / G; ++x) Af[g + x * G] = chan[g + x * G];
+            } else {  // NR: de-rate-match + de-interleave while staging
+                const double* src = P.llr + frow * P.rm_E;
+                for (int x = 0; x < kN / G; ++x) Af[g + x * G] = nr_stage(src, P.rm_src[g + x * G], P.rm_E, kN);
+            }
         }
         uint64_t fm0 = 0, fm1 = 0, fv0 = 0, fv1 = 0;
         if (P.force && fvalid) {
@@ -171,7 +177,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
                     const int e = g + G * q;
                     double c[8];
 #pragma unroll
-                    for (int m = 0; m < 8; ++m) c[m] = Af[e + 16 * m];
+                    for (int m = 0; m < 8; ++m) c[m] = CH ? Af[e + 16 * m] : chan[e + 16 * m];
                     double d1l[4];
 #pragma unroll
                     for (int m = 0; m < 4; ++m) d1l[m] = f_minsum(c[m], c[m + 4]);
@@ -204,9 +210,9 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
                 xs = polar_transform8((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)) & ((1u << w) - 1u));
             }
             if (!(PSCL_ABLATE & 4)) {
-                if (start <= 4) step_depth<LMAX, 4>(A, lane, tab, xs, start == 4, start == 4 && phi);
-                if (start <= 5) step_depth<LMAX, 5>(A, lane, tab, xs, start == 5, start == 5);
-                if (start <= 6) step_depth<LMAX, 6>(A, lane, tab, xs, start == 6, start == 6);
+                if (start <= 4) step_depth<LMAX, CH, 4>(A, lane, tab, xs, start == 4, start == 4 && phi);
+                if (start <= 5) step_depth<LMAX, CH, 5>(A, lane, tab, xs, start == 5, start == 5);
+                if (start <= 6) step_depth<LMAX, CH, 6>(A, lane, tab, xs, start == 6, start == 6);
             }
             if (start <= 6) {
                 const int s0 = start < 3 ? 3 : start;
@@ -362,23 +368,28 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
         atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
 }
 
+template <int LMAX, bool HIST>
+hipError_t launch128h(const pscl_decode_params& P, int wpg, int64_t grid, int lds, hipStream_t s) {
+    if (P.rm_E)
+        hipLaunchKernelGGL((scl128_kernel<LMAX, HIST, true>), dim3((unsigned)grid), dim3(wpg * 64), lds, s, P);
+    else
+        hipLaunchKernelGGL((scl128_kernel<LMAX, HIST, false>), dim3((unsigned)grid), dim3(wpg * 64), lds, s, P);
+    return hipGetLastError();
+}
+
 template <int LMAX>
 hipError_t launch128(const pscl_decode_params& P, int hist, int wpg, int64_t grid, int lds, hipStream_t s) {
-    if (hist)
-        hipLaunchKernelGGL((scl128_kernel<LMAX, true>), dim3((unsigned)grid), dim3(wpg * 64), lds, s, P);
-    else
-        hipLaunchKernelGGL((scl128_kernel<LMAX, false>), dim3((unsigned)grid), dim3(wpg * 64), lds, s, P);
-    return hipGetLastError();
+    return hist ? launch128h<LMAX, true>(P, wpg, grid, lds, s) : launch128h<LMAX, false>(P, wpg, grid, lds, s);
 }
 
 }  // namespace
 
-int pscl_fast128_fstride(int L) {
+int pscl_fast128_fstride(int L, int ch) {
     switch (pscl_decode_lmax(L)) {
-        case 1: return Layout128<1>::FSTRIDE;
-        case 2: return Layout128<2>::FSTRIDE;
-        case 4: return Layout128<4>::FSTRIDE;
-        default: return Layout128<8>::FSTRIDE;
+        case 1: return ch ? Layout128<1, true>::FSTRIDE : Layout128<1, false>::FSTRIDE;
+        case 2: return ch ? Layout128<2, true>::FSTRIDE : Layout128<2, false>::FSTRIDE;
+        case 4: return ch ? Layout128<4, true>::FSTRIDE : Layout128<4, false>::FSTRIDE;
+        default: return ch ? Layout128<8, true>::FSTRIDE : Layout128<8, false>::FSTRIDE;
     }
 }
 

@@ -96,7 +96,7 @@ struct pscl_channel_params {
 int pscl_decode_lmax(int L);
 // fills P.a_bytes / P.wave_bytes / P.fast for the kernel that will decode this shape
 void pscl_decode_layout(pscl_decode_params& P, int hist);
-int pscl_fast128_fstride(int L);
+int pscl_fast128_fstride(int L, int ch);
 hipError_t pscl_launch_decode128(const pscl_decode_params& P, int hist, int wpg, int64_t grid, int lds, hipStream_t s);
 int64_t pscl_decode_grid(const pscl_decode_params& P);
 int pscl_decode_wpg(const pscl_decode_params& P);

@@ -461,7 +461,7 @@ void pscl_decode_layout(pscl_decode_params& P, int hist) {
     const int F = 32 / lmax;  // frames per wavefront
     P.fast = (P.N == 128 && P.L <= 8) ? 1 : 0;
     if (P.fast) {
-        P.a_bytes = F * pscl_fast128_fstride(P.L) * 8;
+        P.a_bytes = F * pscl_fast128_fstride(P.L, P.rm_E != 0) * 8;
         const int wb = P.a_bytes + (hist ? F * P.K * P.L * 9 : 0);
         P.wave_bytes = (wb + 15) & ~15;
     } else {
