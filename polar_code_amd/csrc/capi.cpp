@@ -92,6 +92,8 @@ struct pscl_handle {
     int32_t* d_rm_order = nullptr;    // [N] interleaver order
     DevBuf scratch[28];
     double* d_beta = nullptr;         // [K][K] DL-SCL flip metric (null = |L0|)
+    uint64_t* d_epi = nullptr;        // scl128 epilogue tables (gather + syndrome)
+    int epi_words = 0;
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
@@ -132,6 +134,8 @@ void fill_decode_params(const pscl_handle* h, pscl_decode_params& P, int hist) {
     P.info_set = h->d_info_set;
     P.has_crc = h->crc_poly != 0;
     P.exp_table = h->d_exp_table;
+    P.epi_table = h->d_epi;
+    P.epi_words = h->epi_words;
     P.rm_E = h->rm_E;
     P.rm_src = h->d_rm_src;
     pscl_decode_layout(P, hist);
@@ -251,6 +255,36 @@ int pscl_create(pscl_handle** out, int device, int N, const int32_t* info_set, i
     CREATE_TRY(hipMemcpy(h->d_attach_cols, h->attach_cols.data(), h->attach_cols.size() * 4, hipMemcpyHostToDevice));
     if (K > 0) CREATE_TRY(hipMemcpy(h->d_info_set, h->info_set.data(), (size_t)K * 4, hipMemcpyHostToDevice));
     CREATE_TRY(hipMemcpy(h->d_exp_table, kExpTable, sizeof(kExpTable), hipMemcpyHostToDevice));
+    {
+        // scl128 epilogue: gather[k][v] = the information bits of u-byte k (value v), compacted
+        // in index order; syn[m][v] = XOR of the CRC check columns of info bits 4m..4m+3 set in v
+        const int k4 = (K + 3) / 4;
+        std::vector<uint8_t> epi((size_t)16 * 256 + (size_t)k4 * 16 * 4, 0);
+        for (int k = 0; k < 16; ++k)
+            for (int v = 0; v < 256; ++v) {
+                int c = 0, cntb = 0;
+                for (int t = 0; t < 8; ++t) {
+                    const int p = 8 * k + t;
+                    if (p < 128 && ((h->info_mask[p >> 6] >> (p & 63)) & 1ULL)) {
+                        if ((v >> t) & 1) c |= 1 << cntb;
+                        cntb++;
+                    }
+                }
+                epi[(size_t)k * 256 + v] = (uint8_t)c;
+            }
+        uint32_t* syn = reinterpret_cast<uint32_t*>(epi.data() + 16 * 256);
+        for (int m = 0; m < k4; ++m)
+            for (int v = 0; v < 16; ++v) {
+                uint32_t acc = 0;
+                for (int t = 0; t < 4; ++t)
+                    if (4 * m + t < K && ((v >> t) & 1)) acc ^= h->check_cols[(size_t)(4 * m + t)];
+                syn[m * 16 + v] = acc;
+            }
+        epi.resize((epi.size() + 7) & ~(size_t)7, 0);
+        h->epi_words = (int)(epi.size() / 8);
+        CREATE_TRY(hipMalloc(&h->d_epi, epi.size()));
+        CREATE_TRY(hipMemcpy(h->d_epi, epi.data(), epi.size(), hipMemcpyHostToDevice));
+    }
 #undef CREATE_TRY
     *out = h;
     return PSCL_OK;
@@ -270,6 +304,7 @@ int pscl_destroy(pscl_handle* h) {
     if (h->d_rm_src) hipFree(h->d_rm_src);
     if (h->d_rm_order) hipFree(h->d_rm_order);
     if (h->d_beta) hipFree(h->d_beta);
+    if (h->d_epi) hipFree(h->d_epi);
     if (h->own_stream) hipStreamDestroy(h->own_stream);
     delete h;
     return PSCL_OK;

@@ -96,7 +96,10 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint64_t* T = reinterpret_cast<uint64_t*>(smem);
     for (int i = threadIdx.x; i < PSCL_EXP_TABLE_WORDS; i += blockDim.x) T[i] = P.exp_table[i];
+    for (int i = threadIdx.x; i < P.epi_words; i += blockDim.x) T[PSCL_EXP_TABLE_WORDS + i] = P.epi_table[i];
     __syncthreads();
+    const uint8_t* GT = reinterpret_cast<const uint8_t*>(T + PSCL_EXP_TABLE_WORDS);  // [16][256]
+    const uint32_t* ST = reinterpret_cast<const uint32_t*>(GT + 16 * 256);           // [K4][16]
 
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
@@ -104,7 +107,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
     const int g = lane & (G - 1);
     const int gbase = lane & ~(G - 1);
     const int K = P.K, L = P.L;
-    unsigned char* wbase = smem + PSCL_EXP_TABLE_WORDS * 8 + (size_t)wave * P.wave_bytes;
+    unsigned char* wbase = smem + P.wg_fixed_bytes + (size_t)wave * P.wave_bytes;
     double* A = reinterpret_cast<double*>(wbase);
     double* Af = A + fl * Ly::FSTRIDE;
     double* hist_llr = reinterpret_cast<double*>(wbase + P.a_bytes) + (size_t)fl * K * L;
@@ -158,7 +161,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
             const uint64_t infow = phi < 64 ? info0 : info1;
             const bool is_info = (infow >> (phi & 63)) & 1;
             // ---- depths 1-3 recomputed from the channel (phi % 16 == 0)
-            if (start <= 3 && !(PSCL_ABLATE & 4)) {
+            if (start <= 3 && !(PSCL_ABLATE & 12)) {
                 const bool r1 = phi >= 64, r2 = (phi >> 5) & 1, r3 = (phi >> 4) & 1;
                 // path lanes: partial sums of the left siblings at depths 1, 2, 3
                 uint64_t X1 = 0;
@@ -214,14 +217,10 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
                 if (start <= 5) step_depth<LMAX, CH, 5>(A, lane, tab, xs, start == 5, start == 5);
                 if (start <= 6) step_depth<LMAX, CH, 6>(A, lane, tab, xs, start == 6, start == 6);
             }
-            if (start <= 6) {
+            if (start <= 6) {  // this path's own slot at every depth rewritten this phase
                 const int s0 = start < 3 ? 3 : start;
-                uint32_t mask = 0, val = 0;
-                for (int d = s0; d <= 6; ++d) {
-                    mask |= 15u << (4 * (d - 3));
-                    val |= (uint32_t)cpath << (4 * (d - 3));
-                }
-                tab = (tab & ~mask) | val;
+                const uint32_t mask = (0xffffu << (4 * (s0 - 3))) & 0xffffu;
+                tab = (tab & ~mask) | ((uint32_t)cpath * 0x1111u & mask);
             }
             // ---- leaf LLRs.  Lanes >= LMAX: the sibling leaf (phi+1) given bit 0 here.
             const uint32_t tab_lo = from_lower_half<G, LMAX>(tab, lane);
@@ -229,7 +228,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
             const double* par = Af + Ly::OFF6 + slot_at(ptab, 6) * 2;
             const double la = par[0], lb = par[1];
             const uint32_t xleaf = phi ? (uint32_t)((phi - 1 < 64 ? u0 >> (phi - 1) : u1 >> (phi - 65)) & 1u) : 0u;
-            const double lam = path_lane ? ((phi & 1) ? g_node(la, lb, xleaf) : f_minsum(la, lb)) : lb + la;
+            const double lam = (PSCL_ABLATE & 128) ? la : (path_lane ? ((phi & 1) ? g_node(la, lb, xleaf) : f_minsum(la, lb)) : lb + la);
             // ---- metric tail log1p(exp(-|llr|)) (scl.py:102-105)
             double Lt;
             const uint64_t lpre_up = from_upper_half64<G, LMAX>(pscl_asu64(Lpre), lane);
@@ -260,7 +259,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
                     kt = kt_lo;
                 }
                 uint32_t r = 0;
-                if (!(PSCL_ABLATE & 2)) rank_step_n<G, 1, LMAX>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
+                if (!(PSCL_ABLATE & 18)) rank_step_n<G, 1, LMAX>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
                 if (path_lane) rank = r;
             } else {
                 // info: children (bit 0 in lane g, bit 1 in lane g + LMAX) of every path
@@ -287,14 +286,15 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
                 if (!(PSCL_ABLATE & 2)) rank_step<G, 1>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
                 else r = kt & 15u;
                 // survivor with list position r -> lane r of the group (push), scl.py:174
-                const int c = __builtin_amdgcn_ds_permute((gbase + (int)(r & (G - 1))) << 2, g);
+                const int c = (PSCL_ABLATE & 32) ? g : __builtin_amdgcn_ds_permute((gbase + (int)(r & (G - 1))) << 2, g);
                 const int cc = (g < ncnt) ? c : g;
                 const int par_g = cc & (LMAX - 1);
                 const uint32_t b = cc >= LMAX ? 1u : 0u;
                 const int ps2 = gbase + par_g;
-                const uint64_t nm = shfl_u64(km, gbase + cc);
-                const uint64_t nu0 = shfl_u64(u0, ps2), nu1 = shfl_u64(u1, ps2);
-                const uint32_t ntab = bperm32(tab, ps2);
+                const uint64_t nm = (PSCL_ABLATE & 32) ? km : shfl_u64(km, gbase + cc);
+                const uint64_t nu0 = (PSCL_ABLATE & 32) ? u0 : shfl_u64(u0, ps2);
+                const uint64_t nu1 = (PSCL_ABLATE & 32) ? u1 : shfl_u64(u1, ps2);
+                const uint32_t ntab = (PSCL_ABLATE & 32) ? tab : bperm32(tab, ps2);
                 if (HIST) {
                     const uint64_t plam_h = shfl_u64(pscl_asu64(lam), ps2);
                     if (g < ncnt && path_lane) {
@@ -316,13 +316,29 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
         }
 
         // ---- epilogue: u[info_set] and its CRC syndrome, best = lowest-ranked CRC pass
+        // (LDS tables: u-byte gather, then ib-nibble syndrome)
         uint64_t ib0 = 0, ib1 = 0;
         uint32_t syn = 0;
-        for (int jj = 0; jj < K; ++jj) {
-            const int ph = P.info_set[jj];
-            const uint64_t bit = ((ph < 64 ? u0 : u1) >> (ph & 63)) & 1ULL;
-            if (jj < 64) ib0 |= bit << jj; else ib1 |= bit << (jj - 64);
-            syn ^= bit ? P.crc_cols[jj] : 0u;
+        if (!(PSCL_ABLATE & 64)) {
+            int off = 0;  // information bits below byte k (wave-uniform)
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const uint32_t byte = (uint32_t)(((k < 8 ? u0 : u1) >> (8 * (k & 7))) & 255u);
+                const uint64_t c = GT[k * 256 + byte];
+                if (off < 64) {
+                    ib0 |= c << off;
+                    if (off > 56) ib1 |= c >> (64 - off);
+                } else {
+                    ib1 |= c << (off - 64);
+                }
+                off += __builtin_popcount((uint32_t)(((k < 8 ? info0 : info1) >> (8 * (k & 7))) & 255u));
+            }
+            if (P.has_crc) {
+                const int k4 = (K + 3) >> 2;
+                const int m0 = k4 < 16 ? k4 : 16;
+                for (int m = 0; m < m0; ++m) syn ^= ST[m * 16 + (uint32_t)((ib0 >> (4 * m)) & 15u)];
+                for (int m = 16; m < k4; ++m) syn ^= ST[m * 16 + (uint32_t)((ib1 >> (4 * (m - 16))) & 15u)];
+            }
         }
         const bool active = path_lane && g < cnt && fvalid;
         uint32_t pm = (active && syn == 0) ? (1u << rank) : 0u;

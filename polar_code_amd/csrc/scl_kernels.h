@@ -34,6 +34,10 @@ struct pscl_decode_params {
     const uint64_t* ref;         // [B][W] or null
     int k_payload;
     int64_t* counters;           // [PSCL_NCOUNT] (device)
+    const uint64_t* epi_table;   // scl128 epilogue tables (device): u-byte -> info-bit gather
+                                 // [16][256] uint8, then ib-nibble -> CRC syndrome [K4][16] uint32
+    int epi_words;               // 8-byte words of epi_table staged in LDS
+    int wg_fixed_bytes;          // LDS per workgroup besides the wavefronts' (tables)
     int fast;                    // 1: the specialised N = 128, L <= 8 kernel (scl128.hip)
     int wave_bytes;              // LDS bytes per wavefront
     int a_bytes;                 // LDS bytes of the LLR slots per wavefront

@@ -408,7 +408,7 @@ __global__ void __launch_bounds__(256) channel_kernel(const pscl_channel_params 
 // wavefronts per workgroup: the choice that keeps the most wavefronts resident per CU
 // under the 160 KB LDS budget (each workgroup also holds the 2 KB exp table); 0 if none fits
 int pscl_decode_wpg(const pscl_decode_params& P) {
-    const int cu_lds = 160 * 1024, tbl = PSCL_EXP_TABLE_WORDS * 8;
+    const int cu_lds = 160 * 1024, tbl = P.wg_fixed_bytes;
     int best = 0, best_res = 0;
     for (int w = 1; w <= PSCL_MAX_WAVES_PER_WG; ++w) {
         const int wg = tbl + w * P.wave_bytes;
@@ -425,7 +425,7 @@ int pscl_decode_wpg(const pscl_decode_params& P) {
 
 static int decode_lds_bytes(const pscl_decode_params& P, int hist) {
     (void)hist;
-    return PSCL_EXP_TABLE_WORDS * 8 + pscl_decode_wpg(P) * P.wave_bytes;
+    return P.wg_fixed_bytes + pscl_decode_wpg(P) * P.wave_bytes;
 }
 
 template <int LMAX>
@@ -460,6 +460,7 @@ void pscl_decode_layout(pscl_decode_params& P, int hist) {
     const int lmax = pscl_decode_lmax(P.L);
     const int F = 32 / lmax;  // frames per wavefront
     P.fast = (P.N == 128 && P.L <= 8) ? 1 : 0;
+    P.wg_fixed_bytes = PSCL_EXP_TABLE_WORDS * 8 + (P.fast ? P.epi_words * 8 : 0);
     if (P.fast) {
         P.a_bytes = F * pscl_fast128_fstride(P.L, P.rm_E != 0) * 8;
         const int wb = P.a_bytes + (hist ? F * P.K * P.L * 9 : 0);

@@ -2,7 +2,10 @@
 
   python tools/ablate.py build          # builds tools/_ablate/lib_<mask>.so
   python tools/ablate.py run <mask>     # times one build (separate process per build)
-mask bits: 1 = no softplus, 2 = no rank/sort, 4 = no LLR tree updates.
+mask bits: 1 = no softplus, 2 = no rank/sort, 4 = no LLR tree updates, 8 = no fused depth-1..3
+recompute, 16 = no frozen-phase re-rank, 32 = no survivor gathers, 64 = no epilogue bit gather,
+128 = no leaf f/g.
+  rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES -- python tools/ablate.py run <mask>   # dynamic counts
 """
 import os
 import subprocess
@@ -12,7 +15,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 OUT = ROOT / "tools" / "_ablate"
-MASKS = [0, 1, 2, 4, 3, 7]
+MASKS = [int(m) for m in os.environ.get("MASKS", "0 1 2 4 8 16 7").split()]
 
 
 def build():
@@ -20,7 +23,7 @@ def build():
     csrc, inc = ROOT / "polar_code_amd" / "csrc", ROOT / "include"
     for m in MASKS:
         objs = []
-        for src in ("scl_kernels.hip", "scl128.hip", "capi.cpp"):
+        for src in ("scl_kernels.hip", "scl128.hip", "dlscl.hip", "capi.cpp"):
             o = OUT / f"{Path(src).stem}_{m}.o"
             subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
                                    "-ffp-contract=off", f"-DPSCL_ABLATE={m}", "-Wno-unused-result", "-Wno-unused-value",
