@@ -93,6 +93,8 @@ struct pscl_handle {
     DevBuf scratch[28];
     double* d_beta = nullptr;         // [K][K] DL-SCL flip metric (null = |L0|)
     uint64_t* d_epi = nullptr;        // scl128 epilogue tables (gather + syndrome)
+    uint64_t* d_xtab = nullptr;       // TX: codeword of each message byte value
+    uint32_t* d_crctab = nullptr;     // TX: CRC remainder of each payload byte value
     int epi_words = 0;
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
@@ -285,6 +287,45 @@ int pscl_create(pscl_handle** out, int device, int N, const int32_t* info_set, i
         CREATE_TRY(hipMalloc(&h->d_epi, epi.size()));
         CREATE_TRY(hipMemcpy(h->d_epi, epi.data(), epi.size(), hipMemcpyHostToDevice));
     }
+    {
+        // TX tables: encode and CRC attach are GF(2)-linear, so byte-wise tables give them in
+        // ceil(K/8) (resp. ceil(kp/8)) lookups per frame
+        const int nb = (K + 7) / 8, kp = K - h->crc_deg, nbp = (kp + 7) / 8;
+        std::vector<uint64_t> xt((size_t)(nb > 0 ? nb : 1) * 256 * 2, 0);
+        for (int k = 0; k < nb; ++k)
+            for (int v = 0; v < 256; ++v) {
+                uint64_t u[2] = {0, 0};
+                for (int t = 0; t < 8; ++t) {
+                    const int q = 8 * k + t;
+                    if (q < K && ((v >> t) & 1)) {
+                        const int pos = h->info_set[(size_t)q];
+                        u[pos >> 6] |= 1ULL << (pos & 63);
+                    }
+                }
+                for (int w = 0; w < 2; ++w)  // in-word Arikan stages (polar.py:17-29)
+                    for (int st = 1; st < 64; st <<= 1) {
+                        uint64_t m = 0;
+                        for (int b = 0; b < 64; ++b)
+                            if (!(b & st)) m |= 1ULL << b;
+                        u[w] ^= (u[w] >> st) & m;
+                    }
+                if (h->N > 64) u[0] ^= u[1];
+                xt[((size_t)k * 256 + v) * 2] = u[0];
+                xt[((size_t)k * 256 + v) * 2 + 1] = u[1];
+            }
+        std::vector<uint32_t> ct((size_t)(nbp > 0 ? nbp : 1) * 256, 0);
+        for (int k = 0; k < nbp; ++k)
+            for (int v = 0; v < 256; ++v) {
+                uint32_t r = 0;
+                for (int t = 0; t < 8; ++t)
+                    if (8 * k + t < kp && ((v >> t) & 1)) r ^= h->attach_cols[(size_t)(8 * k + t)];
+                ct[(size_t)k * 256 + v] = r;
+            }
+        CREATE_TRY(hipMalloc(&h->d_xtab, xt.size() * 8));
+        CREATE_TRY(hipMemcpy(h->d_xtab, xt.data(), xt.size() * 8, hipMemcpyHostToDevice));
+        CREATE_TRY(hipMalloc(&h->d_crctab, ct.size() * 4));
+        CREATE_TRY(hipMemcpy(h->d_crctab, ct.data(), ct.size() * 4, hipMemcpyHostToDevice));
+    }
 #undef CREATE_TRY
     *out = h;
     return PSCL_OK;
@@ -305,6 +346,8 @@ int pscl_destroy(pscl_handle* h) {
     if (h->d_rm_order) hipFree(h->d_rm_order);
     if (h->d_beta) hipFree(h->d_beta);
     if (h->d_epi) hipFree(h->d_epi);
+    if (h->d_xtab) hipFree(h->d_xtab);
+    if (h->d_crctab) hipFree(h->d_crctab);
     if (h->own_stream) hipStreamDestroy(h->own_stream);
     delete h;
     return PSCL_OK;
@@ -663,8 +706,8 @@ int pscl_channel_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, doubl
     P.W = h->W;
     P.k_payload = k_payload;
     P.crc_deg = h->crc_deg;
-    P.info_set = h->d_info_set;
-    P.attach_cols = h->d_attach_cols;
+    P.xtab = h->d_xtab;
+    P.crctab = h->d_crctab;
     const double ebno = pow(10.0, ebno_db / 10.0);
     P.noise_var = 1.0 / (2.0 * rate * ebno);
     P.sigma = sqrt(P.noise_var);

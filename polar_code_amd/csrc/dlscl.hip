@@ -39,11 +39,7 @@ __device__ __forceinline__ uint64_t order_key(double q) {
     return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
 }
 
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s);
-    return v;
-}
+using pscl::wave_sum;
 
 // failing baseline frames -> act[] (entry e holds frame act[e]); list[e] = e.
 // One atomic per 1024-thread block.
@@ -255,36 +251,38 @@ __global__ void __launch_bounds__(256) dl_update_kernel(const pscl_dl_params D) 
     if (more) D.next_list[base + __popcll(m & ((1ULL << lane) - 1ULL))] = e;
 }
 
-// FER/BER statistics of the final results against the transmitted words, reduced per
-// wavefront before the atomics
-__global__ void __launch_bounds__(256) dl_count_kernel(const uint64_t* __restrict__ best, const uint8_t* __restrict__ flags,
-                                                       const uint64_t* __restrict__ ref, int64_t B, int W, int k_payload,
-                                                       int64_t* counters) {
+// FER/BER statistics of the final results against the transmitted words: wavefront sums,
+// then one atomic per counter per 1024-thread block
+__global__ void __launch_bounds__(1024) dl_count_kernel(const uint64_t* __restrict__ best, const uint8_t* __restrict__ flags,
+                                                        const uint64_t* __restrict__ ref, int64_t B, int W, int k_payload,
+                                                        int64_t* counters) {
+    __shared__ int part[16][4];
     const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     unsigned long long* C = reinterpret_cast<unsigned long long*>(counters);
     if (f == 0) atomicAdd(C + PSCL_CNT_FRAMES, (unsigned long long)B);
-    int ferr = 0, berr = 0, perr = 0, pbit = 0;
+    int v[4] = {0, 0, 0, 0};  // frame errors, bit errors, payload frame errors, payload bit errors
     if (f < B) {
         const uint64_t d0 = best[f * W] ^ ref[f * W];
         const uint64_t d1 = W > 1 ? best[f * W + 1] ^ ref[f * W + 1] : 0ULL;
         const int kp = k_payload;
         const uint64_t pm0 = kp >= 64 ? ~0ULL : ((1ULL << kp) - 1);
         const uint64_t pm1 = kp >= 128 ? ~0ULL : (kp > 64 ? ((1ULL << (kp - 64)) - 1) : 0ULL);
-        ferr = (flags[f] & PSCL_FLAG_CRC_PASS) ? 0 : 1;
-        berr = __popcll(d0) + __popcll(d1);
-        pbit = __popcll(d0 & pm0) + __popcll(d1 & pm1);
-        perr = pbit ? 1 : 0;
+        v[0] = (flags[f] & PSCL_FLAG_CRC_PASS) ? 0 : 1;
+        v[1] = __popcll(d0) + __popcll(d1);
+        v[3] = __popcll(d0 & pm0) + __popcll(d1 & pm1);
+        v[2] = v[3] ? 1 : 0;
     }
-    if (!__ballot(ferr | berr)) return;
-    ferr = wave_sum(ferr);
-    berr = wave_sum(berr);
-    perr = wave_sum(perr);
-    pbit = wave_sum(pbit);
-    if ((threadIdx.x & 63) == 0) {
-        if (ferr) atomicAdd(C + PSCL_CNT_FRAME_ERR, (unsigned long long)ferr);
-        if (berr) atomicAdd(C + PSCL_CNT_BIT_ERR, (unsigned long long)berr);
-        if (perr) atomicAdd(C + PSCL_CNT_PAYLOAD_ERR, (unsigned long long)perr);
-        if (pbit) atomicAdd(C + PSCL_CNT_PAYLOAD_BIT, (unsigned long long)pbit);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = wave_sum(v[i]);
+    if (lane == 0)
+        for (int i = 0; i < 4; ++i) part[wave][i] = v[i];
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        long long t = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += part[w][threadIdx.x];
+        static const int slot[4] = {PSCL_CNT_FRAME_ERR, PSCL_CNT_BIT_ERR, PSCL_CNT_PAYLOAD_ERR, PSCL_CNT_PAYLOAD_BIT};
+        if (t) atomicAdd(C + slot[threadIdx.x], (unsigned long long)t);
     }
 }
 
@@ -334,8 +332,8 @@ hipError_t pscl_launch_dl_update(const pscl_dl_params& D, int64_t cap, hipStream
 
 hipError_t pscl_launch_dl_count(const uint64_t* best, const uint8_t* flags, const uint64_t* ref, int64_t B, int W,
                                 int k_payload, int64_t* counters, hipStream_t s) {
-    const int64_t grid = (B + 255) / 256;
-    hipLaunchKernelGGL(dl_count_kernel, dim3((unsigned)grid), dim3(256), 0, s, best, flags, ref, B, W, k_payload,
+    const int64_t grid = (B + 1023) / 1024;
+    hipLaunchKernelGGL(dl_count_kernel, dim3((unsigned)grid), dim3(1024), 0, s, best, flags, ref, B, W, k_payload,
                        counters);
     return hipGetLastError();
 }

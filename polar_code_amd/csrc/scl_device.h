@@ -262,6 +262,12 @@ __device__ __forceinline__ double nr_stage(const double* src, int k, int E, int 
 }
 
 // error counters of one decoded frame (run_fer_sweep.py:91-109, run_ber_sweep.py:77-82,156)
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s);
+    return v;
+}
+
 __device__ __forceinline__ void count_errors(int64_t* counters, uint64_t ib0, uint64_t ib1, uint64_t r0, uint64_t r1,
                                              int k_payload, bool pass) {
     const uint64_t d0 = ib0 ^ r0, d1 = ib1 ^ r1;

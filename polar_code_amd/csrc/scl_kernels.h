@@ -87,8 +87,8 @@ struct pscl_channel_params {
     uint64_t seed;
     uint32_t stream_id;
     int N, K, W, k_payload, crc_deg;
-    const int32_t* info_set;     // [K] (device)
-    const uint32_t* attach_cols; // [k_payload] CRC remainder columns (device)
+    const uint64_t* xtab;        // [ceil(K/8)][256][2]: codeword x of message byte k = v (linear)
+    const uint32_t* crctab;      // [ceil(k_payload/8)][256]: CRC remainder of payload byte k = v
     double sigma, noise_var;
     int64_t frame0, B;
     double* llr;                 // [B][N] (or [B][E] with rate matching)

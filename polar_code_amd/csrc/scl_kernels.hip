@@ -334,67 +334,77 @@ __device__ __forceinline__ u32x4 philox4x32(u32x4 c, uint32_t k0, uint32_t k1) {
     return c;
 }
 
+// TX chain, two phases per wavefront of 64 frames:
+//   A  lane = frame: Philox payload, CRC remainder and codeword from byte tables (both maps
+//      are GF(2)-linear), message words stored;
+//   B  per frame: its codeword broadcast through SGPRs, lanes generate the Box-Muller pairs
+//      and store the LLR row with coalesced writes.
+// Stream: payload = Philox(frame, draw 0xffffffff); noise pair c = lane + 64 q of a frame =
+// Philox(frame, c) -> symbols c + 64 q and c + 64 q + 64 (c < 64).
 __global__ void __launch_bounds__(256) channel_kernel(const pscl_channel_params P) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t stride = (int64_t)gridDim.x * 4;
     const uint32_t k0 = (uint32_t)P.seed, k1 = (uint32_t)(P.seed >> 32) ^ (P.stream_id * 0x85EBCA6Bu);
-    for (int64_t idx = (int64_t)blockIdx.x * 4 + wave; idx < P.B; idx += stride) {
+    const int E = P.rm_E ? P.rm_E : P.N;
+    const int kp = P.k_payload;
+    const int nb = (P.K + 7) >> 3, nbp = (kp + 7) >> 3;
+    for (int64_t base = ((int64_t)blockIdx.x * 4 + wave) * 64; base < P.B; base += (int64_t)gridDim.x * 256) {
+        // ---- A: one frame per lane
+        const int64_t idx = base + lane;
         const uint64_t fr = (uint64_t)(P.frame0 + idx);
-        // payload: k_payload uniform bits from one Philox block (draw id 0xffffffff)
         const u32x4 rb = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), 0xffffffffu, 0u}, k0, k1);
         const uint64_t r0 = ((uint64_t)rb.y << 32) | rb.x, r1 = ((uint64_t)rb.w << 32) | rb.z;
-        const int kp = P.k_payload;
         uint64_t m0 = kp >= 64 ? r0 : (r0 & ((1ULL << kp) - 1));
         uint64_t m1 = kp > 64 ? (r1 & ((kp >= 128) ? ~0ULL : ((1ULL << (kp - 64)) - 1))) : 0;
-        // CRC remainder (attach_crc crc.py:19-37) as XOR of per-payload-bit columns
-        uint32_t rem = 0;
-        for (int q = 0; q < kp; ++q) {
-            const uint64_t wq = q < 64 ? m0 : m1;
-            if ((wq >> (q & 63)) & 1) rem ^= P.attach_cols[q];
-        }
-        for (int i = 0; i < P.crc_deg; ++i) {
-            const int q = kp + i;
-            if ((rem >> i) & 1) {
-                if (q < 64) m0 |= 1ULL << q; else m1 |= 1ULL << (q - 64);
+        uint32_t rem = 0;  // attach_crc (crc.py:19-37)
+        for (int k = 0; k < nbp; ++k)
+            rem ^= P.crctab[k * 256 + (uint32_t)(((k < 8 ? m0 : m1) >> (8 * (k & 7))) & 255u)];
+        if (P.crc_deg) {
+            const uint64_t rw = (uint64_t)rem;
+            if (kp < 64) {
+                m0 |= rw << kp;
+                if (kp + P.crc_deg > 64) m1 |= rw >> (64 - kp);
+            } else {
+                m1 |= rw << (kp - 64);
             }
         }
-        // u[info_set[q]] = msg[q]; x = polar transform of u (polar.py:17-29,106-119)
-        uint64_t x0 = 0, x1 = 0;
-        for (int q = 0; q < P.K; ++q) {
-            const uint64_t wq = q < 64 ? m0 : m1;
-            if ((wq >> (q & 63)) & 1) {
-                const int pos = P.info_set[q];
-                if (pos < 64) x0 |= 1ULL << pos; else x1 |= 1ULL << (pos - 64);
-            }
+        uint64_t x0 = 0, x1 = 0;  // u[info_set] = msg, x = u G (polar.py:17-29,106-119)
+        for (int k = 0; k < nb; ++k) {
+            const uint32_t v = (uint32_t)(((k < 8 ? m0 : m1) >> (8 * (k & 7))) & 255u);
+            x0 ^= P.xtab[(k * 256 + v) * 2];
+            x1 ^= P.xtab[(k * 256 + v) * 2 + 1];
         }
-        x0 = polar_transform64(x0);
-        x1 = polar_transform64(x1);
-        if (P.N > 64) x0 ^= x1;  // stage step 64
-        if (P.msg && lane == 0) {
+        if (P.msg && idx < P.B) {
             P.msg[idx * P.W] = m0;
             if (P.W > 1) P.msg[idx * P.W + 1] = m1;
         }
-        // AWGN: each lane handles symbols (lane + 128 q) and (lane + 64 + 128 q) with one
-        // Box-Muller pair per q; NR transmits E symbols, symbol p = x[order[p % N]]
-        const int E = P.rm_E ? P.rm_E : P.N;
-        for (int q = 0; q * 128 < E; ++q) {
-            const u32x4 rn = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), (uint32_t)(lane + 64 * q), 0u}, k0, k1);
-            const uint64_t a = ((uint64_t)rn.y << 32) | rn.x, bb = ((uint64_t)rn.w << 32) | rn.z;
-            const double uu1 = ((double)(a >> 11) + 1.0) * 0x1p-53;  // (0, 1]
-            const double uu2 = (double)(bb >> 11) * 0x1p-53;         // [0, 1)
-            const double rad = sqrt(-2.0 * log(uu1));
-            double sn, cs;
-            sincospi(2.0 * uu2, &sn, &cs);
-            const double z[2] = {rad * cs, rad * sn};
+        // ---- B: AWGN per frame, 2 symbols per lane per Philox block (NR: symbol p = x[order[p % N]])
+        const int nf = (P.B - base) < 64 ? (int)(P.B - base) : 64;
+        for (int j = 0; j < nf; ++j) {
+            const uint64_t fj = (uint64_t)(P.frame0 + base + j);
+            const uint64_t xa = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x0 >> 32), j) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((uint32_t)x0, j);
+            const uint64_t xb = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x1 >> 32), j) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((uint32_t)x1, j);
+            double* row = P.llr + (base + j) * E;
+            for (int q = 0; q * 128 < E; ++q) {
+                const u32x4 rn = philox4x32(u32x4{(uint32_t)fj, (uint32_t)(fj >> 32), (uint32_t)(lane + 64 * q), 0u}, k0, k1);
+                const uint64_t a = ((uint64_t)rn.y << 32) | rn.x, bb = ((uint64_t)rn.w << 32) | rn.z;
+                const double uu1 = ((double)(a >> 11) + 1.0) * 0x1p-53;  // (0, 1]
+                const double uu2 = (double)(bb >> 11) * 0x1p-53;         // [0, 1)
+                const double rad = sqrt(-2.0 * log(uu1));
+                double sn, cs;
+                sincospi(2.0 * uu2, &sn, &cs);
+                const double z[2] = {rad * cs, rad * sn};
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int p = lane + 64 * h + 128 * q;
-                if (p < E) {
-                    const int pos = P.rm_E ? P.rm_order[p % P.N] : p;
-                    const uint64_t xw = pos < 64 ? x0 : x1;
-                    const double sym = ((xw >> (pos & 63)) & 1) ? -1.0 : 1.0;
-                    const double received = sym + P.sigma * z[h];
-                    P.llr[idx * E + p] = 2.0 * received / P.noise_var;
+                for (int h = 0; h < 2; ++h) {
+                    const int p = lane + 64 * h + 128 * q;
+                    if (p < E) {
+                        const int pos = P.rm_E ? P.rm_order[p % P.N] : p;
+                        const uint64_t xw = pos < 64 ? xa : xb;
+                        const double sym = ((xw >> (pos & 63)) & 1) ? -1.0 : 1.0;
+                        const double received = sym + P.sigma * z[h];
+                        row[p] = 2.0 * received / P.noise_var;
+                    }
                 }
             }
         }
@@ -490,7 +500,7 @@ hipError_t pscl_launch_decode(const pscl_decode_params& P, int hist, hipStream_t
 int pscl_decode_lds(const pscl_decode_params& P, int hist) { return decode_lds_bytes(P, hist); }
 
 hipError_t pscl_launch_channel(const pscl_channel_params& P, hipStream_t s) {
-    int64_t grid = (P.B + 3) / 4;
+    int64_t grid = (P.B + 255) / 256;
     if (grid > (1 << 20)) grid = 1 << 20;
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL(channel_kernel, dim3((unsigned)grid), dim3(256), 0, s, P);
