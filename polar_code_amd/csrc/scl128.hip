@@ -175,6 +175,36 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
                     const int lo = phi - 16;
                     X3 = polar_transform16((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)) & 0xffffu);
                 }
+                if (LMAX <= 2 && !CH) {
+                    // few lanes per frame: 16-lane jobs, one (frame, path) each, so every
+                    // channel load instruction reads whole 128-byte rows of 4 frames
+                    const int e = lane & 15, slot = lane >> 4;
+#pragma unroll 2
+                    for (int it = 0; it < F * LMAX / 4; ++it) {
+                        const int job = it * 4 + slot;
+                        const int fj = job / LMAX, p = job % LMAX;
+                        const int owner = fj * G + p;
+                        const double* cj = reinterpret_cast<const double*>(shfl_u64((uint64_t)chan, fj * G));
+                        double c[8];
+#pragma unroll
+                        for (int m = 0; m < 8; ++m) c[m] = cj[e + 16 * m];
+                        uint64_t x1 = 0;
+                        uint32_t x2 = 0, x3 = 0;
+                        if (r1) x1 = shfl_u64(X1, owner);
+                        if (r2) x2 = bperm32(X2, owner);
+                        if (r3) x3 = bperm32(X3, owner);
+                        double d1[4];
+#pragma unroll
+                        for (int m = 0; m < 4; ++m)
+                            d1[m] = r1 ? g_node(c[m], c[m + 4], (uint32_t)(x1 >> (e + 16 * m)) & 1u) : f_minsum(c[m], c[m + 4]);
+                        double d2[2];
+#pragma unroll
+                        for (int s2 = 0; s2 < 2; ++s2)
+                            d2[s2] = r2 ? g_node(d1[s2], d1[s2 + 2], (x2 >> (e + 16 * s2)) & 1u) : f_minsum(d1[s2], d1[s2 + 2]);
+                        const double d3 = r3 ? g_node(d2[0], d2[1], (x3 >> e) & 1u) : f_minsum(d2[0], d2[1]);
+                        A[fj * Ly::FSTRIDE + Ly::OFF3 + p * 16 + e] = d3;
+                    }
+                } else
 #pragma unroll
                 for (int q = 0; q < 16 / G + (G > 16); ++q) {
                     const int e = g + G * q;
