@@ -17,6 +17,8 @@ Fixture sets:
   G8  NR de-rate-match / de-interleave / decode_rate_matched_scl   nr/polar/*
   G9  sc_decode                                                    polar.py:130-168
   G10 odd shapes: N in {2,4,8,16,32,64}, M in {3,5,16}, K=88, no-CRC
+  G11 run_ber_sweep rows                                           eval/run_ber_sweep.py
+  G12 make_dataset shards (abs_l0, flip_idx, meta)                 train/make_dataset.py:24-121
 """
 from __future__ import annotations
 
@@ -279,6 +281,27 @@ def g11():
     np.savez_compressed(OUT / "g11_ber.npz", **d)
 
 
+DATASET_CONFIGS = {"m4_2p5db": ["--M", "4", "--snr_db", "2.5", "--frames", "300", "--seed", "0"],
+                   "m8_3db": ["--M", "8", "--snr_db", "3.0", "--frames", "200", "--seed", "1"]}
+
+
+def g12():
+    """make_dataset shards: the reference's generate_samples on small low-SNR runs."""
+    from dl_scl_polar.train import make_dataset as md
+    import tempfile
+
+    d = {}
+    for name, argv in DATASET_CONFIGS.items():
+        with tempfile.TemporaryDirectory() as td:
+            md.generate_samples(md.build_argparser().parse_args(argv + ["--out", str(Path(td) / "ds")]))
+            z = np.load(Path(td) / "ds_part0.npz")
+            d[name + "_abs_l0"] = z["abs_l0"]
+            d[name + "_flip_idx"] = z["flip_idx"]
+            d[name + "_meta"] = np.array(str(z["meta"]))
+        d[name + "_argv"] = np.array(" ".join(argv))
+    np.savez_compressed(OUT / "g12_dataset.npz", **d)
+
+
 def main():
     if len(sys.argv) > 1:
         for name in sys.argv[1:]:
@@ -302,6 +325,7 @@ def main():
     decode_set("g10_n4", 4, 3, [1, 2, 3], [1.0], 12, seed=16, crc=None)
     decode_set("g10_n2", 2, 1, [1, 2], [0.0], 12, seed=17, crc=None)
     g11()
+    g12()
     for p in sorted(OUT.glob("*.npz")):
         print(p.name, p.stat().st_size)
 
