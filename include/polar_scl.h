@@ -16,6 +16,10 @@
  *   pscl_channel_device         <- the per-frame TX chain of run_fer_sweep.py:79-87
  *                                  (payload, attach_crc crc.py:19-37, encode polar.py:106-119,
  *                                  BPSK, AWGN, LLR) with a counter-based Philox stream
+ *   pscl_uncoded_device         <- the uncoded BPSK baseline of run_fer_sweep.py:111-121
+ *   pscl_dlscl_device           <- decode_with_retries dl_scl_polar/dlscl/flip.py:65-141 over
+ *                                  a device batch (+ pscl_set_beta: the beta checkpoint)
+ *   pscl_path_llrs_device       <- best_path_info_llrs / info_llrs of given paths (scl.py:158,166)
  *
  * Conventions
  *   - Plain pointers and sizes only; no torch/HIP types in signatures (streams are void*).
@@ -81,8 +85,9 @@ int pscl_device_count(void);
 /*
  * Create a decoder for one polar code on one device.
  *   N        code length (power of two, 2..PSCL_MAX_N)
- *   info_set K distinct indices in [0, N), any order; candidate bits follow this order
- *            (u[info_set], scl.py:183)
+ *   info_set K distinct indices in [0, N), ascending (construct_info_set returns them
+ *            sorted, polar.py:103); candidate bit j is u[info_set[j]] (scl.py:183).
+ *            Unsorted sets are rejected with PSCL_EUNSUP.
  *   L        list size M (1..PSCL_MAX_L)
  *   crc_poly CRC generator as the integer value of the reference's hex string
  *            (e.g. 0x1864CFB for CRC-24A); 0 = no CRC (decode_scl crc=None)
@@ -151,6 +156,17 @@ int pscl_decode_device(pscl_handle* h, const double* d_llr, int64_t B, const uin
  */
 int pscl_channel_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate,
                         int k_payload, int64_t frame0, int64_t B, double* d_llr, uint64_t* d_msg);
+
+/*
+ * Uncoded BPSK baseline (run_fer_sweep.py:111-121, --include_uncoded) counted on the device:
+ * per frame k_payload payload bits (the same Philox payload block as pscl_channel_device),
+ * BPSK, AWGN with sigma^2 = 1 / (2 * 10^(ebno_db/10)) (rate 1), hard decision llr < 0.
+ * Noise: Philox(frame, draw 0x40000000 + pair), independent of the coded frame's noise.
+ * Adds frame errors (>= 1 wrong bit) to d_counters[PSCL_CNT_FRAME_ERR], bit errors to
+ * [PSCL_CNT_BIT_ERR] and B to [PSCL_CNT_FRAMES] (int64[PSCL_NCOUNT], device).
+ */
+int pscl_uncoded_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, int k_payload,
+                        int64_t frame0, int64_t B, int64_t* d_counters);
 
 /*
  * NR rate matching (dl_scl_polar/nr/polar/*): after this call the handle's decode entry

@@ -38,7 +38,7 @@ EXPORTS = (
     "pscl_decode_device", "pscl_channel_device", "pscl_device_alloc", "pscl_device_free",
     "pscl_memcpy_htod", "pscl_memcpy_dtoh", "pscl_memset_device", "pscl_timing_enable",
     "pscl_timing_read", "pscl_launch_info", "pscl_set_rate_match", "pscl_set_beta", "pscl_dlscl_device",
-    "pscl_path_llrs_device",
+    "pscl_path_llrs_device", "pscl_uncoded_device",
 )
 
 _vp, _i32, _i64, _u64, _dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
@@ -96,6 +96,7 @@ def lib() -> C.CDLL:
         "pscl_set_rate_match": (C.c_int, [_vp, C.c_int]),
         "pscl_set_beta": (C.c_int, [_vp, _vp]),
         "pscl_path_llrs_device": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
+        "pscl_uncoded_device": (C.c_int, [_vp, _u64, C.c_uint32, _dbl, C.c_int, _i64, _i64, _vp]),
         "pscl_dlscl_device": (C.c_int, [_vp, _vp, _i64, C.c_int, _vp, _vp, _vp, _vp, C.c_int, _vp, C.c_int, _vp,
                                         _vp]),
     }
@@ -287,6 +288,11 @@ class Decoder:
             check(lib().pscl_dlscl_device(self._h, d_llr, int(B), int(retries), d_best, d_flags, d_attempts or None,
                                           d_tried or None, int(tried_stride), d_ref or None, int(k_payload),
                                           d_counters_scl or None, d_counters_dl or None))
+
+    def uncoded_device(self, seed: int, stream_id: int, ebno_db: float, k_payload: int, frame0: int, B: int,
+                       d_counters: int) -> None:
+        check(lib().pscl_uncoded_device(self._h, int(seed) & (2**64 - 1), int(stream_id) & 0xFFFFFFFF,
+                                        float(ebno_db), int(k_payload), int(frame0), int(B), d_counters))
 
     def sync(self) -> None:
         check(lib().pscl_sync(self._h))

@@ -686,6 +686,30 @@ int pscl_sc_decode(pscl_handle* h, const double* llr, int64_t B, int8_t* bits) {
     return decode_host(h, llr, B, nullptr, np.data(), bits, nullptr, nullptr, nullptr, nullptr, nullptr, 1);
 }
 
+int pscl_uncoded_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, int k_payload,
+                        int64_t frame0, int64_t B, int64_t* d_counters) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    if (B < 0 || frame0 < 0) return fail(PSCL_EINVAL, "B and frame0 must be >= 0");
+    if (B == 0) return PSCL_OK;
+    if (!d_counters) return fail(PSCL_EINVAL, "d_counters is NULL");
+    if (k_payload < 0 || k_payload > 128) return fail(PSCL_EINVAL, "k_payload out of range");
+    int rc = set_device(h);
+    if (rc) return rc;
+    pscl_channel_params P;
+    memset(&P, 0, sizeof(P));
+    P.seed = seed;
+    P.stream_id = stream_id;
+    P.k_payload = k_payload;
+    const double ebno = pow(10.0, ebno_db / 10.0);
+    P.noise_var = 1.0 / (2.0 * ebno);  // run_fer_sweep.py:66-67
+    P.sigma = sqrt(P.noise_var);
+    P.frame0 = frame0;
+    P.B = B;
+    hipError_t e = pscl_launch_uncoded(P, d_counters, h->stream);
+    if (e != hipSuccess) return fail(PSCL_EDEVICE, "uncoded kernel launch: %s", hipGetErrorString(e));
+    return PSCL_OK;
+}
+
 int pscl_channel_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
                         int64_t frame0, int64_t B, double* d_llr, uint64_t* d_msg) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");

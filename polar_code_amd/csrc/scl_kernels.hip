@@ -499,6 +499,60 @@ hipError_t pscl_launch_decode(const pscl_decode_params& P, int hist, hipStream_t
 
 int pscl_decode_lds(const pscl_decode_params& P, int hist) { return decode_lds_bytes(P, hist); }
 
+// uncoded BPSK baseline: one frame per lane, kp payload symbols, errors reduced per block
+__global__ void __launch_bounds__(256) uncoded_kernel(const pscl_channel_params P, int64_t* counters) {
+    __shared__ long long part[4][2];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t k0 = (uint32_t)P.seed, k1 = (uint32_t)(P.seed >> 32) ^ (P.stream_id * 0x85EBCA6Bu);
+    const int kp = P.k_payload;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int ferr = 0, berr = 0;
+    if (idx < P.B) {
+        const uint64_t fr = (uint64_t)(P.frame0 + idx);
+        const u32x4 rb = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), 0xffffffffu, 0u}, k0, k1);
+        const uint64_t r0 = ((uint64_t)rb.y << 32) | rb.x, r1 = ((uint64_t)rb.w << 32) | rb.z;
+        for (int c = 0; 2 * c < kp; ++c) {
+            const u32x4 rn = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), 0x40000000u + (uint32_t)c, 0u}, k0, k1);
+            const uint64_t a = ((uint64_t)rn.y << 32) | rn.x, bb = ((uint64_t)rn.w << 32) | rn.z;
+            const double uu1 = ((double)(a >> 11) + 1.0) * 0x1p-53;
+            const double uu2 = (double)(bb >> 11) * 0x1p-53;
+            const double rad = sqrt(-2.0 * log(uu1));
+            double sn, cs;
+            sincospi(2.0 * uu2, &sn, &cs);
+            const double z[2] = {rad * cs, rad * sn};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int q = 2 * c + h;
+                if (q < kp) {
+                    const int bit = (int)(((q < 64 ? r0 : r1) >> (q & 63)) & 1ULL);
+                    const double y = (bit ? -1.0 : 1.0) + P.sigma * z[h];
+                    berr += ((2.0 * y / P.noise_var) < 0.0 ? 1 : 0) != bit;
+                }
+            }
+        }
+        ferr = berr ? 1 : 0;
+    }
+    ferr = pscl::wave_sum(ferr);
+    berr = pscl::wave_sum(berr);
+    if (lane == 0) {
+        part[wave][0] = ferr;
+        part[wave][1] = berr;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        long long t = 0;
+        for (int w = 0; w < 4; ++w) t += part[w][threadIdx.x];
+        unsigned long long* C = reinterpret_cast<unsigned long long*>(counters);
+        if (t) atomicAdd(C + (threadIdx.x == 0 ? PSCL_CNT_FRAME_ERR : PSCL_CNT_BIT_ERR), (unsigned long long)t);
+        if (threadIdx.x == 0 && blockIdx.x == 0) atomicAdd(C + PSCL_CNT_FRAMES, (unsigned long long)P.B);
+    }
+}
+
+hipError_t pscl_launch_uncoded(const pscl_channel_params& P, int64_t* counters, hipStream_t s) {
+    hipLaunchKernelGGL(uncoded_kernel, dim3((unsigned)((P.B + 255) / 256)), dim3(256), 0, s, P, counters);
+    return hipGetLastError();
+}
+
 hipError_t pscl_launch_channel(const pscl_channel_params& P, hipStream_t s) {
     int64_t grid = (P.B + 255) / 256;
     if (grid > (1 << 20)) grid = 1 << 20;

@@ -120,62 +120,87 @@ def _count_block(c, msg, llr, payload, llr_unc, info_set, M, crc, retries, beta,
         c[C_BITS_UNC] += payload.size
 
 
+class _SweepBuffers:
+    """Device buffers of one Philox batch shape, kept across batches and SNR points."""
+
+    def __init__(self, dec, n: int):
+        self.dec, self.n = dec, n
+        N = dec.N
+        self.mem = _native.DeviceArena(dec)
+        self.llr = self.mem.alloc(n * N * 8)
+        self.msg = self.mem.alloc(n * dec.W * 8)
+        self.best = self.mem.alloc(n * dec.W * 8)
+        self.flags = self.mem.alloc(n)
+        self.cnt = self.mem.alloc(3 * _native.PSCL_NCOUNT * 8)  # SCL, DL-SCL, uncoded
+
+    def close(self):
+        self.mem.__exit__(None, None, None)
+
+
+_BUFS: Dict = {}
+
+
+def _buffers(dec, n: int) -> _SweepBuffers:
+    key = (id(dec), n)
+    if key not in _BUFS:
+        for old in _BUFS.values():
+            old.close()
+        _BUFS.clear()
+        _BUFS[key] = _SweepBuffers(dec, n)
+    return _BUFS[key]
+
+
 def _philox_block(c, seed, snr_db, frame0, n, info_set, M, crc, retries, beta, device, include_uncoded,
                   payload_bits, engine="device"):
-    """n frames generated on the device; SCL and DL-SCL counted on the device."""
+    """n frames generated on the device; SCL, DL-SCL and the uncoded baseline counted there."""
     cfg = config.get_config()
     dec = _native.get_decoder(cfg.N, info_set, M, crc, device)
     W = dec.W
-    with _native.DeviceArena(dec) as mem:
-        d_llr = mem.alloc(n * cfg.N * 8)
-        d_msg = mem.alloc(n * W * 8)
-        d_best = mem.alloc(n * W * 8)
-        d_flags = mem.alloc(n)
-        d_cs = mem.alloc(_native.PSCL_NCOUNT * 8)
-        d_cd = mem.alloc(_native.PSCL_NCOUNT * 8)
-        mem.memset(d_cs, 0, _native.PSCL_NCOUNT * 8)
-        mem.memset(d_cd, 0, _native.PSCL_NCOUNT * 8)
-        dec.channel_device(seed, int(round(snr_db * 10)), snr_db, cfg.K / cfg.N, payload_bits, frame0, n, d_llr, d_msg)
-        if engine == "device":
-            dec.dlscl_device(d_llr, n, retries, beta=beta, d_best=d_best, d_flags=d_flags, d_ref=d_msg,
-                             k_payload=payload_bits, d_counters_scl=d_cs, d_counters_dl=d_cd)
-            cs = mem.download(d_cs, 64, np.int64)
-            cd = mem.download(d_cd, 64, np.int64)
-            c[C_DL_ERR] += int(cd[_native.CNT_FRAME_ERR])
-            c[C_DL_BIT] += int(cd[_native.CNT_BIT_ERR])
-            c[C_DL_WORK] += int(cd[_native.CNT_RETRIES])
-        else:
-            dec.decode_device(d_llr, n, d_best=d_best, d_flags=d_flags, d_ref=d_msg, k_payload=payload_bits,
-                              d_counters=d_cs)
-            cs = mem.download(d_cs, 64, np.int64)
-            flags = mem.download(d_flags, n, np.uint8)
-            fail = np.flatnonzero((flags & _native.PSCL_FLAG_CRC_PASS) == 0)
-            dl_bit = int(cs[_native.CNT_BIT_ERR])
-            if fail.size and retries > 0:
-                llr_all = mem.download(d_llr, n * cfg.N * 8, np.float64).reshape(n, cfg.N)
-                msg_f = words_to_bits(mem.download(d_msg, n * W * 8, np.uint64).reshape(n, W)[fail], cfg.K)
-                base_f = words_to_bits(mem.download(d_best, n * W * 8, np.uint64).reshape(n, W)[fail], cfg.K)
-                dl = decode_with_retries_batch(llr_all[fail], info_set, M, retries, crc=crc, beta=beta, device=device,
-                                               baseline={"best_bits": base_f, "crc_pass": np.zeros(fail.size, bool)})
-                c[C_DL_ERR] += int(np.count_nonzero(~dl["success"]))
-                dl_bit += int(np.count_nonzero(dl["best_bits"] != msg_f)) - int(np.count_nonzero(base_f != msg_f))
-                c[C_DL_WORK] += int((dl["attempts"] - 1).sum())
-            else:
-                c[C_DL_ERR] += int(fail.size)
-            c[C_DL_BIT] += dl_bit
-        c[C_FRAMES] += n
-        c[C_SCL_ERR] += int(cs[_native.CNT_FRAME_ERR])
-        c[C_SCL_BIT] += int(cs[_native.CNT_BIT_ERR])
-        c[C_BITS] += n * cfg.K
+    buf = _buffers(dec, n)
+    mem = buf.mem
+    nc = _native.PSCL_NCOUNT
+    d_cs, d_cd, d_cu = buf.cnt, buf.cnt + nc * 8, buf.cnt + 2 * nc * 8
+    mem.memset(buf.cnt, 0, 3 * nc * 8)
+    sid = int(round(snr_db * 10))
+    dec.channel_device(seed, sid, snr_db, cfg.K / cfg.N, payload_bits, frame0, n, buf.llr, buf.msg)
     if include_uncoded:
-        rng = np.random.default_rng([seed, int(round(snr_db * 10)), frame0])
-        _, _, var_u, sig_u = noise_params(snr_db, cfg.K / cfg.N)
-        pay = rng.integers(0, 2, size=(n, payload_bits), dtype=np.int8)
-        y = _bpsk(pay) + rng.normal(0.0, sig_u, size=pay.shape)
-        errs = np.count_nonzero(((2.0 * y / var_u) < 0).astype(np.int8) != pay, axis=1)
-        c[C_UNC_ERR] += int(np.count_nonzero(errs))
-        c[C_UNC_BIT] += int(errs.sum())
-        c[C_BITS_UNC] += pay.size
+        dec.uncoded_device(seed, sid, snr_db, payload_bits, frame0, n, d_cu)
+    if engine == "device":
+        dec.dlscl_device(buf.llr, n, retries, beta=beta, d_best=buf.best, d_flags=buf.flags, d_ref=buf.msg,
+                         k_payload=payload_bits, d_counters_scl=d_cs, d_counters_dl=d_cd)
+        cnt = mem.download(buf.cnt, 3 * nc * 8, np.int64).reshape(3, nc)
+        cs, cd, cu = cnt
+        c[C_DL_ERR] += int(cd[_native.CNT_FRAME_ERR])
+        c[C_DL_BIT] += int(cd[_native.CNT_BIT_ERR])
+        c[C_DL_WORK] += int(cd[_native.CNT_RETRIES])
+    else:
+        dec.decode_device(buf.llr, n, d_best=buf.best, d_flags=buf.flags, d_ref=buf.msg, k_payload=payload_bits,
+                          d_counters=d_cs)
+        cnt = mem.download(buf.cnt, 3 * nc * 8, np.int64).reshape(3, nc)
+        cs, cd, cu = cnt
+        flags = mem.download(buf.flags, n, np.uint8)
+        fail = np.flatnonzero((flags & _native.PSCL_FLAG_CRC_PASS) == 0)
+        dl_bit = int(cs[_native.CNT_BIT_ERR])
+        if fail.size and retries > 0:
+            llr_all = mem.download(buf.llr, n * cfg.N * 8, np.float64).reshape(n, cfg.N)
+            msg_f = words_to_bits(mem.download(buf.msg, n * W * 8, np.uint64).reshape(n, W)[fail], cfg.K)
+            base_f = words_to_bits(mem.download(buf.best, n * W * 8, np.uint64).reshape(n, W)[fail], cfg.K)
+            dl = decode_with_retries_batch(llr_all[fail], info_set, M, retries, crc=crc, beta=beta, device=device,
+                                           baseline={"best_bits": base_f, "crc_pass": np.zeros(fail.size, bool)})
+            c[C_DL_ERR] += int(np.count_nonzero(~dl["success"]))
+            dl_bit += int(np.count_nonzero(dl["best_bits"] != msg_f)) - int(np.count_nonzero(base_f != msg_f))
+            c[C_DL_WORK] += int((dl["attempts"] - 1).sum())
+        else:
+            c[C_DL_ERR] += int(fail.size)
+        c[C_DL_BIT] += dl_bit
+    c[C_FRAMES] += n
+    c[C_SCL_ERR] += int(cs[_native.CNT_FRAME_ERR])
+    c[C_SCL_BIT] += int(cs[_native.CNT_BIT_ERR])
+    c[C_BITS] += n * cfg.K
+    if include_uncoded:
+        c[C_UNC_ERR] += int(cu[_native.CNT_FRAME_ERR])
+        c[C_UNC_BIT] += int(cu[_native.CNT_BIT_ERR])
+        c[C_BITS_UNC] += n * payload_bits
 
 
 def run_sweep(args: argparse.Namespace) -> List[Dict[str, float]]:
@@ -295,7 +320,7 @@ def build_argparser() -> argparse.ArgumentParser:
     # engine options (not in the reference)
     parser.add_argument("--rng", choices=["replay", "philox"], default="replay",
                         help="replay: reference NumPy stream (exact); philox: on-device generation")
-    parser.add_argument("--batch", type=int, default=1 << 16, help="frames per GPU batch")
+    parser.add_argument("--batch", type=int, default=1 << 20, help="frames per GPU batch")
     parser.add_argument("--dl_engine", choices=["device", "host"], default="device",
                         help="device: DL-SCL retry loop on the GPU; host: numpy flip ranking (reference calls)")
     parser.add_argument("--no_plot", action="store_true")
