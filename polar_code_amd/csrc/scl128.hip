@@ -154,6 +154,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
         int cnt = 1;                // live paths of this frame (group-uniform)
         int j = 0;                  // info index (wave-uniform)
         bool pre_ok = false;        // Lpre holds the tail of this phase's leaf (wave-uniform)
+        bool ordered = true;        // every path's lane is its list position (wave-uniform)
         double Lpre = 0.0;
 
         for (int phi = 0; phi < kN; ++phi) {
@@ -276,8 +277,16 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
             const double m1 = metric + i1;
 
             if (!is_info) {
-                // frozen: bit 0, metrics advance, stable re-rank in place (lanes do not move)
+                // frozen: bit 0, metrics advance, stable re-rank in place (lanes do not move).
+                // While lane order is list order, the stable sort is the identity exactly when
+                // the new metrics stay non-decreasing along the lanes: one adjacent compare.
                 metric = m0;
+                bool moved = true;
+                if (ordered && !(PSCL_ABLATE & 256)) {
+                    const uint64_t pv = prev_lane64(pscl_asu64(m0));
+                    moved = __any(path_lane && fvalid && g >= 1 && g < cnt && pv > pscl_asu64(m0));
+                }
+                if (!moved) continue;
                 const bool kv = path_lane && g < cnt;
                 uint64_t km = kv ? pscl_asu64(m0) : 0x7ff0000000000000ULL;
                 uint32_t kt = kv ? rank : 0x7fffffffu;
@@ -291,7 +300,34 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
                 uint32_t r = 0;
                 if (!(PSCL_ABLATE & 18)) rank_step_n<G, 1, LMAX>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
                 if (path_lane) rank = r;
+                ordered = !__any(path_lane && fvalid && g < cnt && rank != (uint32_t)g);
             } else {
+                // info, full list, lane order = list order: when every path's worse child
+                // (against the LLR sign) is strictly worse than every better child and the
+                // better children keep the lane order, the survivors are the better children
+                // in place -- the outcome of the stable sort, with no ranking and no moves
+                if (ordered && !P.sc_hard && !(PSCL_ABLATE & 256)) {
+                    const uint32_t gb = lam < 0.0 ? 1u : 0u;
+                    const uint64_t mg = pscl_asu64(gb ? m1 : m0), mb = pscl_asu64(gb ? m0 : m1);
+                    const uint64_t pv = prev_lane64(mg);
+                    const uint64_t top = shfl_u64(mg, gbase + L - 1);
+                    bool forced_here = false;
+                    if (P.force) forced_here = (((j < 64 ? fm0 : fm1) >> (j & 63)) & 1) != 0;
+                    const bool bad = path_lane && g < L && fvalid &&
+                                     (cnt != L || lam == 0.0 || forced_here || (g >= 1 && pv > mg) || !(mb > top));
+                    if (!__any(bad)) {
+                        if (HIST && path_lane && g < L) {
+                            hist_llr[j * L + g] = lam;
+                            hist_par[j * L + g] = (uint8_t)g;
+                        }
+                        metric = pscl_asf64(mg);
+                        if (gb) {
+                            if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
+                        }
+                        ++j;
+                        continue;
+                    }
+                }
                 // info: children (bit 0 in lane g, bit 1 in lane g + LMAX) of every path
                 const uint64_t pm1 = from_lower_half64<G, LMAX>(pscl_asu64(m1), lane);
                 const uint32_t prank = from_lower_half<G, LMAX>(rank, lane);
@@ -341,6 +377,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
                 }
                 rank = (uint32_t)g;
                 cnt = ncnt;
+                ordered = true;
                 ++j;
             }
         }

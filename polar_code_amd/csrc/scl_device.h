@@ -262,6 +262,13 @@ __device__ __forceinline__ double nr_stage(const double* src, int k, int E, int 
 }
 
 // error counters of one decoded frame (run_fer_sweep.py:91-109, run_ber_sweep.py:77-82,156)
+// value of lane - 1 within each 16-lane row (row_shr:1; lane 0 of a row reads 0)
+__device__ __forceinline__ uint64_t prev_lane64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)v, 0x111, 0xF, 0xF, true);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), 0x111, 0xF, 0xF, true);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll
     for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s);
