@@ -169,7 +169,7 @@ int pscl_uncoded_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, doubl
                         int64_t frame0, int64_t B, int64_t* d_counters);
 
 /*
- * NR rate matching (dl_scl_polar/nr/polar/*): after this call the handle's decode entry
+ * NR rate matching (dl_scl_polar/nr/polar/...): after this call the handle's decode entry
  * points take E received LLRs per frame ([B][E]) and run decode_rate_matched_scl's front end
  * (scl_nr.py:38-57) inside the decode kernel: de-rate-match (rate_match.py:19-39, repeats
  * averaged; E <= N pads with -1.0) then sub-block de-interleave (interleaver.py:26-37).

@@ -10,6 +10,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -90,7 +91,10 @@ struct pscl_handle {
     int rm_E = 0;                     // NR rate matching (0 = off)
     int32_t* d_rm_src = nullptr;      // [N] de-interleave gather index
     int32_t* d_rm_order = nullptr;    // [N] interleaver order
-    DevBuf scratch[28];
+    DevBuf scratch[40];
+    hipStream_t retry_stream = nullptr;  // DL-SCL retry rounds, overlapped with baseline decodes
+    hipEvent_t ev_base[2] = {nullptr, nullptr}, ev_retry[2] = {nullptr, nullptr};
+    int32_t* h_count = nullptr;          // pinned: failing-frame counts of the two chunk parities
     double* d_beta = nullptr;         // [K][K] DL-SCL flip metric (null = |L0|)
     uint64_t* d_epi = nullptr;        // scl128 epilogue tables (gather + syndrome)
     uint64_t* d_xtab = nullptr;       // TX: codeword of each message byte value
@@ -143,7 +147,8 @@ void fill_decode_params(const pscl_handle* h, pscl_decode_params& P, int hist) {
     pscl_decode_layout(P, hist);
 }
 
-int launch_decode(pscl_handle* h, const pscl_decode_params& P, int hist) {
+int launch_decode(pscl_handle* h, const pscl_decode_params& P, int hist, hipStream_t st = nullptr) {
+    if (!st) st = h->stream;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->timing) {
         while (h->ev_pool.size() < h->ev_used + 2) {
@@ -154,11 +159,11 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P, int hist) {
         e0 = h->ev_pool[h->ev_used];
         e1 = h->ev_pool[h->ev_used + 1];
         h->ev_used += 2;
-        HIP_TRY(hipEventRecord(e0, h->stream));
+        HIP_TRY(hipEventRecord(e0, st));
     }
-    hipError_t err = pscl_launch_decode(P, hist, h->stream);
+    hipError_t err = pscl_launch_decode(P, hist, st);
     if (err != hipSuccess) return fail(PSCL_EDEVICE, "decode kernel launch: %s", hipGetErrorString(err));
-    if (h->timing) HIP_TRY(hipEventRecord(e1, h->stream));
+    if (h->timing) HIP_TRY(hipEventRecord(e1, st));
     return PSCL_OK;
 }
 
@@ -348,6 +353,13 @@ int pscl_destroy(pscl_handle* h) {
     if (h->d_epi) hipFree(h->d_epi);
     if (h->d_xtab) hipFree(h->d_xtab);
     if (h->d_crctab) hipFree(h->d_crctab);
+    if (h->retry_stream) hipStreamSynchronize(h->retry_stream);
+    for (int i = 0; i < 2; ++i) {
+        if (h->ev_base[i]) hipEventDestroy(h->ev_base[i]);
+        if (h->ev_retry[i]) hipEventDestroy(h->ev_retry[i]);
+    }
+    if (h->h_count) hipHostFree(h->h_count);
+    if (h->retry_stream) hipStreamDestroy(h->retry_stream);
     if (h->own_stream) hipStreamDestroy(h->own_stream);
     delete h;
     return PSCL_OK;
@@ -451,6 +463,102 @@ int pscl_set_beta(pscl_handle* h, const double* beta) {
     return PSCL_OK;
 }
 
+// retry rounds of one chunk on the retry stream (state sized for the largest chunk)
+namespace {
+struct DlState {
+    int64_t* act;
+    int32_t *list0, *list1, *cnt;
+    double* al0;
+    uint64_t *refw, *tried, *force, *ob;
+    int32_t* nt;
+    int64_t* fidx;
+    uint8_t* of;
+};
+
+int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const double* d_llr, uint64_t* d_best,
+                   uint8_t* d_flags, int32_t* d_attempts, int32_t* d_tried, int tried_stride, int64_t* d_cnt_dl,
+                   hipStream_t st) {
+    const int K = h->K, W = h->W;
+    const size_t a = (size_t)A;
+    hipError_t e;
+    HIP_TRY(hipMemsetAsync(S.tried, 0, a * 16, st));
+    HIP_TRY(hipMemsetAsync(S.nt, 0, a * 4, st));
+    // L0 of the baseline's best path (flip.py:97-102), replayed from its bits; the
+    // reference bits are the baseline's best bits
+    pscl_replay_params Rp;
+    memset(&Rp, 0, sizeof(Rp));
+    Rp.llr = d_llr;
+    Rp.N = h->N;
+    Rp.n = h->n;
+    Rp.K = K;
+    Rp.W = W;
+    Rp.rm_E = h->rm_E;
+    Rp.rm_src = h->d_rm_src;
+    Rp.info_mask[0] = h->info_mask[0];
+    Rp.info_mask[1] = h->info_mask[1];
+    Rp.count = S.cnt;
+    Rp.act = S.act;
+    Rp.bits = d_best;
+    Rp.bits_by_row = 1;
+    Rp.out = S.al0;
+    if ((e = pscl_launch_replay(Rp, A, st)) != hipSuccess) return fail(PSCL_EDEVICE, "replay launch: %s", hipGetErrorString(e));
+    if ((e = pscl_launch_dl_gather(d_best, S.act, S.cnt, A, W, S.refw, st)) != hipSuccess)
+        return fail(PSCL_EDEVICE, "dl_gather launch: %s", hipGetErrorString(e));
+    pscl_dl_params D;
+    memset(&D, 0, sizeof(D));
+    D.K = K;
+    D.W = W;
+    D.rounds = rounds;
+    D.act = S.act;
+    D.al0 = S.al0;
+    D.ref = S.refw;
+    D.tried = S.tried;
+    D.ntried = S.nt;
+    D.beta = h->d_beta;
+    D.force = S.force;
+    D.fidx = S.fidx;
+    D.ob = S.ob;
+    D.oflags = S.of;
+    D.best = d_best;
+    D.flags = d_flags;
+    D.attempts = d_attempts;
+    D.tried_out = d_tried;
+    D.tried_stride = tried_stride;
+    D.counters = d_cnt_dl;
+    int32_t* lists[2] = {S.list0, S.list1};
+    // the retry decodes: plain kernel, LLR rows by indirection, forced prefixes
+    pscl_decode_params H;
+    fill_decode_params(h, H, 0);
+    H.llr = d_llr;
+    H.B = A;
+    H.fidx = D.fidx;
+    H.force = D.force;
+    H.best = S.ob;
+    H.flags = S.of;
+    if (pscl_decode_wpg(H) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
+    Rp.bits = S.ob;  // each round's best bits, by list position
+    Rp.bits_by_row = 0;
+    int rc;
+    for (int r = 0; r < rounds; ++r) {  // no host round trips: the counts stay on the device
+        D.n = S.cnt + r;
+        D.list = lists[r & 1];
+        D.next_list = lists[(r + 1) & 1];
+        D.next_count = S.cnt + r + 1;
+        if ((e = pscl_launch_dl_select(D, A, st)) != hipSuccess)
+            return fail(PSCL_EDEVICE, "dl_select launch: %s", hipGetErrorString(e));
+        H.d_count = D.n;
+        if ((rc = launch_decode(h, H, 0, st))) return rc;
+        Rp.count = D.n;
+        Rp.list = D.list;
+        if ((e = pscl_launch_replay(Rp, A, st)) != hipSuccess)
+            return fail(PSCL_EDEVICE, "replay launch: %s", hipGetErrorString(e));
+        if ((e = pscl_launch_dl_update(D, A, st)) != hipSuccess)
+            return fail(PSCL_EDEVICE, "dl_update launch: %s", hipGetErrorString(e));
+    }
+    return PSCL_OK;
+}
+}  // namespace
+
 int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retries, uint64_t* d_best, uint8_t* d_flags,
                       int32_t* d_attempts, int32_t* d_tried, int tried_stride, const uint64_t* d_ref, int k_payload,
                       int64_t* d_counters_scl, int64_t* d_counters_dl) {
@@ -462,128 +570,104 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
     if (k_payload < 0 || k_payload > h->K) return fail(PSCL_EINVAL, "k_payload out of range");
     const int rounds = h->crc_poly && retries > 0 ? (retries < h->K ? retries : h->K) : 0;
     if (d_tried && tried_stride < rounds) return fail(PSCL_EINVAL, "tried_stride < min(retries, K)");
+    if (B > INT32_MAX) return fail(PSCL_EUNSUP, "B exceeds 2^31-1");
     int rc = set_device(h);
     if (rc) return rc;
     const int K = h->K, W = h->W;
+    const int64_t row = h->rm_E ? h->rm_E : h->N;
     hipStream_t s = h->stream;
-    // baseline SCL (flip.py:79-80)
-    pscl_decode_params P;
-    fill_decode_params(h, P, 0);
-    P.llr = d_llr;
-    P.B = B;
-    P.best = d_best;
-    P.flags = d_flags;
-    P.ref = d_ref;
-    P.k_payload = k_payload;
-    P.counters = d_counters_scl;
-    if (pscl_decode_wpg(P) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
-    if ((rc = launch_decode(h, P, 0))) return rc;
+    hipError_t e;
     if (d_attempts) HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)d_attempts, 1, (size_t)B, s));
     if (d_tried) HIP_TRY(hipMemsetAsync(d_tried, 0xff, (size_t)B * tried_stride * 4, s));
+    // Chunks (PSCL_DL_CHUNKS, default 1): the retry rounds of chunk c run on the retry stream
+    // while the main stream decodes chunk c + 1.  Measured on MI355X (L=4, 1e6 frames, 5 dB):
+    // 1 chunk 9.7 ms, 2 10.4, 4 12.9 -- the rounds are latency-bound and every chunk adds its
+    // own chain of min(retries, K) rounds on the retry stream, so overlap does not pay here.
+    int64_t nch = 1;
+    if (rounds > 0 && getenv("PSCL_DL_CHUNKS")) {  // tuning override
+        const long v = atol(getenv("PSCL_DL_CHUNKS"));
+        if (v >= 1 && v <= 64) nch = v;
+    }
+    const int64_t cap = (B + nch - 1) / nch;
+    DlState S[2];
     if (rounds > 0) {
-        void *d_cnt, *d_act, *d_list0, *d_list1;
-        // cnt[0] = failing frames, cnt[r + 1] = entries still live after round r
-        if ((rc = ensure(h, 12, (size_t)(rounds + 2) * 4, &d_cnt))) return rc;
-        if ((rc = ensure(h, 13, (size_t)B * 8, &d_act))) return rc;
-        if ((rc = ensure(h, 14, (size_t)B * 4, &d_list0))) return rc;
-        int32_t* cnt = (int32_t*)d_cnt;
-        HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)(rounds + 2) * 4, s));
-        hipError_t e = pscl_launch_dl_compact(d_flags, B, (int64_t*)d_act, (int32_t*)d_list0, cnt, s);
-        if (e != hipSuccess) return fail(PSCL_EDEVICE, "dl_compact launch: %s", hipGetErrorString(e));
-        int32_t A = 0;  // the one host read: sizes the entry state
-        HIP_TRY(hipMemcpyAsync(&A, cnt, 4, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        if (A > 0) {
-            void *d_al0, *d_refw, *d_tried_set, *d_nt, *d_force, *d_fidx, *d_ob, *d_of;
-            const size_t a = (size_t)A;
-            if ((rc = ensure(h, 15, a * 4, &d_list1))) return rc;
-            if ((rc = ensure(h, 16, a * K * 8, &d_al0))) return rc;
-            if ((rc = ensure(h, 17, a * W * 8, &d_refw))) return rc;
-            if ((rc = ensure(h, 18, a * 16, &d_tried_set))) return rc;
-            if ((rc = ensure(h, 19, a * 4, &d_nt))) return rc;
-            if ((rc = ensure(h, 20, a * 2 * W * 8, &d_force))) return rc;
-            if ((rc = ensure(h, 21, a * 8, &d_fidx))) return rc;
-            if ((rc = ensure(h, 22, a * W * 8, &d_ob))) return rc;
-            if ((rc = ensure(h, 23, a, &d_of))) return rc;
-            HIP_TRY(hipMemsetAsync(d_tried_set, 0, a * 16, s));
-            HIP_TRY(hipMemsetAsync(d_nt, 0, a * 4, s));
-            // L0 of the baseline's best path for the failing frames (flip.py:97-102),
-            // replayed from its bits; the reference bits are the baseline's best bits
-            pscl_replay_params Rp;
-            memset(&Rp, 0, sizeof(Rp));
-            Rp.llr = d_llr;
-            Rp.N = h->N;
-            Rp.n = h->n;
-            Rp.K = K;
-            Rp.W = W;
-            Rp.rm_E = h->rm_E;
-            Rp.rm_src = h->d_rm_src;
-            Rp.info_mask[0] = h->info_mask[0];
-            Rp.info_mask[1] = h->info_mask[1];
-            Rp.count = cnt;
-            Rp.list = nullptr;
-            Rp.act = (const int64_t*)d_act;
-            Rp.bits = d_best;
-            Rp.bits_by_row = 1;
-            Rp.out = (double*)d_al0;
-            if ((e = pscl_launch_replay(Rp, A, s)) != hipSuccess)
-                return fail(PSCL_EDEVICE, "replay launch: %s", hipGetErrorString(e));
-            if ((e = pscl_launch_dl_gather(d_best, (const int64_t*)d_act, cnt, A, W, (uint64_t*)d_refw, s)) != hipSuccess)
-                return fail(PSCL_EDEVICE, "dl_gather launch: %s", hipGetErrorString(e));
-            pscl_dl_params D;
-            memset(&D, 0, sizeof(D));
-            D.K = K;
-            D.W = W;
-            D.rounds = rounds;
-            D.act = (const int64_t*)d_act;
-            D.al0 = (double*)d_al0;
-            D.ref = (uint64_t*)d_refw;
-            D.tried = (uint64_t*)d_tried_set;
-            D.ntried = (int32_t*)d_nt;
-            D.beta = h->d_beta;
-            D.force = (uint64_t*)d_force;
-            D.fidx = (int64_t*)d_fidx;
-            D.ob = (const uint64_t*)d_ob;
-            D.oflags = (const uint8_t*)d_of;
-            D.best = d_best;
-            D.flags = d_flags;
-            D.attempts = d_attempts;
-            D.tried_out = d_tried;
-            D.tried_stride = tried_stride;
-            D.counters = d_ref ? d_counters_dl : nullptr;
-            int32_t* lists[2] = {(int32_t*)d_list0, (int32_t*)d_list1};
-            // the retry decodes: plain kernel, LLR rows by indirection, forced prefixes
-            pscl_decode_params H;
-            fill_decode_params(h, H, 0);
-            H.llr = d_llr;
-            H.B = A;
-            H.fidx = D.fidx;
-            H.force = D.force;
-            H.best = (uint64_t*)d_ob;
-            H.flags = (uint8_t*)d_of;
-            if (pscl_decode_wpg(H) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
-            Rp.bits = (const uint64_t*)d_ob;  // this round's best bits, by list position
-            Rp.bits_by_row = 0;
-            for (int r = 0; r < rounds; ++r) {  // no host round trips: counts stay on the device
-                D.n = cnt + r;
-                D.list = lists[r & 1];
-                D.next_list = lists[(r + 1) & 1];
-                D.next_count = cnt + r + 1;
-                if ((e = pscl_launch_dl_select(D, A, s)) != hipSuccess)
-                    return fail(PSCL_EDEVICE, "dl_select launch: %s", hipGetErrorString(e));
-                H.d_count = D.n;
-                if ((rc = launch_decode(h, H, 0))) return rc;
-                Rp.count = D.n;
-                Rp.list = D.list;
-                if ((e = pscl_launch_replay(Rp, A, s)) != hipSuccess)
-                    return fail(PSCL_EDEVICE, "replay launch: %s", hipGetErrorString(e));
-                if ((e = pscl_launch_dl_update(D, A, s)) != hipSuccess)
-                    return fail(PSCL_EDEVICE, "dl_update launch: %s", hipGetErrorString(e));
-            }
+        if (!h->retry_stream) HIP_TRY(hipStreamCreateWithFlags(&h->retry_stream, hipStreamNonBlocking));
+        for (int i = 0; i < 2; ++i) {
+            if (!h->ev_base[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_base[i], hipEventDisableTiming));
+            if (!h->ev_retry[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_retry[i], hipEventDisableTiming));
+        }
+        if (!h->h_count) HIP_TRY(hipHostMalloc((void**)&h->h_count, 16, hipHostMallocDefault));
+        // everything sized before any work is queued (an allocation synchronizes the device)
+        const size_t c = (size_t)cap;
+        void* q[12];
+        const size_t sz[12] = {(size_t)(rounds + 2) * 4, c * 8, c * 4, c * 4, c * K * 8, c * W * 8,
+                               c * 16, c * 4, c * 2 * W * 8, c * 8, c * W * 8, c};
+        for (int i = 0; i < 12; ++i)
+            if ((rc = ensure(h, 12 + i, sz[i], &q[i]))) return rc;
+        void *q1[3];
+        if ((rc = ensure(h, 27, sz[0], &q1[0])) || (rc = ensure(h, 28, sz[1], &q1[1])) ||
+            (rc = ensure(h, 29, sz[2], &q1[2])))
+            return rc;
+        for (int i = 0; i < 2; ++i) {
+            S[i].cnt = (int32_t*)(i ? q1[0] : q[0]);
+            S[i].act = (int64_t*)(i ? q1[1] : q[1]);
+            S[i].list0 = (int32_t*)(i ? q1[2] : q[2]);
+            S[i].list1 = (int32_t*)q[3];  // the retry state is used by one chunk at a time
+            S[i].al0 = (double*)q[4];
+            S[i].refw = (uint64_t*)q[5];
+            S[i].tried = (uint64_t*)q[6];
+            S[i].nt = (int32_t*)q[7];
+            S[i].force = (uint64_t*)q[8];
+            S[i].fidx = (int64_t*)q[9];
+            S[i].ob = (uint64_t*)q[10];
+            S[i].of = (uint8_t*)q[11];
         }
     }
+    auto retries_of = [&](int64_t c) -> int {
+        const int p = (int)(c & 1);
+        HIP_TRY(hipEventSynchronize(h->ev_base[p]));
+        const int A = h->h_count[p];
+        if (A > 0) {
+            HIP_TRY(hipStreamWaitEvent(h->retry_stream, h->ev_base[p], 0));
+            int r2 = dl_retry_chunk(h, S[p], A, rounds, d_llr, d_best, d_flags, d_attempts, d_tried, tried_stride,
+                                    d_ref ? d_counters_dl : nullptr, h->retry_stream);
+            if (r2) return r2;
+        }
+        HIP_TRY(hipEventRecord(h->ev_retry[p], h->retry_stream));
+        return PSCL_OK;
+    };
+    for (int64_t c = 0; c < nch; ++c) {
+        const int64_t c0 = c * cap, nc = (B - c0) < cap ? (B - c0) : cap;
+        // baseline SCL (flip.py:79-80) of chunk c
+        pscl_decode_params P;
+        fill_decode_params(h, P, 0);
+        P.llr = d_llr + c0 * row;
+        P.B = nc;
+        P.best = d_best + c0 * W;
+        P.flags = d_flags + c0;
+        P.ref = d_ref ? d_ref + c0 * W : nullptr;
+        P.k_payload = k_payload;
+        P.counters = d_counters_scl;
+        if (pscl_decode_wpg(P) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
+        if ((rc = launch_decode(h, P, 0))) return rc;
+        if (rounds > 0) {
+            const int p = (int)(c & 1);
+            if (c >= 2) HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[p], 0));  // parity buffers free again
+            HIP_TRY(hipMemsetAsync(S[p].cnt, 0, (size_t)(rounds + 2) * 4, s));
+            if ((e = pscl_launch_dl_compact(d_flags + c0, nc, c0, S[p].act, S[p].list0, S[p].cnt, s)) != hipSuccess)
+                return fail(PSCL_EDEVICE, "dl_compact launch: %s", hipGetErrorString(e));
+            HIP_TRY(hipMemcpyAsync(h->h_count + p, S[p].cnt, 4, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipEventRecord(h->ev_base[p], s));
+            if (c >= 1 && (rc = retries_of(c - 1))) return rc;
+        }
+    }
+    if (rounds > 0) {
+        if ((rc = retries_of(nch - 1))) return rc;
+        HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[(nch - 1) & 1], 0));
+        if (nch >= 2) HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[(nch - 2) & 1], 0));
+    }
     if (d_ref) {
-        hipError_t e = pscl_launch_dl_count(d_best, d_flags, d_ref, B, W, k_payload, d_counters_dl, s);
+        e = pscl_launch_dl_count(d_best, d_flags, d_ref, B, W, k_payload, d_counters_dl, s);
         if (e != hipSuccess) return fail(PSCL_EDEVICE, "dl_count launch: %s", hipGetErrorString(e));
     }
     return PSCL_OK;

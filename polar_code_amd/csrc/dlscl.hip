@@ -41,9 +41,9 @@ __device__ __forceinline__ uint64_t order_key(double q) {
 
 using pscl::wave_sum;
 
-// failing baseline frames -> act[] (entry e holds frame act[e]); list[e] = e.
+// failing baseline frames of a chunk -> act[] (entry e holds frame base + f); list[e] = e.
 // One atomic per 1024-thread block.
-__global__ void __launch_bounds__(1024) dl_compact_kernel(const uint8_t* __restrict__ flags, int64_t B,
+__global__ void __launch_bounds__(1024) dl_compact_kernel(const uint8_t* __restrict__ flags, int64_t B, int64_t base,
                                                           int64_t* __restrict__ act, int32_t* __restrict__ list,
                                                           int32_t* __restrict__ count) {
     __shared__ int wcnt[16];
@@ -66,7 +66,7 @@ __global__ void __launch_bounds__(1024) dl_compact_kernel(const uint8_t* __restr
     __syncthreads();
     if (failing) {
         const int pos = bbase + wcnt[wave] + __popcll(m & ((1ULL << lane) - 1ULL));
-        act[pos] = f;
+        act[pos] = base + f;
         list[pos] = pos;
     }
 }
@@ -288,10 +288,10 @@ __global__ void __launch_bounds__(1024) dl_count_kernel(const uint64_t* __restri
 
 }  // namespace
 
-hipError_t pscl_launch_dl_compact(const uint8_t* flags, int64_t B, int64_t* act, int32_t* list, int32_t* count,
-                                  hipStream_t s) {
+hipError_t pscl_launch_dl_compact(const uint8_t* flags, int64_t B, int64_t base, int64_t* act, int32_t* list,
+                                  int32_t* count, hipStream_t s) {
     const int64_t grid = (B + 1023) / 1024;
-    hipLaunchKernelGGL(dl_compact_kernel, dim3((unsigned)grid), dim3(1024), 0, s, flags, B, act, list, count);
+    hipLaunchKernelGGL(dl_compact_kernel, dim3((unsigned)grid), dim3(1024), 0, s, flags, B, base, act, list, count);
     return hipGetLastError();
 }
 

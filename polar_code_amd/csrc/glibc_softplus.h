@@ -53,6 +53,26 @@
 #define PSCL_ANY(c) (c)
 #endif
 
+/* n / d, correctly rounded, for operands the metric guarantees to be "nice": d in [1, 4),
+ * n zero or of magnitude >= 2^-60.  On the device this is the compiler's own IEEE fp64
+ * division sequence (reciprocal, two Newton steps, residual correction) without the
+ * v_div_scale / v_div_fixup instructions, which are the identity for such operands (they
+ * only rescale near the overflow/denormal range and patch special values). */
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ double pscl_div_nice(double n, double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    const double q = n * r;
+    const double rem = __builtin_fma(-d, q, n);
+    return __builtin_fma(rem, r, q);
+}
+#else
+#define pscl_div_nice(n, d) ((n) / (d))
+#endif
+
 /* constants from glibc's __exp_data (N = 128) */
 #define PSCL_EXP_INVLN2N 0x1.71547652b82fep0 * 128.0
 #define PSCL_EXP_SHIFT 0x1.8p52
@@ -275,7 +295,7 @@ PSCL_HD double pscl_log1p_unit(double y) {
         const int32_t hu0 = (int32_t)(pscl_asu64(u) >> 32);
         int32_t ku = (hu0 >> 20) - 1023;
         double cu = (ku > 0) ? 1.0 - (u - y) : y - (u - 1.0);
-        cu = cu / u;
+        cu = pscl_div_nice(cu, u); /* u in [1.41, 2], |cu| = 0 or >= 2^-54 */
         int32_t hum = hu0 & 0x000fffff;
         const uint64_t ulo = pscl_asu64(u) & 0xffffffffULL;
         const bool big = hum >= 0x6a09e;
@@ -289,7 +309,7 @@ PSCL_HD double pscl_log1p_unit(double y) {
     }
     const double hfsq = (0.5 * f) * f;
     /* general case */
-    const double s = f / (2.0 + f);
+    const double s = pscl_div_nice(f, 2.0 + f); /* 2 + f in [1.7, 2.5] */
     const double z = s * s;
     const double z2 = z * z;
     const double z4 = z2 * z2;

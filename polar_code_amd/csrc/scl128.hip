@@ -62,29 +62,24 @@ __device__ __forceinline__ uint64_t seg_transform(uint64_t u0, uint64_t u1, int 
     return polar_transform64(seg);
 }
 
-// depth-d step (d = 4, 5, 6) of the tree walk for all frames and path slots of the wave
+// depth-D step (D = 4, 5, 6) of the tree walk.  Lane (frame, g) works on path p = g mod LMAX
+// of its own frame, half h = g / LMAX of the node's W values, so the parent slot comes from
+// the path's own slot table (tabp: upper lanes hold a copy) and no lane reads another's state.
 template <int LMAX, bool CH, int D>
-__device__ __forceinline__ void step_depth(double* A, int lane, uint32_t tab, uint32_t xs, bool first, bool is_g) {
+__device__ __forceinline__ void step_depth(double* Af, int g, uint32_t tabp, uint32_t xsp, bool first, bool is_g) {
     using Ly = Layout128<LMAX, CH>;
-    constexpr int LW = kn - D, W = 1 << LW;
+    constexpr int LW = kn - D, W = 1 << LW, HW = W / 2;
     constexpr int OFF_OUT = D == 4 ? Ly::OFF4 : (D == 5 ? Ly::OFF5 : Ly::OFF6);
     constexpr int OFF_IN = D == 4 ? Ly::OFF3 : (D == 5 ? Ly::OFF4 : Ly::OFF5);
-    constexpr int CHUNKS = W / 2;  // F * LMAX * W / 64
+    const int p = g & (LMAX - 1), h = g >> Ly::LOG_LM;
+    const int ps = first ? slot_at(tabp, D - 1) : p;
+    const double* par = Af + OFF_IN + ps * (2 * W) + h * HW;
+    double* out = Af + OFF_OUT + p * W + h * HW;
+    const uint32_t xh = xsp >> (h * HW);
 #pragma unroll
-    for (int c = 0; c < CHUNKS; ++c) {
-        const int tt = c * 64 + lane;
-        const int fl2 = tt >> (Ly::LOG_LM + LW);
-        const int i = (tt >> LW) & (LMAX - 1);
-        const int e = tt & (W - 1);
-        const int src = (fl2 << Ly::LOG_G) | i;
-        int ps = i;
-        uint32_t xi = 0;
-        if (first) ps = slot_at(bperm32(tab, src), D - 1);
-        if (is_g) xi = bperm32(xs, src);
-        double* A2 = A + fl2 * Ly::FSTRIDE;
-        const double* par = A2 + OFF_IN + ps * (2 * W);
-        const double a = par[e], b = par[e + W];
-        A2[OFF_OUT + i * W + e] = is_g ? g_node(a, b, (xi >> e) & 1u) : f_minsum(a, b);
+    for (int k = 0; k < HW; ++k) {
+        const double a = par[k], b = par[k + W];
+        out[k] = is_g ? g_node(a, b, (xh >> k) & 1u) : f_minsum(a, b);
     }
     wave_lds_fence();
 }
@@ -243,10 +238,16 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
                 const int w = 1 << (kn - start), lo = phi - w;
                 xs = polar_transform8((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)) & ((1u << w) - 1u));
             }
-            if (!(PSCL_ABLATE & 4)) {
-                if (start <= 4) step_depth<LMAX, CH, 4>(A, lane, tab, xs, start == 4, start == 4 && phi);
-                if (start <= 5) step_depth<LMAX, CH, 5>(A, lane, tab, xs, start == 5, start == 5);
-                if (start <= 6) step_depth<LMAX, CH, 6>(A, lane, tab, xs, start == 6, start == 6);
+            if (!(PSCL_ABLATE & 4) && start <= 6) {
+                // (DPP evaluated by every lane first: inside ?: only the selected lanes would
+                // run it, and a DPP that reads an inactive lane gets 0)
+                const uint32_t tab_src = from_lower_half<G, LMAX>(tab, lane);
+                const uint32_t xs_src = from_lower_half<G, LMAX>(xs, lane);
+                const uint32_t tabp = path_lane ? tab : tab_src;
+                const uint32_t xsp = path_lane ? xs : xs_src;
+                if (start <= 4) step_depth<LMAX, CH, 4>(Af, g, tabp, xsp, start == 4, start == 4 && phi);
+                if (start <= 5) step_depth<LMAX, CH, 5>(Af, g, tabp, xsp, start == 5, start == 5);
+                if (start <= 6) step_depth<LMAX, CH, 6>(Af, g, tabp, xsp, start == 6, start == 6);
             }
             if (start <= 6) {  // this path's own slot at every depth rewritten this phase
                 const int s0 = start < 3 ? 3 : start;

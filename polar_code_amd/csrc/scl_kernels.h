@@ -108,8 +108,8 @@ int pscl_decode_lds(const pscl_decode_params& P, int hist);
 hipError_t pscl_launch_decode(const pscl_decode_params& P, int hist, hipStream_t s);
 hipError_t pscl_launch_channel(const pscl_channel_params& P, hipStream_t s);
 hipError_t pscl_launch_uncoded(const pscl_channel_params& P, int64_t* counters, hipStream_t s);
-hipError_t pscl_launch_dl_compact(const uint8_t* flags, int64_t B, int64_t* act, int32_t* list, int32_t* count,
-                                  hipStream_t s);
+hipError_t pscl_launch_dl_compact(const uint8_t* flags, int64_t B, int64_t base, int64_t* act, int32_t* list,
+                                  int32_t* count, hipStream_t s);
 hipError_t pscl_launch_dl_select(const pscl_dl_params& D, int64_t cap, hipStream_t s);
 hipError_t pscl_launch_dl_update(const pscl_dl_params& D, int64_t cap, hipStream_t s);
 hipError_t pscl_launch_dl_gather(const uint64_t* best, const int64_t* act, const int32_t* count, int64_t cap, int W,
