@@ -46,10 +46,12 @@ struct Layout128 {
     static constexpr int F = 64 / G;
     static constexpr int LOG_G = __builtin_ctz(G);
     static constexpr int LOG_LM = __builtin_ctz(LMAX);
-    static constexpr int OFF3 = CH ? kN : 0;        // [LMAX][16]
-    static constexpr int OFF4 = OFF3 + 16 * LMAX;   // [LMAX][8]
-    static constexpr int OFF5 = OFF4 + 8 * LMAX;    // [LMAX][4]
-    static constexpr int OFF6 = OFF5 + 4 * LMAX;    // [LMAX][2]
+    // depth-d nodes element-major, [element][slot]: the 16 lanes of a frame, each on its own
+    // path, then touch consecutive doubles (no LDS bank conflicts within a lane group)
+    static constexpr int OFF3 = CH ? kN : 0;        // [16][LMAX]
+    static constexpr int OFF4 = OFF3 + 16 * LMAX;   // [8][LMAX]
+    static constexpr int OFF5 = OFF4 + 8 * LMAX;    // [4][LMAX]
+    static constexpr int OFF6 = OFF5 + 4 * LMAX;    // [2][LMAX]
     static constexpr int FSTRIDE = OFF6 + 2 * LMAX;  // doubles per frame
 };
 
@@ -63,8 +65,9 @@ __device__ __forceinline__ uint64_t seg_transform(uint64_t u0, uint64_t u1, int 
 }
 
 // depth-D step (D = 4, 5, 6) of the tree walk.  Lane (frame, g) works on path p = g mod LMAX
-// of its own frame, half h = g / LMAX of the node's W values, so the parent slot comes from
-// the path's own slot table (tabp: upper lanes hold a copy) and no lane reads another's state.
+// of its own frame and the elements e = 2k + h (h = g / LMAX) of the node's W values, so the
+// parent slot comes from the path's own slot table (tabp: upper lanes hold a copy) and no
+// lane reads another's state.
 template <int LMAX, bool CH, int D>
 __device__ __forceinline__ void step_depth(double* Af, int g, uint32_t tabp, uint32_t xsp, bool first, bool is_g) {
     using Ly = Layout128<LMAX, CH>;
@@ -73,13 +76,13 @@ __device__ __forceinline__ void step_depth(double* Af, int g, uint32_t tabp, uin
     constexpr int OFF_IN = D == 4 ? Ly::OFF3 : (D == 5 ? Ly::OFF4 : Ly::OFF5);
     const int p = g & (LMAX - 1), h = g >> Ly::LOG_LM;
     const int ps = first ? slot_at(tabp, D - 1) : p;
-    const double* par = Af + OFF_IN + ps * (2 * W) + h * HW;
-    double* out = Af + OFF_OUT + p * W + h * HW;
-    const uint32_t xh = xsp >> (h * HW);
+    const double* par = Af + OFF_IN + h * LMAX + ps;   // element e of slot s: [e * LMAX + s]
+    double* out = Af + OFF_OUT + h * LMAX + p;
+    const uint32_t xh = xsp >> h;
 #pragma unroll
     for (int k = 0; k < HW; ++k) {
-        const double a = par[k], b = par[k + W];
-        out[k] = is_g ? g_node(a, b, (xh >> k) & 1u) : f_minsum(a, b);
+        const double a = par[2 * k * LMAX], b = par[(2 * k + W) * LMAX];
+        out[2 * k * LMAX] = is_g ? g_node(a, b, (xh >> (2 * k)) & 1u) : f_minsum(a, b);
     }
     wave_lds_fence();
 }
@@ -198,7 +201,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
                         for (int s2 = 0; s2 < 2; ++s2)
                             d2[s2] = r2 ? g_node(d1[s2], d1[s2 + 2], (x2 >> (e + 16 * s2)) & 1u) : f_minsum(d1[s2], d1[s2 + 2]);
                         const double d3 = r3 ? g_node(d2[0], d2[1], (x3 >> e) & 1u) : f_minsum(d2[0], d2[1]);
-                        A[fj * Ly::FSTRIDE + Ly::OFF3 + p * 16 + e] = d3;
+                        A[fj * Ly::FSTRIDE + Ly::OFF3 + e * LMAX + p] = d3;
                     }
                 } else
 #pragma unroll
@@ -227,7 +230,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
                         for (int s2 = 0; s2 < 2; ++s2)
                             d2[s2] = r2 ? g_node(d1[s2], d1[s2 + 2], (x2 >> (e + 16 * s2)) & 1u) : f_minsum(d1[s2], d1[s2 + 2]);
                         const double d3 = r3 ? g_node(d2[0], d2[1], (x3 >> e) & 1u) : f_minsum(d2[0], d2[1]);
-                        Af[Ly::OFF3 + p * 16 + e] = d3;
+                        Af[Ly::OFF3 + e * LMAX + p] = d3;
                     }
                 }
                 wave_lds_fence();
@@ -257,8 +260,8 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
             // ---- leaf LLRs.  Lanes >= LMAX: the sibling leaf (phi+1) given bit 0 here.
             const uint32_t tab_lo = from_lower_half<G, LMAX>(tab, lane);
             const uint32_t ptab = path_lane ? tab : tab_lo;
-            const double* par = Af + Ly::OFF6 + slot_at(ptab, 6) * 2;
-            const double la = par[0], lb = par[1];
+            const double* par = Af + Ly::OFF6 + slot_at(ptab, 6);
+            const double la = par[0], lb = par[LMAX];
             const uint32_t xleaf = phi ? (uint32_t)((phi - 1 < 64 ? u0 >> (phi - 1) : u1 >> (phi - 65)) & 1u) : 0u;
             const double lam = (PSCL_ABLATE & 128) ? la : (path_lane ? ((phi & 1) ? g_node(la, lb, xleaf) : f_minsum(la, lb)) : lb + la);
             // ---- metric tail log1p(exp(-|llr|)) (scl.py:102-105)

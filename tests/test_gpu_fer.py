@@ -107,3 +107,24 @@ def test_philox_fer_matches_reference_statistically(tmp_path):
         z = (p - p_ref) / math.sqrt(pp * (1 - pp) * (1 / 400000 + 1 / 2000))
         assert abs(z) < 3, (key, p, p_ref, z)
     assert abs(r["fer_uncoded"] - 0.218) < 0.01
+
+
+def test_device_retry_loop_chunked_pipeline(monkeypatch):
+    """The chunked retry pipeline (retry rounds of chunk c overlapped with the baseline of c+1)
+    gives the same per-frame results as the host ranking."""
+    from polar_code_amd.polar.polar import construct_info_set, encode
+    from polar_code_amd.polar.crc import attach_crc
+
+    monkeypatch.setenv("PSCL_DL_CHUNKS", "3")
+    rng = np.random.default_rng(77)
+    info = construct_info_set(128, 64)
+    msg = attach_crc(rng.integers(0, 2, size=(5000, 40), dtype=np.int8), "0x1864CFB")
+    var = 1.0 / (2.0 * 0.5 * 10 ** (3.0 / 10))
+    llr = 2.0 * ((1.0 - 2.0 * encode(msg)) + rng.normal(0, math.sqrt(var), size=(5000, 128))) / var
+    beta = np.load(GOLDEN / "beta_M4.npy")
+    dev = decode_with_retries_device(llr, info, 4, 8, crc="0x1864CFB", beta=beta, msg=msg)
+    host = decode_with_retries_batch(llr, info, 4, 8, crc="0x1864CFB", beta=beta)
+    np.testing.assert_array_equal(dev["tried"], host["tried"])
+    np.testing.assert_array_equal(dev["attempts"], host["attempts"])
+    np.testing.assert_array_equal(dev["best_bits"], host["best_bits"])
+    assert dev["counters"]["dl"][1] == int((~host["success"]).sum())
