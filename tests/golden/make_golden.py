@@ -19,6 +19,7 @@ Fixture sets:
   G10 odd shapes: N in {2,4,8,16,32,64}, M in {3,5,16}, K=88, no-CRC
   G11 run_ber_sweep rows                                           eval/run_ber_sweep.py
   G12 make_dataset shards (abs_l0, flip_idx, meta)                 train/make_dataset.py:24-121
+  G13 train_beta on the G12 shard (CPU, one thread): beta + log      train/train_beta.py:64-161
 """
 from __future__ import annotations
 
@@ -302,6 +303,28 @@ def g12():
     np.savez_compressed(OUT / "g12_dataset.npz", **d)
 
 
+def g13():
+    """train_beta (CPU, 1 thread) on the g12 m4 shard: checkpoint beta and the epoch log."""
+    import tempfile
+    import torch
+    from dl_scl_polar.train import train_beta as tb
+
+    torch.set_num_threads(1)
+    z = np.load(OUT / "g12_dataset.npz")
+    d = {}
+    with tempfile.TemporaryDirectory() as td:
+        shard = Path(td) / "ds_part0.npz"
+        np.savez_compressed(shard, abs_l0=z["m4_2p5db_abs_l0"], flip_idx=z["m4_2p5db_flip_idx"],
+                            meta=z["m4_2p5db_meta"])
+        argv = ["--M", "4", "--data", str(shard), "--epochs", "3", "--batch", "16", "--lr", "1e-3",
+                "--lambda_l2", "0.25", "--seed", "7", "--val_frac", "0.25", "--cpu"]
+        tb.train_beta(tb.build_argparser().parse_args(argv + ["--checkpoint_dir", td, "--log_dir", td]))
+        d["beta"] = np.load(Path(td) / "beta_M4.npy")
+        d["log"] = np.array((Path(td) / "train_M4.csv").read_text())
+        d["argv"] = np.array(" ".join(argv))
+    np.savez_compressed(OUT / "g13_train_beta.npz", **d)
+
+
 def main():
     if len(sys.argv) > 1:
         for name in sys.argv[1:]:
@@ -326,6 +349,7 @@ def main():
     decode_set("g10_n2", 2, 1, [1, 2], [0.0], 12, seed=17, crc=None)
     g11()
     g12()
+    g13()
     for p in sorted(OUT.glob("*.npz")):
         print(p.name, p.stat().st_size)
 
