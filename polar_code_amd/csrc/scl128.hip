@@ -290,6 +290,12 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
                     const uint64_t pv = prev_lane64(pscl_asu64(m0));
                     moved = __any(path_lane && fvalid && g >= 1 && g < cnt && pv > pscl_asu64(m0));
                 }
+#ifdef PSCL_STATS  // diagnostic build (tools/fastpath_stats.py): counters[8..11] of a 16-slot buffer
+                if (lane == 0 && P.counters) {
+                    atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + 8, 1ULL);
+                    if (!moved) atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + 9, 1ULL);
+                }
+#endif
                 if (!moved) continue;
                 const bool kv = path_lane && g < cnt;
                 uint64_t km = kv ? pscl_asu64(m0) : 0x7ff0000000000000ULL;
@@ -329,9 +335,15 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
                             if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
                         }
                         ++j;
+#ifdef PSCL_STATS
+                        if (lane == 0 && P.counters) atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + 11, 1ULL);
+#endif
                         continue;
                     }
                 }
+#ifdef PSCL_STATS
+                if (lane == 0 && P.counters) atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + 10, 1ULL);
+#endif
                 // info: children (bit 0 in lane g, bit 1 in lane g + LMAX) of every path
                 const uint64_t pm1 = from_lower_half64<G, LMAX>(pscl_asu64(m1), lane);
                 const uint32_t prank = from_lower_half<G, LMAX>(rank, lane);

@@ -1,0 +1,32 @@
+"""How often the decoder's exact fast paths fire (diagnostic build with -DPSCL_STATS).
+
+    PSCL_LIB_PATH=tools/_variant/lib_stats.so python tools/fastpath_stats.py [L] [ebno]
+Counters (per wavefront): [8] frozen phases, [9] frozen re-ranks skipped, [10] info phases on
+the full ranking path, [11] info phases kept in place.
+"""
+import os
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+import torch  # noqa: E402
+
+from polar_code_amd import _native  # noqa: E402
+from polar_code_amd.polar.polar import construct_info_set  # noqa: E402
+
+L = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+ebno = float(sys.argv[2]) if len(sys.argv) > 2 else 5.0
+B = 200_000
+dec = _native.Decoder(128, construct_info_set(128, 64), L, "0x1864CFB")
+dec.set_stream(torch.cuda.current_stream().cuda_stream)
+llr = torch.empty((B, 128), dtype=torch.float64, device="cuda")
+msg = torch.empty((B, 1), dtype=torch.int64, device="cuda")
+best = torch.empty((B, 1), dtype=torch.int64, device="cuda")
+cnt = torch.zeros(16, dtype=torch.int64, device="cuda")  # the stats build writes slots 8..11
+dec.channel_device(0, int(ebno * 10), ebno, 0.5, 40, 0, B, llr.data_ptr(), msg.data_ptr())
+dec.decode_device(llr.data_ptr(), B, d_best=best.data_ptr(), d_ref=msg.data_ptr(), k_payload=40,
+                  d_counters=cnt.data_ptr())
+torch.cuda.synchronize()
+c = cnt.cpu().tolist()
+print(f"L={L} {ebno} dB: frozen {c[8]} skipped {c[9]} ({c[9] / max(c[8], 1):.1%}); info full {c[10]} "
+      f"kept {c[11]} ({c[11] / max(c[10] + c[11], 1):.1%}); FER {c[1] / B:.4f}")
