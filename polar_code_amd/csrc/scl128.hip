@@ -148,6 +148,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
         double metric = 0.0;
         uint32_t rank = 0;          // list position of this path
         uint64_t u0 = 0, u1 = 0;    // decided bits
+        uint32_t lastbit = 0;       // the bit decided at the previous phase
         uint32_t tab = 0;           // LDS slot of depths 3..6 (4 bits each)
         int cnt = 1;                // live paths of this frame (group-uniform)
         int j = 0;                  // info index (wave-uniform)
@@ -262,7 +263,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
             const uint32_t ptab = path_lane ? tab : tab_lo;
             const double* par = Af + Ly::OFF6 + slot_at(ptab, 6);
             const double la = par[0], lb = par[LMAX];
-            const uint32_t xleaf = phi ? (uint32_t)((phi - 1 < 64 ? u0 >> (phi - 1) : u1 >> (phi - 65)) & 1u) : 0u;
+            const uint32_t xleaf = lastbit;  // u[phi - 1], the left sibling's bit at odd phases
             const double lam = (PSCL_ABLATE & 128) ? la : (path_lane ? ((phi & 1) ? g_node(la, lb, xleaf) : f_minsum(la, lb)) : lb + la);
             // ---- metric tail log1p(exp(-|llr|)) (scl.py:102-105)
             double Lt;
@@ -285,6 +286,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
                 // While lane order is list order, the stable sort is the identity exactly when
                 // the new metrics stay non-decreasing along the lanes: one adjacent compare.
                 metric = m0;
+                lastbit = 0;
                 bool moved = true;
                 if (ordered && !(PSCL_ABLATE & 256)) {
                     const uint64_t pv = prev_lane64(pscl_asu64(m0));
@@ -331,6 +333,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
                             hist_par[j * L + g] = (uint8_t)g;
                         }
                         metric = pscl_asf64(mg);
+                        lastbit = gb;
                         if (gb) {
                             if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
                         }
@@ -375,7 +378,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
                 const int ps2 = gbase + par_g;
                 const uint64_t nm = (PSCL_ABLATE & 32) ? km : shfl_u64(km, gbase + cc);
                 const uint64_t nu0 = (PSCL_ABLATE & 32) ? u0 : shfl_u64(u0, ps2);
-                const uint64_t nu1 = (PSCL_ABLATE & 32) ? u1 : shfl_u64(u1, ps2);
+                const uint64_t nu1 = (PSCL_ABLATE & 32) || phi < 64 ? u1 : shfl_u64(u1, ps2);  // u1 = 0 before 64
                 const uint32_t ntab = (PSCL_ABLATE & 32) ? tab : bperm32(tab, ps2);
                 if (HIST) {
                     const uint64_t plam_h = shfl_u64(pscl_asu64(lam), ps2);
@@ -391,6 +394,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(c
                 if (b) {
                     if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
                 }
+                lastbit = b;
                 rank = (uint32_t)g;
                 cnt = ncnt;
                 ordered = true;
