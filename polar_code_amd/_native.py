@@ -315,10 +315,11 @@ _CACHE: dict = {}
 _CACHE_LOCK = threading.Lock()
 
 
-def get_decoder(N: int, info_set, L: int, crc=None, device: int = 0, E: int = 0) -> Decoder:
-    """Cached Decoder per (N, info set, L, CRC, device, rate-matched length E)."""
+def get_decoder(N: int, info_set, L: int, crc=None, device: int = 0, E: int = 0, slot: int = 0) -> Decoder:
+    """Cached Decoder per (N, info set, L, CRC, device, rate-matched length E, slot).  Distinct
+    slots are distinct handles (own streams and scratch), for concurrent host threads."""
     info = np.asarray(info_set).astype(np.int64).ravel()
-    key = (int(N), info.tobytes(), int(L), poly_value(crc), int(device), int(E))
+    key = (int(N), info.tobytes(), int(L), poly_value(crc), int(device), int(E), int(slot))
     with _CACHE_LOCK:
         dec = _CACHE.get(key)
         if dec is None:

@@ -21,6 +21,7 @@ from __future__ import annotations
 import argparse
 import math
 import time
+from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 from typing import Dict, List, Tuple
 
@@ -141,20 +142,20 @@ _BUFS: Dict = {}
 
 
 def _buffers(dec, n: int) -> _SweepBuffers:
-    key = (id(dec), n)
-    if key not in _BUFS:
-        for old in _BUFS.values():
-            old.close()
-        _BUFS.clear()
-        _BUFS[key] = _SweepBuffers(dec, n)
-    return _BUFS[key]
+    """One buffer set per handle, reallocated when the batch size grows."""
+    buf = _BUFS.get(id(dec))
+    if buf is None or buf.n < n:
+        if buf is not None:
+            buf.close()
+        buf = _BUFS[id(dec)] = _SweepBuffers(dec, n)
+    return buf
 
 
 def _philox_block(c, seed, snr_db, frame0, n, info_set, M, crc, retries, beta, device, include_uncoded,
-                  payload_bits, engine="device"):
+                  payload_bits, engine="device", slot=0):
     """n frames generated on the device; SCL, DL-SCL and the uncoded baseline counted there."""
     cfg = config.get_config()
-    dec = _native.get_decoder(cfg.N, info_set, M, crc, device)
+    dec = _native.get_decoder(cfg.N, info_set, M, crc, device, slot=slot)
     W = dec.W
     buf = _buffers(dec, n)
     mem = buf.mem
@@ -218,16 +219,29 @@ def run_sweep(args: argparse.Namespace) -> List[Dict[str, float]]:
     for snr_db in snr_points:
         c = np.zeros(NCOUNT, np.int64)
         start, stop = dist.shard(args.frames, ctx.rank, ctx.world)
-        for b0 in range(start, stop, args.batch):
-            b1 = min(stop, b0 + args.batch)
-            if args.rng == "replay":
+        blocks = [(b0, min(stop, b0 + args.batch)) for b0 in range(start, stop, args.batch)]
+        if args.rng == "replay":
+            for b0, b1 in blocks:
                 payload, msg, llr, llr_unc = replay_stream(args.seed, float(snr_db), b0, b1, payload_bits,
                                                            cfg.crc_poly, args.include_uncoded)
                 _count_block(c, msg, llr, payload, llr_unc, info_set, args.M, cfg.crc_poly, args.retries, beta, device,
                              args.dl_engine)
+        else:
+            # batches in flight on `--streams` handles (own HIP streams), one host thread each:
+            # one batch's TX and DL-SCL retry chain overlap another's decode; counts add exactly
+            def work(slot):
+                cs = np.zeros(NCOUNT, np.int64)
+                for b0, b1 in blocks[slot::nstreams]:
+                    _philox_block(cs, args.seed, float(snr_db), b0, b1 - b0, info_set, args.M, cfg.crc_poly,
+                                  args.retries, beta, device, args.include_uncoded, payload_bits, args.dl_engine, slot)
+                return cs
+            nstreams = max(1, min(args.streams, len(blocks)))
+            if nstreams == 1:
+                c += work(0)
             else:
-                _philox_block(c, args.seed, float(snr_db), b0, b1 - b0, info_set, args.M, cfg.crc_poly, args.retries,
-                              beta, device, args.include_uncoded, payload_bits, args.dl_engine)
+                with ThreadPoolExecutor(nstreams) as ex:
+                    for cs in ex.map(work, range(nstreams)):
+                        c += cs
         c = dist.allreduce_sum(c, ctx)
         total_frames = args.frames
         scl_fer = c[C_SCL_ERR] / total_frames
@@ -320,7 +334,9 @@ def build_argparser() -> argparse.ArgumentParser:
     # engine options (not in the reference)
     parser.add_argument("--rng", choices=["replay", "philox"], default="replay",
                         help="replay: reference NumPy stream (exact); philox: on-device generation")
-    parser.add_argument("--batch", type=int, default=1 << 20, help="frames per GPU batch")
+    parser.add_argument("--batch", type=int, default=1 << 19, help="frames per GPU batch")
+    parser.add_argument("--streams", type=int, default=2,
+                        help="philox: batches in flight per GPU (one handle/stream and host thread each)")
     parser.add_argument("--dl_engine", choices=["device", "host"], default="device",
                         help="device: DL-SCL retry loop on the GPU; host: numpy flip ranking (reference calls)")
     parser.add_argument("--no_plot", action="store_true")
