@@ -49,7 +49,9 @@
  * device; plain c on the host).  Used to skip rarely needed branch-free sections. */
 #if defined(__HIP_DEVICE_COMPILE__)
 #define PSCL_ANY(c) __any(c)
+#define PSCL_RARE(c) __builtin_expect(__any(c), 0)
 #else
+#define PSCL_RARE(c) (c)
 #define PSCL_ANY(c) (c)
 #endif
 
@@ -259,7 +261,7 @@ PSCL_HD double pscl_exp_neg(double x, const uint64_t* T) {
     const double sc = pscl_asf64(sbits);
     const double ymain = pscl_fma(sc, tmp, sc);
     double y = ymain;
-    if (PSCL_ANY(abstop == 0x408u)) {
+    if (PSCL_RARE(abstop == 0x408u)) {
         /* 512 <= |x| < 1024, k < 0: glibc specialcase, rounded once into the subnormal range */
         const double scale = pscl_asf64(sbits + (1022ULL << 52));
         const double st = tmp * scale;
@@ -321,13 +323,13 @@ PSCL_HD double pscl_log1p_unit(double y) {
         const double kd = (double)k;
         const double bk = kd * ln2_hi - ((hfsq - ((kd * ln2_lo + c) + sR)) - f);
         res = k == 0 ? res : bk;
-        if (PSCL_ANY(hu == 0)) { /* |f| < 2^-20 */
+        if (PSCL_RARE(hu == 0)) { /* |f| < 2^-20 */
             const double R0 = (1.0 - 0.66666666666666666 * f) * hfsq;
             const double a_f0 = k == 0 ? 0.0 : (kd * ln2_lo + c) + kd * ln2_hi;
             const double a_nz = k == 0 ? f - R0 : kd * ln2_hi - ((R0 - (kd * ln2_lo + c)) - f);
             res = hu == 0 ? (f == 0.0 ? a_f0 : a_nz) : res;
         }
-    } else if (PSCL_ANY(hu == 0)) { /* k == 0 with |f| < 2^-20 */
+    } else if (PSCL_RARE(hu == 0)) { /* k == 0 with |f| < 2^-20 */
         const double R0 = (1.0 - 0.66666666666666666 * f) * hfsq;
         res = hu == 0 ? (f == 0.0 ? 0.0 : f - R0) : res;
     }
