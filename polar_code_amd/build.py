@@ -22,8 +22,35 @@ LIB = PKG / "libpolar_mi355x.so"
 ARCH = os.environ.get("PSCL_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-HIP_SOURCES = ["scl_kernels.hip", "scl128.hip", "dlscl.hip", "capi.cpp"]
-HIP_DEPS = HIP_SOURCES + ["scl_kernels.h", "scl_device.h", "glibc_softplus.h", "exp_table.inc"]
+HIP_SOURCES = ["scl_kernels.hip", "scl128.hip", "scl128_spec.hip", "dlscl.hip", "capi.cpp"]
+HIP_DEPS = HIP_SOURCES + ["scl_kernels.h", "scl_device.h", "scl128_impl.h", "glibc_softplus.h", "exp_table.inc"]
+# scl128_spec.hip is compiled once per (information-set code, list size): 8 objects
+SPEC_UNITS = [(c, l) for c in (1, 2) for l in (1, 2, 4, 8)]
+
+
+def hip_units(objdir: Path, tag: str = "") -> list[tuple[Path, list[str], Path]]:
+    """(source, extra flags, object) for every compile of the HIP library."""
+    units = []
+    for src in HIP_SOURCES:
+        if src == "scl128_spec.hip":
+            for c, l in SPEC_UNITS:
+                units.append((CSRC / src, [f"-DPSCL_SPEC_CODE={c}", f"-DPSCL_SPEC_LMAX={l}"],
+                              objdir / f"scl128_spec_{c}_{l}{tag}.o"))
+        else:
+            units.append((CSRC / src, [], objdir / (Path(src).stem + tag + ".o")))
+    return units
+
+
+def compile_units(units, flags: list[str], jobs: int | None = None) -> list[str]:
+    """Compile the units in parallel (the spec instances take ~40 s each)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    base = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+            "-Wno-unused-result", "-Wno-unused-value", f"-I{INCLUDE}", f"-I{CSRC}", *flags]
+    jobs = jobs or min(len(units), max(1, min(16, os.cpu_count() or 1)))
+    with ThreadPoolExecutor(jobs) as ex:
+        list(ex.map(lambda u: _run([*base, *u[1], "-c", str(u[0]), "-o", str(u[2])]), units))
+    return [str(u[2]) for u in units]
 
 
 def _run(cmd: list[str]) -> None:
@@ -46,13 +73,7 @@ def build_hip(force: bool = False) -> Path:
         return LIB
     objdir = PKG / "_build"
     objdir.mkdir(exist_ok=True)
-    objs = []
-    for src in HIP_SOURCES:
-        obj = objdir / (Path(src).stem + ".o")
-        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-              "-Wno-unused-result", "-Wno-unused-value", f"-I{INCLUDE}", f"-I{CSRC}",
-              "-c", str(CSRC / src), "-o", str(obj)])
-        objs.append(str(obj))
+    objs = compile_units(hip_units(objdir), [])
     tmp = LIB.with_suffix(".so.tmp")
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", str(tmp)])
     os.replace(tmp, LIB)

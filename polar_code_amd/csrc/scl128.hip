@@ -1,514 +1,69 @@
-// scl128.hip -- specialised list decoder for N = 128 and list sizes L <= 8 (every BASELINE
-// configuration).  Same contract and bit-exact results as the generic kernel in
-// scl_kernels.hip (decode_scl, dl_scl_polar/polar/scl.py:108-209); the N = 128 shape is
-// compiled in so the tree walk is straight-line code.
-//
-// Wavefront layout: F = 64/G frames per wavefront, G = 2*LMAX lanes per frame.  Lane g < L
-// of a frame group holds list path g (metric, list position `rank`, decided bits u, and the
-// LDS slot of each stored depth); lane g + LMAX is that path's bit-1 child while the list is
-// extended, and otherwise evaluates the sibling leaf's metric tail (below).
-//
-// LLR tree, per frame in LDS: (with rate matching) the 128 channel LLRs and, per path slot, depths 3..6
-// (16 + 8 + 4 + 2 values).  Depths 1 and 2 are never stored: every 16th phase the lanes
-// recompute the 16 depth-3 values of each path directly from 8 channel LLRs each (f/g through
-// depths 1-3), which halves the LDS footprint per frame and with it raises occupancy.
-//
-// List update per phase:
-//   frozen  (all paths take bit 0, scl.py:149-153): metrics advance and the stable order is
-//           re-ranked in place (rank on (metric, rank)); no path state moves.
-//   info    (free, forced or SC-hard): 2L children ranked on (metric, 2*rank + bit) with a
-//           rotation count (python's stable sort, scl.py:173), survivors gathered into lanes
-//           0..L-1 in list order (scl.py:174).
-// Metric tail: at a frozen even leaf the right sibling's LLR for the known left bit is
-// already fixed, so lanes g >= LMAX evaluate its log1p(exp(-|llr|)) in the same pass; the
-// next phase reuses it (48 of 128 evaluations per frame for the (128,64) code).
-#include <hip/hip_runtime.h>
-#include <stdint.h>
+// scl128.hip -- launches of the specialised N = 128, L <= 8 list decoder (scl128_impl.h).
+// The general instances (any information set, decision history, rate matching) live here;
+// the BASELINE codes' compiled-in instances come from scl128_spec.hip objects.
+#include "scl128_impl.h"
 
-#include <type_traits>
-
-#include "glibc_softplus.h"
-#include "scl_device.h"
-#include "scl_kernels.h"
+#define PSCL_SPEC_DECL(c, l) \
+    hipError_t pscl_launch_spec_##c##_##l(const pscl_decode_params& P, bool fs, int wpg, int64_t grid, int lds, hipStream_t s);
+PSCL_SPEC_DECL(1, 1)
+PSCL_SPEC_DECL(1, 2)
+PSCL_SPEC_DECL(1, 4)
+PSCL_SPEC_DECL(1, 8)
+PSCL_SPEC_DECL(2, 1)
+PSCL_SPEC_DECL(2, 2)
+PSCL_SPEC_DECL(2, 4)
+PSCL_SPEC_DECL(2, 8)
 
 namespace {
 
-using namespace pscl;
-
-constexpr int kN = 128;
-constexpr int kn = 7;
-
-// CH: the frame's channel LLRs are staged in LDS (needed when the decode input is rate
-// matched: the de-rate-matched values exist nowhere else); otherwise the depth-1..3
-// recomputes read them straight from the (L2/MALL-resident) input row, which halves the
-// LDS per frame and lets the wave count reach the register limit.
-template <int LMAX, bool CH>
-struct Layout128 {
-    static constexpr int G = 2 * LMAX;
-    static constexpr int F = 64 / G;
-    static constexpr int LOG_G = __builtin_ctz(G);
-    static constexpr int LOG_LM = __builtin_ctz(LMAX);
-    // depth-d nodes element-major, [element][slot]: the 16 lanes of a frame, each on its own
-    // path, then touch consecutive doubles (no LDS bank conflicts within a lane group)
-    static constexpr int OFF3 = CH ? kN : 0;        // [16][LMAX]
-    static constexpr int OFF4 = OFF3 + 16 * LMAX;   // [8][LMAX]
-    static constexpr int OFF5 = OFF4 + 8 * LMAX;    // [4][LMAX]
-    static constexpr int OFF6 = OFF5 + 4 * LMAX;    // [2][LMAX]
-    static constexpr int FSTRIDE = OFF6 + 2 * LMAX;  // doubles per frame
-};
-
-__device__ __forceinline__ int slot_at(uint32_t tab, int d) { return (int)((tab >> (4 * (d - 3))) & 15u); }
-
-// Arikan transform of the w-bit segment u[lo, lo+w), w <= 64, lo a multiple of w
-__device__ __forceinline__ uint64_t seg_transform(uint64_t u0, uint64_t u1, int lo, int w) {
-    const uint64_t word = lo >= 64 ? u1 : u0;
-    const uint64_t seg = (w == 64) ? word : (word >> (lo & 63)) & ((1ULL << w) - 1);
-    return polar_transform64(seg);
-}
-
-// depth-D step (D = 4, 5, 6) of the tree walk.  Lane (frame, g) works on path p = g mod LMAX
-// of its own frame and the elements e = 2k + h (h = g / LMAX) of the node's W values, so the
-// parent slot comes from the path's own slot table (tabp: upper lanes hold a copy) and no
-// lane reads another's state.
-template <int LMAX, bool CH, int D>
-__device__ __forceinline__ void step_depth(double* Af, int g, uint32_t tabp, uint32_t xsp, bool first, bool is_g) {
-    using Ly = Layout128<LMAX, CH>;
-    constexpr int LW = kn - D, W = 1 << LW, HW = W / 2;
-    constexpr int OFF_OUT = D == 4 ? Ly::OFF4 : (D == 5 ? Ly::OFF5 : Ly::OFF6);
-    constexpr int OFF_IN = D == 4 ? Ly::OFF3 : (D == 5 ? Ly::OFF4 : Ly::OFF5);
-    const int p = g & (LMAX - 1), h = g >> Ly::LOG_LM;
-    const int ps = first ? slot_at(tabp, D - 1) : p;
-    const double* par = Af + OFF_IN + h * LMAX + ps;   // element e of slot s: [e * LMAX + s]
-    double* out = Af + OFF_OUT + h * LMAX + p;
-    const uint32_t xh = xsp >> h;
-#pragma unroll
-    for (int k = 0; k < HW; ++k) {
-        const double a = par[2 * k * LMAX], b = par[(2 * k + W) * LMAX];
-        out[2 * k * LMAX] = is_g ? g_node(a, b, (xh >> (2 * k)) & 1u) : f_minsum(a, b);
-    }
-    wave_lds_fence();
-}
-
-template <int LMAX, bool HIST, bool CH>
-__global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, 4) scl128_kernel(const pscl_decode_params P) {
-    using Ly = Layout128<LMAX, CH>;
-    constexpr int G = Ly::G, F = Ly::F, LOG_G = Ly::LOG_G;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint64_t* T = reinterpret_cast<uint64_t*>(smem);
-    for (int i = threadIdx.x; i < PSCL_EXP_TABLE_WORDS; i += blockDim.x) T[i] = P.exp_table[i];
-    for (int i = threadIdx.x; i < P.epi_words; i += blockDim.x) T[PSCL_EXP_TABLE_WORDS + i] = P.epi_table[i];
-    __syncthreads();
-    const uint8_t* GT = reinterpret_cast<const uint8_t*>(T + PSCL_EXP_TABLE_WORDS);  // [16][256]
-    const uint32_t* ST = reinterpret_cast<const uint32_t*>(GT + 16 * 256);           // [K4][16]
-
-    const int wave = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
-    const int fl = lane >> LOG_G;
-    const int g = lane & (G - 1);
-    const int gbase = lane & ~(G - 1);
-    const int K = P.K, L = P.L;
-    unsigned char* wbase = smem + P.wg_fixed_bytes + (size_t)wave * P.wave_bytes;
-    double* A = reinterpret_cast<double*>(wbase);
-    double* Af = A + fl * Ly::FSTRIDE;
-    double* hist_llr = reinterpret_cast<double*>(wbase + P.a_bytes) + (size_t)fl * K * L;
-    uint8_t* hist_par = wbase + P.a_bytes + (size_t)F * K * L * 8 + (size_t)fl * K * L;
-
-    const int wpg = (int)(blockDim.x >> 6);
-    const int64_t wstride = (int64_t)gridDim.x * wpg * F;
-    const bool path_lane = g < LMAX;
-    const int cpath = g & (LMAX - 1);
-    const uint32_t cbit = g >= LMAX ? 1u : 0u;
-    const uint64_t info0 = P.info_mask[0], info1 = P.info_mask[1];
-
-    // live batch size: P.B, or a device-side count bounded by P.B (DL-SCL retry rounds)
-    const int64_t Bn = P.d_count ? (*P.d_count < P.B ? (int64_t)*P.d_count : P.B) : P.B;
-    for (int64_t f0 = ((int64_t)blockIdx.x * wpg + wave) * F; f0 < Bn; f0 += wstride) {
-        const int64_t f = f0 + fl;
-        const bool fvalid = f < Bn;
-        const int64_t frow = P.fidx ? P.fidx[fvalid ? f : f0] : (fvalid ? f : f0);
-        const double* chan = P.llr + frow * kN;  // !CH: channel LLRs read in place
-        if (CH) {
-            if (P.rm_E == 0) {
-#pragma unroll
-                for (int x = 0; x < kN / G; ++x) Af[g + x * G] = chan[g + x * G];
-            } else {  // NR: de-rate-match + de-interleave while staging
-                const double* src = P.llr + frow * P.rm_E;
-                for (int x = 0; x < kN / G; ++x) Af[g + x * G] = nr_stage(src, P.rm_src[g + x * G], P.rm_E, kN);
-            }
-        }
-        uint64_t fm0 = 0, fm1 = 0, fv0 = 0, fv1 = 0;
-        if (P.force && fvalid) {
-            const uint64_t* fr = P.force + f * 2 * P.W;
-            fm0 = fr[0];
-            fv0 = fr[P.W];
-            if (P.W > 1) {
-                fm1 = fr[1];
-                fv1 = fr[P.W + 1];
-            }
-        }
-        wave_lds_fence();
-        double metric = 0.0;
-        uint32_t rank = 0;          // list position of this path
-        uint64_t u0 = 0, u1 = 0;    // decided bits
-        uint32_t lastbit = 0;       // the bit decided at the previous phase
-        uint32_t tab = 0;           // LDS slot of depths 3..6 (4 bits each)
-        int cnt = 1;                // live paths of this frame (group-uniform)
-        int j = 0;                  // info index (wave-uniform)
-        bool pre_ok = false;        // Lpre holds the tail of this phase's leaf (wave-uniform)
-        bool ordered = true;        // every path's lane is its list position (wave-uniform)
-        double Lpre = 0.0;
-
-        // phase body, specialised on t = phi mod 16 (the subtree shape of the phase is fixed by t)
-        auto phase = [&](const int blk, auto TC) {
-            constexpr int PT = decltype(TC)::value;
-            const int phi = blk * 16 + PT;
-                const int start = PT ? kn - __builtin_ctz((unsigned)PT) : (blk ? 3 - __builtin_ctz((unsigned)blk) : 1);
-                const uint64_t infow = phi < 64 ? info0 : info1;
-                const bool is_info = (infow >> (phi & 63)) & 1;
-                // ---- depths 1-3 recomputed from the channel (phi % 16 == 0)
-                if (start <= 3 && !(PSCL_ABLATE & 12)) {
-                    const bool r1 = phi >= 64, r2 = (phi >> 5) & 1, r3 = (phi >> 4) & 1;
-                    // path lanes: partial sums of the left siblings at depths 1, 2, 3
-                    uint64_t X1 = 0;
-                    uint32_t X2 = 0, X3 = 0;
-                    if (r1) X1 = polar_transform64(u0);
-                    if (r2) {  // u[32(k2-1), 32 k2), k2 = phi >> 5 odd
-                        const int lo = phi - (phi & 31) - 32;
-                        X2 = polar_transform32((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)));
-                    }
-                    if (r3) {  // u[phi-16, phi)
-                        const int lo = phi - 16;
-                        X3 = polar_transform16((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)) & 0xffffu);
-                    }
-                    if (LMAX <= 2 && !CH) {
-                        // few lanes per frame: 16-lane jobs, one (frame, path) each, so every
-                        // channel load instruction reads whole 128-byte rows of 4 frames
-                        const int e = lane & 15, slot = lane >> 4;
-    #pragma unroll 2
-                        for (int it = 0; it < F * LMAX / 4; ++it) {
-                            const int job = it * 4 + slot;
-                            const int fj = job / LMAX, p = job % LMAX;
-                            const int owner = fj * G + p;
-                            const double* cj = reinterpret_cast<const double*>(shfl_u64((uint64_t)chan, fj * G));
-                            double c[8];
-    #pragma unroll
-                            for (int m = 0; m < 8; ++m) c[m] = cj[e + 16 * m];
-                            uint64_t x1 = 0;
-                            uint32_t x2 = 0, x3 = 0;
-                            if (r1) x1 = shfl_u64(X1, owner);
-                            if (r2) x2 = bperm32(X2, owner);
-                            if (r3) x3 = bperm32(X3, owner);
-                            double d1[4];
-    #pragma unroll
-                            for (int m = 0; m < 4; ++m)
-                                d1[m] = r1 ? g_node(c[m], c[m + 4], (uint32_t)(x1 >> (e + 16 * m)) & 1u) : f_minsum(c[m], c[m + 4]);
-                            double d2[2];
-    #pragma unroll
-                            for (int s2 = 0; s2 < 2; ++s2)
-                                d2[s2] = r2 ? g_node(d1[s2], d1[s2 + 2], (x2 >> (e + 16 * s2)) & 1u) : f_minsum(d1[s2], d1[s2 + 2]);
-                            const double d3 = r3 ? g_node(d2[0], d2[1], (x3 >> e) & 1u) : f_minsum(d2[0], d2[1]);
-                            A[fj * Ly::FSTRIDE + Ly::OFF3 + e * LMAX + p] = d3;
-                        }
-                    } else
-    #pragma unroll
-                    for (int q = 0; q < 16 / G + (G > 16); ++q) {
-                        const int e = g + G * q;
-                        double c[8];
-    #pragma unroll
-                        for (int m = 0; m < 8; ++m) c[m] = CH ? Af[e + 16 * m] : chan[e + 16 * m];
-                        double d1l[4];
-    #pragma unroll
-                        for (int m = 0; m < 4; ++m) d1l[m] = f_minsum(c[m], c[m + 4]);
-    #pragma unroll
-                        for (int p = 0; p < LMAX; ++p) {
-                            const int src = gbase + p;
-                            uint64_t x1 = 0;
-                            uint32_t x2 = 0, x3 = 0;
-                            if (r1) x1 = shfl_u64(X1, src);
-                            if (r2) x2 = bperm32(X2, src);
-                            if (r3) x3 = bperm32(X3, src);
-                            double d1[4];
-    #pragma unroll
-                            for (int m = 0; m < 4; ++m)
-                                d1[m] = r1 ? g_node(c[m], c[m + 4], (uint32_t)(x1 >> (e + 16 * m)) & 1u) : d1l[m];
-                            double d2[2];
-    #pragma unroll
-                            for (int s2 = 0; s2 < 2; ++s2)
-                                d2[s2] = r2 ? g_node(d1[s2], d1[s2 + 2], (x2 >> (e + 16 * s2)) & 1u) : f_minsum(d1[s2], d1[s2 + 2]);
-                            const double d3 = r3 ? g_node(d2[0], d2[1], (x3 >> e) & 1u) : f_minsum(d2[0], d2[1]);
-                            Af[Ly::OFF3 + e * LMAX + p] = d3;
-                        }
-                    }
-                    wave_lds_fence();
-                }
-                // ---- depths 4..6 (partial sums of the g node's left sibling: xs, <= 8 bits)
-                uint32_t xs = 0;
-                if (phi && start >= 4 && start <= 6) {  // u[phi-w, phi), w = 8, 4, 2
-                    const int w = 1 << (kn - start), lo = phi - w;
-                    xs = polar_transform8((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)) & ((1u << w) - 1u));
-                }
-                if (!(PSCL_ABLATE & 4) && start <= 6) {
-                    // (DPP evaluated by every lane first: inside ?: only the selected lanes would
-                    // run it, and a DPP that reads an inactive lane gets 0)
-                    const uint32_t tab_src = from_lower_half<G, LMAX>(tab, lane);
-                    const uint32_t xs_src = from_lower_half<G, LMAX>(xs, lane);
-                    const uint32_t tabp = path_lane ? tab : tab_src;
-                    const uint32_t xsp = path_lane ? xs : xs_src;
-                    if (start <= 4) step_depth<LMAX, CH, 4>(Af, g, tabp, xsp, start == 4, start == 4 && phi);
-                    if (start <= 5) step_depth<LMAX, CH, 5>(Af, g, tabp, xsp, start == 5, start == 5);
-                    if (start <= 6) step_depth<LMAX, CH, 6>(Af, g, tabp, xsp, start == 6, start == 6);
-                }
-                if (start <= 6) {  // this path's own slot at every depth rewritten this phase
-                    const int s0 = start < 3 ? 3 : start;
-                    const uint32_t mask = (0xffffu << (4 * (s0 - 3))) & 0xffffu;
-                    tab = (tab & ~mask) | ((uint32_t)cpath * 0x1111u & mask);
-                }
-                // ---- leaf LLRs.  Lanes >= LMAX: the sibling leaf (phi+1) given bit 0 here.
-                const uint32_t tab_lo = from_lower_half<G, LMAX>(tab, lane);
-                const uint32_t ptab = path_lane ? tab : tab_lo;
-                const double* par = Af + Ly::OFF6 + slot_at(ptab, 6);
-                const double la = par[0], lb = par[LMAX];
-                const uint32_t xleaf = lastbit;  // u[phi - 1], the left sibling's bit at odd phases
-                const double lam = (PSCL_ABLATE & 128) ? la : (path_lane ? ((phi & 1) ? g_node(la, lb, xleaf) : f_minsum(la, lb)) : lb + la);
-                // ---- metric tail log1p(exp(-|llr|)) (scl.py:102-105)
-                double Lt;
-                const uint64_t lpre_up = from_upper_half64<G, LMAX>(pscl_asu64(Lpre), lane);
-                if (pre_ok) {
-                    Lt = pscl_asf64(lpre_up);
-                } else {
-                    Lt = (PSCL_ABLATE & 1) ? lam * 0.5 : pscl_softplus_tail_bf(lam, T);
-                }
-                const bool frozen_even = !is_info && !(phi & 1);
-                Lpre = Lt;
-                pre_ok = frozen_even;
-                double i0, i1;
-                metric_incr(lam, Lt, i0, i1);
-                const double m0 = metric + i0;
-                const double m1 = metric + i1;
-
-                if (!is_info) {
-                    // frozen: bit 0, metrics advance, stable re-rank in place (lanes do not move).
-                    // While lane order is list order, the stable sort is the identity exactly when
-                    // the new metrics stay non-decreasing along the lanes: one adjacent compare.
-                    metric = m0;
-                    lastbit = 0;
-                    bool moved = true;
-                    if (ordered && !(PSCL_ABLATE & 256)) {
-                        const uint64_t pv = prev_lane64(pscl_asu64(m0));
-                        moved = __any(path_lane && fvalid && g >= 1 && g < cnt && pv > pscl_asu64(m0));
-                    }
-    #ifdef PSCL_STATS  // diagnostic build (tools/fastpath_stats.py): counters[8..11] of a 16-slot buffer
-                    if (lane == 0 && P.counters) {
-                        atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + 8, 1ULL);
-                        if (!moved) atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + 9, 1ULL);
-                    }
-    #endif
-                    if (!moved) return;
-                    const bool kv = path_lane && g < cnt;
-                    uint64_t km = kv ? pscl_asu64(m0) : 0x7ff0000000000000ULL;
-                    uint32_t kt = kv ? rank : 0x7fffffffu;
-                    // duplicate the path keys into the upper half: LMAX-1 rotations then see every path
-                    const uint64_t km_lo = from_lower_half64<G, LMAX>(km, lane);
-                    const uint32_t kt_lo = from_lower_half<G, LMAX>(kt, lane);
-                    if (!path_lane) {
-                        km = km_lo;
-                        kt = kt_lo;
-                    }
-                    uint32_t r = 0;
-                    if (!(PSCL_ABLATE & 18)) rank_step_n<G, 1, LMAX>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
-                    if (path_lane) rank = r;
-                    ordered = !__any(path_lane && fvalid && g < cnt && rank != (uint32_t)g);
-                } else {
-                    // info, full list, lane order = list order: when every path's worse child
-                    // (against the LLR sign) is strictly worse than every better child and the
-                    // better children keep the lane order, the survivors are the better children
-                    // in place -- the outcome of the stable sort, with no ranking and no moves
-                    if (ordered && !P.sc_hard && !(PSCL_ABLATE & 256)) {
-                        const uint32_t gb = lam < 0.0 ? 1u : 0u;
-                        const uint64_t mg = pscl_asu64(gb ? m1 : m0), mb = pscl_asu64(gb ? m0 : m1);
-                        const uint64_t pv = prev_lane64(mg);
-                        const uint64_t top = shfl_u64(mg, gbase + L - 1);
-                        bool forced_here = false;
-                        if (P.force) forced_here = (((j < 64 ? fm0 : fm1) >> (j & 63)) & 1) != 0;
-                        const bool bad = path_lane && g < L && fvalid &&
-                                         (cnt != L || lam == 0.0 || forced_here || (g >= 1 && pv > mg) || !(mb > top));
-                        if (!__any(bad)) {
-                            if (HIST && path_lane && g < L) {
-                                hist_llr[j * L + g] = lam;
-                                hist_par[j * L + g] = (uint8_t)g;
-                            }
-                            metric = pscl_asf64(mg);
-                            lastbit = gb;
-                            if (gb) {
-                                if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
-                            }
-                            ++j;
-    #ifdef PSCL_STATS
-                            if (lane == 0 && P.counters) atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + 11, 1ULL);
-    #endif
-                            return;
-                        }
-                    }
-    #ifdef PSCL_STATS
-                    if (lane == 0 && P.counters) atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + 10, 1ULL);
-    #endif
-                    // info: children (bit 0 in lane g, bit 1 in lane g + LMAX) of every path
-                    const uint64_t pm1 = from_lower_half64<G, LMAX>(pscl_asu64(m1), lane);
-                    const uint32_t prank = from_lower_half<G, LMAX>(rank, lane);
-                    uint64_t km = cbit ? pm1 : pscl_asu64(m0);
-                    const uint32_t myrank = cbit ? prank : rank;
-                    bool kval = cpath < cnt;
-                    int ncnt = 2 * cnt < L ? 2 * cnt : L;  // both children (scl.py:163-168)
-                    if (P.sc_hard) {                      // sc_decode polar.py:149-153
-                        const double plam = pscl_asf64(from_lower_half64<G, LMAX>(pscl_asu64(lam), lane));
-                        kval = kval && cbit == (uint32_t)((cbit ? plam : lam) < 0.0);
-                        ncnt = cnt;
-                    } else if (P.force) {                 // forced bits (scl.py:146-161), per frame
-                        const uint64_t fmw = j < 64 ? fm0 : fm1, fvw = j < 64 ? fv0 : fv1;
-                        if ((fmw >> (j & 63)) & 1) {
-                            kval = kval && cbit == (uint32_t)((fvw >> (j & 63)) & 1);
-                            ncnt = cnt;
-                        }
-                    }
-                    if (!kval) km = 0x7ff0000000000000ULL;
-                    const uint32_t kt = kval ? 2u * myrank + cbit : 0x7fffffffu;
-                    uint32_t r = 0;
-                    if (!(PSCL_ABLATE & 2)) rank_step<G, 1>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
-                    else r = kt & 15u;
-                    // survivor with list position r -> lane r of the group (push), scl.py:174
-                    const int c = (PSCL_ABLATE & 32) ? g : __builtin_amdgcn_ds_permute((gbase + (int)(r & (G - 1))) << 2, g);
-                    const int cc = (g < ncnt) ? c : g;
-                    const int par_g = cc & (LMAX - 1);
-                    const uint32_t b = cc >= LMAX ? 1u : 0u;
-                    const int ps2 = gbase + par_g;
-                    const uint64_t nm = (PSCL_ABLATE & 32) ? km : shfl_u64(km, gbase + cc);
-                    const uint64_t nu0 = (PSCL_ABLATE & 32) ? u0 : shfl_u64(u0, ps2);
-                    const uint64_t nu1 = (PSCL_ABLATE & 32) || phi < 64 ? u1 : shfl_u64(u1, ps2);  // u1 = 0 before 64
-                    const uint32_t ntab = (PSCL_ABLATE & 32) ? tab : bperm32(tab, ps2);
-                    if (HIST) {
-                        const uint64_t plam_h = shfl_u64(pscl_asu64(lam), ps2);
-                        if (g < ncnt && path_lane) {
-                            hist_llr[j * L + g] = pscl_asf64(plam_h);  // decision LLR (scl.py:158,166)
-                            hist_par[j * L + g] = (uint8_t)par_g;
-                        }
-                    }
-                    metric = pscl_asf64(nm);
-                    u0 = nu0;
-                    u1 = nu1;
-                    tab = ntab;
-                    if (b) {
-                        if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
-                    }
-                    lastbit = b;
-                    rank = (uint32_t)g;
-                    cnt = ncnt;
-                    ordered = true;
-                    ++j;
-                }
-        };
-        for (int blk = 0; blk < kN / 16; ++blk) {
-            phase(blk, std::integral_constant<int, 0>{});
-            phase(blk, std::integral_constant<int, 1>{});
-            phase(blk, std::integral_constant<int, 2>{});
-            phase(blk, std::integral_constant<int, 3>{});
-            phase(blk, std::integral_constant<int, 4>{});
-            phase(blk, std::integral_constant<int, 5>{});
-            phase(blk, std::integral_constant<int, 6>{});
-            phase(blk, std::integral_constant<int, 7>{});
-            phase(blk, std::integral_constant<int, 8>{});
-            phase(blk, std::integral_constant<int, 9>{});
-            phase(blk, std::integral_constant<int, 10>{});
-            phase(blk, std::integral_constant<int, 11>{});
-            phase(blk, std::integral_constant<int, 12>{});
-            phase(blk, std::integral_constant<int, 13>{});
-            phase(blk, std::integral_constant<int, 14>{});
-            phase(blk, std::integral_constant<int, 15>{});
-        }
-
-        // ---- epilogue: u[info_set] and its CRC syndrome, best = lowest-ranked CRC pass
-        // (LDS tables: u-byte gather, then ib-nibble syndrome)
-        uint64_t ib0 = 0, ib1 = 0;
-        uint32_t syn = 0;
-        if (!(PSCL_ABLATE & 64)) {
-            int off = 0;  // information bits below byte k (wave-uniform)
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const uint32_t byte = (uint32_t)(((k < 8 ? u0 : u1) >> (8 * (k & 7))) & 255u);
-                const uint64_t c = GT[k * 256 + byte];
-                if (off < 64) {
-                    ib0 |= c << off;
-                    if (off > 56) ib1 |= c >> (64 - off);
-                } else {
-                    ib1 |= c << (off - 64);
-                }
-                off += __builtin_popcount((uint32_t)(((k < 8 ? info0 : info1) >> (8 * (k & 7))) & 255u));
-            }
-            if (P.has_crc) {
-                const int k4 = (K + 3) >> 2;
-                const int m0 = k4 < 16 ? k4 : 16;
-                for (int m = 0; m < m0; ++m) syn ^= ST[m * 16 + (uint32_t)((ib0 >> (4 * m)) & 15u)];
-                for (int m = 16; m < k4; ++m) syn ^= ST[m * 16 + (uint32_t)((ib1 >> (4 * (m - 16))) & 15u)];
-            }
-        }
-        const bool active = path_lane && g < cnt && fvalid;
-        uint32_t pm = (active && syn == 0) ? (1u << rank) : 0u;
-        pm = or_reduce_group<G>(pm, lane);
-        const int best = (P.has_crc && pm) ? __builtin_ctz(pm) : 0;
-        if (active) {
-            const int64_t row = f * L + rank;
-            if (P.metrics) P.metrics[row] = metric;
-            if (P.cands) {
-                P.cands[row * P.W] = ib0;
-                if (P.W > 1) P.cands[row * P.W + 1] = ib1;
-            }
-            if (HIST && P.info_llrs) {
-                int cur = g;
-                for (int jj = K - 1; jj >= 0; --jj) {
-                    P.info_llrs[row * K + jj] = hist_llr[jj * L + cur];
-                    cur = hist_par[jj * L + cur];
-                }
-            }
-            if ((int)rank == best) {
-                const bool bpass = P.has_crc ? (syn == 0) : true;
-                if (HIST && P.best_info_llrs) {
-                    int cur = g;
-                    for (int jj = K - 1; jj >= 0; --jj) {
-                        P.best_info_llrs[f * K + jj] = hist_llr[jj * L + cur];
-                        cur = hist_par[jj * L + cur];
-                    }
-                }
-                if (P.best) {
-                    P.best[f * P.W] = ib0;
-                    if (P.W > 1) P.best[f * P.W + 1] = ib1;
-                }
-                if (P.flags) P.flags[f] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
-                if (P.n_paths) P.n_paths[f] = cnt;
-                if (P.ref)
-                    count_errors(P.counters, ib0, ib1, P.ref[f * P.W], P.W > 1 ? P.ref[f * P.W + 1] : 0, P.k_payload,
-                                 bpass);
-            }
-        }
-        wave_lds_fence();
-    }
-    if (P.ref && blockIdx.x == 0 && threadIdx.x == 0)
-        atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
-}
-
-template <int LMAX, bool HIST>
-hipError_t launch128h(const pscl_decode_params& P, int wpg, int64_t grid, int lds, hipStream_t s) {
-    if (P.rm_E)
-        hipLaunchKernelGGL((scl128_kernel<LMAX, HIST, true>), dim3((unsigned)grid), dim3(wpg * 64), lds, s, P);
-    else
-        hipLaunchKernelGGL((scl128_kernel<LMAX, HIST, false>), dim3((unsigned)grid), dim3(wpg * 64), lds, s, P);
+template <int LMAX, bool HIST, bool CH, bool FS>
+hipError_t launch128k(const pscl_decode_params& P, int wpg, int64_t grid, int lds, hipStream_t s) {
+    hipLaunchKernelGGL((scl128_kernel<LMAX, HIST, CH, FS, 0>), dim3((unsigned)grid), dim3(wpg * 64), lds, s, P);
     return hipGetLastError();
 }
 
+int spec_code(const pscl_decode_params& P) {
+    if (PSCL_ABLATE) return 0;  // diagnostic builds time the general kernel
+    for (int c = 1; c < 3; ++c)
+        if (P.K == kSpecK[c] && P.info_mask[0] == kSpecInfo[c][0] && P.info_mask[1] == kSpecInfo[c][1]) return c;
+    return 0;
+}
+
+// Kernel choice: the decision-history variant (tests, info_llrs outputs) always takes the
+// general form; plain decodes of the BASELINE codes take a compiled-in information set
+// ((128,64) without rate matching, (128,88) with it), with or without forced bits.
 template <int LMAX>
 hipError_t launch128(const pscl_decode_params& P, int hist, int wpg, int64_t grid, int lds, hipStream_t s) {
-    return hist ? launch128h<LMAX, true>(P, wpg, grid, lds, s) : launch128h<LMAX, false>(P, wpg, grid, lds, s);
+    const bool fs = P.force || P.sc_hard;
+    if (hist)
+        return P.rm_E ? launch128k<LMAX, true, true, true>(P, wpg, grid, lds, s)
+                      : launch128k<LMAX, true, false, true>(P, wpg, grid, lds, s);
+    const int code = spec_code(P);
+    if (code == 1 && !P.rm_E) {
+        switch (LMAX) {
+            case 1: return pscl_launch_spec_1_1(P, fs, wpg, grid, lds, s);
+            case 2: return pscl_launch_spec_1_2(P, fs, wpg, grid, lds, s);
+            case 4: return pscl_launch_spec_1_4(P, fs, wpg, grid, lds, s);
+            default: return pscl_launch_spec_1_8(P, fs, wpg, grid, lds, s);
+        }
+    }
+    if (code == 2 && P.rm_E) {
+        switch (LMAX) {
+            case 1: return pscl_launch_spec_2_1(P, fs, wpg, grid, lds, s);
+            case 2: return pscl_launch_spec_2_2(P, fs, wpg, grid, lds, s);
+            case 4: return pscl_launch_spec_2_4(P, fs, wpg, grid, lds, s);
+            default: return pscl_launch_spec_2_8(P, fs, wpg, grid, lds, s);
+        }
+    }
+    if (P.rm_E)
+        return fs ? launch128k<LMAX, false, true, true>(P, wpg, grid, lds, s)
+                  : launch128k<LMAX, false, true, false>(P, wpg, grid, lds, s);
+    return fs ? launch128k<LMAX, false, false, true>(P, wpg, grid, lds, s)
+              : launch128k<LMAX, false, false, false>(P, wpg, grid, lds, s);
 }
 
 }  // namespace
+
 
 int pscl_fast128_fstride(int L, int ch) {
     switch (pscl_decode_lmax(L)) {

@@ -178,3 +178,52 @@ def test_path_llr_replay_equals_decoder_history(N, K, L, E):
     got = dec.path_llrs(llr[rows[valid]], cands)
     want = out["info_llrs"].reshape(B * L, K)[valid]
     np.testing.assert_array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("forced", [False, True])
+def test_compiled_info_set_kernels_vs_oracle(M, forced):
+    """Decodes without decision history of the BASELINE (128,64) code run the kernels with the
+    information set compiled in (csrc/scl128_spec.hip), with and without forced bits; every
+    candidate, fp64 metric, path count and best index against the oracle, bit for bit."""
+    rng = np.random.default_rng(500 + M + 10 * forced)
+    info = construct_info_set(128, 64)
+    B = 900
+    llr = np.concatenate([_frames(rng, B // 3, info, s) for s in (1.0, 3.0, 5.0)])
+    force = None
+    if forced:
+        force = np.full((B, 64), -1, np.int8)
+        for f in range(0, B, 2):
+            i = rng.integers(0, 64)
+            force[f, :i] = rng.integers(0, 2, size=i)
+            force[f, i] = rng.integers(0, 2)
+    out = _native.get_decoder(128, info, M, POLY).decode(llr, force, want_info_llrs=False)
+    for f in range(B):
+        n, c, m, il, b = oracle.decode_scl(llr[f], info, M, crc=POLY, force=None if force is None else force[f])
+        assert out["n_paths"][f] == n, f
+        np.testing.assert_array_equal(out["cands"][f, :n], c[:n], err_msg=f"M={M} f={f}")
+        np.testing.assert_array_equal(out["metrics"][f, :n].view(np.int64), m[:n].view(np.int64))
+        assert out["best_idx"][f] == b
+        np.testing.assert_array_equal(out["best_bits"][f], c[b])
+
+
+@pytest.mark.parametrize("M", [2, 8])
+@pytest.mark.parametrize("E", [100, 256, 300])
+def test_compiled_nr_kernels_vs_oracle(M, E):
+    """The (128,88) NR code with rate matching runs the compiled-in kernels (CODE 2); metrics
+    and candidates against the oracle decoding the host front-end's internal LLRs."""
+    from polar_code_amd.nr.polar import derate_match_polar, subblock_deinterleave
+
+    rng = np.random.default_rng(E + M)
+    info = construct_info_set(128, 88)
+    llrE = rng.normal(2.0, 3.0, size=(300, E)) * rng.choice([1.0, -1.0], size=(300, E), p=[0.9, 0.1])
+    dec = _native.Decoder(128, info, M, POLY)
+    dec.set_rate_match(E)
+    out = dec.decode(llrE, want_info_llrs=False)
+    for f in range(llrE.shape[0]):
+        internal = subblock_deinterleave(derate_match_polar(llrE[f], 128), 128)
+        n, c, m, il, b = oracle.decode_scl(internal, info, M, crc=POLY)
+        assert out["n_paths"][f] == n
+        np.testing.assert_array_equal(out["cands"][f, :n], c[:n])
+        np.testing.assert_array_equal(out["metrics"][f, :n].view(np.int64), m[:n].view(np.int64))
+        assert out["best_idx"][f] == b

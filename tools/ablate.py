@@ -19,16 +19,12 @@ MASKS = [int(m) for m in os.environ.get("MASKS", "0 1 2 4 8 16 7").split()]
 
 
 def build():
+    sys.path.insert(0, str(ROOT))
+    from polar_code_amd import build as B
+
     OUT.mkdir(exist_ok=True)
-    csrc, inc = ROOT / "polar_code_amd" / "csrc", ROOT / "include"
     for m in MASKS:
-        objs = []
-        for src in ("scl_kernels.hip", "scl128.hip", "dlscl.hip", "capi.cpp"):
-            o = OUT / f"{Path(src).stem}_{m}.o"
-            subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
-                                   "-ffp-contract=off", f"-DPSCL_ABLATE={m}", "-Wno-unused-result", "-Wno-unused-value",
-                                   f"-I{inc}", f"-I{csrc}", "-c", str(csrc / src), "-o", str(o)])
-            objs.append(str(o))
+        objs = B.compile_units(B.hip_units(OUT, f"_{m}"), [f"-DPSCL_ABLATE={m}"])
         subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o",
                                str(OUT / f"lib_{m}.so")])
 
