@@ -46,9 +46,12 @@ __device__ __forceinline__ void wave_lds_fence() {
 
 // f(a,b) = sign(a) sign(b) min(|a|,|b|)  (polar.py:122-123).  Exact: the result is one of the
 // inputs' magnitudes with the XOR of the signs (sign(0) = 0 makes a +-0 result either way, and
-// the sign of a zero never reaches a decision or a metric).  v_min_f64 + v_xor + v_bfi.
+// the sign of a zero never reaches a decision or a metric).  v_min_f64 with |.| source
+// modifiers (written out: fmin would add two canonicalising v_max_f64 for signalling NaNs,
+// which finite LLRs never are) + v_xor + v_and_or.
 __device__ __forceinline__ double f_minsum(double a, double b) {
-    const double m = fmin(fabs(a), fabs(b));
+    double m;
+    asm("v_min_f64 %0, |%1|, |%2|" : "=v"(m) : "v"(a), "v"(b));
     const uint64_t ab = pscl_asu64(a), bb = pscl_asu64(b), mb = pscl_asu64(m);
     const uint32_t hi = (uint32_t)(mb >> 32) | (((uint32_t)(ab >> 32) ^ (uint32_t)(bb >> 32)) & 0x80000000u);
     return pscl_asf64(((uint64_t)hi << 32) | (uint32_t)mb);
@@ -97,12 +100,18 @@ __device__ __forceinline__ uint32_t polar_transform8(uint32_t x) {
 
 // metric increments of both bit hypotheses, np.logaddexp(0, -+llr) (scl.py:102-105):
 // max(0,v) + L with v = -llr (bit 0) / +llr (bit 1); L = log1p(exp(-|llr|)); llr == 0 -> LOGE2.
-// The "bad" child pays |llr| + L (|llr| = -v exactly), the "good" one 0.0 + L = L.
+// The "bad" child pays |llr| + L (|llr| = -v exactly), the "good" one 0.0 + L = L.  An exactly
+// zero LLR is a wave-uniform rare branch.
 __device__ __forceinline__ void metric_incr(double lam, double L, double& i0, double& i1) {
     const double t = fabs(lam) + L;
-    const bool z = lam == 0.0;
-    i0 = z ? PSCL_LOGE2 : (lam < 0.0 ? t : L);
-    i1 = z ? PSCL_LOGE2 : (lam > 0.0 ? t : L);
+    const bool neg = lam < 0.0;
+    i0 = neg ? t : L;
+    i1 = neg ? L : t;
+    if (PSCL_RARE(lam == 0.0)) {
+        const bool z = lam == 0.0;
+        i0 = z ? PSCL_LOGE2 : i0;
+        i1 = z ? PSCL_LOGE2 : i1;
+    }
 }
 
 __device__ __forceinline__ uint64_t pick_word(uint64_t w0, uint64_t w1, int idx) { return idx ? w1 : w0; }
@@ -119,14 +128,14 @@ __device__ __forceinline__ uint32_t grot32c(uint32_t v, int lane) {
     if constexpr (G == 16) {
         return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x120 + K, 0xF, 0xF, true);  // row_ror:K
     } else if constexpr (G == 8) {
-        const uint32_t a = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + K, 0xF, 0xF, false);
-        const uint32_t b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + K + 8, 0xF, 0xF, false);
+        const uint32_t a = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x120 + K, 0xF, 0xF, true);
+        const uint32_t b = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x120 + K + 8, 0xF, 0xF, true);
         return ((lane & 7) >= K) ? a : b;  // row_ror:K reads lane x-K; wrap inside the 8-lane group
     } else if constexpr (G == 4) {
         constexpr int q = ((0 + K) & 3) | (((1 + K) & 3) << 2) | (((2 + K) & 3) << 4) | (((3 + K) & 3) << 6);
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, q, 0xF, 0xF, false);  // quad_perm
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, q, 0xF, 0xF, true);  // quad_perm
     } else if constexpr (G == 2) {
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
     } else {
         return bperm32(v, (lane & ~(G - 1)) | ((lane + K) & (G - 1)));
     }
@@ -215,7 +224,7 @@ __device__ __forceinline__ uint32_t or_reduce_group(uint32_t v, int lane, uint32
 template <int G, int LMAX>
 __device__ __forceinline__ uint32_t from_lower_half(uint32_t v, int lane) {
     if constexpr (G <= 16) {
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + LMAX, 0xF, 0xF, false);  // row_ror:LMAX
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x120 + LMAX, 0xF, 0xF, true);  // row_ror:LMAX
     } else {
         return bperm32(v, lane - LMAX);
     }
@@ -226,7 +235,7 @@ __device__ __forceinline__ uint32_t from_lower_half(uint32_t v, int lane) {
 template <int G, int LMAX>
 __device__ __forceinline__ uint32_t from_upper_half(uint32_t v, int lane) {
     if constexpr (G <= 16) {
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + ((16 - LMAX) & 15), 0xF, 0xF, false);
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x120 + ((16 - LMAX) & 15), 0xF, 0xF, true);
     } else {
         return bperm32(v, lane + LMAX);
     }
