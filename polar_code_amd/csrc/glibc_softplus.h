@@ -27,6 +27,7 @@
 #ifndef PSCL_GLIBC_SOFTPLUS_H
 #define PSCL_GLIBC_SOFTPLUS_H
 
+#include <math.h>
 #include <stdint.h>
 #include <string.h>
 #ifndef __cplusplus
@@ -241,42 +242,76 @@ PSCL_HD double pscl_log1p(double x) {
  */
 PSCL_HD double pscl_sel(bool c, double a, double b) { return c ? a : b; }
 
-PSCL_HD double pscl_exp_neg(double x, const uint64_t* T) {
-    const uint64_t ix = pscl_asu64(x);
-    const uint32_t abstop = (uint32_t)(ix >> 52) & 0x7ff;
-    const double kd0 = pscl_fma(x, PSCL_EXP_INVLN2N, PSCL_EXP_SHIFT);
+/* Device forms of three steps of the exp below, written out: fma(-|v|, s, c) with the sign
+ * and magnitude as source modifiers, fma(a, s, c) as one VOP3 instead of a copy of the
+ * constant addend plus v_fmac, and the high word of the scale, hi + (k << 13). */
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ double pscl_fma_negabs(double v, double s, double c) {
+    double d;
+    asm("v_fma_f64 %0, -|%1|, %2, %3" : "=v"(d) : "v"(v), "s"(s), "v"(c));
+    return d;
+}
+__device__ __forceinline__ double pscl_fma3(double a, double s, double c) {
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "s"(s), "v"(c));
+    return d;
+}
+__device__ __forceinline__ uint32_t pscl_shl13_add(uint32_t k, uint32_t hi) {
+    uint32_t d;
+    asm("v_lshl_add_u32 %0, %1, 13, %2" : "=v"(d) : "v"(k), "v"(hi));
+    return d;
+}
+#else
+#define pscl_fma_negabs(v, s, c) pscl_fma(-fabs(v), (s), (c))
+#define pscl_fma3(a, s, c) pscl_fma((a), (s), (c))
+#define pscl_shl13_add(k, hi) ((uint32_t)(hi) + ((uint32_t)(k) << 13))
+#endif
+
+/* exp(-|v|) */
+PSCL_HD double pscl_exp_negabs(double v, const uint64_t* T) {
+    const uint32_t abstop = (uint32_t)(pscl_asu64(v) >> 52) & 0x7ff;
+    const double kd0 = pscl_fma_negabs(v, PSCL_EXP_INVLN2N, PSCL_EXP_SHIFT);
     const uint64_t ki = pscl_asu64(kd0);
     const double kd = kd0 - PSCL_EXP_SHIFT;
-    double r = pscl_fma(kd, PSCL_EXP_NEGLN2HIN, x);
+    double r = pscl_fma(kd, PSCL_EXP_NEGLN2HIN, -fabs(v));
     r = pscl_fma(kd, PSCL_EXP_NEGLN2LON, r);
     const uint64_t idx = 2 * (ki & 127);
-    const double p1 = pscl_fma(r, PSCL_EXP_C3, PSCL_EXP_C2);
+    const double p1 = pscl_fma3(r, PSCL_EXP_C3, PSCL_EXP_C2);
     const double tr = r + pscl_asf64(T[idx]);
-    const uint64_t sbits = T[idx + 1] + (ki << 45);
+    /* sbits = T[idx+1] + (ki << 45): the shifted term has no low word, so only the high word
+     * takes the sum (mod 2^32, as the 64-bit sum does mod 2^64) */
+    const uint64_t tw = T[idx + 1];
+    const uint32_t shi = pscl_shl13_add((uint32_t)ki, (uint32_t)(tw >> 32));
+    const uint64_t sbits = ((uint64_t)shi << 32) | (uint32_t)tw;
     const double r2 = r * r;
-    const double p2 = pscl_fma(r, PSCL_EXP_C5, PSCL_EXP_C4);
+    const double p2 = pscl_fma3(r, PSCL_EXP_C5, PSCL_EXP_C4);
     const double t = pscl_fma(p1, r2, tr);
     const double tmp = pscl_fma(r2 * r2, p2, t);
     /* main range */
     const double sc = pscl_asf64(sbits);
-    const double ymain = pscl_fma(sc, tmp, sc);
-    double y = ymain;
-    if (PSCL_RARE(abstop == 0x408u)) {
-        /* 512 <= |x| < 1024, k < 0: glibc specialcase, rounded once into the subnormal range */
-        const double scale = pscl_asf64(sbits + (1022ULL << 52));
-        const double st = tmp * scale;
-        const double y0 = scale + st;
-        const double hi = y0 + 1.0;
-        const double lo = ((1.0 - hi) + y0) + ((scale - y0) + st);
-        double yr = (lo + hi) - 1.0;
-        yr = yr == 0.0 ? 0.0 : yr;
-        const double yspec = pscl_sel(y0 < 1.0, yr, y0) * 0x1p-1022;
-        y = abstop == 0x408u ? yspec : ymain;
+    double y = pscl_fma(sc, tmp, sc);
+    if (PSCL_RARE(abstop - 0x3c9u >= 0x3fu)) {
+        /* outside 2^-54 <= |v| < 512 (glibc's abstop test) */
+        if (PSCL_ANY(abstop == 0x408u)) {
+            /* 512 <= |v| < 1024, k < 0: glibc specialcase, rounded once into the subnormal range */
+            const double scale = pscl_asf64(sbits + (1022ULL << 52));
+            const double st = tmp * scale;
+            const double y0 = scale + st;
+            const double hi = y0 + 1.0;
+            const double lo = ((1.0 - hi) + y0) + ((scale - y0) + st);
+            double yr = (lo + hi) - 1.0;
+            yr = yr == 0.0 ? 0.0 : yr;
+            const double yspec = pscl_sel(y0 < 1.0, yr, y0) * 0x1p-1022;
+            y = abstop == 0x408u ? yspec : y;
+        }
+        y = abstop > 0x408u ? 0.0 : y;            /* |v| >= 1024 and inf: underflow to +0 */
+        y = abstop < 0x3c9u ? 1.0 - fabs(v) : y;  /* |v| < 2^-54 and +-0: 1 + x, x = -|v| */
     }
-    y = abstop > 0x408u ? 0.0 : y;          /* |x| >= 1024 and -inf: underflow to +0 */
-    y = abstop < 0x3c9u ? 1.0 + x : y;      /* |x| < 2^-54 and -0 */
     return y;
 }
+
+/* exp(x) for x <= 0 */
+PSCL_HD double pscl_exp_neg(double x, const uint64_t* T) { return pscl_exp_negabs(x, T); }
 
 PSCL_HD double pscl_log1p_unit(double y) {
     const double ln2_hi = 6.93147180369123816490e-01;
@@ -338,8 +373,7 @@ PSCL_HD double pscl_log1p_unit(double y) {
 
 /* branch-free L = log1p(exp(-|v|)) (identical to pscl_softplus_tail for finite v and +-inf) */
 PSCL_HD double pscl_softplus_tail_bf(double v, const uint64_t* T) {
-    const double a = v < 0 ? -v : v;
-    return pscl_log1p_unit(pscl_exp_neg(-a, T));
+    return pscl_log1p_unit(pscl_exp_negabs(v, T));
 }
 
 /* L = log1p(exp(-|v|)), the part of logaddexp(0, +-v) shared by both bit hypotheses. */
