@@ -185,7 +185,8 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
         uint32_t rank = 0;          // list position of this path
         uint64_t u0 = 0, u1 = 0;    // decided bits
         uint32_t lastbit = 0;       // the bit decided at the previous phase
-        uint32_t tab = 0;           // LDS slot of depths 3..6 (4 bits each)
+        uint32_t tab = 0;           // LDS slot of depths 3..6 (4 bits each); lanes >= LMAX hold
+                                    // a copy of their path's table
         int cnt = 1;                // live paths of this frame (group-uniform)
         int j = 0;                  // info index (wave-uniform)
         bool pre_ok = false;        // Lpre holds the tail of this phase's leaf (wave-uniform)
@@ -288,23 +289,22 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 if (!(PSCL_ABLATE & 4) && start <= 6) {
                     // (DPP evaluated by every lane first: inside ?: only the selected lanes would
                     // run it, and a DPP that reads an inactive lane gets 0)
-                    const uint32_t tab_src = from_lower_half<G, LMAX>(tab, lane);
                     const uint32_t xs_src = from_lower_half<G, LMAX>(xs, lane);
-                    const uint32_t tabp = path_lane ? tab : tab_src;
+                    const uint32_t tabp = tab;
                     const uint32_t xsp = path_lane ? xs : xs_src;
                     if (start <= 4) step_depth<LMAX, CH, 4>(Af, g, tabp, xsp, start == 4, start == 4 && phi);
                     if (start <= 5) step_depth<LMAX, CH, 5>(Af, g, tabp, xsp, start == 5, start == 5);
                     if (start <= 6) step_depth<LMAX, CH, 6>(Af, g, tabp, xsp, start == 6, start == 6);
                 }
                 if (start <= 6) {  // this path's own slot at every depth rewritten this phase
+                    // (same update in the upper lane's copy: cpath is the path of both lanes)
                     const int s0 = start < 3 ? 3 : start;
                     const uint32_t mask = (0xffffu << (4 * (s0 - 3))) & 0xffffu;
                     tab = (tab & ~mask) | ((uint32_t)cpath * 0x1111u & mask);
                 }
                 // ---- leaf LLRs.  Lanes >= LMAX: the sibling leaf (phi+1) given bit 0 here.
-                const uint32_t tab_lo = from_lower_half<G, LMAX>(tab, lane);
-                const uint32_t ptab = path_lane ? tab : tab_lo;
-                const double* par = Af + Ly::OFF6 + slot_at(ptab, 6);
+                // (depth 6 was just rewritten into the path's own slot at even phases)
+                const double* par = Af + Ly::OFF6 + (start <= 6 ? cpath : slot_at(tab, 6));
                 const double la = par[0], lb = par[LMAX];
                 const uint32_t xleaf = lastbit;  // u[phi - 1], the left sibling's bit at odd phases
                 const double lam = (PSCL_ABLATE & 128) ? la : (path_lane ? ((phi & 1) ? g_node(la, lb, xleaf) : f_minsum(la, lb)) : lb + la);
@@ -319,15 +319,17 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 const bool frozen_even = !is_info && !(phi & 1);
                 Lpre = Lt;
                 pre_ok = frozen_even;
-                double i0, i1;
-                metric_incr(lam, Lt, i0, i1);
-                const double m0 = metric + i0;
-                const double m1 = metric + i1;
+                // children metrics (scl.py:102-105): the child along the LLR sign pays Lt, the
+                // other |lam| + Lt; an exactly zero LLR gives both LOGE2 (rare wave branch)
+                const bool neg = lam < 0.0;
+                const double mgd = metric + Lt, mbd = metric + (fabs(lam) + Lt);
 
                 if (!is_info) {
                     // frozen: bit 0, metrics advance, stable re-rank in place (lanes do not move).
                     // While lane order is list order, the stable sort is the identity exactly when
                     // the new metrics stay non-decreasing along the lanes: one adjacent compare.
+                    double m0 = neg ? mbd : mgd;
+                    if (PSCL_RARE(lam == 0.0)) m0 = lam == 0.0 ? metric + PSCL_LOGE2 : m0;
                     metric = m0;
                     lastbit = 0;
                     bool moved = true;
@@ -362,8 +364,8 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     // better children keep the lane order, the survivors are the better children
                     // in place -- the outcome of the stable sort, with no ranking and no moves
                     if (ordered && !sc_hard && !(PSCL_ABLATE & 256)) {
-                        const uint32_t gb = lam < 0.0 ? 1u : 0u;
-                        const uint64_t mg = pscl_asu64(gb ? m1 : m0), mb = pscl_asu64(gb ? m0 : m1);
+                        const uint32_t gb = neg ? 1u : 0u;
+                        const uint64_t mg = pscl_asu64(mgd), mb = pscl_asu64(mbd);
                         const uint64_t pv = prev_lane64(mg);
                         const uint64_t top = shfl_u64(mg, gbase + L - 1);
                         bool forced_here = false;
@@ -391,6 +393,11 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     if (lane == 0 && P.counters) atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + 10, 1ULL);
     #endif
                     // info: children (bit 0 in lane g, bit 1 in lane g + LMAX) of every path
+                    double m0 = neg ? mbd : mgd, m1 = neg ? mgd : mbd;
+                    if (PSCL_RARE(lam == 0.0)) {
+                        m0 = lam == 0.0 ? metric + PSCL_LOGE2 : m0;
+                        m1 = lam == 0.0 ? metric + PSCL_LOGE2 : m1;
+                    }
                     const uint64_t pm1 = from_lower_half64<G, LMAX>(pscl_asu64(m1), lane);
                     const uint32_t prank = from_lower_half<G, LMAX>(rank, lane);
                     uint64_t km = cbit ? pm1 : pscl_asu64(m0);
@@ -433,7 +440,9 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     metric = pscl_asf64(nm);
                     u0 = nu0;
                     u1 = nu1;
-                    tab = ntab;
+                    // the upper lanes copy their (new) path's table
+                    const uint32_t ntab_lo = from_lower_half<G, LMAX>(ntab, lane);
+                    tab = path_lane ? ntab : ntab_lo;
                     if (b) {
                         if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
                     }
