@@ -49,8 +49,9 @@
 /* PSCL_ANY(c): true if c holds in any lane of the wavefront (wave-uniform branch on the
  * device; plain c on the host).  Used to skip rarely needed branch-free sections. */
 #if defined(__HIP_DEVICE_COMPILE__)
-#define PSCL_ANY(c) __any(c)
-#define PSCL_RARE(c) __builtin_expect(__any(c), 0)
+/* (ballot of the i1 itself: __any() takes an int and costs a select + compare per test) */
+#define PSCL_ANY(c) (__builtin_amdgcn_ballot_w64((bool)(c)) != 0)
+#define PSCL_RARE(c) __builtin_expect(__builtin_amdgcn_ballot_w64((bool)(c)) != 0, 0)
 #else
 #define PSCL_RARE(c) (c)
 #define PSCL_ANY(c) (c)

@@ -38,7 +38,8 @@ hipError_t launch128(const pscl_decode_params& P, int hist, int wpg, int64_t gri
     if (hist)
         return P.rm_E ? launch128k<LMAX, true, true, true>(P, wpg, grid, lds, s)
                       : launch128k<LMAX, true, false, true>(P, wpg, grid, lds, s);
-    const int code = spec_code(P);
+    // (without forced bits the compiled-in kernels assume a full list, L == LMAX)
+    const int code = (fs || P.L == LMAX) ? spec_code(P) : 0;
     if (code == 1 && !P.rm_E) {
         switch (LMAX) {
             case 1: return pscl_launch_spec_1_1(P, fs, wpg, grid, lds, s);

@@ -138,7 +138,10 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
     const int fl = lane >> LOG_G;
     const int g = lane & (G - 1);
     const int gbase = lane & ~(G - 1);
-    const int K = P.K, L = P.L;
+    // with a compiled-in information set and no forced bits the list is full-size (launches
+    // with L != LMAX take the CODE 0 kernels) and its length at every phase is known
+    constexpr bool kFixedList = CODE != 0 && !FS;
+    const int K = P.K, L = kFixedList ? LMAX : P.L;
     unsigned char* wbase = smem + P.wg_fixed_bytes + (size_t)wave * P.wave_bytes;
     double* A = reinterpret_cast<double*>(wbase);
     double* Af = A + fl * Ly::FSTRIDE;
@@ -201,6 +204,11 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 const int start = PT ? kn - __builtin_ctz((unsigned)PT) : ((int)blk ? 3 - __builtin_ctz((unsigned)(int)blk) : 1);
                 const uint64_t infow = phi < 64 ? info0 : info1;
                 const bool is_info = (infow >> (phi & 63)) & 1;
+                if constexpr (kFixedList) {  // min(2^j, L) paths after j information bits
+                    const int jb = phi < 64 ? __builtin_popcountll(info0 & ((1ULL << (phi & 63)) - 1))
+                                            : __builtin_popcountll(info0) + __builtin_popcountll(info1 & ((1ULL << (phi & 63)) - 1));
+                    cnt = jb >= Ly::LOG_LM ? LMAX : (1 << jb);
+                }
 #ifdef PSCL_PHASE_MARKERS  // asm listing analysis only
                 asm volatile("; PHASE %0" ::"n"(PT));
 #endif
@@ -335,7 +343,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     bool moved = true;
                     if (ordered && !(PSCL_ABLATE & 256)) {
                         const uint64_t pv = prev_lane64(pscl_asu64(m0));
-                        moved = __any(path_lane && fvalid && g >= 1 && g < cnt && pv > pscl_asu64(m0));
+                        moved = PSCL_ANY(path_lane & fvalid & (g >= 1) & (g < cnt) & (pv > pscl_asu64(m0)));
                     }
     #ifdef PSCL_STATS  // diagnostic build (tools/fastpath_stats.py): counters[8..11] of a 16-slot buffer
                     if (lane == 0 && P.counters) {
@@ -357,7 +365,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     uint32_t r = 0;
                     if (!(PSCL_ABLATE & 18)) rank_step_n<G, 1, LMAX>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
                     if (path_lane) rank = r;
-                    ordered = !__any(path_lane && fvalid && g < cnt && rank != (uint32_t)g);
+                    ordered = !PSCL_ANY(path_lane & fvalid & (g < cnt) & (rank != (uint32_t)g));
                 } else {
                     // info, full list, lane order = list order: when every path's worse child
                     // (against the LLR sign) is strictly worse than every better child and the
@@ -370,9 +378,9 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                         const uint64_t top = shfl_u64(mg, gbase + L - 1);
                         bool forced_here = false;
                         if (FS && force) forced_here = (((j < 64 ? fm0 : fm1) >> (j & 63)) & 1) != 0;
-                        const bool bad = path_lane && g < L && fvalid &&
-                                         (cnt != L || lam == 0.0 || forced_here || (g >= 1 && pv > mg) || !(mb > top));
-                        if (!__any(bad)) {
+                        const bool bad = path_lane & (g < L) & fvalid &
+                                         ((cnt != L) | (lam == 0.0) | forced_here | ((g >= 1) & (pv > mg)) | !(mb > top));
+                        if (!PSCL_ANY(bad)) {
                             if (HIST && path_lane && g < L) {
                                 hist_llr[j * L + g] = lam;
                                 hist_par[j * L + g] = (uint8_t)g;
