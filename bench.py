@@ -71,20 +71,24 @@ def load_traffic(workload_key: str):
 
 
 def load_valu_profile(workload_key: str):
-    """(VALU wave-instructions per frame, VALU-active fraction) of the decode kernel for this
-    workload, from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json)."""
+    """The committed rocprofv3 PMC entry of the decode kernel for this workload
+    (profiles/pmc_traffic.json): VALU instructions per frame, instruction mix, VALU-active."""
     p = ROOT / "profiles" / "pmc_traffic.json"
     if not p.exists():
         return None
     try:
         e = json.loads(p.read_text()).get(workload_key) or {}
-        return (float(e["valu_instr_per_frame"]), e.get("valu_active_frac")) if "valu_instr_per_frame" in e else None
+        return e if "valu_instr_per_frame" in e else None
     except Exception:
         return None
 
 
-# VALU issue peak of MI355X: 256 CUs x 4 SIMDs x 2.4 GHz; a wave64 f32/int VALU instruction
-# takes 2 cycles on a SIMD-32, an fp64 add/mul/fma 4 (MI355X_MICROARCH.md constants table)
+# VALU issue peak of MI355X: 256 CUs x 4 SIMDs x 2.4 GHz, one wave64 instruction per SIMD per
+# 4 cycles.  That is the fp64 rate (16 lanes/clk: the 78.6 TF FP64 vector spec) and what a wave
+# sustains alone (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'); f32/int ops can
+# pipeline at 2 cycles between waves (SIMD-32), so the mix-weighted bound (fp64 at 4, the rest
+# at 2) is reported beside it.  This kernel measures 4.1 cycles per VALU instruction with the
+# VALU active ~100 % of SIMD cycles (profiles/pmc_traffic.json).
 SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
 
 
@@ -227,14 +231,22 @@ def main():
         vp = load_valu_profile(wkey)
         compute = None
         if vp is not None:
-            rate = vp[0] * B / (per_batch_ms * 1e-3)
-            peak32, peak64 = SIMDS * CLOCK_HZ / 2, SIMDS * CLOCK_HZ / 4
-            compute = {"bound": "valu-issue", "unit": "wave-instr/s", "instr_per_frame": vp[0],
-                       "achieved": rate, "peak_f32_issue": peak32, "peak_f64_issue": peak64,
-                       "frac_of_f32_issue": rate / peak32, "frac_of_f64_issue": rate / peak64,
-                       "valu_active_frac_pmc": vp[1],
-                       "note": "instr/frame from SQ_INSTS_VALU (profiles/pmc_traffic.json) x live frames/s; the "
-                               "mix is fp64 (4 cyc) and int/f32 (2 cyc) ops, so the true issue peak lies between"}
+            ipf = float(vp["valu_instr_per_frame"])
+            rate = ipf * B / (per_batch_ms * 1e-3)
+            peak4 = SIMDS * CLOCK_HZ / 4
+            compute = {"bound": "valu-issue", "unit": "wave-instr/s", "instr_per_frame": ipf,
+                       "achieved": rate, "peak": peak4, "frac": rate / peak4,
+                       "valu_active_frac_pmc": vp.get("valu_active_frac"),
+                       "cycles_per_valu_instr_pmc": vp.get("cycles_per_valu_instr")}
+            mix = vp.get("valu_mix_per_frame")
+            if mix:
+                f64 = sum(mix.get(k, 0.0) for k in ("add_f64", "mul_f64", "fma_f64", "trans_f64"))
+                cyc = (4 * f64 + 2 * (ipf - f64)) * B / SIMDS  # SIMD-cycles per launch, mix-weighted
+                compute["fp64_share"] = f64 / ipf
+                compute["frac_mix_weighted"] = cyc / CLOCK_HZ / (per_batch_ms * 1e-3)
+            compute["note"] = ("instr/frame and mix from rocprofv3 PMC (profiles/pmc_traffic.json) x live frames/s; "
+                               "peak = one wave64 VALU instruction per 4 cycles per SIMD (fp64 rate); "
+                               "frac_mix_weighted prices non-fp64 ops at 2 cycles")
         fer = c[1] / max(c[0], 1)
         p0 = REF_FER_L8[0] / REF_FER_L8[1]
         pp = (c[1] + REF_FER_L8[0]) / (c[0] + REF_FER_L8[1])

@@ -44,6 +44,22 @@ def main():
                 print(f"{k} per wave = {c[k] / w:.0f}")
     if "GRBM_GUI_ACTIVE" in c:
         print(f"GRBM_GUI_ACTIVE = {c['GRBM_GUI_ACTIVE']:.4g}")
+    for k, name in (("SQ_INSTS_VALU", "valu"), ("SQ_INSTS_SALU", "salu"), ("SQ_INSTS_LDS", "lds")):
+        if k in c:
+            out[f"{name}_instr_per_frame"] = round(c[k] / frames, 2)
+    if "SQ_ACTIVE_INST_VALU" in c and "GRBM_GUI_ACTIVE" in c:
+        # quad-cycles summed over waves, x4 -> cycles; 1024 SIMDs; GRBM counts per XCD (8)
+        cyc = c["GRBM_GUI_ACTIVE"] / 8
+        out["valu_active_frac"] = round(c["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * cyc), 4)
+        out["valu_active_frac_def"] = "SQ_ACTIVE_INST_VALU*4 / (1024 SIMDs * GRBM_GUI_ACTIVE/8)"
+        if "SQ_INSTS_VALU" in c:
+            out["cycles_per_valu_instr"] = round(1024 * cyc / c["SQ_INSTS_VALU"], 3)
+            print(f"SIMD cycles per VALU instruction = {out['cycles_per_valu_instr']}")
+    mix = {k[len("SQ_INSTS_VALU_"):].lower(): round(c[k] / frames, 1) for k in c if k.startswith("SQ_INSTS_VALU_")}
+    if mix:
+        out["valu_mix_per_frame"] = mix
+    if "SQ_LDS_BANK_CONFLICT" in c:
+        out["lds_bank_conflict_cycles"] = c["SQ_LDS_BANK_CONFLICT"]
     if "--json" in sys.argv:
         print(json.dumps(out))
 
