@@ -128,9 +128,13 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint64_t* T = reinterpret_cast<uint64_t*>(smem);
     for (int i = threadIdx.x; i < PSCL_EXP_TABLE_WORDS; i += blockDim.x) T[i] = P.exp_table[i];
+#if PSCL_EPI_LDS
     for (int i = threadIdx.x; i < P.epi_words; i += blockDim.x) T[PSCL_EXP_TABLE_WORDS + i] = P.epi_table[i];
-    __syncthreads();
     const uint8_t* GT = reinterpret_cast<const uint8_t*>(T + PSCL_EXP_TABLE_WORDS);  // [16][256]
+#else  // epilogue tables read from global memory (L1/L2-resident): less LDS per workgroup
+    const uint8_t* GT = reinterpret_cast<const uint8_t*>(P.epi_table);
+#endif
+    __syncthreads();
     const uint32_t* ST = reinterpret_cast<const uint32_t*>(GT + 16 * 256);           // [K4][16]
 
     const int wave = threadIdx.x >> 6;

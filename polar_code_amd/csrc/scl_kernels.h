@@ -8,6 +8,11 @@
 #include "polar_scl.h"
 
 #define PSCL_MAX_WAVES_PER_WG 4
+// 1: the scl128 epilogue tables (u-byte gather, CRC syndrome) are staged in LDS per workgroup;
+// 0: read from global memory
+#ifndef PSCL_EPI_LDS
+#define PSCL_EPI_LDS 1
+#endif
 
 struct pscl_decode_params {
     const double* llr;  // [B][N]
