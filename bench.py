@@ -47,13 +47,17 @@ def parse():
                     help="DL-SCL flip retries per CRC-failing frame (BASELINE config 4: --list 4 --retries 8)")
     ap.add_argument("--beta", type=str, default="auto",
                     help="flip metric .npy ('auto': tests/golden/beta_M{L}.npy, the reference checkpoint; 'none')")
+    ap.add_argument("--nr-E", type=int, default=0,
+                    help="NR config 5: (128,88) = 64 payload + CRC-24 bits, rate matched to E transmitted "
+                         "bits (run_ber_sweep.py nr_polar_scl); the TX kernel interleaves/repeats, the "
+                         "decoder de-rate-matches in its channel staging")
     return ap.parse_args()
 
 
-def frame_bytes(N: int, W: int) -> int:
-    """Algorithmic HBM bytes per decoded frame: read N fp64 LLRs and W reference words,
-    write W best-candidate words and one flag byte."""
-    return N * 8 + W * 8 + W * 8 + 1
+def frame_bytes(n_in: int, W: int) -> int:
+    """Algorithmic HBM bytes per decoded frame: read n_in fp64 LLRs (N, or E rate matched) and
+    W reference words, write W best-candidate words and one flag byte."""
+    return n_in * 8 + W * 8 + W * 8 + 1
 
 
 def load_traffic(workload_key: str):
@@ -144,18 +148,22 @@ def main():
     from polar_code_amd import _native
     from polar_code_amd.polar.polar import construct_info_set
 
-    N, K, L, B = 128, 64, args.list, args.frames
+    E = args.nr_E
+    N, K, L, B = 128, (88 if E else 64), args.list, args.frames
     info = construct_info_set(N, K)
     dec = _native.Decoder(N, info, L, POLY, device=device_index)
+    if E:
+        dec.set_rate_match(E)
+    n_in = E or N
     stream = torch.cuda.current_stream(dev)
     dec.set_stream(stream.cuda_stream)
     W = dec.W
     kp = K - 24
-    rate = K / N
+    rate = kp / E if E else K / N  # run_ber_sweep.py: R = K_payload / E; run_fer_sweep.py: K / N
 
     # ---- inputs resident in HBM: distinct frames per (rank, step), generated on device
-    nbuf = max(1, min(args.steps, int(48e9 // (B * N * 8))))
-    llr = [torch.empty((B, N), dtype=torch.float64, device=dev) for _ in range(nbuf)]
+    nbuf = max(1, min(args.steps, int(48e9 // (B * n_in * 8))))
+    llr = [torch.empty((B, n_in), dtype=torch.float64, device=dev) for _ in range(nbuf)]
     msg = [torch.empty((B, W), dtype=torch.int64, device=dev) for _ in range(nbuf)]
     best = torch.empty((B, W), dtype=torch.int64, device=dev)
     flags = torch.empty((B,), dtype=torch.uint8, device=dev)
@@ -215,18 +223,18 @@ def main():
     frames_total = B * args.steps * world
 
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline and not E:
         host = llr[0][: min(B, 1_000_000)].cpu().numpy()
         cpu = cpu_baseline(host, info, L, args.cpu_seconds, args.retries, beta)
 
     if rank == 0:
         avg_ms = kern_ms / max(launches, 1)
-        fb = frame_bytes(N, W)
+        fb = frame_bytes(n_in, W)
         # DL mode: the step's decode launches (baseline + retry rounds) priced as one pass
         # over the batch; otherwise one launch = one batch
         per_batch_ms = kern_ms / args.steps if args.retries > 0 else avg_ms
         achieved = fb * B / (per_batch_ms * 1e-3) / 1e9
-        wkey = f"scl_L{L}_N{N}_K{K}_B{B}" + (f"_dl{args.retries}" if args.retries > 0 else "")
+        wkey = f"scl_L{L}_N{N}_K{K}_B{B}" + (f"_E{E}" if E else "") + (f"_dl{args.retries}" if args.retries > 0 else "")
         traffic = load_traffic(wkey)
         vp = load_valu_profile(wkey)
         compute = None
@@ -259,8 +267,12 @@ def main():
         metric = "decoded frames/sec, P(128,64)+CRC24 SCL L=8 @ Eb/N0=5 dB; FER match"
         workload = (f"SCL L={L} P({N},{K})+CRC24 (0x1864CFB) @ Eb/N0={args.ebno:g} dB, "
                     f"{B} frames/GPU/step, decode+CRC select+FER/BER count")
+        if E:
+            metric = f"decoded frames/sec, NR polar N=128 E={E} K=64+CRC24 SCL L={L}"
+            workload = (f"NR SCL L={L} (128,88) rate matched E={E}, R={rate:g} @ Eb/N0={args.ebno:g} dB, {B} "
+                        f"frames/GPU/step, de-rate-match + decode + CRC select + FER/BER count")
         if args.retries > 0:
-            metric = f"decoded frames/sec, P(128,64)+CRC24 DL-SCL L={L} + {args.retries} flip retries"
+            metric = f"decoded frames/sec, P(128,{K})+CRC24 DL-SCL L={L} + {args.retries} flip retries"
             workload = (f"DL-SCL L={L} + {args.retries} flips (beta) P({N},{K})+CRC24 @ Eb/N0={args.ebno:g} dB, "
                         f"{B} frames/GPU/step, SCL + retry rounds + FER/BER count")
         line = {
@@ -276,7 +288,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: on-device Philox4x32 BPSK/AWGN frames (payload->CRC24->polar->LLR), resident in HBM",
-            "config": {"workload": workload, "retries": args.retries,
+            "config": {"workload": workload, "retries": args.retries, "E": E or None,
                        "N": N, "K": K, "list_size": L, "ebno_db": args.ebno, "frames_per_gpu_per_step": B,
                        "global_batch": B * world, "parallelism": f"frame-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -287,8 +299,9 @@ def main():
                          "bytes_per_frame": fb, "compute": compute},
             "cpu_baseline": cpu,
             "fer": {"frames": int(c[0]), "frame_errors": int(c[1]), "fer": fer, "ber": c[2] / max(c[0] * K, 1),
-                    "reference_fer": p0 if L == 8 else None,
-                    "z_vs_reference": (fer - p0) / se if (L == 8 and args.ebno == 5.0) else None},
+                    "payload_fer": c[3] / max(c[0], 1), "payload_ber": c[4] / max(c[0] * kp, 1),
+                    "reference_fer": p0 if (L == 8 and not E) else None,
+                    "z_vs_reference": (fer - p0) / se if (L == 8 and args.ebno == 5.0 and not E) else None},
             "dl_scl": dl,
         }
         print(json.dumps(line), flush=True)
