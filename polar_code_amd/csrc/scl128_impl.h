@@ -205,265 +205,265 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
         auto phase = [&](const auto blk, auto TC) {
             constexpr int PT = decltype(TC)::value;
             const int phi = (int)blk * 16 + PT;
-                const int start = PT ? kn - __builtin_ctz((unsigned)PT) : ((int)blk ? 3 - __builtin_ctz((unsigned)(int)blk) : 1);
-                const uint64_t infow = phi < 64 ? info0 : info1;
-                const bool is_info = (infow >> (phi & 63)) & 1;
-                if constexpr (kFixedList) {  // min(2^j, L) paths after j information bits
-                    const int jb = phi < 64 ? __builtin_popcountll(info0 & ((1ULL << (phi & 63)) - 1))
-                                            : __builtin_popcountll(info0) + __builtin_popcountll(info1 & ((1ULL << (phi & 63)) - 1));
-                    cnt = jb >= Ly::LOG_LM ? LMAX : (1 << jb);
-                }
+            const int start = PT ? kn - __builtin_ctz((unsigned)PT) : ((int)blk ? 3 - __builtin_ctz((unsigned)(int)blk) : 1);
+            const uint64_t infow = phi < 64 ? info0 : info1;
+            const bool is_info = (infow >> (phi & 63)) & 1;
+            if constexpr (kFixedList) {  // min(2^j, L) paths after j information bits
+                const int jb = phi < 64 ? __builtin_popcountll(info0 & ((1ULL << (phi & 63)) - 1))
+                                        : __builtin_popcountll(info0) + __builtin_popcountll(info1 & ((1ULL << (phi & 63)) - 1));
+                cnt = jb >= Ly::LOG_LM ? LMAX : (1 << jb);
+            }
 #ifdef PSCL_PHASE_MARKERS  // asm listing analysis only
-                asm volatile("; PHASE %0" ::"n"(PT));
+            asm volatile("; PHASE %0" ::"n"(PT));
 #endif
-                // ---- depths 1-3 recomputed from the channel (phi % 16 == 0)
-                if (start <= 3 && !(PSCL_ABLATE & 12)) {
-                    const bool r1 = phi >= 64, r2 = (phi >> 5) & 1, r3 = (phi >> 4) & 1;
-                    // path lanes: partial sums of the left siblings at depths 1, 2, 3
-                    uint64_t X1 = 0;
-                    uint32_t X2 = 0, X3 = 0;
-                    if (r1) X1 = polar_transform64(u0);
-                    if (r2) {  // u[32(k2-1), 32 k2), k2 = phi >> 5 odd
-                        const int lo = phi - (phi & 31) - 32;
-                        X2 = polar_transform32((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)));
-                    }
-                    if (r3) {  // u[phi-16, phi)
-                        const int lo = phi - 16;
-                        X3 = polar_transform16((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)) & 0xffffu);
-                    }
-                    if (LMAX <= 2 && !CH) {
-                        // few lanes per frame: 16-lane jobs, one (frame, path) each, so every
-                        // channel load instruction reads whole 128-byte rows of 4 frames
-                        const int e = lane & 15, slot = lane >> 4;
-    #pragma unroll 2
-                        for (int it = 0; it < F * LMAX / 4; ++it) {
-                            const int job = it * 4 + slot;
-                            const int fj = job / LMAX, p = job % LMAX;
-                            const int owner = fj * G + p;
-                            const double* cj = reinterpret_cast<const double*>(shfl_u64((uint64_t)chan, fj * G));
-                            double c[8];
-    #pragma unroll
-                            for (int m = 0; m < 8; ++m) c[m] = cj[e + 16 * m];
-                            uint64_t x1 = 0;
-                            uint32_t x2 = 0, x3 = 0;
-                            if (r1) x1 = shfl_u64(X1, owner);
-                            if (r2) x2 = bperm32(X2, owner);
-                            if (r3) x3 = bperm32(X3, owner);
-                            double d1[4];
-    #pragma unroll
-                            for (int m = 0; m < 4; ++m)
-                                d1[m] = r1 ? g_node(c[m], c[m + 4], (uint32_t)(x1 >> (e + 16 * m)) & 1u) : f_minsum(c[m], c[m + 4]);
-                            double d2[2];
-    #pragma unroll
-                            for (int s2 = 0; s2 < 2; ++s2)
-                                d2[s2] = r2 ? g_node(d1[s2], d1[s2 + 2], (x2 >> (e + 16 * s2)) & 1u) : f_minsum(d1[s2], d1[s2 + 2]);
-                            const double d3 = r3 ? g_node(d2[0], d2[1], (x3 >> e) & 1u) : f_minsum(d2[0], d2[1]);
-                            A[fj * Ly::FSTRIDE + Ly::OFF3 + e * LMAX + p] = d3;
-                        }
-                    } else
-    #pragma unroll
-                    for (int q = 0; q < 16 / G + (G > 16); ++q) {
-                        const int e = g + G * q;
+            // ---- depths 1-3 recomputed from the channel (phi % 16 == 0)
+            if (start <= 3 && !(PSCL_ABLATE & 12)) {
+                const bool r1 = phi >= 64, r2 = (phi >> 5) & 1, r3 = (phi >> 4) & 1;
+                // path lanes: partial sums of the left siblings at depths 1, 2, 3
+                uint64_t X1 = 0;
+                uint32_t X2 = 0, X3 = 0;
+                if (r1) X1 = polar_transform64(u0);
+                if (r2) {  // u[32(k2-1), 32 k2), k2 = phi >> 5 odd
+                    const int lo = phi - (phi & 31) - 32;
+                    X2 = polar_transform32((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)));
+                }
+                if (r3) {  // u[phi-16, phi)
+                    const int lo = phi - 16;
+                    X3 = polar_transform16((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)) & 0xffffu);
+                }
+                if (LMAX <= 2 && !CH) {
+                    // few lanes per frame: 16-lane jobs, one (frame, path) each, so every
+                    // channel load instruction reads whole 128-byte rows of 4 frames
+                    const int e = lane & 15, slot = lane >> 4;
+#pragma unroll 2
+                    for (int it = 0; it < F * LMAX / 4; ++it) {
+                        const int job = it * 4 + slot;
+                        const int fj = job / LMAX, p = job % LMAX;
+                        const int owner = fj * G + p;
+                        const double* cj = reinterpret_cast<const double*>(shfl_u64((uint64_t)chan, fj * G));
                         double c[8];
-    #pragma unroll
-                        for (int m = 0; m < 8; ++m) c[m] = CH ? Af[e + 16 * m] : chan[e + 16 * m];
-                        double d1l[4];
-    #pragma unroll
-                        for (int m = 0; m < 4; ++m) d1l[m] = f_minsum(c[m], c[m + 4]);
-    #pragma unroll
-                        for (int p = 0; p < LMAX; ++p) {
-                            const int src = gbase + p;
-                            uint64_t x1 = 0;
-                            uint32_t x2 = 0, x3 = 0;
-                            if (r1) x1 = shfl_u64(X1, src);
-                            if (r2) x2 = bperm32(X2, src);
-                            if (r3) x3 = bperm32(X3, src);
-                            double d1[4];
-    #pragma unroll
-                            for (int m = 0; m < 4; ++m)
-                                d1[m] = r1 ? g_node(c[m], c[m + 4], (uint32_t)(x1 >> (e + 16 * m)) & 1u) : d1l[m];
-                            double d2[2];
-    #pragma unroll
-                            for (int s2 = 0; s2 < 2; ++s2)
-                                d2[s2] = r2 ? g_node(d1[s2], d1[s2 + 2], (x2 >> (e + 16 * s2)) & 1u) : f_minsum(d1[s2], d1[s2 + 2]);
-                            const double d3 = r3 ? g_node(d2[0], d2[1], (x3 >> e) & 1u) : f_minsum(d2[0], d2[1]);
-                            Af[Ly::OFF3 + e * LMAX + p] = d3;
-                        }
+#pragma unroll
+                        for (int m = 0; m < 8; ++m) c[m] = cj[e + 16 * m];
+                        uint64_t x1 = 0;
+                        uint32_t x2 = 0, x3 = 0;
+                        if (r1) x1 = shfl_u64(X1, owner);
+                        if (r2) x2 = bperm32(X2, owner);
+                        if (r3) x3 = bperm32(X3, owner);
+                        double d1[4];
+#pragma unroll
+                        for (int m = 0; m < 4; ++m)
+                            d1[m] = r1 ? g_node(c[m], c[m + 4], (uint32_t)(x1 >> (e + 16 * m)) & 1u) : f_minsum(c[m], c[m + 4]);
+                        double d2[2];
+#pragma unroll
+                        for (int s2 = 0; s2 < 2; ++s2)
+                            d2[s2] = r2 ? g_node(d1[s2], d1[s2 + 2], (x2 >> (e + 16 * s2)) & 1u) : f_minsum(d1[s2], d1[s2 + 2]);
+                        const double d3 = r3 ? g_node(d2[0], d2[1], (x3 >> e) & 1u) : f_minsum(d2[0], d2[1]);
+                        A[fj * Ly::FSTRIDE + Ly::OFF3 + e * LMAX + p] = d3;
                     }
-                    wave_lds_fence();
+                } else
+#pragma unroll
+                for (int q = 0; q < 16 / G + (G > 16); ++q) {
+                    const int e = g + G * q;
+                    double c[8];
+#pragma unroll
+                    for (int m = 0; m < 8; ++m) c[m] = CH ? Af[e + 16 * m] : chan[e + 16 * m];
+                    double d1l[4];
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) d1l[m] = f_minsum(c[m], c[m + 4]);
+#pragma unroll
+                    for (int p = 0; p < LMAX; ++p) {
+                        const int src = gbase + p;
+                        uint64_t x1 = 0;
+                        uint32_t x2 = 0, x3 = 0;
+                        if (r1) x1 = shfl_u64(X1, src);
+                        if (r2) x2 = bperm32(X2, src);
+                        if (r3) x3 = bperm32(X3, src);
+                        double d1[4];
+#pragma unroll
+                        for (int m = 0; m < 4; ++m)
+                            d1[m] = r1 ? g_node(c[m], c[m + 4], (uint32_t)(x1 >> (e + 16 * m)) & 1u) : d1l[m];
+                        double d2[2];
+#pragma unroll
+                        for (int s2 = 0; s2 < 2; ++s2)
+                            d2[s2] = r2 ? g_node(d1[s2], d1[s2 + 2], (x2 >> (e + 16 * s2)) & 1u) : f_minsum(d1[s2], d1[s2 + 2]);
+                        const double d3 = r3 ? g_node(d2[0], d2[1], (x3 >> e) & 1u) : f_minsum(d2[0], d2[1]);
+                        Af[Ly::OFF3 + e * LMAX + p] = d3;
+                    }
                 }
-                // ---- depths 4..6 (partial sums of the g node's left sibling: xs, <= 8 bits)
-                uint32_t xs = 0;
-                if (phi && start >= 4 && start <= 6) {  // u[phi-w, phi), w = 8, 4, 2
-                    const int w = 1 << (kn - start), lo = phi - w;
-                    xs = polar_transform8((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)) & ((1u << w) - 1u));
-                }
-                if (!(PSCL_ABLATE & 4) && start <= 6) {
-                    // (DPP evaluated by every lane first: inside ?: only the selected lanes would
-                    // run it, and a DPP that reads an inactive lane gets 0)
-                    const uint32_t xs_src = from_lower_half<G, LMAX>(xs, lane);
-                    const uint32_t tabp = tab;
-                    const uint32_t xsp = path_lane ? xs : xs_src;
-                    if (start <= 4) step_depth<LMAX, CH, 4>(Af, g, tabp, xsp, start == 4, start == 4 && phi);
-                    if (start <= 5) step_depth<LMAX, CH, 5>(Af, g, tabp, xsp, start == 5, start == 5);
-                    if (start <= 6) step_depth<LMAX, CH, 6>(Af, g, tabp, xsp, start == 6, start == 6);
-                }
-                if (start <= 6) {  // this path's own slot at every depth rewritten this phase
-                    // (same update in the upper lane's copy: cpath is the path of both lanes)
-                    const int s0 = start < 3 ? 3 : start;
-                    const uint32_t mask = (0xffffu << (4 * (s0 - 3))) & 0xffffu;
-                    tab = (tab & ~mask) | ((uint32_t)cpath * 0x1111u & mask);
-                }
-                // ---- leaf LLRs.  Lanes >= LMAX: the sibling leaf (phi+1) given bit 0 here.
-                // (depth 6 was just rewritten into the path's own slot at even phases)
-                const double* par = Af + Ly::OFF6 + (start <= 6 ? cpath : slot_at(tab, 6));
-                const double la = par[0], lb = par[LMAX];
-                const uint32_t xleaf = lastbit;  // u[phi - 1], the left sibling's bit at odd phases
-                const double lam = (PSCL_ABLATE & 128) ? la : (path_lane ? ((phi & 1) ? g_node(la, lb, xleaf) : f_minsum(la, lb)) : lb + la);
-                // ---- metric tail log1p(exp(-|llr|)) (scl.py:102-105)
-                double Lt;
-                const uint64_t lpre_up = from_upper_half64<G, LMAX>(pscl_asu64(Lpre), lane);
-                if (pre_ok) {
-                    Lt = pscl_asf64(lpre_up);
-                } else {
-                    Lt = (PSCL_ABLATE & 1) ? lam * 0.5 : pscl_softplus_tail_bf(lam, T);
-                }
-                const bool frozen_even = !is_info && !(phi & 1);
-                Lpre = Lt;
-                pre_ok = frozen_even;
-                // children metrics (scl.py:102-105): the child along the LLR sign pays Lt, the
-                // other |lam| + Lt; an exactly zero LLR gives both LOGE2 (rare wave branch)
-                const bool neg = lam < 0.0;
-                const double mgd = metric + Lt, mbd = metric + (fabs(lam) + Lt);
+                wave_lds_fence();
+            }
+            // ---- depths 4..6 (partial sums of the g node's left sibling: xs, <= 8 bits)
+            uint32_t xs = 0;
+            if (phi && start >= 4 && start <= 6) {  // u[phi-w, phi), w = 8, 4, 2
+                const int w = 1 << (kn - start), lo = phi - w;
+                xs = polar_transform8((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)) & ((1u << w) - 1u));
+            }
+            if (!(PSCL_ABLATE & 4) && start <= 6) {
+                // (DPP evaluated by every lane first: inside ?: only the selected lanes would
+                // run it, and a DPP that reads an inactive lane gets 0)
+                const uint32_t xs_src = from_lower_half<G, LMAX>(xs, lane);
+                const uint32_t tabp = tab;
+                const uint32_t xsp = path_lane ? xs : xs_src;
+                if (start <= 4) step_depth<LMAX, CH, 4>(Af, g, tabp, xsp, start == 4, start == 4 && phi);
+                if (start <= 5) step_depth<LMAX, CH, 5>(Af, g, tabp, xsp, start == 5, start == 5);
+                if (start <= 6) step_depth<LMAX, CH, 6>(Af, g, tabp, xsp, start == 6, start == 6);
+            }
+            if (start <= 6) {  // this path's own slot at every depth rewritten this phase
+                // (same update in the upper lane's copy: cpath is the path of both lanes)
+                const int s0 = start < 3 ? 3 : start;
+                const uint32_t mask = (0xffffu << (4 * (s0 - 3))) & 0xffffu;
+                tab = (tab & ~mask) | ((uint32_t)cpath * 0x1111u & mask);
+            }
+            // ---- leaf LLRs.  Lanes >= LMAX: the sibling leaf (phi+1) given bit 0 here.
+            // (depth 6 was just rewritten into the path's own slot at even phases)
+            const double* par = Af + Ly::OFF6 + (start <= 6 ? cpath : slot_at(tab, 6));
+            const double la = par[0], lb = par[LMAX];
+            const uint32_t xleaf = lastbit;  // u[phi - 1], the left sibling's bit at odd phases
+            const double lam = (PSCL_ABLATE & 128) ? la : (path_lane ? ((phi & 1) ? g_node(la, lb, xleaf) : f_minsum(la, lb)) : lb + la);
+            // ---- metric tail log1p(exp(-|llr|)) (scl.py:102-105)
+            double Lt;
+            const uint64_t lpre_up = from_upper_half64<G, LMAX>(pscl_asu64(Lpre), lane);
+            if (pre_ok) {
+                Lt = pscl_asf64(lpre_up);
+            } else {
+                Lt = (PSCL_ABLATE & 1) ? lam * 0.5 : pscl_softplus_tail_bf(lam, T);
+            }
+            const bool frozen_even = !is_info && !(phi & 1);
+            Lpre = Lt;
+            pre_ok = frozen_even;
+            // children metrics (scl.py:102-105): the child along the LLR sign pays Lt, the
+            // other |lam| + Lt; an exactly zero LLR gives both LOGE2 (rare wave branch)
+            const bool neg = lam < 0.0;
+            const double mgd = metric + Lt, mbd = metric + (fabs(lam) + Lt);
 
-                if (!is_info) {
-                    // frozen: bit 0, metrics advance, stable re-rank in place (lanes do not move).
-                    // While lane order is list order, the stable sort is the identity exactly when
-                    // the new metrics stay non-decreasing along the lanes: one adjacent compare.
-                    double m0 = neg ? mbd : mgd;
-                    if (PSCL_RARE(lam == 0.0)) m0 = lam == 0.0 ? metric + PSCL_LOGE2 : m0;
-                    metric = m0;
-                    lastbit = 0;
-                    bool moved = true;
-                    if (ordered && !(PSCL_ABLATE & 256)) {
-                        const uint64_t pv = prev_lane64(pscl_asu64(m0));
-                        moved = PSCL_ANY(path_lane & fvalid & (g >= 1) & (g < cnt) & (pv > pscl_asu64(m0)));
-                    }
-    #ifdef PSCL_STATS  // diagnostic build (tools/fastpath_stats.py): counters[8..11] of a 16-slot buffer
-                    if (lane == 0 && P.counters) {
-                        atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + 8, 1ULL);
-                        if (!moved) atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + 9, 1ULL);
-                    }
-    #endif
-                    if (!moved) return;
-                    const bool kv = path_lane && g < cnt;
-                    uint64_t km = kv ? pscl_asu64(m0) : 0x7ff0000000000000ULL;
-                    uint32_t kt = kv ? rank : 0x7fffffffu;
-                    // duplicate the path keys into the upper half: LMAX-1 rotations then see every path
-                    const uint64_t km_lo = from_lower_half64<G, LMAX>(km, lane);
-                    const uint32_t kt_lo = from_lower_half<G, LMAX>(kt, lane);
-                    if (!path_lane) {
-                        km = km_lo;
-                        kt = kt_lo;
-                    }
-                    uint32_t r = 0;
-                    if (!(PSCL_ABLATE & 18)) rank_step_n<G, 1, LMAX>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
-                    if (path_lane) rank = r;
-                    ordered = !PSCL_ANY(path_lane & fvalid & (g < cnt) & (rank != (uint32_t)g));
-                } else {
-                    // info, full list, lane order = list order: when every path's worse child
-                    // (against the LLR sign) is strictly worse than every better child and the
-                    // better children keep the lane order, the survivors are the better children
-                    // in place -- the outcome of the stable sort, with no ranking and no moves
-                    if (ordered && !sc_hard && !(PSCL_ABLATE & 256)) {
-                        const uint32_t gb = neg ? 1u : 0u;
-                        const uint64_t mg = pscl_asu64(mgd), mb = pscl_asu64(mbd);
-                        const uint64_t pv = prev_lane64(mg);
-                        const uint64_t top = shfl_u64(mg, gbase + L - 1);
-                        bool forced_here = false;
-                        if (FS && force) forced_here = (((j < 64 ? fm0 : fm1) >> (j & 63)) & 1) != 0;
-                        const bool bad = path_lane & (g < L) & fvalid &
-                                         ((cnt != L) | (lam == 0.0) | forced_here | ((g >= 1) & (pv > mg)) | !(mb > top));
-                        if (!PSCL_ANY(bad)) {
-                            if (HIST && path_lane && g < L) {
-                                hist_llr[j * L + g] = lam;
-                                hist_par[j * L + g] = (uint8_t)g;
-                            }
-                            metric = pscl_asf64(mg);
-                            lastbit = gb;
-                            if (gb) {
-                                if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
-                            }
-                            ++j;
-    #ifdef PSCL_STATS
-                            if (lane == 0 && P.counters) atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + 11, 1ULL);
-    #endif
-                            return;
-                        }
-                    }
-    #ifdef PSCL_STATS
-                    if (lane == 0 && P.counters) atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + 10, 1ULL);
-    #endif
-                    // info: children (bit 0 in lane g, bit 1 in lane g + LMAX) of every path
-                    double m0 = neg ? mbd : mgd, m1 = neg ? mgd : mbd;
-                    if (PSCL_RARE(lam == 0.0)) {
-                        m0 = lam == 0.0 ? metric + PSCL_LOGE2 : m0;
-                        m1 = lam == 0.0 ? metric + PSCL_LOGE2 : m1;
-                    }
-                    const uint64_t pm1 = from_lower_half64<G, LMAX>(pscl_asu64(m1), lane);
-                    const uint32_t prank = from_lower_half<G, LMAX>(rank, lane);
-                    uint64_t km = cbit ? pm1 : pscl_asu64(m0);
-                    const uint32_t myrank = cbit ? prank : rank;
-                    bool kval = cpath < cnt;
-                    int ncnt = 2 * cnt < L ? 2 * cnt : L;  // both children (scl.py:163-168)
-                    if (FS && sc_hard) {                  // sc_decode polar.py:149-153
-                        const double plam = pscl_asf64(from_lower_half64<G, LMAX>(pscl_asu64(lam), lane));
-                        kval = kval && cbit == (uint32_t)((cbit ? plam : lam) < 0.0);
-                        ncnt = cnt;
-                    } else if (FS && force) {             // forced bits (scl.py:146-161), per frame
-                        const uint64_t fmw = j < 64 ? fm0 : fm1, fvw = j < 64 ? fv0 : fv1;
-                        if ((fmw >> (j & 63)) & 1) {
-                            kval = kval && cbit == (uint32_t)((fvw >> (j & 63)) & 1);
-                            ncnt = cnt;
-                        }
-                    }
-                    if (!kval) km = 0x7ff0000000000000ULL;
-                    const uint32_t kt = kval ? 2u * myrank + cbit : 0x7fffffffu;
-                    uint32_t r = 0;
-                    if (!(PSCL_ABLATE & 2)) rank_step<G, 1>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
-                    else r = kt & 15u;
-                    // survivor with list position r -> lane r of the group (push), scl.py:174
-                    const int c = (PSCL_ABLATE & 32) ? g : __builtin_amdgcn_ds_permute((gbase + (int)(r & (G - 1))) << 2, g);
-                    const int cc = (g < ncnt) ? c : g;
-                    const int par_g = cc & (LMAX - 1);
-                    const uint32_t b = cc >= LMAX ? 1u : 0u;
-                    const int ps2 = gbase + par_g;
-                    const uint64_t nm = (PSCL_ABLATE & 32) ? km : shfl_u64(km, gbase + cc);
-                    const uint64_t nu0 = (PSCL_ABLATE & 32) ? u0 : shfl_u64(u0, ps2);
-                    const uint64_t nu1 = (PSCL_ABLATE & 32) || phi < 64 ? u1 : shfl_u64(u1, ps2);  // u1 = 0 before 64
-                    const uint32_t ntab = (PSCL_ABLATE & 32) ? tab : bperm32(tab, ps2);
-                    if (HIST) {
-                        const uint64_t plam_h = shfl_u64(pscl_asu64(lam), ps2);
-                        if (g < ncnt && path_lane) {
-                            hist_llr[j * L + g] = pscl_asf64(plam_h);  // decision LLR (scl.py:158,166)
-                            hist_par[j * L + g] = (uint8_t)par_g;
-                        }
-                    }
-                    metric = pscl_asf64(nm);
-                    u0 = nu0;
-                    u1 = nu1;
-                    // the upper lanes copy their (new) path's table
-                    const uint32_t ntab_lo = from_lower_half<G, LMAX>(ntab, lane);
-                    tab = path_lane ? ntab : ntab_lo;
-                    if (b) {
-                        if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
-                    }
-                    lastbit = b;
-                    rank = (uint32_t)g;
-                    cnt = ncnt;
-                    ordered = true;
-                    ++j;
+            if (!is_info) {
+                // frozen: bit 0, metrics advance, stable re-rank in place (lanes do not move).
+                // While lane order is list order, the stable sort is the identity exactly when
+                // the new metrics stay non-decreasing along the lanes: one adjacent compare.
+                double m0 = neg ? mbd : mgd;
+                if (PSCL_RARE(lam == 0.0)) m0 = lam == 0.0 ? metric + PSCL_LOGE2 : m0;
+                metric = m0;
+                lastbit = 0;
+                bool moved = true;
+                if (ordered && !(PSCL_ABLATE & 256)) {
+                    const uint64_t pv = prev_lane64(pscl_asu64(m0));
+                    moved = PSCL_ANY(path_lane & fvalid & (g >= 1) & (g < cnt) & (pv > pscl_asu64(m0)));
                 }
+#ifdef PSCL_STATS  // diagnostic build (tools/fastpath_stats.py): counters[8..11] of a 16-slot buffer
+                if (lane == 0 && P.counters) {
+                    atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + 8, 1ULL);
+                    if (!moved) atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + 9, 1ULL);
+                }
+#endif
+                if (!moved) return;
+                const bool kv = path_lane && g < cnt;
+                uint64_t km = kv ? pscl_asu64(m0) : 0x7ff0000000000000ULL;
+                uint32_t kt = kv ? rank : 0x7fffffffu;
+                // duplicate the path keys into the upper half: LMAX-1 rotations then see every path
+                const uint64_t km_lo = from_lower_half64<G, LMAX>(km, lane);
+                const uint32_t kt_lo = from_lower_half<G, LMAX>(kt, lane);
+                if (!path_lane) {
+                    km = km_lo;
+                    kt = kt_lo;
+                }
+                uint32_t r = 0;
+                if (!(PSCL_ABLATE & 18)) rank_step_n<G, 1, LMAX>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
+                if (path_lane) rank = r;
+                ordered = !PSCL_ANY(path_lane & fvalid & (g < cnt) & (rank != (uint32_t)g));
+            } else {
+                // info, full list, lane order = list order: when every path's worse child
+                // (against the LLR sign) is strictly worse than every better child and the
+                // better children keep the lane order, the survivors are the better children
+                // in place -- the outcome of the stable sort, with no ranking and no moves
+                if (ordered && !sc_hard && !(PSCL_ABLATE & 256)) {
+                    const uint32_t gb = neg ? 1u : 0u;
+                    const uint64_t mg = pscl_asu64(mgd), mb = pscl_asu64(mbd);
+                    const uint64_t pv = prev_lane64(mg);
+                    const uint64_t top = shfl_u64(mg, gbase + L - 1);
+                    bool forced_here = false;
+                    if (FS && force) forced_here = (((j < 64 ? fm0 : fm1) >> (j & 63)) & 1) != 0;
+                    const bool bad = path_lane & (g < L) & fvalid &
+                                     ((cnt != L) | (lam == 0.0) | forced_here | ((g >= 1) & (pv > mg)) | !(mb > top));
+                    if (!PSCL_ANY(bad)) {
+                        if (HIST && path_lane && g < L) {
+                            hist_llr[j * L + g] = lam;
+                            hist_par[j * L + g] = (uint8_t)g;
+                        }
+                        metric = pscl_asf64(mg);
+                        lastbit = gb;
+                        if (gb) {
+                            if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
+                        }
+                        ++j;
+#ifdef PSCL_STATS
+                        if (lane == 0 && P.counters) atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + 11, 1ULL);
+#endif
+                        return;
+                    }
+                }
+#ifdef PSCL_STATS
+                if (lane == 0 && P.counters) atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + 10, 1ULL);
+#endif
+                // info: children (bit 0 in lane g, bit 1 in lane g + LMAX) of every path
+                double m0 = neg ? mbd : mgd, m1 = neg ? mgd : mbd;
+                if (PSCL_RARE(lam == 0.0)) {
+                    m0 = lam == 0.0 ? metric + PSCL_LOGE2 : m0;
+                    m1 = lam == 0.0 ? metric + PSCL_LOGE2 : m1;
+                }
+                const uint64_t pm1 = from_lower_half64<G, LMAX>(pscl_asu64(m1), lane);
+                const uint32_t prank = from_lower_half<G, LMAX>(rank, lane);
+                uint64_t km = cbit ? pm1 : pscl_asu64(m0);
+                const uint32_t myrank = cbit ? prank : rank;
+                bool kval = cpath < cnt;
+                int ncnt = 2 * cnt < L ? 2 * cnt : L;  // both children (scl.py:163-168)
+                if (FS && sc_hard) {                  // sc_decode polar.py:149-153
+                    const double plam = pscl_asf64(from_lower_half64<G, LMAX>(pscl_asu64(lam), lane));
+                    kval = kval && cbit == (uint32_t)((cbit ? plam : lam) < 0.0);
+                    ncnt = cnt;
+                } else if (FS && force) {             // forced bits (scl.py:146-161), per frame
+                    const uint64_t fmw = j < 64 ? fm0 : fm1, fvw = j < 64 ? fv0 : fv1;
+                    if ((fmw >> (j & 63)) & 1) {
+                        kval = kval && cbit == (uint32_t)((fvw >> (j & 63)) & 1);
+                        ncnt = cnt;
+                    }
+                }
+                if (!kval) km = 0x7ff0000000000000ULL;
+                const uint32_t kt = kval ? 2u * myrank + cbit : 0x7fffffffu;
+                uint32_t r = 0;
+                if (!(PSCL_ABLATE & 2)) rank_step<G, 1>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
+                else r = kt & 15u;
+                // survivor with list position r -> lane r of the group (push), scl.py:174
+                const int c = (PSCL_ABLATE & 32) ? g : __builtin_amdgcn_ds_permute((gbase + (int)(r & (G - 1))) << 2, g);
+                const int cc = (g < ncnt) ? c : g;
+                const int par_g = cc & (LMAX - 1);
+                const uint32_t b = cc >= LMAX ? 1u : 0u;
+                const int ps2 = gbase + par_g;
+                const uint64_t nm = (PSCL_ABLATE & 32) ? km : shfl_u64(km, gbase + cc);
+                const uint64_t nu0 = (PSCL_ABLATE & 32) ? u0 : shfl_u64(u0, ps2);
+                const uint64_t nu1 = (PSCL_ABLATE & 32) || phi < 64 ? u1 : shfl_u64(u1, ps2);  // u1 = 0 before 64
+                const uint32_t ntab = (PSCL_ABLATE & 32) ? tab : bperm32(tab, ps2);
+                if (HIST) {
+                    const uint64_t plam_h = shfl_u64(pscl_asu64(lam), ps2);
+                    if (g < ncnt && path_lane) {
+                        hist_llr[j * L + g] = pscl_asf64(plam_h);  // decision LLR (scl.py:158,166)
+                        hist_par[j * L + g] = (uint8_t)par_g;
+                    }
+                }
+                metric = pscl_asf64(nm);
+                u0 = nu0;
+                u1 = nu1;
+                // the upper lanes copy their (new) path's table
+                const uint32_t ntab_lo = from_lower_half<G, LMAX>(ntab, lane);
+                tab = path_lane ? ntab : ntab_lo;
+                if (b) {
+                    if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
+                }
+                lastbit = b;
+                rank = (uint32_t)g;
+                cnt = ncnt;
+                ordered = true;
+                ++j;
+            }
         };
         // all 128 phases unrolled with phi a compile-time constant (with CODE != 0 the
         // information set is too: every frozen/info branch and the info index fold away)
