@@ -227,3 +227,37 @@ def test_compiled_nr_kernels_vs_oracle(M, E):
         np.testing.assert_array_equal(out["cands"][f, :n], c[:n])
         np.testing.assert_array_equal(out["metrics"][f, :n].view(np.int64), m[:n].view(np.int64))
         assert out["best_idx"][f] == b
+
+
+def test_ties_golden_plain_kernels(golden):
+    """The exact-tie golden cases (noiseless LLRs: equal metrics across paths) through the
+    kernels without decision history, whose frozen re-ranks move paths between lanes and
+    whose rankings take the tie key from the lane position (scl128_impl.h, kReorder)."""
+    g = golden("g5_ties.npz")
+    for key in map(str, g["keys"]):
+        M = int(key.split("_M")[1])
+        out = _native.get_decoder(128, g["info"], M, POLY).decode(g[key + "_llr"], want_info_llrs=False)
+        n = g[key + "_npaths"]
+        np.testing.assert_array_equal(out["n_paths"], n, err_msg=key)
+        for f in range(len(n)):
+            np.testing.assert_array_equal(out["cands"][f, :n[f]], g[key + "_cands"][f, :n[f]], err_msg=f"{key} f{f}")
+            np.testing.assert_array_equal(out["metrics"][f, :n[f]], g[key + "_metrics"][f, :n[f]], err_msg=f"{key} f{f}")
+        np.testing.assert_array_equal(out["best_idx"], g[key + "_best"], err_msg=key)
+
+
+@pytest.mark.parametrize("M", [4, 8])
+def test_quantized_llrs_plain_kernels_vs_oracle(M):
+    """Integer-valued LLRs make exact metric ties common (equal increments in different orders);
+    the plain kernels' lane-position tie keys and path moves against the oracle, bit for bit."""
+    rng = np.random.default_rng(900 + M)
+    info = construct_info_set(128, 64)
+    B = 900
+    llr = rng.integers(-4, 9, size=(B, 128)).astype(np.float64)
+    llr[: B // 3] = rng.choice([-2.0, -1.0, 1.0, 2.0, 3.0], size=(B // 3, 128))
+    out = _native.get_decoder(128, info, M, POLY).decode(llr, want_info_llrs=False)
+    for f in range(B):
+        n, c, m, il, b = oracle.decode_scl(llr[f], info, M, crc=POLY)
+        assert out["n_paths"][f] == n, f
+        np.testing.assert_array_equal(out["cands"][f, :n], c[:n], err_msg=f"M={M} f={f}")
+        np.testing.assert_array_equal(out["metrics"][f, :n].view(np.int64), m[:n].view(np.int64))
+        assert out["best_idx"][f] == b, f
