@@ -225,6 +225,17 @@ int pscl_memcpy_dtoh(pscl_handle* h, void* dst, const void* d_src, int64_t bytes
 int pscl_memset_device(pscl_handle* h, void* d_dst, int value, int64_t bytes);
 
 /*
+ * Screening decode (default on).  Plain decodes of the compiled-in N = 128 codes (no metrics,
+ * candidates, decision LLRs, path counts, forced bits) run a screening pass whose path metrics
+ * carry a proven relative error below 2^-41 (log1p by a truncated atanh series instead of
+ * glibc's log1p); every list ordering it decides must clear a margin of 2^16 ulps, and frames
+ * where one does not are re-decoded by the exact kernel.  Decoded bits, CRC flags and best
+ * indices are identical to the exact decode (decode_scl, dl_scl_polar/polar/scl.py:108-209).
+ * enable = 0 runs the exact kernel only.
+ */
+int pscl_set_screening(pscl_handle* h, int enable);
+
+/*
  * Kernel timing with HIP events recorded on the launch stream around every decode kernel
  * launch (enable = 1 starts a fresh accumulation).  pscl_timing_read returns the number of
  * timed launches and their summed duration in milliseconds (synchronizes the stream).

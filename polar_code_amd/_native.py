@@ -38,7 +38,7 @@ EXPORTS = (
     "pscl_decode_device", "pscl_channel_device", "pscl_device_alloc", "pscl_device_free",
     "pscl_memcpy_htod", "pscl_memcpy_dtoh", "pscl_memset_device", "pscl_timing_enable",
     "pscl_timing_read", "pscl_launch_info", "pscl_set_rate_match", "pscl_set_beta", "pscl_dlscl_device",
-    "pscl_path_llrs_device", "pscl_uncoded_device",
+    "pscl_path_llrs_device", "pscl_uncoded_device", "pscl_set_screening",
 )
 
 _vp, _i32, _i64, _u64, _dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
@@ -91,6 +91,7 @@ def lib() -> C.CDLL:
         "pscl_memcpy_dtoh": (C.c_int, [_vp, _vp, _vp, _i64]),
         "pscl_memset_device": (C.c_int, [_vp, _vp, C.c_int, _i64]),
         "pscl_timing_enable": (C.c_int, [_vp, C.c_int]),
+        "pscl_set_screening": (C.c_int, [_vp, C.c_int]),
         "pscl_timing_read": (C.c_int, [_vp, P(_i64), P(_dbl)]),
         "pscl_launch_info": (C.c_int, [_vp, _i64, P(C.c_int), P(_i64), P(C.c_int)]),
         "pscl_set_rate_match": (C.c_int, [_vp, C.c_int]),
@@ -101,6 +102,8 @@ def lib() -> C.CDLL:
                                         _vp]),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("PSCL_LIB_PATH") and not hasattr(L, name):
+            continue  # an older variant library under A/B timing (tools/ab_bench.sh)
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
@@ -296,6 +299,10 @@ class Decoder:
 
     def sync(self) -> None:
         check(lib().pscl_sync(self._h))
+
+    def set_screening(self, on: bool = True) -> None:
+        """Screening decode for plain decodes (default on; include/polar_scl.h)."""
+        check(lib().pscl_set_screening(self._h, 1 if on else 0))
 
     def timing_enable(self, on: bool = True) -> None:
         check(lib().pscl_timing_enable(self._h, 1 if on else 0))

@@ -101,6 +101,7 @@ struct pscl_handle {
     uint32_t* d_crctab = nullptr;     // TX: CRC remainder of each payload byte value
     int epi_words = 0;
     bool timing = false;
+    bool screen = true;               // screening decode for plain decodes (pscl_set_screening)
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
 };
@@ -161,7 +162,33 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P, int hist, hipStre
         h->ev_used += 2;
         HIP_TRY(hipEventRecord(e0, st));
     }
-    hipError_t err = pscl_launch_decode(P, hist, st);
+    // Plain decodes of the compiled-in N = 128 codes (no metrics, candidates, decision LLRs,
+    // forced bits or row indirection requested) run as a screening decode plus an exact
+    // re-decode of the frames it could not certify; the two launches count as one decode.
+    const bool screen = h->screen && P.fast && !hist && !P.metrics && !P.cands && !P.force && !P.sc_hard && !P.fidx &&
+                        !P.d_count;
+    hipError_t err;
+    if (screen) {
+        void *d_cnt, *d_list;
+        int rc;
+        if ((rc = ensure(h, 36, 4, &d_cnt))) return rc;
+        if ((rc = ensure(h, 37, (size_t)P.B * 8, &d_list))) return rc;
+        HIP_TRY(hipMemsetAsync(d_cnt, 0, 4, st));
+        pscl_decode_params S = P;
+        S.apx = 1;
+        S.amb_list = (int64_t*)d_list;
+        S.amb_count = (int32_t*)d_cnt;
+        err = pscl_launch_decode(S, hist, st);
+        if (err == hipSuccess) {
+            pscl_decode_params X = P;  // exact decode of the listed frames, outputs at their rows
+            X.fidx = (const int64_t*)d_list;
+            X.d_count = (const int32_t*)d_cnt;
+            X.out_by_row = 1;
+            err = pscl_launch_decode(X, hist, st);
+        }
+    } else {
+        err = pscl_launch_decode(P, hist, st);
+    }
     if (err != hipSuccess) return fail(PSCL_EDEVICE, "decode kernel launch: %s", hipGetErrorString(err));
     if (h->timing) HIP_TRY(hipEventRecord(e1, st));
     return PSCL_OK;
@@ -886,6 +913,12 @@ int pscl_memcpy_dtoh(pscl_handle* h, void* dst, const void* d_src, int64_t bytes
 int pscl_memset_device(pscl_handle* h, void* d_dst, int value, int64_t bytes) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
     HIP_TRY(hipMemsetAsync(d_dst, value, (size_t)bytes, h->stream));
+    return PSCL_OK;
+}
+
+int pscl_set_screening(pscl_handle* h, int enable) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    h->screen = enable != 0;
     return PSCL_OK;
 }
 

@@ -377,6 +377,50 @@ PSCL_HD double pscl_softplus_tail_bf(double v, const uint64_t* T) {
     return pscl_log1p_unit(pscl_exp_negabs(v, T));
 }
 
+/*
+ * Bounded-error tail for the screening decoder (scl128_kernel<..., APX = true>):
+ *     log1p(y) = 2 atanh(s) = 2 s sum_k s^(2k) / (2k + 1),  s = y / (2 + y) in [0, 1/3],
+ * y = exp(-|v|) from the exact exp above.  The series is cut after k = 11: the omitted terms
+ * are below (1/9)^12 / 25 * 9/8 = 1.6e-13 = 2^-42.5 of the sum, the division (reciprocal + two
+ * Newton steps) and the Horner steps add a few 2^-53, so the result is within 2^-42 of
+ * log1p(exp(-|v|)) relatively (tests/test_softplus_host.py checks 2^-41 on a dense grid).  With
+ * positive increments every path metric then stays within 2^-41.5 of the exact metric
+ * relatively (128 additions add at most 128 * 2^-53 more), far inside the screening margin
+ * the kernel uses to decide whether an ordering is certain (PSCL_APX_ULPS).
+ */
+#define PSCL_APX_TERMS 12
+PSCL_HD double pscl_log1p_apx(double y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double d = 2.0 + y;
+    double r = __builtin_amdgcn_rcp(d);
+    double e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    const double s = y * r;
+#else
+    const double s = y / (2.0 + y);
+#endif
+    const double w = s * s;
+    double p = 1.0 / 23.0;
+    p = pscl_fma(p, w, 1.0 / 21.0);
+    p = pscl_fma(p, w, 1.0 / 19.0);
+    p = pscl_fma(p, w, 1.0 / 17.0);
+    p = pscl_fma(p, w, 1.0 / 15.0);
+    p = pscl_fma(p, w, 1.0 / 13.0);
+    p = pscl_fma(p, w, 1.0 / 11.0);
+    p = pscl_fma(p, w, 1.0 / 9.0);
+    p = pscl_fma(p, w, 1.0 / 7.0);
+    p = pscl_fma(p, w, 1.0 / 5.0);
+    p = pscl_fma(p, w, 1.0 / 3.0);
+    p = pscl_fma(p, w, 1.0);
+    return (s + s) * p;
+}
+
+PSCL_HD double pscl_softplus_tail_apx(double v, const uint64_t* T) {
+    return pscl_log1p_apx(pscl_exp_negabs(v, T));
+}
+
 /* L = log1p(exp(-|v|)), the part of logaddexp(0, +-v) shared by both bit hypotheses. */
 PSCL_HD double pscl_softplus_tail(double v, const uint64_t* T) {
     double a = v < 0 ? -v : v;

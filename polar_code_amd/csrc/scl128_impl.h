@@ -113,13 +113,25 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
     static_for_impl(fn, std::make_integer_sequence<int, N>{});
 }
 
+// info phases rank the 2L children on the metric alone and fall back to the full tie key
+// only when equal metrics leave a list position unclaimed
+#ifndef PSCL_RANK_M
+#define PSCL_RANK_M 1
+#endif
+
 #ifndef PSCL_WAVES_PER_EU
 #define PSCL_WAVES_PER_EU 4
 #endif
 
 // FS: the launch may carry forced bits or SC hard decisions (P.force / P.sc_hard).  Without
 // them (every plain SCL decode) the per-frame force words and their tests compile away.
-template <int LMAX, bool HIST, bool CH, bool FS, int CODE>
+// APX: screening decode (plain decodes of the compiled-in codes): metric tails from the
+// bounded-error pscl_softplus_tail_apx; every ordering decision must clear a margin of
+// PSCL_APX_ULPS ulps, else the frame is appended to P.amb_list for an exact re-decode.
+#ifndef PSCL_APX_ULPS
+#define PSCL_APX_ULPS 65536
+#endif
+template <int LMAX, bool HIST, bool CH, bool FS, int CODE, bool APX = false>
 __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU) scl128_kernel(const pscl_decode_params P) {
     using Ly = Layout128<LMAX, CH>;
     const uint64_t* const force = FS ? P.force : nullptr;
@@ -199,6 +211,13 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
         bool pre_ok = false;        // Lpre holds the tail of this phase's leaf (wave-uniform)
         bool ordered = true;        // every path's lane is its list position (wave-uniform)
         double Lpre = 0.0;
+        // wave masks of lane predicates (ballots of plain compares, ANDed in SGPRs)
+        const uint64_t vmask = wmask(fvalid);
+        constexpr uint64_t KPATH = group_prefix_mask<G>(LMAX), KGE1 = ~group_prefix_mask<G>(1);
+        const uint64_t LMASK = group_prefix_mask<G>(L);
+        uint64_t amb = 0;  // APX: lanes that saw an ordering closer than the margin
+        // (b - a, as signed 64-bit on the metrics' bit patterns) <= margin: a < b not certain
+        auto near_or_below = [](uint64_t a, uint64_t b) { return (int64_t)(b - a) <= (int64_t)PSCL_APX_ULPS; };
 
         // phase body, specialised on t = phi mod 16 (the subtree shape of the phase is fixed by
         // t); blk = phi / 16 is a compile-time constant too in the CODE != 0 kernels
@@ -213,6 +232,8 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                                         : __builtin_popcountll(info0) + __builtin_popcountll(info1 & ((1ULL << (phi & 63)) - 1));
                 cnt = jb >= Ly::LOG_LM ? LMAX : (1 << jb);
             }
+            // lanes g < cnt (cnt is group-uniform; a compile-time constant with kFixedList)
+            const uint64_t cmask = kFixedList ? group_prefix_mask<G>(cnt) : wmask(g < cnt);
 #ifdef PSCL_PHASE_MARKERS  // asm listing analysis only
             asm volatile("; PHASE %0" ::"n"(PT));
 #endif
@@ -301,9 +322,8 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
             if (!(PSCL_ABLATE & 4) && start <= 6) {
                 // (DPP evaluated by every lane first: inside ?: only the selected lanes would
                 // run it, and a DPP that reads an inactive lane gets 0)
-                const uint32_t xs_src = from_lower_half<G, LMAX>(xs, lane);
                 const uint32_t tabp = tab;
-                const uint32_t xsp = path_lane ? xs : xs_src;
+                const uint32_t xsp = merge_from_lower<G, LMAX>(xs, xs, lane);
                 if (start <= 4) step_depth<LMAX, CH, 4>(Af, g, tabp, xsp, start == 4, start == 4 && phi);
                 if (start <= 5) step_depth<LMAX, CH, 5>(Af, g, tabp, xsp, start == 5, start == 5);
                 if (start <= 6) step_depth<LMAX, CH, 6>(Af, g, tabp, xsp, start == 6, start == 6);
@@ -326,7 +346,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
             if (pre_ok) {
                 Lt = pscl_asf64(lpre_up);
             } else {
-                Lt = (PSCL_ABLATE & 1) ? lam * 0.5 : pscl_softplus_tail_bf(lam, T);
+                Lt = (PSCL_ABLATE & 1) ? lam * 0.5 : (APX ? pscl_softplus_tail_apx(lam, T) : pscl_softplus_tail_bf(lam, T));
             }
             const bool frozen_even = !is_info && !(phi & 1);
             Lpre = Lt;
@@ -347,7 +367,8 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 bool moved = true;
                 if (ordered && !(PSCL_ABLATE & 256)) {
                     const uint64_t pv = prev_lane64(pscl_asu64(m0));
-                    moved = PSCL_ANY(path_lane & fvalid & (g >= 1) & (g < cnt) & (pv > pscl_asu64(m0)));
+                    const bool mv = APX ? near_or_below(pv, pscl_asu64(m0)) : pv > pscl_asu64(m0);
+                    moved = (wmask(mv) & vmask & KPATH & KGE1 & cmask) != 0;
                 }
 #ifdef PSCL_STATS  // diagnostic build (tools/fastpath_stats.py): counters[8..11] of a 16-slot buffer
                 if (lane == 0 && P.counters) {
@@ -356,20 +377,24 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 }
 #endif
                 if (!moved) return;
-                const bool kv = path_lane && g < cnt;
+                // (a full list needs no empty-slot keys: the upper lanes are overwritten next)
+                const bool kv = (kFixedList && cnt == LMAX) || g < cnt;
                 uint64_t km = kv ? pscl_asu64(m0) : 0x7ff0000000000000ULL;
                 uint32_t kt = kv ? rank : 0x7fffffffu;
                 // duplicate the path keys into the upper half: LMAX-1 rotations then see every path
-                const uint64_t km_lo = from_lower_half64<G, LMAX>(km, lane);
-                const uint32_t kt_lo = from_lower_half<G, LMAX>(kt, lane);
-                if (!path_lane) {
-                    km = km_lo;
-                    kt = kt_lo;
-                }
+                km = merge_from_lower64<G, LMAX>(km, km, lane);
+                kt = merge_from_lower<G, LMAX>(kt, kt, lane);
                 uint32_t r = 0;
                 if (!(PSCL_ABLATE & 18)) rank_step_n<G, 1, LMAX>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
                 if (path_lane) rank = r;
-                ordered = !PSCL_ANY(path_lane & fvalid & (g < cnt) & (rank != (uint32_t)g));
+                if (APX) {  // sorted neighbours: lane r receives the path ranked r (twins push the same key)
+                    const int dst = (gbase + (int)(r & (G - 1))) << 2;
+                    const uint32_t slo = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)km);
+                    const uint32_t shi = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)(km >> 32));
+                    const uint64_t sk = ((uint64_t)shi << 32) | slo;
+                    amb |= wmask(near_or_below(prev_lane64(sk), sk)) & vmask & KGE1 & cmask;
+                }
+                ordered = (wmask(rank != (uint32_t)g) & vmask & KPATH & cmask) == 0;
             } else {
                 // info, full list, lane order = list order: when every path's worse child
                 // (against the LLR sign) is strictly worse than every better child and the
@@ -382,9 +407,15 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     const uint64_t top = shfl_u64(mg, gbase + L - 1);
                     bool forced_here = false;
                     if (FS && force) forced_here = (((j < 64 ? fm0 : fm1) >> (j & 63)) & 1) != 0;
-                    const bool bad = path_lane & (g < L) & fvalid &
-                                     ((cnt != L) | (lam == 0.0) | forced_here | ((g >= 1) & (pv > mg)) | !(mb > top));
-                    if (!PSCL_ANY(bad)) {
+                    uint64_t badm = APX ? (wmask(lam == 0.0) | (wmask(near_or_below(pv, mg)) & KGE1) | wmask(near_or_below(top, mb)))
+                                        : (wmask(lam == 0.0) | (wmask(pv > mg) & KGE1) | wmask(mb <= top));
+                    if (FS && force) badm |= wmask(forced_here);
+                    if (kFixedList) {
+                        if (cnt != L) badm = ~0ULL;
+                    } else {
+                        badm |= wmask(cnt != L);
+                    }
+                    if ((badm & vmask & KPATH & LMASK) == 0) {
                         if (HIST && path_lane && g < L) {
                             hist_llr[j * L + g] = lam;
                             hist_par[j * L + g] = (uint8_t)g;
@@ -410,10 +441,9 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     m0 = lam == 0.0 ? metric + PSCL_LOGE2 : m0;
                     m1 = lam == 0.0 ? metric + PSCL_LOGE2 : m1;
                 }
-                const uint64_t pm1 = from_lower_half64<G, LMAX>(pscl_asu64(m1), lane);
-                const uint32_t prank = from_lower_half<G, LMAX>(rank, lane);
-                uint64_t km = cbit ? pm1 : pscl_asu64(m0);
-                const uint32_t myrank = cbit ? prank : rank;
+                // bit-0 child in lane g, bit-1 child (from lane g - LMAX) in lane g + LMAX
+                uint64_t km = merge_from_lower64<G, LMAX>(pscl_asu64(m0), pscl_asu64(m1), lane);
+                const uint32_t myrank = merge_from_lower<G, LMAX>(rank, rank, lane);
                 bool kval = cpath < cnt;
                 int ncnt = 2 * cnt < L ? 2 * cnt : L;  // both children (scl.py:163-168)
                 if (FS && sc_hard) {                  // sc_decode polar.py:149-153
@@ -430,15 +460,44 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 if (!kval) km = 0x7ff0000000000000ULL;
                 const uint32_t kt = kval ? 2u * myrank + cbit : 0x7fffffffu;
                 uint32_t r = 0;
+                int c;
+#if PSCL_RANK_M
+                if (APX) {  // unique ranks (full key): the neighbour check below sees every pair
+                    rank_step<G, 1>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
+                    c = __builtin_amdgcn_ds_permute((gbase + (int)(r & (G - 1))) << 2, g);
+                } else {
+                // rank on the metric alone, then check that the ranks 0..ncnt are all claimed
+                // (lane g pulls the rank of the lane it received); equal metrics among the
+                // candidates that matter leave a hole and take the full (metric, 2*rank + bit) key
+                rank_step_m<G, 1, G>((uint32_t)(km >> 32), (uint32_t)km, lane, r);
+                c = __builtin_amdgcn_ds_permute((gbase + (int)(r & (G - 1))) << 2, g);
+                {
+                    const uint32_t rr = bperm32(r, gbase + (c & (G - 1)));
+                    const uint64_t chk = kFixedList ? group_prefix_mask<G>(ncnt + 1) : wmask(g <= ncnt);
+                    if (__builtin_expect((wmask(rr != (uint32_t)g) & chk) != 0, 0)) {
+                        r = 0;
+                        rank_step<G, 1>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
+                        c = __builtin_amdgcn_ds_permute((gbase + (int)(r & (G - 1))) << 2, g);
+                    }
+                }
+                }
+#else
                 if (!(PSCL_ABLATE & 2)) rank_step<G, 1>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
                 else r = kt & 15u;
                 // survivor with list position r -> lane r of the group (push), scl.py:174
-                const int c = (PSCL_ABLATE & 32) ? g : __builtin_amdgcn_ds_permute((gbase + (int)(r & (G - 1))) << 2, g);
+                c = (PSCL_ABLATE & 32) ? g : __builtin_amdgcn_ds_permute((gbase + (int)(r & (G - 1))) << 2, g);
+#endif
                 const int cc = (g < ncnt) ? c : g;
                 const int par_g = cc & (LMAX - 1);
                 const uint32_t b = cc >= LMAX ? 1u : 0u;
                 const int ps2 = gbase + par_g;
-                const uint64_t nm = (PSCL_ABLATE & 32) ? km : shfl_u64(km, gbase + cc);
+                // (APX: lane ncnt fetches the first pruned key too, for the neighbour check)
+                const int ccm = APX ? ((g <= ncnt) ? c : g) : cc;
+                const uint64_t nm = (PSCL_ABLATE & 32) ? km : shfl_u64(km, gbase + ccm);
+                if (APX) {
+                    const uint64_t chk = kFixedList ? group_prefix_mask<G>(ncnt + 1) : wmask(g <= ncnt);
+                    amb |= wmask(near_or_below(prev_lane64(nm), nm)) & vmask & KGE1 & chk;
+                }
                 const uint64_t nu0 = (PSCL_ABLATE & 32) ? u0 : shfl_u64(u0, ps2);
                 const uint64_t nu1 = (PSCL_ABLATE & 32) || phi < 64 ? u1 : shfl_u64(u1, ps2);  // u1 = 0 before 64
                 const uint32_t ntab = (PSCL_ABLATE & 32) ? tab : bperm32(tab, ps2);
@@ -453,8 +512,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 u0 = nu0;
                 u1 = nu1;
                 // the upper lanes copy their (new) path's table
-                const uint32_t ntab_lo = from_lower_half<G, LMAX>(ntab, lane);
-                tab = path_lane ? ntab : ntab_lo;
+                tab = merge_from_lower<G, LMAX>(ntab, ntab, lane);
                 if (b) {
                     if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
                 }
@@ -499,12 +557,16 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 for (int m = 16; m < k4; ++m) syn ^= ST[m * 16 + (uint32_t)((ib1 >> (4 * (m - 16))) & 15u)];
             }
         }
-        const bool active = path_lane && g < cnt && fvalid;
+        // APX: a frame with an uncertain ordering is handed to the exact re-decode
+        const bool famb = APX && ((amb >> gbase) & (G == 64 ? ~0ULL : ((1ULL << (G & 63)) - 1))) != 0;
+        if (APX && famb && g == 0 && fvalid) P.amb_list[atomicAdd(P.amb_count, 1)] = f;
+        const bool active = path_lane && g < cnt && fvalid && !famb;
+        const int64_t fo = P.out_by_row ? frow : f;  // output row
         uint32_t pm = (active && syn == 0) ? (1u << rank) : 0u;
         pm = or_reduce_group<G>(pm, lane);
         const int best = (P.has_crc && pm) ? __builtin_ctz(pm) : 0;
         if (active) {
-            const int64_t row = f * L + rank;
+            const int64_t row = fo * L + rank;
             if (P.metrics) P.metrics[row] = metric;
             if (P.cands) {
                 P.cands[row * P.W] = ib0;
@@ -522,24 +584,24 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 if (HIST && P.best_info_llrs) {
                     int cur = g;
                     for (int jj = K - 1; jj >= 0; --jj) {
-                        P.best_info_llrs[f * K + jj] = hist_llr[jj * L + cur];
+                        P.best_info_llrs[fo * K + jj] = hist_llr[jj * L + cur];
                         cur = hist_par[jj * L + cur];
                     }
                 }
                 if (P.best) {
-                    P.best[f * P.W] = ib0;
-                    if (P.W > 1) P.best[f * P.W + 1] = ib1;
+                    P.best[fo * P.W] = ib0;
+                    if (P.W > 1) P.best[fo * P.W + 1] = ib1;
                 }
-                if (P.flags) P.flags[f] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
-                if (P.n_paths) P.n_paths[f] = cnt;
+                if (P.flags) P.flags[fo] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
+                if (P.n_paths) P.n_paths[fo] = cnt;
                 if (P.ref)
-                    count_errors(P.counters, ib0, ib1, P.ref[f * P.W], P.W > 1 ? P.ref[f * P.W + 1] : 0, P.k_payload,
+                    count_errors(P.counters, ib0, ib1, P.ref[fo * P.W], P.W > 1 ? P.ref[fo * P.W + 1] : 0, P.k_payload,
                                  bpass);
             }
         }
         wave_lds_fence();
     }
-    if (P.ref && blockIdx.x == 0 && threadIdx.x == 0)
+    if (P.ref && !P.out_by_row && blockIdx.x == 0 && threadIdx.x == 0)
         atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
 }
 

@@ -208,6 +208,40 @@ __device__ __forceinline__ void rank_step_n(uint32_t mh, uint32_t ml, uint32_t t
     }
 }
 
+// Metric-only rank: the number of keys of the group (rotations K .. KEND-1) whose 64-bit
+// metric is strictly smaller than this lane's.  Equals the stable rank whenever the metrics
+// of the keys that matter are distinct; equal metrics give two lanes the same rank, which the
+// callers detect (a list position nobody claims) and then redo with the full tie key.
+// 3 VALU per rotation instead of 4.
+template <int K>
+__device__ __forceinline__ void rank_rot16_m(uint32_t mh, uint32_t ml, uint32_t& r) {
+    uint32_t tmp;
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_sub_co_u32_dpp %0, vcc, %2, %2 row_ror:%4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_subb_co_u32_dpp %0, vcc, %3, %3, vcc row_ror:%4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_addc_co_u32 %1, vcc, 0, %1, vcc"
+        : "=&v"(tmp), "+v"(r)
+        : "v"(ml), "v"(mh), "i"(K)
+        : "vcc");
+}
+
+template <int G, int K, int KEND>
+__device__ __forceinline__ void rank_step_m(uint32_t mh, uint32_t ml, int lane, uint32_t& r) {
+    if constexpr (G == 16 && K < KEND) {
+        rank_rot16_m<K>(mh, ml, r);
+        rank_step_m<G, K + 1, KEND>(mh, ml, lane, r);
+    } else if constexpr (K < KEND) {
+        const uint32_t lh = grot32c<G, K>(ml, lane);
+        const uint32_t hh = grot32c<G, K>(mh, lane);
+        unsigned c1, c2;
+        (void)__builtin_subc(lh, ml, 0u, &c1);
+        (void)__builtin_subc(hh, mh, c1, &c2);
+        r += c2;
+        rank_step_m<G, K + 1, KEND>(mh, ml, lane, r);
+    }
+}
+
 // OR of v over the G lanes of the group
 template <int G, int K = 1>
 __device__ __forceinline__ uint32_t or_reduce_group(uint32_t v, int lane, uint32_t acc = 0) {
@@ -240,6 +274,41 @@ __device__ __forceinline__ uint32_t from_upper_half(uint32_t v, int lane) {
         return bperm32(v, lane + LMAX);
     }
 }
+
+// Lanes g >= LMAX of the group take `up` from lane g - LMAX, lanes g < LMAX keep `own`:
+// `path_lane ? own : from_lower_half(up)` as one DPP move whose bank mask leaves the lower
+// half unwritten (its old value is `own`).  G = 16: the upper half is banks 2, 3 of the row;
+// G = 8: banks 1, 3 (row_ror:4 stays inside the 8-lane group for those lanes).
+template <int G, int LMAX>
+__device__ __forceinline__ uint32_t merge_from_lower(uint32_t own, uint32_t up, int lane) {
+    if constexpr (G == 16) {
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)own, (int)up, 0x128, 0xF, 0xC, false);
+    } else if constexpr (G == 8) {
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)own, (int)up, 0x124, 0xF, 0xA, false);
+    } else {
+        const uint32_t x = from_lower_half<G, LMAX>(up, lane);
+        return (lane & (G - 1)) < LMAX ? own : x;
+    }
+}
+
+template <int G, int LMAX>
+__device__ __forceinline__ uint64_t merge_from_lower64(uint64_t own, uint64_t up, int lane) {
+    return ((uint64_t)merge_from_lower<G, LMAX>((uint32_t)(own >> 32), (uint32_t)(up >> 32), lane) << 32) |
+           merge_from_lower<G, LMAX>((uint32_t)own, (uint32_t)up, lane);
+}
+
+// Wave masks of lane-position predicates: bits [0, n) of every G-lane group.
+template <int G>
+__device__ __forceinline__ constexpr uint64_t group_rep() {
+    uint64_t m = 0;
+    for (int k = 0; k < 64; k += G) m |= 1ULL << k;
+    return m;
+}
+template <int G>
+__device__ __forceinline__ constexpr uint64_t group_prefix_mask(int n) {
+    return (n >= G ? ((G == 64) ? ~0ULL : ((1ULL << G) - 1)) : ((1ULL << n) - 1)) * group_rep<G>();
+}
+__device__ __forceinline__ uint64_t wmask(bool c) { return __builtin_amdgcn_ballot_w64(c); }
 
 template <int G, int LMAX>
 __device__ __forceinline__ uint64_t from_lower_half64(uint64_t v, int lane) {

@@ -46,6 +46,12 @@ struct pscl_decode_params {
     int fast;                    // 1: the specialised N = 128, L <= 8 kernel (scl128.hip)
     int wave_bytes;              // LDS bytes per wavefront
     int a_bytes;                 // LDS bytes of the LLR slots per wavefront
+    // screening decode (scl128 compiled-in codes, plain decodes): bounded-error metric tails,
+    // frames whose list order is not certain are appended to amb_list instead of finishing
+    int apx;
+    int64_t* amb_list;           // [B] frame indices to re-decode exactly
+    int32_t* amb_count;
+    int out_by_row;              // 1: outputs, reference words and counts at LLR row fidx[b]
 };
 
 // Decision-LLR replay (dlscl.hip): leaf LLRs of a known path, recomputed top-down

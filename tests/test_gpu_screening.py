@@ -1,0 +1,115 @@
+"""GPU: the screening decode (include/polar_scl.h pscl_set_screening) against the exact kernel.
+
+Plain decodes of the compiled-in codes run a pass with bounded-error metric tails that hands
+every frame whose list ordering it cannot certify to the exact kernel.  Its outputs — decoded
+bits, CRC flag, best index, path count, device-side FER/BER counters — must equal the exact
+decode's bit for bit, including on inputs built to produce exact metric ties (integer and
+noiseless LLRs), where the screening pass must defer to the exact kernel."""
+import numpy as np
+import pytest
+
+import oracle
+from polar_code_amd import _native
+from polar_code_amd.polar import crc as pcrc
+from polar_code_amd.polar.polar import _polar_transform, construct_info_set
+
+pytestmark = pytest.mark.gpu
+POLY = "0x1864CFB"
+
+
+def _frames(rng, B, info, ebno_db, K=64):
+    msg = pcrc.attach_crc(rng.integers(0, 2, size=(B, K - 24), dtype=np.int8), POLY)
+    u = np.zeros((B, 128), np.int8)
+    u[:, info] = msg
+    nv = 1.0 / (2.0 * (K - 24) / 128 * 10 ** (ebno_db / 10))
+    return 2.0 * ((1.0 - 2.0 * _polar_transform(u)) + rng.normal(0.0, np.sqrt(nv), size=(B, 128))) / nv
+
+
+def _pair(N, info, M):
+    scr, ex = _native.Decoder(N, info, M, POLY), _native.Decoder(N, info, M, POLY)
+    ex.set_screening(False)
+    return scr, ex
+
+
+def _plain(dec, llr):
+    return dec.decode(llr, want_metrics=False, want_cands=False, want_info_llrs=False)
+
+
+def _assert_same(a, b, tag):
+    for k in ("n_paths", "best_bits", "crc_pass", "best_idx"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=f"{tag}: {k}")
+
+
+@pytest.mark.parametrize("M", [1, 2, 4, 8])
+def test_screening_equals_exact_awgn(M):
+    rng = np.random.default_rng(7100 + M)
+    info = construct_info_set(128, 64)
+    llr = np.concatenate([_frames(rng, 4000, info, s) for s in (0.0, 1.5, 3.0, 4.5, 6.0)])
+    scr, ex = _pair(128, info, M)
+    _assert_same(_plain(scr, llr), _plain(ex, llr), f"M={M}")
+
+
+@pytest.mark.parametrize("M", [2, 4, 8])
+def test_screening_ties_defer_to_exact(M):
+    """Integer-valued and noiseless LLRs: exact metric ties are common, so many frames must be
+    deferred; the results still equal the exact kernel's and the oracle's."""
+    rng = np.random.default_rng(7200 + M)
+    info = construct_info_set(128, 64)
+    B = 1200
+    llr = rng.integers(-4, 9, size=(B, 128)).astype(np.float64)
+    llr[: B // 3] = rng.choice([-2.0, -1.0, 1.0, 2.0, 3.0], size=(B // 3, 128))
+    llr[B // 3: 2 * B // 3] = 50.0 * np.sign(_frames(rng, B // 3, info, 60.0))  # noiseless
+    scr, ex = _pair(128, info, M)
+    a = _plain(scr, llr)
+    _assert_same(a, _plain(ex, llr), f"ties M={M}")
+    for f in range(0, B, 7):
+        n, c, m, il, b = oracle.decode_scl(llr[f], info, M, crc=POLY)
+        assert a["n_paths"][f] == n and a["best_idx"][f] == b, f
+        np.testing.assert_array_equal(a["best_bits"][f], c[b], err_msg=f"f={f}")
+
+
+@pytest.mark.parametrize("M", [4, 8])
+def test_screening_nr_rate_matched(M):
+    from polar_code_amd.nr.polar import derate_match_polar, subblock_deinterleave
+
+    rng = np.random.default_rng(7300 + M)
+    info = construct_info_set(128, 88)
+    E = 256
+    llrE = rng.normal(2.0, 3.0, size=(3000, E)) * rng.choice([1.0, -1.0], size=(3000, E), p=[0.9, 0.1])
+    scr, ex = _pair(128, info, M)
+    for d in (scr, ex):
+        d.set_rate_match(E)
+    a = _plain(scr, llrE)
+    _assert_same(a, _plain(ex, llrE), f"NR M={M}")
+    for f in range(0, 3000, 50):
+        internal = subblock_deinterleave(derate_match_polar(llrE[f], 128), 128)
+        n, c, m, il, b = oracle.decode_scl(internal, info, M, crc=POLY)
+        assert a["best_idx"][f] == b
+        np.testing.assert_array_equal(a["best_bits"][f], c[b])
+
+
+def test_screening_device_counters_equal_exact():
+    """Device path with in-kernel FER/BER counting (the bench's step): deferred frames are
+    counted by the exact re-decode at their own rows, once."""
+    info = construct_info_set(128, 64)
+    B = 200_000
+    out = {}
+    for on in (True, False):
+        dec = _native.Decoder(128, info, 8, POLY)
+        dec.set_screening(on)
+        with _native.DeviceArena(dec) as mem:
+            d_llr, d_msg = mem.alloc(B * 128 * 8), mem.alloc(B * 8)
+            d_best, d_flags, d_cnt = mem.alloc(B * 8), mem.alloc(B), mem.alloc(8 * 8)
+            mem.memset(d_cnt, 0, 64)
+            dec.channel_device(0, 3, 2.0, 0.5, 40, 0, B, d_llr, d_msg)
+            # a quarter of the frames quantised to integers (ties -> deferred frames)
+            llr = mem.download(d_llr, B * 128 * 8, np.float64).reshape(B, 128)
+            llr[: B // 4] = np.round(llr[: B // 4] / 4.0)
+            mem.upload(d_llr, llr)
+            dec.decode_device(d_llr, B, d_best=d_best, d_flags=d_flags, d_ref=d_msg, k_payload=40, d_counters=d_cnt)
+            dec.sync()
+            out[on] = (mem.download(d_best, B * 8, np.uint64), mem.download(d_flags, B, np.uint8),
+                       mem.download(d_cnt, 64, np.int64))
+    for i, k in enumerate(("best", "flags", "counters")):
+        np.testing.assert_array_equal(out[True][i], out[False][i], err_msg=k)
+    assert out[True][2][0] == B
