@@ -356,6 +356,83 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
             const bool neg = lam < 0.0;
             const double mgd = metric + Lt, mbd = metric + (fabs(lam) + Lt);
 
+            if constexpr (APX) {
+                // Screening: with every ordering decision beyond the margin, the stable sort's
+                // tie keys never act, so the list order in between does not matter -- only which
+                // children survive a full list (the boundary between the L-th and (L+1)-th
+                // smallest metric) and, at the end, the final order.  Paths stay in lanes
+                // 0..cnt-1 in any order; frozen phases only advance the metrics.
+                if (!is_info) {
+                    double m0 = neg ? mbd : mgd;
+                    if (PSCL_RARE(lam == 0.0)) m0 = lam == 0.0 ? metric + PSCL_LOGE2 : m0;
+                    metric = m0;
+                    lastbit = 0;
+                    return;
+                }
+                double m0 = neg ? mbd : mgd, m1 = neg ? mgd : mbd;  // bit-0 / bit-1 child
+                if (PSCL_RARE(lam == 0.0)) {
+                    m0 = lam == 0.0 ? metric + PSCL_LOGE2 : m0;
+                    m1 = lam == 0.0 ? metric + PSCL_LOGE2 : m1;
+                }
+                const int ncnt = 2 * cnt < L ? 2 * cnt : L;
+                int src;
+                uint32_t b;
+                uint64_t nm;
+                if (2 * cnt <= L) {
+                    // every child survives: bit 0 stays in lane p, bit 1 goes to lane cnt + p
+                    src = gbase + (g & (cnt - 1));
+                    b = (g & cnt) ? 1u : 0u;
+                    const uint64_t pm1 = shfl_u64(pscl_asu64(m1), src);
+                    nm = b ? pm1 : pscl_asu64(m0);
+                } else {
+                    // full list: the better children survive when every worse child exceeds the
+                    // largest better child by the margin (group max over duplicated keys)
+                    double mx = pscl_asf64(merge_from_lower64<G, LMAX>(pscl_asu64(mgd), pscl_asu64(mgd), lane));
+                    static_for<Ly::LOG_LM>([&](auto SC) {
+                        constexpr int S = 1 << decltype(SC)::value;
+                        const double o = grot64c<G, S>(mx, lane);
+                        asm("v_max_f64 %0, %1, %2" : "=v"(mx) : "v"(mx), "v"(o));
+                    });
+                    const uint64_t badm = wmask(lam == 0.0) | wmask(near_or_below(pscl_asu64(mx), pscl_asu64(mbd)));
+                    if ((badm & vmask & KPATH) == 0) {
+                        const uint32_t gb = neg ? 1u : 0u;
+                        metric = mgd;
+                        lastbit = gb;
+                        if (gb) {
+                            if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
+                        }
+                        ++j;
+                        return;
+                    }
+                    // rank the 2L children on the metric; lane r takes the child ranked r.  Each
+                    // position 0..L claimed exactly once and the L-th / (L+1)-th smallest apart by
+                    // the margin certify the survivor set (ties leave a position unclaimed).
+                    const uint64_t km = merge_from_lower64<G, LMAX>(pscl_asu64(m0), pscl_asu64(m1), lane);
+                    uint32_t r = 0;
+                    rank_step_m<G, 1, G>((uint32_t)(km >> 32), (uint32_t)km, lane, r);
+                    const int c = __builtin_amdgcn_ds_permute((gbase + (int)(r & (G - 1))) << 2, g) & (G - 1);
+                    const uint32_t rr = bperm32(r, gbase + c);
+                    nm = shfl_u64(km, gbase + c);
+                    const uint64_t claim = group_prefix_mask<G>(L + 1);
+                    const uint64_t bnd = claim & ~group_prefix_mask<G>(L);
+                    amb |= ((wmask(rr != (uint32_t)g) & claim) | (wmask(near_or_below(prev_lane64(nm), nm)) & bnd)) & vmask;
+                    src = gbase + (c & (LMAX - 1));
+                    b = c >= LMAX ? 1u : 0u;
+                }
+                metric = pscl_asf64(nm);
+                u0 = shfl_u64(u0, src);
+                if (phi >= 64) u1 = shfl_u64(u1, src);
+                const uint32_t ntab = bperm32(tab, src);
+                tab = merge_from_lower<G, LMAX>(ntab, ntab, lane);
+                if (b) {
+                    if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
+                }
+                lastbit = b;
+                cnt = ncnt;
+                ++j;
+                return;
+            }
+
             if (!is_info) {
                 // frozen: bit 0, metrics advance, stable re-rank in place (lanes do not move).
                 // While lane order is list order, the stable sort is the identity exactly when
@@ -367,8 +444,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 bool moved = true;
                 if (ordered && !(PSCL_ABLATE & 256)) {
                     const uint64_t pv = prev_lane64(pscl_asu64(m0));
-                    const bool mv = APX ? near_or_below(pv, pscl_asu64(m0)) : pv > pscl_asu64(m0);
-                    moved = (wmask(mv) & vmask & KPATH & KGE1 & cmask) != 0;
+                    moved = (wmask(pv > pscl_asu64(m0)) & vmask & KPATH & KGE1 & cmask) != 0;
                 }
 #ifdef PSCL_STATS  // diagnostic build (tools/fastpath_stats.py): counters[8..11] of a 16-slot buffer
                 if (lane == 0 && P.counters) {
@@ -387,13 +463,6 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 uint32_t r = 0;
                 if (!(PSCL_ABLATE & 18)) rank_step_n<G, 1, LMAX>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
                 if (path_lane) rank = r;
-                if (APX) {  // sorted neighbours: lane r receives the path ranked r (twins push the same key)
-                    const int dst = (gbase + (int)(r & (G - 1))) << 2;
-                    const uint32_t slo = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)km);
-                    const uint32_t shi = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)(km >> 32));
-                    const uint64_t sk = ((uint64_t)shi << 32) | slo;
-                    amb |= wmask(near_or_below(prev_lane64(sk), sk)) & vmask & KGE1 & cmask;
-                }
                 ordered = (wmask(rank != (uint32_t)g) & vmask & KPATH & cmask) == 0;
             } else {
                 // info, full list, lane order = list order: when every path's worse child
@@ -407,8 +476,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     const uint64_t top = shfl_u64(mg, gbase + L - 1);
                     bool forced_here = false;
                     if (FS && force) forced_here = (((j < 64 ? fm0 : fm1) >> (j & 63)) & 1) != 0;
-                    uint64_t badm = APX ? (wmask(lam == 0.0) | (wmask(near_or_below(pv, mg)) & KGE1) | wmask(near_or_below(top, mb)))
-                                        : (wmask(lam == 0.0) | (wmask(pv > mg) & KGE1) | wmask(mb <= top));
+                    uint64_t badm = wmask(lam == 0.0) | (wmask(pv > mg) & KGE1) | wmask(mb <= top);
                     if (FS && force) badm |= wmask(forced_here);
                     if (kFixedList) {
                         if (cnt != L) badm = ~0ULL;
@@ -462,10 +530,6 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 uint32_t r = 0;
                 int c;
 #if PSCL_RANK_M
-                if (APX) {  // unique ranks (full key): the neighbour check below sees every pair
-                    rank_step<G, 1>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
-                    c = __builtin_amdgcn_ds_permute((gbase + (int)(r & (G - 1))) << 2, g);
-                } else {
                 // rank on the metric alone, then check that the ranks 0..ncnt are all claimed
                 // (lane g pulls the rank of the lane it received); equal metrics among the
                 // candidates that matter leave a hole and take the full (metric, 2*rank + bit) key
@@ -480,7 +544,6 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                         c = __builtin_amdgcn_ds_permute((gbase + (int)(r & (G - 1))) << 2, g);
                     }
                 }
-                }
 #else
                 if (!(PSCL_ABLATE & 2)) rank_step<G, 1>((uint32_t)(km >> 32), (uint32_t)km, kt, lane, r);
                 else r = kt & 15u;
@@ -491,13 +554,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 const int par_g = cc & (LMAX - 1);
                 const uint32_t b = cc >= LMAX ? 1u : 0u;
                 const int ps2 = gbase + par_g;
-                // (APX: lane ncnt fetches the first pruned key too, for the neighbour check)
-                const int ccm = APX ? ((g <= ncnt) ? c : g) : cc;
-                const uint64_t nm = (PSCL_ABLATE & 32) ? km : shfl_u64(km, gbase + ccm);
-                if (APX) {
-                    const uint64_t chk = kFixedList ? group_prefix_mask<G>(ncnt + 1) : wmask(g <= ncnt);
-                    amb |= wmask(near_or_below(prev_lane64(nm), nm)) & vmask & KGE1 & chk;
-                }
+                const uint64_t nm = (PSCL_ABLATE & 32) ? km : shfl_u64(km, gbase + cc);
                 const uint64_t nu0 = (PSCL_ABLATE & 32) ? u0 : shfl_u64(u0, ps2);
                 const uint64_t nu1 = (PSCL_ABLATE & 32) || phi < 64 ? u1 : shfl_u64(u1, ps2);  // u1 = 0 before 64
                 const uint32_t ntab = (PSCL_ABLATE & 32) ? tab : bperm32(tab, ps2);
@@ -556,6 +613,22 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 for (int m = 0; m < m0; ++m) syn ^= ST[m * 16 + (uint32_t)((ib0 >> (4 * m)) & 15u)];
                 for (int m = 16; m < k4; ++m) syn ^= ST[m * 16 + (uint32_t)((ib1 >> (4 * (m - 16))) & 15u)];
             }
+        }
+        if constexpr (APX) {
+            // the final list order (best = first CRC pass, and its index): rank on the metric,
+            // certified by every position 0..cnt-1 claimed once and sorted neighbours apart by
+            // the margin.  Upper lanes hold copies, rank among the same keys and push into the
+            // upper half.
+            uint64_t km = g < cnt ? pscl_asu64(metric) : 0x7ff0000000000000ULL;
+            km = merge_from_lower64<G, LMAX>(km, km, lane);
+            uint32_t r = 0;
+            rank_step_m<G, 1, LMAX>((uint32_t)(km >> 32), (uint32_t)km, lane, r);
+            const int c = __builtin_amdgcn_ds_permute((gbase + (g & LMAX) + (int)(r & (LMAX - 1))) << 2, g) & (G - 1);
+            const uint32_t rr = bperm32(r, gbase + c);
+            const uint64_t nm = shfl_u64(km, gbase + c);
+            const uint64_t live = kFixedList ? group_prefix_mask<G>(cnt) : wmask(g < cnt);
+            amb |= ((wmask(rr != (uint32_t)g) & live) | (wmask(near_or_below(prev_lane64(nm), nm)) & live & KGE1)) & vmask;
+            rank = r;
         }
         // APX: a frame with an uncertain ordering is handed to the exact re-decode
         const bool famb = APX && ((amb >> gbase) & (G == 64 ? ~0ULL : ((1ULL << (G & 63)) - 1))) != 0;
