@@ -389,6 +389,27 @@ PSCL_HD double pscl_softplus_tail_bf(double v, const uint64_t* T) {
  * the kernel uses to decide whether an ordering is certain (PSCL_APX_ULPS).
  */
 #define PSCL_APX_TERMS 12
+/* fma(a, w, c) for the Horner steps below as one VOP3 with the constant addend c in an SGPR
+ * pair (PSCL_APX_FMA = 1) or a VGPR (= 2); left to the compiler (= 0) it picks v_fmac and first
+ * copies the constant into the destination, one 64-bit move per step.  Same rounding either way. */
+#ifndef PSCL_APX_FMA
+#define PSCL_APX_FMA 0
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && PSCL_APX_FMA == 1
+__device__ __forceinline__ double pscl_fma_h(double a, double b, double c) {
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+    return d;
+}
+#elif defined(__HIP_DEVICE_COMPILE__) && PSCL_APX_FMA == 2
+__device__ __forceinline__ double pscl_fma_h(double a, double b, double c) {
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+#else
+#define pscl_fma_h(a, b, c) pscl_fma((a), (b), (c))
+#endif
 PSCL_HD double pscl_log1p_apx(double y) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const double d = 2.0 + y;
@@ -403,17 +424,17 @@ PSCL_HD double pscl_log1p_apx(double y) {
 #endif
     const double w = s * s;
     double p = 1.0 / 23.0;
-    p = pscl_fma(p, w, 1.0 / 21.0);
-    p = pscl_fma(p, w, 1.0 / 19.0);
-    p = pscl_fma(p, w, 1.0 / 17.0);
-    p = pscl_fma(p, w, 1.0 / 15.0);
-    p = pscl_fma(p, w, 1.0 / 13.0);
-    p = pscl_fma(p, w, 1.0 / 11.0);
-    p = pscl_fma(p, w, 1.0 / 9.0);
-    p = pscl_fma(p, w, 1.0 / 7.0);
-    p = pscl_fma(p, w, 1.0 / 5.0);
-    p = pscl_fma(p, w, 1.0 / 3.0);
-    p = pscl_fma(p, w, 1.0);
+    p = pscl_fma_h(p, w, 1.0 / 21.0);
+    p = pscl_fma_h(p, w, 1.0 / 19.0);
+    p = pscl_fma_h(p, w, 1.0 / 17.0);
+    p = pscl_fma_h(p, w, 1.0 / 15.0);
+    p = pscl_fma_h(p, w, 1.0 / 13.0);
+    p = pscl_fma_h(p, w, 1.0 / 11.0);
+    p = pscl_fma_h(p, w, 1.0 / 9.0);
+    p = pscl_fma_h(p, w, 1.0 / 7.0);
+    p = pscl_fma_h(p, w, 1.0 / 5.0);
+    p = pscl_fma_h(p, w, 1.0 / 3.0);
+    p = pscl_fma_h(p, w, 1.0);
     return (s + s) * p;
 }
 
