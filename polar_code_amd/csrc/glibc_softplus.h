@@ -393,7 +393,7 @@ PSCL_HD double pscl_softplus_tail_bf(double v, const uint64_t* T) {
  * pair (PSCL_APX_FMA = 1) or a VGPR (= 2); left to the compiler (= 0) it picks v_fmac and first
  * copies the constant into the destination, one 64-bit move per step.  Same rounding either way. */
 #ifndef PSCL_APX_FMA
-#define PSCL_APX_FMA 0
+#define PSCL_APX_FMA 1
 #endif
 #if defined(__HIP_DEVICE_COMPILE__) && PSCL_APX_FMA == 1
 __device__ __forceinline__ double pscl_fma_h(double a, double b, double c) {
