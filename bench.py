@@ -8,6 +8,17 @@ counting, i.e. run_fer_sweep.py:79-109 without the TX chain.  The batches are ge
 on the device before the timed region by the Philox TX kernel (payload -> CRC-24 ->
 polar encode -> BPSK -> AWGN -> LLR), distinct frames per step and per rank.
 
+The line also carries
+  parity        the step-0 batch decoded again after the timed region and compared frame by
+                frame (best bits, CRC flag, best index) with the oracle's outputs for the
+                frames the CPU baseline decoded (oracle/: C restatement of decode_scl);
+  roofline      HBM (algorithmic bytes / live launch time) and, from the committed rocprofv3
+                PMC entry of the SAME library build (profiles/pmc_traffic.json, keyed by the
+                library's source hash), the VALU issue bound priced per instruction class;
+  extra_configs BASELINE configs 2 (L=4), 4 (DL-SCL L=4 + 8 flips, beta_M4) and 5 (NR
+                E=256 L=8): ms/step, frames/s, FER (z vs the reference's results/fer_M4.csv
+                where one applies) and an oracle parity sample each.
+
 Multi-GPU: one process per GPU (torchrun), frames sharded by global frame index, no
 data-path collective; one RCCL all-reduce of the error counters and one of the timings.
 Rank 0 prints ONE JSON line.
@@ -28,8 +39,16 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-REF_FER_L8 = (26, 2000)  # results/fer_M8.csv:2, SCL L=8 @ 5 dB, CRC-fail FER
 POLY = "0x1864CFB"
+# reference CRC-fail frame errors out of 2000 at 5 dB, seed 0 (results/fer_M{8,4}.csv:2)
+REF_ERRS = {("scl", 8): 26, ("dl", 8): 20, ("scl", 4): 91, ("dl", 4): 71}
+
+# VALU issue peak of MI355X per instruction class (MI355X_MICROARCH.md, constants table):
+# 256 CUs x 4 SIMD-32 at 2.4 GHz; a wave64 instruction takes 2 SIMD cycles (fp32/int/logic,
+# moves, DPP, selects, compares: 32 lanes per cycle, with more than one wave per SIMD), 4 for
+# fp64 add/mul/fma (16 lanes per cycle), 8 for transcendentals.
+SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
+CYC_F64, CYC_TRANS, CYC_OTHER = 4, 8, 2
 
 
 def parse():
@@ -51,6 +70,10 @@ def parse():
                     help="NR config 5: (128,88) = 64 payload + CRC-24 bits, rate matched to E transmitted "
                          "bits (run_ber_sweep.py nr_polar_scl); the TX kernel interleaves/repeats, the "
                          "decoder de-rate-matches in its channel staging")
+    ap.add_argument("--extra", choices=["auto", "none"], default="auto",
+                    help="auto: also time BASELINE configs 2, 4, 5 (extra_configs) after the headline")
+    ap.add_argument("--extra-steps", type=int, default=5)
+    ap.add_argument("--extra-parity", type=int, default=50_000, help="oracle parity frames per extra config")
     return ap.parse_args()
 
 
@@ -60,67 +83,267 @@ def frame_bytes(n_in: int, W: int) -> int:
     return n_in * 8 + W * 8 + W * 8 + 1
 
 
-def load_traffic(workload_key: str):
-    """HBM bytes per decode launch measured by rocprofv3 PMC passes (tools/pmc_traffic.py),
-    if a summary for this exact workload is committed under profiles/."""
-    p = ROOT / "profiles" / "pmc_traffic.json"
-    if not p.exists():
-        return None
-    try:
-        d = json.loads(p.read_text())
-        e = d.get(workload_key)
-        return None if e is None else float(e["hbm_bytes_per_launch"])
-    except Exception:
-        return None
-
-
-def load_valu_profile(workload_key: str):
+def pmc_entry(workload_key: str, build_hash: str):
     """The committed rocprofv3 PMC entry of the decode kernel for this workload
-    (profiles/pmc_traffic.json): VALU instructions per frame, instruction mix, VALU-active."""
+    (profiles/pmc_traffic.json), only if it was measured on this exact library build."""
     p = ROOT / "profiles" / "pmc_traffic.json"
     if not p.exists():
-        return None
+        return None, "no profiles/pmc_traffic.json"
     try:
-        e = json.loads(p.read_text()).get(workload_key) or {}
-        return e if "valu_instr_per_frame" in e else None
-    except Exception:
-        return None
+        e = json.loads(p.read_text()).get(workload_key)
+    except Exception as ex:  # malformed file: report, do not guess
+        return None, f"unreadable profiles/pmc_traffic.json ({ex})"
+    if e is None:
+        return None, f"no PMC entry for {workload_key}"
+    if e.get("build_hash") != build_hash:
+        return None, f"PMC entry for {workload_key} is from build {e.get('build_hash')}, timed build is {build_hash}"
+    return e, None
 
 
-# VALU issue peak of MI355X: 256 CUs x 4 SIMDs x 2.4 GHz, one wave64 instruction per SIMD per
-# 4 cycles.  That is the fp64 rate (16 lanes/clk: the 78.6 TF FP64 vector spec) and what a wave
-# sustains alone (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'); f32/int ops can
-# pipeline at 2 cycles between waves (SIMD-32), so the mix-weighted bound (fp64 at 4, the rest
-# at 2) is reported beside it.  This kernel measures 4.1 cycles per VALU instruction with the
-# VALU active ~100 % of SIMD cycles (profiles/pmc_traffic.json).
-SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
+def compute_roofline(e: dict, frames: int, launch_ms: float):
+    """VALU issue bound of the dominant kernel: SIMD cycles its measured instruction mix needs
+    at the guide's per-class rates, over the SIMD cycles available in the live launch time."""
+    ipf = float(e["valu_instr_per_frame"])
+    mix = e.get("valu_mix_per_frame") or {}
+    f64 = sum(float(mix.get(k, 0.0)) for k in ("add_f64", "mul_f64", "fma_f64"))
+    trans = float(mix.get("trans_f64", 0.0)) + float(mix.get("trans_f32", 0.0))
+    other = ipf - f64 - trans
+    need = (CYC_F64 * f64 + CYC_TRANS * trans + CYC_OTHER * other) * frames  # SIMD cycles per launch
+    avail = SIMDS * CLOCK_HZ * launch_ms * 1e-3
+    return {"bound": "valu-issue", "unit": "SIMD-cycles/launch", "achieved": need, "peak": avail,
+            "frac": need / avail, "instr_per_frame": ipf, "fp64_per_frame": f64, "trans_per_frame": trans,
+            "other_per_frame": other, "wave_instr_per_s": ipf * frames / (launch_ms * 1e-3),
+            "valu_active_frac_pmc": e.get("valu_active_frac"),
+            "cycles_per_valu_instr_pmc": e.get("cycles_per_valu_instr"),
+            "build_hash": e.get("build_hash"),
+            "note": ("instr/frame and class mix: rocprofv3 PMC of this library build (profiles/pmc_traffic.json); "
+                     f"price per wave64 instruction: fp64 {CYC_F64}, transcendental {CYC_TRANS}, other {CYC_OTHER} "
+                     f"SIMD cycles (MI355X_MICROARCH.md constants table); {SIMDS} SIMDs x {CLOCK_HZ / 1e9:g} GHz")}
 
 
-def cpu_baseline(llr_host: np.ndarray, info, L: int, budget_s: float, retries: int = 0, beta=None):
-    """The oracle (C restatement of the reference, OpenMP over frames) on host cores."""
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import oracle  # test/baseline infrastructure only
+def fer_z(errs: int, frames: int, ref_errs: int, ref_frames: int = 2000):
+    """Two-proportion z of errs/frames against the reference's ref_errs/ref_frames."""
+    p, p0 = errs / max(frames, 1), ref_errs / ref_frames
+    pp = (errs + ref_errs) / (frames + ref_frames)
+    se = math.sqrt(max(pp * (1 - pp) * (1 / max(frames, 1) + 1 / ref_frames), 1e-30))
+    return (p - p0) / se
 
-    if retries > 0:
-        run = lambda x: oracle.dl_batch(x, info, L, retries, POLY, beta)  # noqa: E731
-        what = f"decode_with_retries (SCL L={L} + up to {retries} flips, beta)"
-    else:
-        run = lambda x: oracle.decode_batch(x, info, L, POLY)  # noqa: E731
-        what = f"decode_scl L={L} + CRC select"
+
+class Oracle:
+    """The checker (oracle/: C restatement of the reference, OpenMP over frames).  Used for the
+    CPU baseline and the parity comparisons only, outside every timed region."""
+
+    def __init__(self):
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import oracle
+
+        self.o = oracle
+
+    def run(self, llr, info, L, retries=0, beta=None):
+        if retries > 0:
+            bits, ok, _ = self.o.dl_batch(llr, info, L, retries, POLY, beta)
+            return bits, ok, None
+        return self.o.decode_batch(llr, info, L, POLY, want_idx=True)
+
+
+def host_internal_llrs(llrE: np.ndarray, N: int) -> np.ndarray:
+    """NR received LLRs -> the decoder's internal LLRs (decode_rate_matched_scl's front end,
+    scl_nr.py:47-48) with the package's host mirrors, for the oracle."""
+    from polar_code_amd.nr.polar import derate_match_polar, subblock_deinterleave
+
+    return np.stack([subblock_deinterleave(derate_match_polar(r, N), N) for r in llrE])
+
+
+def cpu_baseline(orc: Oracle, llr_host: np.ndarray, info, L: int, budget_s: float, retries: int = 0, beta=None):
+    """The oracle timed on the host cores on a bounded sample of the step-0 batch.  Returns the
+    baseline record and the oracle's outputs for the first pass (kept for the parity check)."""
     n0 = min(4000, llr_host.shape[0])
     t0 = time.perf_counter()
-    run(llr_host[:n0])  # warm-up / calibration
+    orc.run(llr_host[:n0], info, L, retries, beta)  # warm-up / calibration
     rate = n0 / max(time.perf_counter() - t0, 1e-6)
     n = int(min(llr_host.shape[0], max(n0, rate * budget_s)))
-    done, dt = 0, 0.0
+    done, dt, first = 0, 0.0, None
     t0 = time.perf_counter()
     while dt < budget_s * 0.8 or done == 0:  # repeat the sample until the budget is spent
-        run(llr_host[:n])
+        out = orc.run(llr_host[:n], info, L, retries, beta)
+        first = first or out
         done += n
         dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "frames/s", "cores": oracle.num_threads(), "kind": "port",
-            "sample": f"{done} frames ({n} distinct frames of the step-0 batch, same LLRs as the GPU) through "
-                      f"oracle/scl_oracle.c (C restatement of {what}), OpenMP over frames, {dt:.1f} s"}
+    what = (f"decode_with_retries (SCL L={L} + up to {retries} flips, beta)" if retries > 0
+            else f"decode_scl L={L} + CRC select")
+    rec = {"value": done / dt, "unit": "frames/s", "cores": orc.o.num_threads(), "kind": "port",
+           "sample": f"{done} frames ({n} distinct frames of the step-0 batch, same LLRs as the GPU) through "
+                     f"oracle/scl_oracle.c (C restatement of {what}), OpenMP over frames, {dt:.1f} s"}
+    return rec, first, n
+
+
+def parity(gpu_best_words: np.ndarray, gpu_flags: np.ndarray, ref, K: int, check_idx: bool):
+    """Frames whose best bits, CRC flag or (plain decodes) best index differ from the oracle."""
+    from polar_code_amd.dlscl.flip import words_to_bits
+
+    bits, ok, idx = ref
+    n = bits.shape[0]
+    gb = words_to_bits(gpu_best_words[:n], K)
+    gpass = (gpu_flags[:n] & 0x80) != 0
+    bad = np.any(gb != bits, axis=1) | (gpass != ok)
+    if check_idx and idx is not None:
+        bad |= (gpu_flags[:n] & 0x3F).astype(np.int32) != idx
+    return {"frames": int(n), "mismatches": int(np.count_nonzero(bad)),
+            "compared": "best bits, CRC flag" + (", best index" if check_idx else "") + " vs oracle"}
+
+
+class Ctx:
+    def __init__(self, torch, dev, device_index, dist, rank, world):
+        self.torch, self.dev, self.device_index = torch, dev, device_index
+        self.dist, self.rank, self.world = dist, rank, world
+
+    def max_over_ranks(self, x: float) -> float:
+        if not self.dist:
+            return x
+        red = self.dev if self.dist.get_backend() == "nccl" else "cpu"
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=red)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_over_ranks(self, v):
+        if not self.dist:
+            return v.cpu().numpy()
+        red = self.dev if self.dist.get_backend() == "nccl" else self.torch.device("cpu")
+        t = v.to(red)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return t.cpu().numpy()
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+
+def run_workload(ctx: Ctx, *, L: int, E: int, retries: int, beta, B: int, steps: int, warmup: int, ebno: float,
+                 seed: int, keep_buffers: bool = False):
+    """Generate the batches on the device, run W untimed + K timed steps (barrier and
+    synchronize on both sides, max over ranks), then decode the step-0 batch once more
+    (untimed) for the parity check.  Returns the measurements."""
+    torch, dev = ctx.torch, ctx.dev
+    from polar_code_amd import _native
+    from polar_code_amd.polar.polar import construct_info_set
+
+    N, K = 128, (88 if E else 64)
+    info = construct_info_set(N, K)
+    dec = _native.Decoder(N, info, L, POLY, device=ctx.device_index)
+    if E:
+        dec.set_rate_match(E)
+    n_in = E or N
+    stream = torch.cuda.current_stream(dev)
+    dec.set_stream(stream.cuda_stream)
+    W = dec.W
+    kp = K - 24
+    rate = kp / E if E else K / N  # run_ber_sweep.py: R = K_payload / E; run_fer_sweep.py: K / N
+
+    # ---- inputs resident in HBM: distinct frames per (rank, step), generated on device
+    nbuf = max(1, min(steps, int(48e9 // (B * n_in * 8))))
+    llr = [torch.empty((B, n_in), dtype=torch.float64, device=dev) for _ in range(nbuf)]
+    msg = [torch.empty((B, W), dtype=torch.int64, device=dev) for _ in range(nbuf)]
+    best = torch.empty((B, W), dtype=torch.int64, device=dev)
+    flags = torch.empty((B,), dtype=torch.uint8, device=dev)
+    counters = torch.zeros(8, dtype=torch.int64, device=dev)
+    counters_dl = torch.zeros(8, dtype=torch.int64, device=dev)
+    snr_idx = int(round(ebno * 10))
+    for i in range(nbuf):
+        frame0 = (ctx.rank * nbuf + i) * B
+        dec.channel_device(seed, snr_idx, ebno, rate, kp, frame0, B, llr[i].data_ptr(), msg[i].data_ptr())
+    torch.cuda.synchronize(dev)
+
+    def step(j, count=True):
+        c_scl = counters.data_ptr() if count else 0
+        ref = msg[j].data_ptr() if count else 0
+        if retries > 0:  # SCL + DL-SCL retry rounds, all on the device
+            dec.dlscl_device(llr[j].data_ptr(), B, retries, beta=beta, d_best=best.data_ptr(),
+                             d_flags=flags.data_ptr(), d_ref=ref, k_payload=kp, d_counters_scl=c_scl,
+                             d_counters_dl=counters_dl.data_ptr() if count else 0)
+        else:
+            dec.decode_device(llr[j].data_ptr(), B, d_best=best.data_ptr(), d_flags=flags.data_ptr(), d_ref=ref,
+                              k_payload=kp, d_counters=c_scl)
+
+    for i in range(warmup):
+        step(i % nbuf)
+    torch.cuda.synchronize(dev)
+    counters.zero_()
+    counters_dl.zero_()
+    dec.timing_enable(True)
+    ctx.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i % nbuf)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    ctx.barrier()
+    launches, kern_ms = dec.timing_read()
+    dec.timing_enable(False)
+    elapsed = ctx.max_over_ranks(elapsed)
+    c = ctx.sum_over_ranks(counters)
+    cdl = ctx.sum_over_ranks(counters_dl)
+    # untimed: the step-0 batch once more, outputs kept for the parity check
+    step(0, count=False)
+    torch.cuda.synchronize(dev)
+    res = {"N": N, "K": K, "W": W, "L": L, "E": E, "B": B, "n_in": n_in, "info": info, "retries": retries,
+           "elapsed": elapsed, "launches": launches, "kern_ms": kern_ms, "c": c, "cdl": cdl, "kp": kp,
+           "rate": rate, "build_hash": _native.build_hash(),
+           "best0": best.cpu().numpy().view(np.uint64), "flags0": flags.cpu().numpy()}
+    if keep_buffers:
+        res["llr0"] = llr[0]
+    del llr, msg, best, flags
+    dec.close()
+    torch.cuda.empty_cache()
+    return res
+
+
+def extra_configs(args, ctx: Ctx, orc: Oracle | None):
+    """BASELINE configs 2, 4, 5 (1 GPU each per rank, frame-sharded like the headline)."""
+    cfgs = [
+        ("config2_scl_L4", dict(L=4, E=0, retries=0), "scl", 4),
+        ("config4_dlscl_L4_r8_beta4", dict(L=4, E=0, retries=8), "dl", 4),
+        ("config5_nr_E256_L8", dict(L=8, E=256, retries=0), None, None),
+    ]
+    out = {}
+    for name, kw, ref_kind, ref_L in cfgs:
+        beta = np.load(ROOT / "tests" / "golden" / "beta_M4.npy") if kw["retries"] else None
+        r = run_workload(ctx, **kw, beta=beta, B=args.frames, steps=args.extra_steps, warmup=1, ebno=args.ebno,
+                         seed=args.seed, keep_buffers=orc is not None)
+        if ctx.rank != 0:
+            continue
+        c, cdl = r["c"], r["cdl"]
+        frames = int(c[0])
+        rec = {"ms_per_step": r["elapsed"] * 1e3 / args.extra_steps,
+               "value": args.frames * args.extra_steps * ctx.world / r["elapsed"], "unit": "frames/s",
+               "steps": args.extra_steps, "frames_per_gpu_per_step": args.frames,
+               "decode_ms_per_step": r["kern_ms"] / args.extra_steps, "launches": r["launches"],
+               "kernel": ("scl128_kernel<4> screening + exact re-decode" if name.startswith("config2") else
+                          "scl128_kernel<4> baseline + dl_select/replay/dl_update + scl128_kernel<4,FS> retry rounds"
+                          if name.startswith("config4") else
+                          "scl128_kernel<8,CH,CODE=2> screening (de-rate-match in staging) + exact re-decode"),
+               "fer": {"frames": frames, "frame_errors": int(c[1]), "fer": c[1] / max(frames, 1),
+                       "payload_fer": c[3] / max(frames, 1)}}
+        if kw["retries"]:
+            rec["dl_scl"] = {"frame_errors": int(cdl[1]), "fer": cdl[1] / max(cdl[0], 1),
+                             "redecodes_per_frame": cdl[5] / max(cdl[0], 1), "beta": "tests/golden/beta_M4.npy"}
+        if ref_kind:
+            rec["fer"]["reference"] = f"results/fer_M{ref_L}.csv:2 fer_scl {REF_ERRS[('scl', ref_L)]}/2000"
+            rec["fer"]["z_vs_reference"] = fer_z(int(c[1]), frames, REF_ERRS[("scl", ref_L)])
+            if kw["retries"]:
+                rec["dl_scl"]["reference"] = f"results/fer_M{ref_L}.csv:2 fer_dl {REF_ERRS[('dl', ref_L)]}/2000"
+                rec["dl_scl"]["z_vs_reference"] = fer_z(int(cdl[1]), int(cdl[0]), REF_ERRS[("dl", ref_L)])
+        if orc is not None:
+            n = min(args.extra_parity, args.frames)
+            host = r["llr0"][:n].cpu().numpy()
+            if kw["E"]:
+                host = host_internal_llrs(host, 128)
+            ref = orc.run(host, r["info"], kw["L"], kw["retries"], beta)
+            rec["parity"] = parity(r["best0"], r["flags0"], ref, r["K"], check_idx=kw["retries"] == 0)
+        out[name] = rec
+        del r
+        ctx.torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -144,90 +367,35 @@ def main():
             dist.init_process_group(backend="nccl", device_id=dev)
         else:
             dist.init_process_group(backend=backend)
+    ctx = Ctx(torch, dev, device_index, dist, rank, world)
 
-    from polar_code_amd import _native
-    from polar_code_amd.polar.polar import construct_info_set
-
-    E = args.nr_E
-    N, K, L, B = 128, (88 if E else 64), args.list, args.frames
-    info = construct_info_set(N, K)
-    dec = _native.Decoder(N, info, L, POLY, device=device_index)
-    if E:
-        dec.set_rate_match(E)
-    n_in = E or N
-    stream = torch.cuda.current_stream(dev)
-    dec.set_stream(stream.cuda_stream)
-    W = dec.W
-    kp = K - 24
-    rate = kp / E if E else K / N  # run_ber_sweep.py: R = K_payload / E; run_fer_sweep.py: K / N
-
-    # ---- inputs resident in HBM: distinct frames per (rank, step), generated on device
-    nbuf = max(1, min(args.steps, int(48e9 // (B * n_in * 8))))
-    llr = [torch.empty((B, n_in), dtype=torch.float64, device=dev) for _ in range(nbuf)]
-    msg = [torch.empty((B, W), dtype=torch.int64, device=dev) for _ in range(nbuf)]
-    best = torch.empty((B, W), dtype=torch.int64, device=dev)
-    flags = torch.empty((B,), dtype=torch.uint8, device=dev)
-    counters = torch.zeros(8, dtype=torch.int64, device=dev)
-    snr_idx = int(round(args.ebno * 10))
-    for i in range(nbuf):
-        frame0 = (rank * nbuf + i) * B
-        dec.channel_device(args.seed, snr_idx, args.ebno, rate, kp, frame0, B, llr[i].data_ptr(), msg[i].data_ptr())
-    torch.cuda.synchronize(dev)
-
+    E, L, B = args.nr_E, args.list, args.frames
     beta = None
     if args.retries > 0 and args.beta != "none":
         bp = ROOT / "tests" / "golden" / f"beta_M{L}.npy" if args.beta == "auto" else Path(args.beta)
         beta = np.load(bp) if bp.exists() else None
-    counters_dl = torch.zeros(8, dtype=torch.int64, device=dev)
-
-    def step(i):
-        j = i % nbuf
-        if args.retries > 0:  # SCL + DL-SCL retry rounds, all on the device
-            dec.dlscl_device(llr[j].data_ptr(), B, args.retries, beta=beta, d_best=best.data_ptr(),
-                             d_flags=flags.data_ptr(), d_ref=msg[j].data_ptr(), k_payload=kp,
-                             d_counters_scl=counters.data_ptr(), d_counters_dl=counters_dl.data_ptr())
-        else:
-            dec.decode_device(llr[j].data_ptr(), B, d_best=best.data_ptr(), d_flags=flags.data_ptr(),
-                              d_ref=msg[j].data_ptr(), k_payload=kp, d_counters=counters.data_ptr())
-
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize(dev)
-    counters.zero_()
-    counters_dl.zero_()
-    dec.timing_enable(True)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if dist:
-        dist.barrier()
-    launches, kern_ms = dec.timing_read()
-    dec.timing_enable(False)
-
-    red_dev = dev if (dist is None or dist.get_backend() == "nccl") else torch.device("cpu")
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
-    if dist:
-        counters = counters.to(red_dev)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        counters_dl = counters_dl.to(red_dev)
-        dist.all_reduce(counters, op=dist.ReduceOp.SUM)
-        dist.all_reduce(counters_dl, op=dist.ReduceOp.SUM)
-    elapsed = float(tmax.item())
-    c = counters.cpu().numpy()
-    cdl = counters_dl.cpu().numpy()
+    r = run_workload(ctx, L=L, E=E, retries=args.retries, beta=beta, B=B, steps=args.steps, warmup=args.warmup,
+                     ebno=args.ebno, seed=args.seed, keep_buffers=(rank == 0))
+    N, K, W, n_in, info, kp = r["N"], r["K"], r["W"], r["n_in"], r["info"], r["kp"]
+    c, cdl, elapsed = r["c"], r["cdl"], r["elapsed"]
     frames_total = B * args.steps * world
 
-    cpu = None
-    if rank == 0 and not args.no_cpu_baseline and not E:
-        host = llr[0][: min(B, 1_000_000)].cpu().numpy()
-        cpu = cpu_baseline(host, info, L, args.cpu_seconds, args.retries, beta)
+    cpu = par = None
+    orc = Oracle() if (rank == 0 and not args.no_cpu_baseline) else None
+    if orc is not None:
+        host = r["llr0"][: min(B, 1_000_000)].cpu().numpy()
+        if E:
+            host = host_internal_llrs(host[: min(host.shape[0], 100_000)], N)
+        cpu, ref, n = cpu_baseline(orc, host, info, L, args.cpu_seconds, args.retries, beta)
+        par = parity(r["best0"], r["flags0"], ref, K, check_idx=args.retries == 0)
+    r.pop("llr0", None)
+    torch.cuda.empty_cache()
+    extra = None
+    if args.extra == "auto" and not E and args.retries == 0 and L == 8:
+        extra = extra_configs(args, ctx, orc)
 
     if rank == 0:
+        launches, kern_ms = r["launches"], r["kern_ms"]
         avg_ms = kern_ms / max(launches, 1)
         fb = frame_bytes(n_in, W)
         # DL mode: the step's decode launches (baseline + retry rounds) priced as one pass
@@ -235,41 +403,24 @@ def main():
         per_batch_ms = kern_ms / args.steps if args.retries > 0 else avg_ms
         achieved = fb * B / (per_batch_ms * 1e-3) / 1e9
         wkey = f"scl_L{L}_N{N}_K{K}_B{B}" + (f"_E{E}" if E else "") + (f"_dl{args.retries}" if args.retries > 0 else "")
-        traffic = load_traffic(wkey)
-        vp = load_valu_profile(wkey)
-        compute = None
-        if vp is not None:
-            ipf = float(vp["valu_instr_per_frame"])
-            rate = ipf * B / (per_batch_ms * 1e-3)
-            peak4 = SIMDS * CLOCK_HZ / 4
-            compute = {"bound": "valu-issue", "unit": "wave-instr/s", "instr_per_frame": ipf,
-                       "achieved": rate, "peak": peak4, "frac": rate / peak4,
-                       "valu_active_frac_pmc": vp.get("valu_active_frac"),
-                       "cycles_per_valu_instr_pmc": vp.get("cycles_per_valu_instr")}
-            mix = vp.get("valu_mix_per_frame")
-            if mix:
-                f64 = sum(mix.get(k, 0.0) for k in ("add_f64", "mul_f64", "fma_f64", "trans_f64"))
-                cyc = (4 * f64 + 2 * (ipf - f64)) * B / SIMDS  # SIMD-cycles per launch, mix-weighted
-                compute["fp64_share"] = f64 / ipf
-                compute["frac_mix_weighted"] = cyc / CLOCK_HZ / (per_batch_ms * 1e-3)
-            compute["note"] = ("instr/frame and mix from rocprofv3 PMC (profiles/pmc_traffic.json) x live frames/s; "
-                               "peak = one wave64 VALU instruction per 4 cycles per SIMD (fp64 rate); "
-                               "frac_mix_weighted prices non-fp64 ops at 2 cycles")
+        e, why = pmc_entry(wkey, r["build_hash"])
+        traffic = float(e["hbm_bytes_per_launch"]) if e and "hbm_bytes_per_launch" in e else None
+        compute = compute_roofline(e, B, per_batch_ms) if e and "valu_instr_per_frame" in e else None
         fer = c[1] / max(c[0], 1)
-        p0 = REF_FER_L8[0] / REF_FER_L8[1]
-        pp = (c[1] + REF_FER_L8[0]) / (c[0] + REF_FER_L8[1])
-        se = math.sqrt(max(pp * (1 - pp) * (1 / max(c[0], 1) + 1 / REF_FER_L8[1]), 1e-30))
+        ref_scl = REF_ERRS.get(("scl", L)) if not E else None
         dl = None
         if args.retries > 0:
+            ref_dl = REF_ERRS.get(("dl", L)) if not E else None
             dl = {"retries": args.retries, "beta": None if beta is None else "tests/golden/beta_M%d.npy" % L,
                   "frame_errors": int(cdl[1]), "fer": cdl[1] / max(cdl[0], 1), "ber": cdl[2] / max(cdl[0] * K, 1),
-                  "redecodes": int(cdl[5]), "redecodes_per_frame": cdl[5] / max(cdl[0], 1)}
+                  "redecodes": int(cdl[5]), "redecodes_per_frame": cdl[5] / max(cdl[0], 1),
+                  "z_vs_reference": fer_z(int(cdl[1]), int(cdl[0]), ref_dl) if ref_dl and args.ebno == 5.0 else None}
         metric = "decoded frames/sec, P(128,64)+CRC24 SCL L=8 @ Eb/N0=5 dB; FER match"
         workload = (f"SCL L={L} P({N},{K})+CRC24 (0x1864CFB) @ Eb/N0={args.ebno:g} dB, "
                     f"{B} frames/GPU/step, decode+CRC select+FER/BER count")
         if E:
             metric = f"decoded frames/sec, NR polar N=128 E={E} K=64+CRC24 SCL L={L}"
-            workload = (f"NR SCL L={L} (128,88) rate matched E={E}, R={rate:g} @ Eb/N0={args.ebno:g} dB, {B} "
+            workload = (f"NR SCL L={L} (128,88) rate matched E={E}, R={r['rate']:g} @ Eb/N0={args.ebno:g} dB, {B} "
                         f"frames/GPU/step, de-rate-match + decode + CRC select + FER/BER count")
         if args.retries > 0:
             metric = f"decoded frames/sec, P(128,{K})+CRC24 DL-SCL L={L} + {args.retries} flip retries"
@@ -296,13 +447,16 @@ def main():
                          "traffic": traffic,
                          "kernel": "scl128_kernel" if N == 128 and L <= 8 else "scl_decode_kernel",
                          "avg_launch_ms": avg_ms, "launches": launches, "decode_ms_per_step": kern_ms / args.steps,
-                         "bytes_per_frame": fb, "compute": compute},
+                         "bytes_per_frame": fb, "build_hash": r["build_hash"], "pmc": why or "matched build",
+                         "compute": compute},
             "cpu_baseline": cpu,
+            "parity": par,
             "fer": {"frames": int(c[0]), "frame_errors": int(c[1]), "fer": fer, "ber": c[2] / max(c[0] * K, 1),
                     "payload_fer": c[3] / max(c[0], 1), "payload_ber": c[4] / max(c[0] * kp, 1),
-                    "reference_fer": p0 if (L == 8 and not E) else None,
-                    "z_vs_reference": (fer - p0) / se if (L == 8 and args.ebno == 5.0 and not E) else None},
+                    "reference_fer": ref_scl / 2000 if ref_scl else None,
+                    "z_vs_reference": fer_z(int(c[1]), int(c[0]), ref_scl) if ref_scl and args.ebno == 5.0 else None},
             "dl_scl": dl,
+            "extra_configs": extra,
         }
         print(json.dumps(line), flush=True)
     if dist:

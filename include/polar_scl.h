@@ -79,6 +79,10 @@ const char* pscl_last_error(void);
 /* ABI version compiled into the library (PSCL_ABI_VERSION). */
 int pscl_abi_version(void);
 
+/* Hash (hex) of the sources and compile flags the library was built from; the build and the
+ * Python layer compare it with the sources in the tree, so a stale library is never used. */
+const char* pscl_build_hash(void);
+
 /* Number of visible HIP devices (0 when there is no GPU); negative on runtime failure. */
 int pscl_device_count(void);
 
@@ -234,6 +238,17 @@ int pscl_memset_device(pscl_handle* h, void* d_dst, int value, int64_t bytes);
  * enable = 0 runs the exact kernel only.
  */
 int pscl_set_screening(pscl_handle* h, int enable);
+
+/* Frames the last screening decode on this handle handed to the exact re-decode (synchronizes
+ * the stream; 0 if no screening decode ran).  Diagnostic / test hook. */
+int pscl_screening_count(pscl_handle* h, int64_t* count);
+
+/*
+ * Diagnostic: the metric tail log1p(exp(-|v|)) (scl.py:102-105) of n device values, evaluated
+ * as the decode kernels do -- d_exact by the bit-exact glibc port, d_apx by the screening
+ * decode's bounded-error form.  Device buffers, handle stream.
+ */
+int pscl_softplus_tails_device(pscl_handle* h, const double* d_v, int64_t n, double* d_exact, double* d_apx);
 
 /*
  * Kernel timing with HIP events recorded on the launch stream around every decode kernel

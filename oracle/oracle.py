@@ -32,7 +32,7 @@ def lib() -> C.CDLL:
         L.oracle_decode_with_retries.argtypes = [dp, C.c_int, ip, C.c_int, C.c_int, C.c_int, C.c_uint64,
                                                  C.POINTER(C.c_float), bp, ip, ip, ip, ip]
         L.oracle_decode_batch.argtypes = [dp, C.c_int64, C.c_int, ip, C.c_int, C.c_int, C.c_uint64, bp,
-                                          C.POINTER(C.c_uint8)]
+                                          C.POINTER(C.c_uint8), ip]
         L.oracle_dl_batch.argtypes = [dp, C.c_int64, C.c_int, ip, C.c_int, C.c_int, C.c_int, C.c_uint64,
                                       C.POINTER(C.c_float), bp, ip, ip]
         L.oracle_num_threads.restype = C.c_int
@@ -128,18 +128,20 @@ def decode_with_retries(llr, info, M, retries, crc=None, beta=None):
     return dict(bits=bits, success=bool(succ[0]), attempts=int(att[0]), tried=tried[: nt[0]].tolist())
 
 
-def decode_batch(llr, info, M, crc=None):
-    """Parallel (OpenMP) batch decode: returns (best_bits[B,K], crc_pass[B])."""
+def decode_batch(llr, info, M, crc=None, want_idx=False):
+    """Parallel (OpenMP) batch decode: returns (best_bits[B,K], crc_pass[B]) and, with
+    want_idx, best_index[B] (the best candidate's list position) as a third element."""
     llr = np.ascontiguousarray(llr, np.float64)
     info = np.ascontiguousarray(info, np.int32)
     B, N = llr.shape
     K = info.size
     bits = np.zeros((B, K), np.int8)
     ok = np.zeros(B, np.uint8)
+    idx = np.zeros(B, np.int32) if want_idx else None
     if lib().oracle_decode_batch(_p(llr, C.c_double), B, N, _p(info, C.c_int32), K, M, poly_int(crc),
-                                 _p(bits, C.c_int8), _p(ok, C.c_uint8)):
+                                 _p(bits, C.c_int8), _p(ok, C.c_uint8), None if idx is None else _p(idx, C.c_int32)):
         raise ValueError("oracle_decode_batch failed")
-    return bits, ok.astype(bool)
+    return (bits, ok.astype(bool), idx) if want_idx else (bits, ok.astype(bool))
 
 
 def dl_batch(llr, info, M, retries, crc=None, beta=None):

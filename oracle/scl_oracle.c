@@ -509,7 +509,7 @@ fail:
  * Parallel over frames with OpenMP when built with -fopenmp (threads = OMP_NUM_THREADS).
  */
 int oracle_decode_batch(const double* llr, int64_t B, int N, const int32_t* info, int K, int M,
-                        uint64_t crc_poly, int8_t* best_bits, uint8_t* crc_pass) {
+                        uint64_t crc_poly, int8_t* best_bits, uint8_t* crc_pass, int32_t* best_idx) {
     int err = 0;
 #pragma omp parallel for schedule(dynamic, 4) reduction(| : err)
     for (int64_t b = 0; b < B; b++) {
@@ -523,6 +523,7 @@ int oracle_decode_batch(const double* llr, int64_t B, int N, const int32_t* info
         }
         memcpy(best_bits + b * K, cands + (size_t)bi * K, (size_t)K);
         crc_pass[b] = (uint8_t)(crc_poly ? oracle_check_crc(cands + (size_t)bi * K, K, crc_poly) == 1 : 1);
+        if (best_idx) best_idx[b] = bi;
     }
     return err ? -1 : 0;
 }

@@ -51,3 +51,11 @@ int64_t log1p_unit_compare(const double* y, int64_t n) {
         if (pscl_asu64(pscl_log1p_unit(y[i])) != pscl_asu64(log1p(y[i]))) bad++;
     return bad;
 }
+
+/* exact and screening (bounded-error) metric tails, host forms */
+void softplus_tails_batch(const double* v, int64_t n, double* exact, double* apx) {
+    for (int64_t i = 0; i < n; i++) {
+        exact[i] = pscl_softplus_tail_bf(v[i], kT);
+        apx[i] = pscl_softplus_tail_apx(v[i], kT);
+    }
+}

@@ -38,7 +38,8 @@ EXPORTS = (
     "pscl_decode_device", "pscl_channel_device", "pscl_device_alloc", "pscl_device_free",
     "pscl_memcpy_htod", "pscl_memcpy_dtoh", "pscl_memset_device", "pscl_timing_enable",
     "pscl_timing_read", "pscl_launch_info", "pscl_set_rate_match", "pscl_set_beta", "pscl_dlscl_device",
-    "pscl_path_llrs_device", "pscl_uncoded_device", "pscl_set_screening",
+    "pscl_path_llrs_device", "pscl_uncoded_device", "pscl_set_screening", "pscl_build_hash",
+    "pscl_screening_count", "pscl_softplus_tails_device",
 )
 
 _vp, _i32, _i64, _u64, _dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
@@ -63,6 +64,20 @@ def _bind_hip_runtime() -> None:
         C.CDLL(str(cand), mode=C.RTLD_GLOBAL)
 
 
+def _check_fresh() -> None:
+    """Refuse a library built from other sources than the ones in this tree (its embedded
+    build hash, polar_code_amd/build.py).  Skipped where the sources are absent."""
+    from . import build
+
+    if not all((build.CSRC / s).exists() for s in build.HIP_DEPS):
+        return
+    want, got = build.source_hash(), build.library_hash(LIB_PATH)
+    if got != want:
+        raise PolarNativeError(
+            f"{LIB_PATH} is stale (built from sources {got}, tree has {want}): "
+            "run `python -m polar_code_amd.build`")
+
+
 @functools.lru_cache(maxsize=1)
 def lib() -> C.CDLL:
     _bind_hip_runtime()
@@ -70,11 +85,16 @@ def lib() -> C.CDLL:
         raise PolarNativeError(
             f"{LIB_PATH} not built: run `python -m polar_code_amd.build` (hipcc, gfx950). "
             "There is no CPU fallback for the decoder.")
+    if not os.environ.get("PSCL_LIB_PATH"):
+        _check_fresh()
     L = C.CDLL(str(LIB_PATH))
     P = C.POINTER
     sig = {
         "pscl_last_error": (C.c_char_p, []),
         "pscl_abi_version": (C.c_int, []),
+        "pscl_build_hash": (C.c_char_p, []),
+        "pscl_screening_count": (C.c_int, [_vp, P(_i64)]),
+        "pscl_softplus_tails_device": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
         "pscl_device_count": (C.c_int, []),
         "pscl_create": (C.c_int, [P(_vp), C.c_int, C.c_int, P(_i32), C.c_int, C.c_int, _u64]),
         "pscl_destroy": (C.c_int, [_vp]),
@@ -108,6 +128,12 @@ def lib() -> C.CDLL:
         fn.restype = res
         fn.argtypes = args
     return L
+
+
+def build_hash() -> str:
+    """The loaded library's embedded source hash ("" for variant libraries without one)."""
+    fn = getattr(lib(), "pscl_build_hash", None)
+    return fn().decode() if fn is not None else ""
 
 
 def last_error() -> str:
@@ -299,6 +325,21 @@ class Decoder:
 
     def sync(self) -> None:
         check(lib().pscl_sync(self._h))
+
+    def screening_count(self) -> int:
+        """Frames the last screening decode handed to the exact re-decode (synchronizes)."""
+        n = _i64()
+        check(lib().pscl_screening_count(self._h, C.byref(n)))
+        return int(n.value)
+
+    def softplus_tails(self, v: np.ndarray):
+        """(exact, screening) metric tails log1p(exp(-|v|)) of v as the kernels evaluate them."""
+        v = np.ascontiguousarray(v, dtype=np.float64).ravel()
+        with DeviceArena(self) as mem:
+            d_v, d_e, d_a = mem.alloc(v.nbytes), mem.alloc(v.nbytes), mem.alloc(v.nbytes)
+            mem.upload(d_v, v)
+            check(lib().pscl_softplus_tails_device(self._h, d_v, v.size, d_e, d_a))
+            return mem.download(d_e, v.nbytes, np.float64), mem.download(d_a, v.nbytes, np.float64)
 
     def set_screening(self, on: bool = True) -> None:
         """Screening decode for plain decodes (default on; include/polar_scl.h)."""

@@ -8,6 +8,7 @@ Run:  python -m polar_code_amd.build   (or __graft_entry__.build()).
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -28,7 +29,33 @@ HIP_DEPS = HIP_SOURCES + ["scl_kernels.h", "scl_device.h", "scl128_impl.h", "gli
 SPEC_UNITS = [(c, l) for c in (1, 2) for l in (1, 2, 4, 8)]
 
 
-def hip_units(objdir: Path, tag: str = "") -> list[tuple[Path, list[str], Path]]:
+BASE_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wno-unused-result", "-Wno-unused-value"]
+HASH_MARK = b"PSCL_BUILD_HASH="
+
+
+def source_hash(flags: list[str] | None = None) -> str:
+    """sha256 (16 hex digits) of every source and header the library is compiled from, the
+    target, the compile flags and the unit list.  Embedded in the library (pscl_build_hash)."""
+    h = hashlib.sha256()
+    h.update(" ".join([ARCH, *BASE_FLAGS, *(flags or []), repr(SPEC_UNITS), *HIP_SOURCES]).encode())
+    for f in [*(CSRC / s for s in HIP_DEPS), INCLUDE / "polar_scl.h"]:
+        h.update(f.name.encode() + b"\0" + f.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def library_hash(lib: Path = LIB) -> str | None:
+    """The hash embedded in a built library (read from its bytes; nothing is loaded)."""
+    try:
+        data = lib.read_bytes()
+    except OSError:
+        return None
+    i = data.find(HASH_MARK)
+    if i < 0:
+        return None
+    return data[i + len(HASH_MARK): i + len(HASH_MARK) + 16].decode(errors="replace")
+
+
+def hip_units(objdir: Path, tag: str = "", hash_: str | None = None) -> list[tuple[Path, list[str], Path]]:
     """(source, extra flags, object) for every compile of the HIP library."""
     units = []
     for src in HIP_SOURCES:
@@ -37,7 +64,8 @@ def hip_units(objdir: Path, tag: str = "") -> list[tuple[Path, list[str], Path]]
                 units.append((CSRC / src, [f"-DPSCL_SPEC_CODE={c}", f"-DPSCL_SPEC_LMAX={l}"],
                               objdir / f"scl128_spec_{c}_{l}{tag}.o"))
         else:
-            units.append((CSRC / src, [], objdir / (Path(src).stem + tag + ".o")))
+            extra = [f'-DPSCL_BUILD_HASH="{hash_}"'] if (src == "capi.cpp" and hash_) else []
+            units.append((CSRC / src, extra, objdir / (Path(src).stem + tag + ".o")))
     return units
 
 
@@ -45,8 +73,7 @@ def compile_units(units, flags: list[str], jobs: int | None = None) -> list[str]
     """Compile the units in parallel (the spec instances take ~40 s each)."""
     from concurrent.futures import ThreadPoolExecutor
 
-    base = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-            "-Wno-unused-result", "-Wno-unused-value", f"-I{INCLUDE}", f"-I{CSRC}", *flags]
+    base = [HIPCC, f"--offload-arch={ARCH}", *BASE_FLAGS, f"-I{INCLUDE}", f"-I{CSRC}", *flags]
     jobs = jobs or min(len(units), max(1, min(16, os.cpu_count() or 1)))
     with ThreadPoolExecutor(jobs) as ex:
         list(ex.map(lambda u: _run([*base, *u[1], "-c", str(u[0]), "-o", str(u[2])]), units))
@@ -68,12 +95,14 @@ def _stale(target: Path, deps: list[Path]) -> bool:
 
 
 def build_hip(force: bool = False) -> Path:
-    deps = [CSRC / s for s in HIP_DEPS] + [INCLUDE / "polar_scl.h"]
-    if not force and not _stale(LIB, deps):
+    """Rebuild unless the library's embedded hash equals the hash of the sources in the tree
+    (modification times are not trusted: a copied or pushed library may look newer)."""
+    want = source_hash()
+    if not force and library_hash() == want:
         return LIB
     objdir = PKG / "_build"
     objdir.mkdir(exist_ok=True)
-    objs = compile_units(hip_units(objdir), [])
+    objs = compile_units(hip_units(objdir, hash_=want), [])
     tmp = LIB.with_suffix(".so.tmp")
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", str(tmp)])
     os.replace(tmp, LIB)

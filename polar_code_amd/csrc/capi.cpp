@@ -41,6 +41,12 @@ int fail(int code, const char* fmt, ...) {
                         #expr, hipGetErrorString(_e));                                    \
     } while (0)
 
+#ifndef PSCL_BUILD_HASH
+#define PSCL_BUILD_HASH "unhashed"
+#endif
+// marker + hash, found in the .so bytes by polar_code_amd/build.py's staleness check
+__attribute__((used)) const char kBuildHash[] = "PSCL_BUILD_HASH=" PSCL_BUILD_HASH;
+
 const uint64_t kExpTable[256] = {
 #include "exp_table.inc"
 };
@@ -102,6 +108,7 @@ struct pscl_handle {
     int epi_words = 0;
     bool timing = false;
     bool screen = true;               // screening decode for plain decodes (pscl_set_screening)
+    bool screened = false;            // a screening decode ran (scratch 36 holds its count)
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
 };
@@ -179,11 +186,15 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P, int hist, hipStre
         S.amb_list = (int64_t*)d_list;
         S.amb_count = (int32_t*)d_cnt;
         err = pscl_launch_decode(S, hist, st);
+        h->screened = true;
         if (err == hipSuccess) {
             pscl_decode_params X = P;  // exact decode of the listed frames, outputs at their rows
             X.fidx = (const int64_t*)d_list;
             X.d_count = (const int32_t*)d_cnt;
             X.out_by_row = 1;
+            // few frames: one resident set of workgroups (4 waves/SIMD on 256 CUs), striding
+            // over the listed frames, instead of a grid sized for the whole batch
+            X.grid_cap = (int64_t)256 * 16 / (pscl_decode_wpg(X) > 0 ? pscl_decode_wpg(X) : 1);
             err = pscl_launch_decode(X, hist, st);
         }
     } else {
@@ -201,6 +212,8 @@ extern "C" {
 const char* pscl_last_error(void) { return g_err.c_str(); }
 
 int pscl_abi_version(void) { return PSCL_ABI_VERSION; }
+
+const char* pscl_build_hash(void) { return kBuildHash + 16; }
 
 int pscl_device_count(void) {
     int n = 0;
@@ -919,6 +932,30 @@ int pscl_memset_device(pscl_handle* h, void* d_dst, int value, int64_t bytes) {
 int pscl_set_screening(pscl_handle* h, int enable) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
     h->screen = enable != 0;
+    return PSCL_OK;
+}
+
+int pscl_screening_count(pscl_handle* h, int64_t* count) {
+    if (!h || !count) return fail(PSCL_EINVAL, "bad arguments");
+    *count = 0;
+    if (!h->screened || !h->scratch[36].p) return PSCL_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    int32_t c = 0;
+    HIP_TRY(hipMemcpy(&c, h->scratch[36].p, 4, hipMemcpyDeviceToHost));
+    *count = c;
+    return PSCL_OK;
+}
+
+int pscl_softplus_tails_device(pscl_handle* h, const double* d_v, int64_t n, double* d_exact, double* d_apx) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    if (n < 0) return fail(PSCL_EINVAL, "n must be >= 0");
+    if (n == 0) return PSCL_OK;
+    if (!d_v || !d_exact || !d_apx) return fail(PSCL_EINVAL, "d_v, d_exact and d_apx are required");
+    int rc = set_device(h);
+    if (rc) return rc;
+    hipError_t e = pscl_launch_softplus_tails(d_v, n, h->d_exp_table, d_exact, d_apx, h->stream);
+    if (e != hipSuccess) return fail(PSCL_EDEVICE, "softplus tails launch: %s", hipGetErrorString(e));
     return PSCL_OK;
 }
 

@@ -380,15 +380,34 @@ PSCL_HD double pscl_softplus_tail_bf(double v, const uint64_t* T) {
 /*
  * Bounded-error tail for the screening decoder (scl128_kernel<..., APX = true>):
  *     log1p(y) = 2 atanh(s) = 2 s sum_k s^(2k) / (2k + 1),  s = y / (2 + y) in [0, 1/3],
- * y = exp(-|v|) from the exact exp above.  The series is cut after k = 11: the omitted terms
- * are below (1/9)^12 / 25 * 9/8 = 1.6e-13 = 2^-42.5 of the sum, the division (reciprocal + two
- * Newton steps) and the Horner steps add a few 2^-53, so the result is within 2^-42 of
- * log1p(exp(-|v|)) relatively (tests/test_softplus_host.py checks 2^-41 on a dense grid).  With
- * positive increments every path metric then stays within 2^-41.5 of the exact metric
- * relatively (128 additions add at most 128 * 2^-53 more), far inside the screening margin
- * the kernel uses to decide whether an ordering is certain (PSCL_APX_ULPS).
+ * y = exp(-|v|) from the exact exp above.  The series is cut after PSCL_APX_TERMS terms
+ * (k = 0..11): the omitted terms are below (1/9)^12 / 25 * 9/8 = 1.6e-13 = 2^-42.5 of the sum,
+ * the division (device: reciprocal + two Newton steps) and the Horner steps add a few 2^-53,
+ * so the result is within 2^-42 of log1p(exp(-|v|)) relatively.  With positive increments
+ * every path metric then stays within 2^-41.5 of the exact metric relatively (128 additions
+ * add at most 128 * 2^-53 more): about 2^11.5 ulps, far inside the margin of PSCL_APX_ULPS ulps
+ * the kernel requires before it trusts an ordering (checked at compile time below).
+ * Tests: tests/test_softplus_host.py (host form, <= 2^12 ulps from the exact tail on a dense
+ * grid incl. the 708..745 underflow range) and tests/test_gpu_screening.py (the device form,
+ * through pscl_softplus_tails_device, same bound).
  */
 #define PSCL_APX_TERMS 12
+/* ordering margin of the screening decode, in ulps of the metrics' bit patterns */
+#ifndef PSCL_APX_ULPS
+#define PSCL_APX_ULPS 65536
+#endif
+#ifdef __cplusplus
+/* relative truncation error of the series after t terms: sum_{k>=t} (1/9)^k / (2k+1) */
+constexpr double pscl_apx_trunc_bound(int t) {
+    double p = 1.0;
+    for (int i = 0; i < t; ++i) p /= 9.0;
+    return p / (2 * t + 1) * 9.0 / 8.0;
+}
+/* truncation in ulps, x8 for the division, Horner and 128-term metric roundings, must stay
+ * within half the margin (the margin compares two metrics that can both be off) */
+static_assert(pscl_apx_trunc_bound(PSCL_APX_TERMS) * 9007199254740992.0 * 8.0 <= PSCL_APX_ULPS / 2.0,
+              "PSCL_APX_TERMS too small for the screening margin PSCL_APX_ULPS");
+#endif
 /* fma(a, w, c) for the Horner steps below as one VOP3 with the constant addend c in an SGPR
  * pair (PSCL_APX_FMA = 1) or a VGPR (= 2); left to the compiler (= 0) it picks v_fmac and first
  * copies the constant into the destination, one 64-bit move per step.  Same rounding either way. */
@@ -423,18 +442,10 @@ PSCL_HD double pscl_log1p_apx(double y) {
     const double s = y / (2.0 + y);
 #endif
     const double w = s * s;
-    double p = 1.0 / 23.0;
-    p = pscl_fma_h(p, w, 1.0 / 21.0);
-    p = pscl_fma_h(p, w, 1.0 / 19.0);
-    p = pscl_fma_h(p, w, 1.0 / 17.0);
-    p = pscl_fma_h(p, w, 1.0 / 15.0);
-    p = pscl_fma_h(p, w, 1.0 / 13.0);
-    p = pscl_fma_h(p, w, 1.0 / 11.0);
-    p = pscl_fma_h(p, w, 1.0 / 9.0);
-    p = pscl_fma_h(p, w, 1.0 / 7.0);
-    p = pscl_fma_h(p, w, 1.0 / 5.0);
-    p = pscl_fma_h(p, w, 1.0 / 3.0);
-    p = pscl_fma_h(p, w, 1.0);
+    /* Horner over k = PSCL_APX_TERMS-1 .. 0 of 1/(2k+1) */
+    double p = 1.0 / (2 * PSCL_APX_TERMS - 1);
+#pragma unroll
+    for (int k = PSCL_APX_TERMS - 2; k >= 0; --k) p = pscl_fma_h(p, w, 1.0 / (2 * k + 1));
     return (s + s) * p;
 }
 

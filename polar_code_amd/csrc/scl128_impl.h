@@ -128,9 +128,6 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 // APX: screening decode (plain decodes of the compiled-in codes): metric tails from the
 // bounded-error pscl_softplus_tail_apx; every ordering decision must clear a margin of
 // PSCL_APX_ULPS ulps, else the frame is appended to P.amb_list for an exact re-decode.
-#ifndef PSCL_APX_ULPS
-#define PSCL_APX_ULPS 65536
-#endif
 template <int LMAX, bool HIST, bool CH, bool FS, int CODE, bool APX = false>
 __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU) scl128_kernel(const pscl_decode_params P) {
     using Ly = Layout128<LMAX, CH>;

@@ -52,6 +52,8 @@ struct pscl_decode_params {
     int64_t* amb_list;           // [B] frame indices to re-decode exactly
     int32_t* amb_count;
     int out_by_row;              // 1: outputs, reference words and counts at LLR row fidx[b]
+    int64_t grid_cap;            // 0, or an upper bound on the workgroups of the launch (the
+                                 // kernels stride over frames; a d_count launch of few frames)
 };
 
 // Decision-LLR replay (dlscl.hip): leaf LLRs of a known path, recomputed top-down
@@ -127,6 +129,8 @@ hipError_t pscl_launch_dl_gather(const uint64_t* best, const int64_t* act, const
                                  uint64_t* ref, hipStream_t s);
 hipError_t pscl_launch_iota64(int64_t* out, int64_t n, hipStream_t s);
 hipError_t pscl_launch_replay(const pscl_replay_params& R, int64_t cap, hipStream_t s);
+hipError_t pscl_launch_softplus_tails(const double* v, int64_t n, const uint64_t* exp_table, double* exact,
+                                     double* apx, hipStream_t s);
 hipError_t pscl_launch_dl_count(const uint64_t* best, const uint8_t* flags, const uint64_t* ref, int64_t B, int W,
                                 int k_payload, int64_t* counters, hipStream_t s);
 

@@ -462,7 +462,7 @@ int pscl_decode_lmax(int L) {
 int64_t pscl_decode_grid(const pscl_decode_params& P) {
     const int per_wg = pscl_decode_wpg(P) * (32 / pscl_decode_lmax(P.L));  // frames per workgroup
     int64_t g = (P.B + per_wg - 1) / per_wg;
-    const int64_t cap = 1 << 20;
+    const int64_t cap = P.grid_cap > 0 && P.grid_cap < (1 << 20) ? P.grid_cap : (1 << 20);
     return g < 1 ? 1 : (g > cap ? cap : g);
 }
 
@@ -550,6 +550,28 @@ __global__ void __launch_bounds__(256) uncoded_kernel(const pscl_channel_params 
 
 hipError_t pscl_launch_uncoded(const pscl_channel_params& P, int64_t* counters, hipStream_t s) {
     hipLaunchKernelGGL(uncoded_kernel, dim3((unsigned)((P.B + 255) / 256)), dim3(256), 0, s, P, counters);
+    return hipGetLastError();
+}
+
+// diagnostic: both metric-tail evaluations of the decode kernels on n values
+__global__ void __launch_bounds__(256) softplus_tails_kernel(const double* v, int64_t n, const uint64_t* exp_table,
+                                                              double* exact, double* apx) {
+    __shared__ uint64_t T[PSCL_EXP_TABLE_WORDS];
+    for (int i = threadIdx.x; i < PSCL_EXP_TABLE_WORDS; i += blockDim.x) T[i] = exp_table[i];
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double x = v[i];
+        exact[i] = pscl_softplus_tail_bf(x, T);
+        apx[i] = pscl_softplus_tail_apx(x, T);
+    }
+}
+
+hipError_t pscl_launch_softplus_tails(const double* v, int64_t n, const uint64_t* exp_table, double* exact,
+                                     double* apx, hipStream_t s) {
+    int64_t grid = (n + 255) / 256;
+    if (grid > 4096) grid = 4096;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(softplus_tails_kernel, dim3((unsigned)grid), dim3(256), 0, s, v, n, exp_table, exact, apx);
     return hipGetLastError();
 }
 

@@ -25,6 +25,16 @@ class Context:
     def is_root(self) -> bool:
         return self.rank == 0
 
+    @property
+    def device(self) -> int:
+        """GPU of this rank: its local rank (one process per GPU).  PSCL_SHARE_GPU=1 (one-GPU
+        rehearsals of the multi-rank path, gloo backend) folds the ranks onto the visible GPUs."""
+        if os.environ.get("PSCL_SHARE_GPU") == "1":
+            from . import _native
+
+            return self.local_rank % max(_native.device_count(), 1)
+        return self.local_rank
+
 
 _CTX: Context | None = None
 
@@ -42,8 +52,8 @@ def init(backend: str | None = None) -> Context:
         import torch
         import torch.distributed as dist
 
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend is None:  # PSCL_DIST_BACKEND overrides (gloo rehearsals on a shared GPU)
+            backend = os.environ.get("PSCL_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if not dist.is_initialized():
             if backend == "nccl":
                 torch.cuda.set_device(local)

@@ -57,32 +57,58 @@ def noise_params(snr_db: float, rate: float) -> Tuple[float, float, float, float
     return var_c, math.sqrt(var_c), var_u, math.sqrt(var_u)
 
 
+class ReplayStream:
+    """The reference's per-SNR stream default_rng(seed + int(snr*10)) (run_fer_sweep.py:61),
+    drawn in its order per frame: integers(0,2,payload) -> normal(0,sigma,N) ->
+    [normal(0,sigma_u,payload)] (:79-87, :111-113).  One generator per sweep point, advanced
+    block by block: frames [start, stop) cost O(stop - position) draws, so a whole point costs
+    O(frames) (a rank of a sharded run still draws past the frames of the ranks before it:
+    ziggurat normals consume a variable number of words, the stream cannot jump)."""
+
+    def __init__(self, seed: int, snr_db: float, payload_bits: int, crc_poly: str, include_uncoded: bool):
+        cfg = config.get_config()
+        self.N = cfg.N
+        self.seed, self.snr_db = seed, snr_db
+        self.payload_bits, self.crc_poly, self.include_uncoded = payload_bits, crc_poly, include_uncoded
+        self.var_c, self.sig_c, self.var_u, self.sig_u = noise_params(snr_db, cfg.K / cfg.N)
+        self._restart()
+
+    def _restart(self) -> None:
+        self.rng = np.random.default_rng(self.seed + int(self.snr_db * 10))
+        self.pos = 0
+
+    def _draw(self):
+        p = self.rng.integers(0, 2, size=self.payload_bits, dtype=np.int8)
+        z = self.rng.normal(0.0, self.sig_c, size=self.N)
+        zu = self.rng.normal(0.0, self.sig_u, size=self.payload_bits) if self.include_uncoded else None
+        self.pos += 1
+        return p, z, zu
+
+    def take(self, start: int, stop: int):
+        """(payload, msg, llr, llr_unc) of frames [start, stop); blocks in increasing order
+        continue the stream, an earlier start restarts it."""
+        if start < self.pos:
+            self._restart()
+        while self.pos < start:
+            self._draw()
+        n = stop - start
+        payload = np.empty((n, self.payload_bits), np.int8)
+        noise = np.empty((n, self.N))
+        unc = np.empty((n, self.payload_bits)) if self.include_uncoded else None
+        for i in range(n):
+            payload[i], noise[i], zu = self._draw()
+            if self.include_uncoded:
+                unc[i] = zu
+        msg = attach_crc(payload, self.crc_poly)
+        llr = 2.0 * (_bpsk(encode(msg)) + noise) / self.var_c
+        llr_unc = 2.0 * (_bpsk(payload) + unc) / self.var_u if self.include_uncoded else None
+        return payload, msg, llr, llr_unc
+
+
 def replay_stream(seed: int, snr_db: float, start: int, stop: int, payload_bits: int, crc_poly: str,
                   include_uncoded: bool):
-    """Frames [start, stop) of the reference's per-SNR stream default_rng(seed + int(snr*10)),
-    drawn in its order: integers(0,2,payload) -> normal(0,sigma,N) -> [normal(0,sigma_u,payload)]."""
-    cfg = config.get_config()
-    rng = np.random.default_rng(seed + int(snr_db * 10))
-    var_c, sig_c, var_u, sig_u = noise_params(snr_db, cfg.K / cfg.N)
-    n = stop - start
-    payload = np.empty((n, payload_bits), np.int8)
-    noise = np.empty((n, cfg.N))
-    unc = np.empty((n, payload_bits)) if include_uncoded else None
-    for fr in range(stop):
-        p = rng.integers(0, 2, size=payload_bits, dtype=np.int8)
-        z = rng.normal(0.0, sig_c, size=cfg.N)
-        zu = rng.normal(0.0, sig_u, size=payload_bits) if include_uncoded else None
-        if fr >= start:
-            payload[fr - start], noise[fr - start] = p, z
-            if include_uncoded:
-                unc[fr - start] = zu
-    msg = attach_crc(payload, crc_poly)
-    code = encode(msg)
-    llr = 2.0 * (_bpsk(code) + noise) / var_c
-    llr_unc = None
-    if include_uncoded:
-        llr_unc = 2.0 * (_bpsk(payload) + unc) / var_u
-    return payload, msg, llr, llr_unc
+    """Frames [start, stop) of the reference's per-SNR stream (a fresh ReplayStream)."""
+    return ReplayStream(seed, snr_db, payload_bits, crc_poly, include_uncoded).take(start, stop)
 
 
 def scl_batch(llr, info_set, M, crc, device):
@@ -208,7 +234,7 @@ def run_sweep(args: argparse.Namespace) -> List[Dict[str, float]]:
     cfg = config.get_config()
     seed_all(args.seed)
     ctx = dist.init()
-    device = ctx.local_rank
+    device = ctx.device
     info_set = construct_info_set(cfg.N, cfg.K)
     payload_bits = cfg.K - cfg.crc_bits
     snr_points = (np.arange(args.snr_lo, args.snr_hi + 1e-9, args.snr_step) if args.snr_step > 0
@@ -221,9 +247,9 @@ def run_sweep(args: argparse.Namespace) -> List[Dict[str, float]]:
         start, stop = dist.shard(args.frames, ctx.rank, ctx.world)
         blocks = [(b0, min(stop, b0 + args.batch)) for b0 in range(start, stop, args.batch)]
         if args.rng == "replay":
+            stream = ReplayStream(args.seed, float(snr_db), payload_bits, cfg.crc_poly, args.include_uncoded)
             for b0, b1 in blocks:
-                payload, msg, llr, llr_unc = replay_stream(args.seed, float(snr_db), b0, b1, payload_bits,
-                                                           cfg.crc_poly, args.include_uncoded)
+                payload, msg, llr, llr_unc = stream.take(b0, b1)
                 _count_block(c, msg, llr, payload, llr_unc, info_set, args.M, cfg.crc_poly, args.retries, beta, device,
                              args.dl_engine)
         else:

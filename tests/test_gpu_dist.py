@@ -1,0 +1,76 @@
+"""GPU rehearsal of the multi-rank product path on one MI355X.
+
+Two fresh child processes (subprocess, never an exec of the test process) share the GPU
+(PSCL_SHARE_GPU=1) and talk over gloo: the same sharding and counter all-reduces as the
+RCCL runs on an 8-GPU node, with the Philox channel and the device DL-SCL retry loop.
+  (a) run_fer_sweep --rng philox --dl_engine device at world 2 writes the same CSV as world 1;
+  (b) bench.py at world 2 counts 2*B*steps frames and the same frame errors as world 1 over
+      the same global frame range.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch(world, argv, timeout=240):
+    """world ranks of `python argv...` with torchrun's environment; returns their stdouts."""
+    port = _port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), PSCL_SHARE_GPU="1", PSCL_DIST_BACKEND="gloo",
+                   PYTHONPATH=str(ROOT) + os.pathsep + os.environ.get("PYTHONPATH", ""))
+        procs.append(subprocess.Popen([sys.executable, *argv], cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=timeout)
+            outs.append(out)
+            assert p.returncode == 0, out[-3000:]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return outs
+
+
+def test_fer_sweep_philox_world2_equals_world1(tmp_path):
+    args = ["-m", "polar_code_amd.eval.run_fer_sweep", "--M", "4", "--frames", "120001", "--snr_lo", "3.5",
+            "--snr_hi", "4.5", "--snr_step", "0.5", "--retries", "8", "--beta", str(GOLDEN / "beta_M4.npy"),
+            "--rng", "philox", "--dl_engine", "device", "--batch", "40000", "--include_uncoded", "--no_plot"]
+    csv = {}
+    for world in (1, 2):
+        d = tmp_path / f"w{world}"
+        _launch(world, args + ["--out_dir", str(d), "--plot_dir", str(d)])
+        csv[world] = (d / "fer_M4.csv").read_text()
+    assert csv[1] == csv[2] and csv[1].count("\n") == 4
+
+
+def test_bench_world2_counts_every_frame_once():
+    B = 50_000
+    base = ["bench.py", "--frames", str(B), "--warmup", "1", "--no-cpu-baseline", "--extra", "none"]
+    line = {}
+    for world, steps in ((1, 4), (2, 2)):  # the same global frames [0, 4B): rank r owns [2rB, 2rB + 2B)
+        out = _launch(world, base + ["--steps", str(steps), "--gpus", str(world)])
+        line[world] = json.loads([x for x in out[0].splitlines() if x.startswith("{")][-1])
+    assert line[2]["n_gpus"] == 2 and line[2]["fer"]["frames"] == 2 * B * 2
+    assert line[1]["fer"]["frames"] == 4 * B
+    for k in ("frame_errors", "ber", "payload_fer", "payload_ber"):
+        assert line[1]["fer"][k] == line[2]["fer"][k], k

@@ -49,7 +49,7 @@ def test_screening_equals_exact_awgn(M):
     _assert_same(_plain(scr, llr), _plain(ex, llr), f"M={M}")
 
 
-@pytest.mark.parametrize("M", [2, 4, 8])
+@pytest.mark.parametrize("M", [1, 2, 4, 8])
 def test_screening_ties_defer_to_exact(M):
     """Integer-valued and noiseless LLRs: exact metric ties are common, so many frames must be
     deferred; the results still equal the exact kernel's and the oracle's."""
@@ -113,3 +113,48 @@ def test_screening_device_counters_equal_exact():
     for i, k in enumerate(("best", "flags", "counters")):
         np.testing.assert_array_equal(out[True][i], out[False][i], err_msg=k)
     assert out[True][2][0] == B
+
+
+@pytest.mark.parametrize("M", [1, 2, 4, 8])
+def test_screening_boundary_ties_every_frame(M):
+    """Crafted worst cases for the screening pass: exactly zero leaf LLRs (every child pays
+    LOGE2: equal child metrics straddle list position L at every full-list info phase, and
+    ds_permute leaves positions unclaimed) and sparse zeros among small integers.  Every such
+    frame must be handed to the exact re-decode (count > 0) and every frame must equal the oracle."""
+    rng = np.random.default_rng(7400 + M)
+    info = construct_info_set(128, 64)
+    B = 384
+    llr = rng.integers(-3, 4, size=(B, 128)).astype(np.float64)
+    llr[: B // 4] = 0.0                                           # all leaves exactly zero
+    llr[B // 4: B // 2] *= rng.random((B // 4, 128)) < 0.5        # half the channel LLRs zero
+    llr[B // 2: 3 * B // 4, :64] = 0.0                            # zero left half: zero depth-1 f outputs
+    scr, ex = _pair(128, info, M)
+    a = _plain(scr, llr)
+    assert scr.screening_count() >= B // 4
+    _assert_same(a, _plain(ex, llr), f"boundary ties M={M}")
+    for f in range(B):
+        n, c, m, il, b = oracle.decode_scl(llr[f], info, M, crc=POLY)
+        assert a["n_paths"][f] == n and a["best_idx"][f] == b, f
+        np.testing.assert_array_equal(a["best_bits"][f], c[b], err_msg=f"f={f}")
+        assert bool(a["crc_pass"][f]) == oracle.check_crc(c[b], POLY), f
+
+
+def test_screening_tail_within_bound_device():
+    """The device forms of both metric tails (pscl_softplus_tails_device): the exact one is
+    bit-identical to the host port (itself bit-identical to libm, test_softplus_host.py), the
+    screening one -- reciprocal + Newton division, SGPR-addend Horner FMAs -- stays within 2^12
+    ulps of it, 16x inside the kernel's 2^16-ulp ordering margin."""
+    import ctypes as C
+
+    from test_softplus_host import _lib, apx_grid, ulp_distance
+
+    v = apx_grid()
+    dec = _native.Decoder(128, construct_info_set(128, 64), 8, POLY)
+    ex_d, ap_d = dec.softplus_tails(v)
+    ex_h, ap_h = np.empty_like(v), np.empty_like(v)
+    L = _lib()
+    L.softplus_tails_batch.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
+    L.softplus_tails_batch(v.ctypes.data, v.size, ex_h.ctypes.data, ap_h.ctypes.data)
+    np.testing.assert_array_equal(ex_d.view(np.int64), ex_h.view(np.int64))
+    d = ulp_distance(ex_d, ap_d)
+    assert d.max() <= 2 ** 12, (d.max(), v[d.argmax()])

@@ -43,6 +43,38 @@ def test_oracle_reproduces_reference_scl_row(M):
     assert f"{np.count_nonzero(bits != msg) / msg.size:.6e}" == row["ber_scl"]
 
 
+def test_oracle_reproduces_reference_m1_csv():
+    """BASELINE config 1 (SC, M=1): results/fer_M1.csv -- seed 0, 3000 frames per point,
+    4.5..6.0 dB, --include_uncoded, 8 retries with checkpoints/beta_M1.npy -- every column of
+    every row, from the replayed stream and the oracle."""
+    lines = (GOLDEN / "ref_fer_M1.csv").read_text().splitlines()
+    info = construct_info_set(128, 64)
+    beta = np.load(GOLDEN / "beta_M1.npy", allow_pickle=False)
+    got = [lines[0]]
+    for snr in (4.5, 5.0, 5.5, 6.0):
+        payload, msg, llr, llr_unc = replay_stream(0, snr, 0, 3000, 40, "0x1864CFB", True)
+        errs = np.count_nonzero((llr_unc < 0).astype(np.int8) != payload, axis=1)
+        bits, ok = oracle.decode_batch(llr, info, 1, "0x1864CFB")
+        dbits, dok, _ = oracle.dl_batch(llr, info, 1, 8, "0x1864CFB", beta)
+        vals = [np.count_nonzero(errs) / 3000, errs.sum() / payload.size, np.count_nonzero(~ok) / 3000,
+                np.count_nonzero(bits != msg) / msg.size, np.count_nonzero(~dok) / 3000,
+                np.count_nonzero(dbits != msg) / msg.size]
+        got.append(",".join([f"{snr:.3f}"] + [f"{v:.6e}" for v in vals]))
+    assert got == lines
+
+
+def test_replay_stream_blocks_continue_the_stream():
+    from polar_code_amd.eval.run_fer_sweep import ReplayStream
+
+    whole = replay_stream(0, 5.5, 0, 500, 40, "0x1864CFB", True)
+    s = ReplayStream(0, 5.5, 40, "0x1864CFB", True)
+    parts = [s.take(0, 130), s.take(130, 131), s.take(131, 500)]
+    assert s.pos == 500
+    for k in range(4):
+        np.testing.assert_array_equal(whole[k], np.concatenate([p[k] for p in parts]))
+    np.testing.assert_array_equal(s.take(10, 20)[2], whole[2][10:20])  # an earlier block restarts
+
+
 def test_oracle_reproduces_reference_dl_row():
     M = 8
     payload, msg, llr, _ = replay_stream(0, 5.0, 0, 2000, 40, "0x1864CFB", True)

@@ -43,3 +43,31 @@ def test_port_matches_numpy_logaddexp():
     _lib().softplus_port_batch(v.ctypes.data, v.size, out.ctypes.data)
     ref = np.array([float(np.logaddexp(0.0, float(x))) for x in v])
     np.testing.assert_array_equal(out.view(np.int64), ref.view(np.int64))
+
+
+def apx_grid():
+    """|v| grid for the screening tail: dense over the decoder's working range, the 708..745
+    range where exp(-|v|) goes subnormal, tiny and huge magnitudes, both signs."""
+    parts = [np.arange(0.0, 40.0, 1e-4), np.arange(708.0, 745.2, 1e-3), 2.0 ** -np.arange(0.0, 80.0, 0.25),
+             np.array([745.13, 745.14, 745.2, 746.0, 800.0, 1e3, 1e6, 2 ** -1074])]
+    v = np.concatenate(parts)
+    return np.ascontiguousarray(np.concatenate([v, -v[::7]]))
+
+
+def ulp_distance(a, b):
+    """|a - b| in ulps of the (non-negative) tails' bit patterns."""
+    return np.abs(a.view(np.int64) - b.view(np.int64))
+
+
+def test_screening_tail_within_bound_host():
+    """The bounded-error tail (pscl_softplus_tail_apx, host form: correctly rounded division)
+    stays within 2^12 ulps of the exact tail -- a 16x guard below the kernel's 2^16-ulp
+    ordering margin (glibc_softplus.h static_assert)."""
+    v = apx_grid()
+    ex, ap = np.empty_like(v), np.empty_like(v)
+    L = _lib()
+    L.softplus_tails_batch.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
+    L.softplus_tails_batch(v.ctypes.data, v.size, ex.ctypes.data, ap.ctypes.data)
+    assert np.all(ex >= 0) and np.all(ap >= 0)
+    d = ulp_distance(ex, ap)
+    assert d.max() <= 2 ** 12, (d.max(), v[d.argmax()])

@@ -1,6 +1,6 @@
 """Summarise rocprofv3 PMC passes (tools/profile_pmc.sh output) for the decode kernel.
 
-    python tools/pmc_summary.py gpurun_out/pmc_<tag> [frames_per_launch]
+    python tools/pmc_summary.py gpurun_out/pmc_<tag> [frames_per_launch] [--json] [--write KEY]
 
 Prints per-launch averages and derived figures, and (with --json) the HBM traffic entry
 bench.py reads from profiles/pmc_traffic.json.  Corrections follow MI355X_MICROARCH.md
@@ -66,8 +66,27 @@ def main():
         out["valu_mix_per_frame"] = mix
     if "SQ_LDS_BANK_CONFLICT" in c:
         out["lds_bank_conflict_cycles"] = c["SQ_LDS_BANK_CONFLICT"]
+    for k in ("SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES"):
+        if k in c:
+            out[k.lower()] = c[k]
+    if "GRBM_GUI_ACTIVE" in c:
+        out["grbm_gui_active"] = c["GRBM_GUI_ACTIVE"]
+    # the library the passes ran (its embedded source hash): bench.py only uses an entry
+    # measured on the build it times
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    from polar_code_amd import build
+
+    out["build_hash"] = build.library_hash()
+    out["source"] = f"{d}: rocprofv3 --pmc passes (tools/profile_pmc.sh), one counter group per pass"
     if "--json" in sys.argv:
         print(json.dumps(out))
+    if "--write" in sys.argv:
+        key = sys.argv[sys.argv.index("--write") + 1]
+        p = Path(__file__).resolve().parent.parent / "profiles" / "pmc_traffic.json"
+        db = json.loads(p.read_text()) if p.exists() else {}
+        db[key] = out
+        p.write_text(json.dumps(db, indent=1, sort_keys=True) + "\n")
+        print(f"wrote {key} to {p}")
 
 
 if __name__ == "__main__":

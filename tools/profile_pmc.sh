@@ -13,5 +13,5 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INS
            "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_ACTIVE_INST_VALU2"; do
     i=$((i+1))
     timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$out/p$i" -o pmc -- \
-        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > "$out/p$i.log" 2>&1 || { echo "pass $i failed"; exit 1; }
+        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --extra none "$@" > "$out/p$i.log" 2>&1 || { echo "pass $i failed"; exit 1; }
 done
