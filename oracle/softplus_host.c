@@ -56,6 +56,6 @@ int64_t log1p_unit_compare(const double* y, int64_t n) {
 void softplus_tails_batch(const double* v, int64_t n, double* exact, double* apx) {
     for (int64_t i = 0; i < n; i++) {
         exact[i] = pscl_softplus_tail_bf(v[i], kT);
-        apx[i] = pscl_softplus_tail_apx(v[i], kT);
+        apx[i] = pscl_softplus_tail_scr(v[i]);
     }
 }

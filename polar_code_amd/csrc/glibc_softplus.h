@@ -378,79 +378,82 @@ PSCL_HD double pscl_softplus_tail_bf(double v, const uint64_t* T) {
 }
 
 /*
- * Bounded-error tail for the screening decoder (scl128_kernel<..., APX = true>):
- *     log1p(y) = 2 atanh(s) = 2 s sum_k s^(2k) / (2k + 1),  s = y / (2 + y) in [0, 1/3],
- * y = exp(-|v|) from the exact exp above.  The series is cut after PSCL_APX_TERMS terms
- * (k = 0..11): the omitted terms are below (1/9)^12 / 25 * 9/8 = 1.6e-13 = 2^-42.5 of the sum,
- * the division (device: reciprocal + two Newton steps) and the Horner steps add a few 2^-53,
- * so the result is within 2^-42 of log1p(exp(-|v|)) relatively.  With positive increments
- * every path metric then stays within 2^-41.5 of the exact metric relatively (128 additions
- * add at most 128 * 2^-53 more): about 2^11.5 ulps, far inside the margin of PSCL_APX_ULPS ulps
- * the kernel requires before it trusts an ordering (checked at compile time below).
- * Tests: tests/test_softplus_host.py (host form, <= 2^12 ulps from the exact tail on a dense
- * grid incl. the 708..745 underflow range) and tests/test_gpu_screening.py (the device form,
- * through pscl_softplus_tails_device, same bound).
+ * Screening tail for scl128_kernel<..., APX = true>: L = log1p(exp(-x)), x = |v|, to a proven
+ * relative error below PSCL_SCR_EPS = 6 * 2^-23 (about 2^-20.4), mostly in fp32:
+ *
+ *   k = round(x / ln2), r = x - k ln2 (fp64, Cody-Waite: |r| <= ln2/2, error < 2^-55)
+ *   u = e^-r = 2^(-r log2 e)             fp32: cvt + mul + v_exp_f32, u in [0.7, 1.42]
+ *   t = u 2^-k = e^-x                    fp32 ldexp (exact while normal; tiny t only feeds s)
+ *   log1p(t) = 2 atanh(s), s = t/(2 + t) in [0, 1/3]:
+ *   log1p(t) = 2 s P(s^2) = 2^-k * [u * rcp(2 + t) * 2P(s^2)]     (P: 7 terms, fp32 Horner)
+ *   L = ldexp((double)q, -k), q = u * rcp(2 + t) * 2P(s^2)
+ *
+ * Relative error of q, in units of 2^-23 (v_exp_f32 and v_rcp_f32 within 1 ulp, roundings
+ * 2^-24 each): u 1.39 (exp 1, r rounding to fp32 0.09, product with log2 e 0.18, constant
+ * 0.12), rcp 1 + its argument 0.5 + t's error through 2 + t 0.46, P 1.45 (Horner roundings
+ * 0.56, coefficients 0.56, truncation (1/9)^7/15*9/8 = 0.13, s^2 error x dP/dw 0.2), the two
+ * products 1: 5.8 < 6.  The final cvt and ldexp are exact (until fp64 underflow, where the
+ * exact tail is subnormal too: then the error is at most one ulp of the result).  x is
+ * clamped to 4096 (the exact tail is 0 above ~745.2; the clamp keeps k in int range).
+ *
+ * With positive increments every screening path metric is within PSCL_SCR_EPS + 2^-52 of
+ * the exact metric relatively, and the kernel trusts an ordering of two metrics only when
+ * their high words (sign, exponent, 20 mantissa bits) differ by more than PSCL_SCR_H: then
+ * the larger exceeds the smaller by at least PSCL_SCR_H * 2^-21 relatively (one high-word
+ * unit is 2^-21..2^-20 of the value), which must beat the 2 * (PSCL_SCR_EPS + 2^-52) the two
+ * errors can close -- checked at compile time below.  Tests: tests/test_softplus_host.py
+ * (host form) and tests/test_gpu_screening.py (device form, pscl_softplus_tails_device).
  */
-#define PSCL_APX_TERMS 12
-/* ordering margin of the screening decode, in ulps of the metrics' bit patterns */
-#ifndef PSCL_APX_ULPS
-#define PSCL_APX_ULPS 65536
+#define PSCL_SCR_TERMS 7
+#define PSCL_SCR_EPS (6.0 / 8388608.0)
+#ifndef PSCL_SCR_H
+#define PSCL_SCR_H 16
 #endif
 #ifdef __cplusplus
-/* relative truncation error of the series after t terms: sum_{k>=t} (1/9)^k / (2k+1) */
-constexpr double pscl_apx_trunc_bound(int t) {
-    double p = 1.0;
-    for (int i = 0; i < t; ++i) p /= 9.0;
-    return p / (2 * t + 1) * 9.0 / 8.0;
-}
-/* truncation in ulps, x8 for the division, Horner and 128-term metric roundings, must stay
- * within half the margin (the margin compares two metrics that can both be off) */
-static_assert(pscl_apx_trunc_bound(PSCL_APX_TERMS) * 9007199254740992.0 * 8.0 <= PSCL_APX_ULPS / 2.0,
-              "PSCL_APX_TERMS too small for the screening margin PSCL_APX_ULPS");
+static_assert(PSCL_SCR_H / 2097152.0 >= 4.0 * (PSCL_SCR_EPS + 2.220446049250313e-16),
+              "screening margin PSCL_SCR_H does not cover twice the metric error (with 2x safety)");
 #endif
-/* fma(a, w, c) for the Horner steps below as one VOP3 with the constant addend c in an SGPR
- * pair (PSCL_APX_FMA = 1) or a VGPR (= 2); left to the compiler (= 0) it picks v_fmac and first
- * copies the constant into the destination, one 64-bit move per step.  Same rounding either way. */
-#ifndef PSCL_APX_FMA
-#define PSCL_APX_FMA 1
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && PSCL_APX_FMA == 1
-__device__ __forceinline__ double pscl_fma_h(double a, double b, double c) {
-    double d;
-    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
-    return d;
-}
-#elif defined(__HIP_DEVICE_COMPILE__) && PSCL_APX_FMA == 2
-__device__ __forceinline__ double pscl_fma_h(double a, double b, double c) {
-    double d;
-    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-    return d;
-}
-#else
-#define pscl_fma_h(a, b, c) pscl_fma((a), (b), (c))
-#endif
-PSCL_HD double pscl_log1p_apx(double y) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    const double d = 2.0 + y;
-    double r = __builtin_amdgcn_rcp(d);
-    double e = __builtin_fma(-d, r, 1.0);
-    r = __builtin_fma(r, e, r);
-    e = __builtin_fma(-d, r, 1.0);
-    r = __builtin_fma(r, e, r);
-    const double s = y * r;
-#else
-    const double s = y / (2.0 + y);
-#endif
-    const double w = s * s;
-    /* Horner over k = PSCL_APX_TERMS-1 .. 0 of 1/(2k+1) */
-    double p = 1.0 / (2 * PSCL_APX_TERMS - 1);
-#pragma unroll
-    for (int k = PSCL_APX_TERMS - 2; k >= 0; --k) p = pscl_fma_h(p, w, 1.0 / (2 * k + 1));
-    return (s + s) * p;
-}
+#define PSCL_LN2HI 6.93147180369123816490e-01 /* 32 trailing zero bits: k * LN2HI exact */
+#define PSCL_LN2LO 1.90821492927058770002e-10
+#define PSCL_INVLN2 0x1.71547652b82fep0
+#define PSCL_LOG2E_F 1.44269504088896341f
 
-PSCL_HD double pscl_softplus_tail_apx(double v, const uint64_t* T) {
-    return pscl_log1p_apx(pscl_exp_negabs(v, T));
+#if defined(__HIP_DEVICE_COMPILE__)
+/* min(|v|, c): one v_min_f64 with the magnitude as a source modifier (fmin would add
+ * canonicalising maxes for signalling NaNs) */
+__device__ __forceinline__ double pscl_absmin(double v, double c) {
+    double d;
+    asm("v_min_f64 %0, |%1|, %2" : "=v"(d) : "v"(v), "s"(c));
+    return d;
+}
+__device__ __forceinline__ float pscl_exp2_f32(float a) { return __builtin_amdgcn_exp2f(a); }
+__device__ __forceinline__ float pscl_rcp_f32(float a) { return __builtin_amdgcn_rcpf(a); }
+__device__ __forceinline__ double pscl_ldexp_f64(double a, int e) { return __builtin_amdgcn_ldexp(a, e); }
+#else
+#define pscl_absmin(v, c) (fabs(v) < (c) ? fabs(v) : (c))
+#define pscl_exp2_f32(a) exp2f(a)
+#define pscl_rcp_f32(a) (1.0f / (a))
+#define pscl_ldexp_f64(a, e) ldexp((a), (e))
+#endif
+
+PSCL_HD double pscl_softplus_tail_scr(double v) {
+    const double x = pscl_absmin(v, 4096.0);
+    const double kd0 = pscl_fma(-x, PSCL_INVLN2, PSCL_EXP_SHIFT); /* low word = -k */
+    const int32_t nk = (int32_t)(uint32_t)pscl_asu64(kd0);
+    const double kd = kd0 - PSCL_EXP_SHIFT;                      /* -k */
+    double r = pscl_fma(kd, -PSCL_LN2HI, -x);                   /* -x + k ln2 = -r */
+    r = pscl_fma(kd, -PSCL_LN2LO, r);
+    const float u = pscl_exp2_f32((float)r * PSCL_LOG2E_F);     /* e^-r */
+    const float t = ldexpf(u, nk);                               /* e^-x */
+    const float rc = pscl_rcp_f32(2.0f + t);
+    const float s = t * rc;
+    const float w = s * s;
+    /* 2 P(w) = sum_i 2 w^i / (2i + 1), i < PSCL_SCR_TERMS, Horner */
+    float p = 2.0f / (2 * PSCL_SCR_TERMS - 1);
+#pragma unroll
+    for (int i = PSCL_SCR_TERMS - 2; i >= 0; --i) p = fmaf(p, w, 2.0f / (2 * i + 1));
+    const float q = (u * rc) * p;
+    return pscl_ldexp_f64((double)q, nk);
 }
 
 /* L = log1p(exp(-|v|)), the part of logaddexp(0, +-v) shared by both bit hypotheses. */

@@ -126,8 +126,9 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 // FS: the launch may carry forced bits or SC hard decisions (P.force / P.sc_hard).  Without
 // them (every plain SCL decode) the per-frame force words and their tests compile away.
 // APX: screening decode (plain decodes of the compiled-in codes): metric tails from the
-// bounded-error pscl_softplus_tail_apx; every ordering decision must clear a margin of
-// PSCL_APX_ULPS ulps, else the frame is appended to P.amb_list for an exact re-decode.
+// bounded-error pscl_softplus_tail_scr; every ordering decision is made on the metrics' high
+// words and must clear a margin of PSCL_SCR_H units (glibc_softplus.h: proven to exceed twice
+// the metric error), else the frame is appended to P.amb_list for an exact re-decode.
 template <int LMAX, bool HIST, bool CH, bool FS, int CODE, bool APX = false>
 __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU) scl128_kernel(const pscl_decode_params P) {
     using Ly = Layout128<LMAX, CH>;
@@ -213,8 +214,10 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
         constexpr uint64_t KPATH = group_prefix_mask<G>(LMAX), KGE1 = ~group_prefix_mask<G>(1);
         const uint64_t LMASK = group_prefix_mask<G>(L);
         uint64_t amb = 0;  // APX: lanes that saw an ordering closer than the margin
-        // (b - a, as signed 64-bit on the metrics' bit patterns) <= margin: a < b not certain
-        auto near_or_below = [](uint64_t a, uint64_t b) { return (int64_t)(b - a) <= (int64_t)PSCL_APX_ULPS; };
+        // high words of two metrics (non-negative doubles: the words order like the values):
+        // b - a <= margin, a < b not certain
+        auto near_or_below = [](uint32_t a, uint32_t b) { return (int32_t)(b - a) <= (int32_t)PSCL_SCR_H; };
+        auto hiw = [](double m) { return (uint32_t)(pscl_asu64(m) >> 32); };
 
         // phase body, specialised on t = phi mod 16 (the subtree shape of the phase is fixed by
         // t); blk = phi / 16 is a compile-time constant too in the CODE != 0 kernels
@@ -343,7 +346,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
             if (pre_ok) {
                 Lt = pscl_asf64(lpre_up);
             } else {
-                Lt = (PSCL_ABLATE & 1) ? lam * 0.5 : (APX ? pscl_softplus_tail_apx(lam, T) : pscl_softplus_tail_bf(lam, T));
+                Lt = (PSCL_ABLATE & 1) ? lam * 0.5 : (APX ? pscl_softplus_tail_scr(lam) : pscl_softplus_tail_bf(lam, T));
             }
             const bool frozen_even = !is_info && !(phi & 1);
             Lpre = Lt;
@@ -358,19 +361,15 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 // tie keys never act, so the list order in between does not matter -- only which
                 // children survive a full list (the boundary between the L-th and (L+1)-th
                 // smallest metric) and, at the end, the final order.  Paths stay in lanes
-                // 0..cnt-1 in any order; frozen phases only advance the metrics.
+                // 0..cnt-1 in any order; frozen phases only advance the metrics.  An exactly
+                // zero LLR needs no special case: both children get metric + tail(0) (= the
+                // exact LOGE2 within the tail's bound), a tie the margin tests catch.
                 if (!is_info) {
-                    double m0 = neg ? mbd : mgd;
-                    if (PSCL_RARE(lam == 0.0)) m0 = lam == 0.0 ? metric + PSCL_LOGE2 : m0;
-                    metric = m0;
+                    metric = neg ? mbd : mgd;
                     lastbit = 0;
                     return;
                 }
-                double m0 = neg ? mbd : mgd, m1 = neg ? mgd : mbd;  // bit-0 / bit-1 child
-                if (PSCL_RARE(lam == 0.0)) {
-                    m0 = lam == 0.0 ? metric + PSCL_LOGE2 : m0;
-                    m1 = lam == 0.0 ? metric + PSCL_LOGE2 : m1;
-                }
+                const double m0 = neg ? mbd : mgd, m1 = neg ? mgd : mbd;  // bit-0 / bit-1 child
                 const int ncnt = 2 * cnt < L ? 2 * cnt : L;
                 int src;
                 uint32_t b;
@@ -383,14 +382,15 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     nm = b ? pm1 : pscl_asu64(m0);
                 } else {
                     // full list: the better children survive when every worse child exceeds the
-                    // largest better child by the margin (group max over duplicated keys)
-                    double mx = pscl_asf64(merge_from_lower64<G, LMAX>(pscl_asu64(mgd), pscl_asu64(mgd), lane));
+                    // largest better child by the margin (group max of the high words over
+                    // duplicated keys)
+                    uint32_t mx = merge_from_lower<G, LMAX>(hiw(mgd), hiw(mgd), lane);
                     static_for<Ly::LOG_LM>([&](auto SC) {
                         constexpr int S = 1 << decltype(SC)::value;
-                        const double o = grot64c<G, S>(mx, lane);
-                        asm("v_max_f64 %0, %1, %2" : "=v"(mx) : "v"(mx), "v"(o));
+                        const uint32_t o = grot32c<G, S>(mx, lane);
+                        mx = o > mx ? o : mx;
                     });
-                    const uint64_t badm = wmask(lam == 0.0) | wmask(near_or_below(pscl_asu64(mx), pscl_asu64(mbd)));
+                    const uint64_t badm = wmask(near_or_below(mx, hiw(mbd)));
                     if ((badm & vmask & KPATH) == 0) {
                         const uint32_t gb = neg ? 1u : 0u;
                         metric = mgd;
@@ -401,18 +401,19 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                         ++j;
                         return;
                     }
-                    // rank the 2L children on the metric; lane r takes the child ranked r.  Each
-                    // position 0..L claimed exactly once and the L-th / (L+1)-th smallest apart by
-                    // the margin certify the survivor set (ties leave a position unclaimed).
+                    // rank the 2L children on the high words; lane r takes the child ranked r.
+                    // Each position 0..L claimed exactly once and the L-th / (L+1)-th smallest
+                    // apart by the margin certify the survivor set (ties leave a position unclaimed).
                     const uint64_t km = merge_from_lower64<G, LMAX>(pscl_asu64(m0), pscl_asu64(m1), lane);
                     uint32_t r = 0;
-                    rank_step_m<G, 1, G>((uint32_t)(km >> 32), (uint32_t)km, lane, r);
+                    rank_step_h<G, 1, G>((uint32_t)(km >> 32), lane, r);
                     const int c = __builtin_amdgcn_ds_permute((gbase + (int)(r & (G - 1))) << 2, g) & (G - 1);
                     const uint32_t rr = bperm32(r, gbase + c);
                     nm = shfl_u64(km, gbase + c);
                     const uint64_t claim = group_prefix_mask<G>(L + 1);
                     const uint64_t bnd = claim & ~group_prefix_mask<G>(L);
-                    amb |= ((wmask(rr != (uint32_t)g) & claim) | (wmask(near_or_below(prev_lane64(nm), nm)) & bnd)) & vmask;
+                    const uint32_t nmh = (uint32_t)(nm >> 32);
+                    amb |= ((wmask(rr != (uint32_t)g) & claim) | (wmask(near_or_below(prev_lane32(nmh), nmh)) & bnd)) & vmask;
                     src = gbase + (c & (LMAX - 1));
                     b = c >= LMAX ? 1u : 0u;
                 }
@@ -616,15 +617,15 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
             // certified by every position 0..cnt-1 claimed once and sorted neighbours apart by
             // the margin.  Upper lanes hold copies, rank among the same keys and push into the
             // upper half.
-            uint64_t km = g < cnt ? pscl_asu64(metric) : 0x7ff0000000000000ULL;
-            km = merge_from_lower64<G, LMAX>(km, km, lane);
+            uint32_t kh = g < cnt ? hiw(metric) : 0x7ff00000u;
+            kh = merge_from_lower<G, LMAX>(kh, kh, lane);
             uint32_t r = 0;
-            rank_step_m<G, 1, LMAX>((uint32_t)(km >> 32), (uint32_t)km, lane, r);
+            rank_step_h<G, 1, LMAX>(kh, lane, r);
             const int c = __builtin_amdgcn_ds_permute((gbase + (g & LMAX) + (int)(r & (LMAX - 1))) << 2, g) & (G - 1);
             const uint32_t rr = bperm32(r, gbase + c);
-            const uint64_t nm = shfl_u64(km, gbase + c);
+            const uint32_t nh = bperm32(kh, gbase + c);
             const uint64_t live = kFixedList ? group_prefix_mask<G>(cnt) : wmask(g < cnt);
-            amb |= ((wmask(rr != (uint32_t)g) & live) | (wmask(near_or_below(prev_lane64(nm), nm)) & live & KGE1)) & vmask;
+            amb |= ((wmask(rr != (uint32_t)g) & live) | (wmask(near_or_below(prev_lane32(nh), nh)) & live & KGE1)) & vmask;
             rank = r;
         }
         // APX: a frame with an uncertain ordering is handed to the exact re-decode

@@ -242,6 +242,48 @@ __device__ __forceinline__ void rank_step_m(uint32_t mh, uint32_t ml, int lane, 
     }
 }
 
+// Screening rank on 32-bit keys (the high words of the metrics): +1 for every key of the
+// group, rotations K .. KEND-1, strictly below this lane's.  16-lane groups: one DPP-fused
+// subtract (borrow = "that key is smaller") + one add-with-carry per rotation; FIRST carries
+// the s_nop that covers a VALU write of the key just before (inline asm is not hazard-checked;
+// the later rotations read the same, unchanged key register).
+template <int K, bool FIRST>
+__device__ __forceinline__ void rank_rot16_h(uint32_t h, uint32_t& r) {
+    uint32_t tmp;
+    if constexpr (FIRST)
+        asm volatile(
+            "s_nop 1\n\t"
+            "v_sub_co_u32_dpp %0, vcc, %2, %2 row_ror:%3 row_mask:0xf bank_mask:0xf\n\t"
+            "v_addc_co_u32 %1, vcc, 0, %1, vcc"
+            : "=&v"(tmp), "+v"(r)
+            : "v"(h), "i"(K)
+            : "vcc");
+    else
+        asm volatile(
+            "v_sub_co_u32_dpp %0, vcc, %2, %2 row_ror:%3 row_mask:0xf bank_mask:0xf\n\t"
+            "v_addc_co_u32 %1, vcc, 0, %1, vcc"
+            : "=&v"(tmp), "+v"(r)
+            : "v"(h), "i"(K)
+            : "vcc");
+}
+
+template <int G, int K, int KEND>
+__device__ __forceinline__ void rank_step_h(uint32_t h, int lane, uint32_t& r) {
+    if constexpr (G == 16 && K < KEND) {
+        rank_rot16_h<K, K == 1>(h, r);
+        rank_step_h<G, K + 1, KEND>(h, lane, r);
+    } else if constexpr (K < KEND) {
+        const uint32_t o = grot32c<G, K>(h, lane);
+        r += o < h ? 1u : 0u;
+        rank_step_h<G, K + 1, KEND>(h, lane, r);
+    }
+}
+
+// value of lane - 1 within each 16-lane row (row_shr:1; lane 0 of a row reads 0)
+__device__ __forceinline__ uint32_t prev_lane32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x111, 0xF, 0xF, true);
+}
+
 // OR of v over the G lanes of the group
 template <int G, int K = 1>
 __device__ __forceinline__ uint32_t or_reduce_group(uint32_t v, int lane, uint32_t acc = 0) {

@@ -562,7 +562,7 @@ __global__ void __launch_bounds__(256) softplus_tails_kernel(const double* v, in
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const double x = v[i];
         exact[i] = pscl_softplus_tail_bf(x, T);
-        apx[i] = pscl_softplus_tail_apx(x, T);
+        apx[i] = pscl_softplus_tail_scr(x);
     }
 }
 

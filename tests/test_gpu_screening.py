@@ -142,11 +142,11 @@ def test_screening_boundary_ties_every_frame(M):
 def test_screening_tail_within_bound_device():
     """The device forms of both metric tails (pscl_softplus_tails_device): the exact one is
     bit-identical to the host port (itself bit-identical to libm, test_softplus_host.py), the
-    screening one -- reciprocal + Newton division, SGPR-addend Horner FMAs -- stays within 2^12
-    ulps of it, 16x inside the kernel's 2^16-ulp ordering margin."""
+    screening one (fp64 range reduction, v_exp_f32, v_rcp_f32, fp32 series) stays within its
+    proven relative bound PSCL_SCR_EPS -- the bound the kernel's ordering margin is built on."""
     import ctypes as C
 
-    from test_softplus_host import _lib, apx_grid, ulp_distance
+    from test_softplus_host import SCR_EPS, _lib, apx_grid, tail_error_ok
 
     v = apx_grid()
     dec = _native.Decoder(128, construct_info_set(128, 64), 8, POLY)
@@ -156,5 +156,8 @@ def test_screening_tail_within_bound_device():
     L.softplus_tails_batch.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
     L.softplus_tails_batch(v.ctypes.data, v.size, ex_h.ctypes.data, ap_h.ctypes.data)
     np.testing.assert_array_equal(ex_d.view(np.int64), ex_h.view(np.int64))
-    d = ulp_distance(ex_d, ap_d)
-    assert d.max() <= 2 ** 12, (d.max(), v[d.argmax()])
+    ok = tail_error_ok(ex_d, ap_d)
+    assert ok.all(), (v[~ok][:5], ex_d[~ok][:5], ap_d[~ok][:5])
+    nrm = ex_d > 2.0 ** -1000
+    rel = np.abs(ap_d - ex_d)[nrm] / ex_d[nrm]
+    print(f"screening tail: max relative error {rel.max():.3e} = 2^{np.log2(rel.max()):.2f} (bound 2^{np.log2(SCR_EPS):.2f})")

@@ -54,20 +54,25 @@ def apx_grid():
     return np.ascontiguousarray(np.concatenate([v, -v[::7]]))
 
 
-def ulp_distance(a, b):
-    """|a - b| in ulps of the (non-negative) tails' bit patterns."""
-    return np.abs(a.view(np.int64) - b.view(np.int64))
+SCR_EPS = 6.0 * 2.0 ** -23  # glibc_softplus.h PSCL_SCR_EPS: proven relative bound of the screening tail
+
+
+def tail_error_ok(exact, apx):
+    """|apx - exact| <= PSCL_SCR_EPS * exact (+ one subnormal ulp where the tail underflows)."""
+    return np.abs(apx - exact) <= SCR_EPS * exact + 2.0 ** -1074
 
 
 def test_screening_tail_within_bound_host():
-    """The bounded-error tail (pscl_softplus_tail_apx, host form: correctly rounded division)
-    stays within 2^12 ulps of the exact tail -- a 16x guard below the kernel's 2^16-ulp
-    ordering margin (glibc_softplus.h static_assert)."""
+    """The screening tail (pscl_softplus_tail_scr, host form: libm exp2f, correctly rounded
+    reciprocal) is within PSCL_SCR_EPS of the exact tail relatively on a dense grid."""
     v = apx_grid()
     ex, ap = np.empty_like(v), np.empty_like(v)
     L = _lib()
     L.softplus_tails_batch.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
     L.softplus_tails_batch(v.ctypes.data, v.size, ex.ctypes.data, ap.ctypes.data)
     assert np.all(ex >= 0) and np.all(ap >= 0)
-    d = ulp_distance(ex, ap)
-    assert d.max() <= 2 ** 12, (d.max(), v[d.argmax()])
+    ok = tail_error_ok(ex, ap)
+    assert ok.all(), (v[~ok][:5], ex[~ok][:5], ap[~ok][:5])
+    nrm = ex > 2.0 ** -1000  # normal range (subnormal tails: absolute bound above)
+    rel = np.abs(ap - ex)[nrm] / ex[nrm]
+    assert rel.max() < SCR_EPS / 2  # typical case: well inside the proven bound
