@@ -414,6 +414,12 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     const uint64_t bnd = claim & ~group_prefix_mask<G>(L);
                     const uint32_t nmh = (uint32_t)(nm >> 32);
                     amb |= ((wmask(rr != (uint32_t)g) & claim) | (wmask(near_or_below(prev_lane32(nmh), nmh)) & bnd)) & vmask;
+#ifdef PSCL_DEBUG_AMB
+                    {
+                        const uint64_t cm = wmask(rr != (uint32_t)g) & claim & vmask, bm = wmask(near_or_below(prev_lane32(nmh), nmh)) & bnd & vmask;
+                        if (f0 == 0 && lane < 16 && (cm | bm)) printf("phi %d lane %d r %u c %d rr %u nmh %08x prev %08x claimfail %d bndfail %d\n", phi, lane, r, c, rr, nmh, prev_lane32(nmh), (int)((cm >> lane) & 1), (int)((bm >> lane) & 1));
+                    }
+#endif
                     src = gbase + (c & (LMAX - 1));
                     b = c >= LMAX ? 1u : 0u;
                 }
@@ -626,6 +632,9 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
             const uint32_t nh = bperm32(kh, gbase + c);
             const uint64_t live = kFixedList ? group_prefix_mask<G>(cnt) : wmask(g < cnt);
             amb |= ((wmask(rr != (uint32_t)g) & live) | (wmask(near_or_below(prev_lane32(nh), nh)) & live & KGE1)) & vmask;
+#ifdef PSCL_DEBUG_AMB
+            if (f0 == 0 && lane < 16) printf("final lane %d r %u c %d rr %u kh %08x nh %08x prev %08x\n", lane, r, c, rr, kh, nh, prev_lane32(nh));
+#endif
             rank = r;
         }
         // APX: a frame with an uncertain ordering is handed to the exact re-decode

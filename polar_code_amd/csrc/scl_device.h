@@ -279,9 +279,15 @@ __device__ __forceinline__ void rank_step_h(uint32_t h, int lane, uint32_t& r) {
     }
 }
 
-// value of lane - 1 within each 16-lane row (row_shr:1; lane 0 of a row reads 0)
+// value of lane - 1 within each 16-lane row (row_shr:1; lane 0 of a row reads 0).  A plain
+// DPP move in inline asm: left to the compiler, the move is folded into the consumer
+// (v_subrev_u32_dpp of the very next instruction), which measured wrong on gfx950 right
+// after the ds_bpermute that produces v (every frame flagged ambiguous).  The s_nop covers a
+// VALU write of v just before (inline asm is not hazard-checked).
 __device__ __forceinline__ uint32_t prev_lane32(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x111, 0xF, 0xF, true);
+    uint32_t d;
+    asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(v));
+    return d;
 }
 
 // OR of v over the G lanes of the group
