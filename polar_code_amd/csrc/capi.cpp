@@ -183,11 +183,15 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P, int hist, hipStre
         HIP_TRY(hipMemsetAsync(d_cnt, 0, 4, st));
         pscl_decode_params S = P;
         S.apx = 1;
+        pscl_decode_layout(S, hist);  // (no exp table in LDS)
         S.amb_list = (int64_t*)d_list;
         S.amb_count = (int32_t*)d_cnt;
         err = pscl_launch_decode(S, hist, st);
         h->screened = true;
-        if (err == hipSuccess) {
+        // PSCL_DIAG_SCREEN_ONLY=1: timing diagnostics of the screening pass alone (tools/ablate
+        // variants); the deferred frames are then left undecoded
+        static const bool screen_only = getenv("PSCL_DIAG_SCREEN_ONLY") && atoi(getenv("PSCL_DIAG_SCREEN_ONLY")) == 1;
+        if (err == hipSuccess && !screen_only) {
             pscl_decode_params X = P;  // exact decode of the listed frames, outputs at their rows
             X.fidx = (const int64_t*)d_list;
             X.d_count = (const int32_t*)d_cnt;

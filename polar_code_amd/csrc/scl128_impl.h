@@ -52,13 +52,25 @@ struct Layout128 {
     static constexpr int F = 64 / G;
     static constexpr int LOG_G = __builtin_ctz(G);
     static constexpr int LOG_LM = __builtin_ctz(LMAX);
-    // depth-d nodes element-major, [element][slot]: the 16 lanes of a frame, each on its own
-    // path, then touch consecutive doubles (no LDS bank conflicts within a lane group)
-    static constexpr int OFF3 = CH ? kN : 0;        // [16][LMAX]
-    static constexpr int OFF4 = OFF3 + 16 * LMAX;   // [8][LMAX]
-    static constexpr int OFF5 = OFF4 + 8 * LMAX;    // [4][LMAX]
-    static constexpr int OFF6 = OFF5 + 4 * LMAX;    // [2][LMAX]
-    static constexpr int FSTRIDE = OFF6 + 2 * LMAX;  // doubles per frame
+    // depth-d nodes (W = 2^(7-d) values per slot) pair-major, [W/2][slot][2]: element e of
+    // slot s at ((e mod W/2) * LMAX + s) * 2 + e div W/2, so the two inputs a = e, b = e + W/2
+    // of every f/g of the next depth (and of the leaf) are one 16-byte ds_read_b128 (4 LDS
+    // cycles per wave, against 8 for the ds_read2_b64 of two separate doubles), and the
+    // 16 lanes of a frame, each on its own path, read 256 contiguous bytes
+    static constexpr int OFF3 = CH ? kN : 0;        // [8][LMAX][2]
+    static constexpr int OFF4 = OFF3 + 16 * LMAX;   // [4][LMAX][2]
+    static constexpr int OFF5 = OFF4 + 8 * LMAX;    // [2][LMAX][2]
+    static constexpr int OFF6 = OFF5 + 4 * LMAX;    // [1][LMAX][2]
+    // the paths' left-sibling partial sums {X1 lo, X1 hi, X2, X3} at a depth-1..3 recompute,
+    // 16 B per path: every lane reads them for all paths with ds_read_b128
+    static constexpr int OFFX = OFF6 + 2 * LMAX;
+    // doubles per frame, padded to 256 B: the frames of a wave then start on bank 0 and the
+    // ds_read_b128 lane groups (which mix lanes of neighbouring frames) stay conflict-free
+    static constexpr int FSTRIDE = (OFFX + 2 * LMAX + 31) & ~31;
+    // position of element e of slot s in a node of width w
+    static constexpr __device__ __forceinline__ int at(int w, int e, int s) {
+        return ((e & (w / 2 - 1)) * LMAX + s) * 2 + e / (w / 2);
+    }
 };
 
 __device__ __forceinline__ int slot_at(uint32_t tab, int d) { return (int)((tab >> (4 * (d - 3))) & 15u); }
@@ -73,7 +85,7 @@ __device__ __forceinline__ uint64_t seg_transform(uint64_t u0, uint64_t u1, int 
 // depth-D step (D = 4, 5, 6) of the tree walk.  Lane (frame, g) works on path p = g mod LMAX
 // of its own frame and the elements e = 2k + h (h = g / LMAX) of the node's W values, so the
 // parent slot comes from the path's own slot table (tabp: upper lanes hold a copy) and no
-// lane reads another's state.
+// lane reads another's state.  Inputs e and e + W of the parent are one pair (Layout128).
 template <int LMAX, bool CH, int D>
 __device__ __forceinline__ void step_depth(double* Af, int g, uint32_t tabp, uint32_t xsp, bool first, bool is_g) {
     using Ly = Layout128<LMAX, CH>;
@@ -82,13 +94,13 @@ __device__ __forceinline__ void step_depth(double* Af, int g, uint32_t tabp, uin
     constexpr int OFF_IN = D == 4 ? Ly::OFF3 : (D == 5 ? Ly::OFF4 : Ly::OFF5);
     const int p = g & (LMAX - 1), h = g >> Ly::LOG_LM;
     const int ps = first ? slot_at(tabp, D - 1) : p;
-    const double* par = Af + OFF_IN + h * LMAX + ps;   // element e of slot s: [e * LMAX + s]
-    double* out = Af + OFF_OUT + h * LMAX + p;
+    const double2* par = reinterpret_cast<const double2*>(Af + OFF_IN) + ps;  // pair e of slot s: [e * LMAX + s]
     const uint32_t xh = xsp >> h;
 #pragma unroll
     for (int k = 0; k < HW; ++k) {
-        const double a = par[2 * k * LMAX], b = par[(2 * k + W) * LMAX];
-        out[2 * k * LMAX] = is_g ? g_node(a, b, (xh >> (2 * k)) & 1u) : f_minsum(a, b);
+        const int e = 2 * k + h;
+        const double2 ab = par[e * LMAX];
+        Af[OFF_OUT + Ly::at(W, e, p)] = is_g ? g_node(ab.x, ab.y, (xh >> (2 * k)) & 1u) : f_minsum(ab.x, ab.y);
     }
     wave_lds_fence();
 }
@@ -119,6 +131,14 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 #define PSCL_RANK_M 1
 #endif
 
+// Timing-only ablations of the screening kernel (tools/build_variant.py --spec 1_8
+// -DPSCL_APX_ABLATE=m); 0 in the product.  1: tail -> |lam| * 2^-20; 2: no depth-1..3
+// recompute; 4: no depth-4..6 steps; 8: full-list info phases always take the fast path;
+// 16: no final-order certification
+#ifndef PSCL_APX_ABLATE
+#define PSCL_APX_ABLATE 0
+#endif
+
 #ifndef PSCL_WAVES_PER_EU
 #define PSCL_WAVES_PER_EU 4
 #endif
@@ -137,10 +157,13 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
     constexpr int G = Ly::G, F = Ly::F, LOG_G = Ly::LOG_G;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint64_t* T = reinterpret_cast<uint64_t*>(smem);
-    for (int i = threadIdx.x; i < PSCL_EXP_TABLE_WORDS; i += blockDim.x) T[i] = P.exp_table[i];
+    // the exp table of the exact metric tail (the screening tail needs none: pscl_decode_layout
+    // leaves it out of the screening launch's LDS)
+    constexpr int TW = APX ? 0 : PSCL_EXP_TABLE_WORDS;
+    for (int i = threadIdx.x; i < TW; i += blockDim.x) T[i] = P.exp_table[i];
 #if PSCL_EPI_LDS
-    for (int i = threadIdx.x; i < P.epi_words; i += blockDim.x) T[PSCL_EXP_TABLE_WORDS + i] = P.epi_table[i];
-    const uint8_t* GT = reinterpret_cast<const uint8_t*>(T + PSCL_EXP_TABLE_WORDS);  // [16][256]
+    for (int i = threadIdx.x; i < P.epi_words; i += blockDim.x) T[TW + i] = P.epi_table[i];
+    const uint8_t* GT = reinterpret_cast<const uint8_t*>(T + TW);  // [16][256]
 #else  // epilogue tables read from global memory (L1/L2-resident): less LDS per workgroup
     const uint8_t* GT = reinterpret_cast<const uint8_t*>(P.epi_table);
 #endif
@@ -186,6 +209,16 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 const double* src = P.llr + frow * P.rm_E;
                 for (int x = 0; x < kN / G; ++x) Af[g + x * G] = nr_stage(src, P.rm_src[g + x * G], P.rm_E, kN);
             }
+        }
+        // 16-lane frames (L = 8): lane g's 8 channel LLRs (elements g + 16 m) are the same at
+        // all 8 depth-1..3 recomputes: loaded once per frame into registers, so the recomputes
+        // wait on no memory (16 VGPRs; the in-place reads cost 25 % of the screening pass)
+        constexpr bool CREG = G == 16;
+        double creg[CREG ? 8 : 1];
+        if constexpr (CREG) {
+            if (CH) wave_lds_fence();
+#pragma unroll
+            for (int m = 0; m < 8; ++m) creg[m] = CH ? Af[g + 16 * m] : chan[g + 16 * m];
         }
         uint64_t fm0 = 0, fm1 = 0, fv0 = 0, fv1 = 0;
         if (FS && force && fvalid) {
@@ -238,7 +271,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
             asm volatile("; PHASE %0" ::"n"(PT));
 #endif
             // ---- depths 1-3 recomputed from the channel (phi % 16 == 0)
-            if (start <= 3 && !(PSCL_ABLATE & 12)) {
+            if (start <= 3 && !(PSCL_ABLATE & 12) && !(APX && (PSCL_APX_ABLATE & 2))) {
                 const bool r1 = phi >= 64, r2 = (phi >> 5) & 1, r3 = (phi >> 4) & 1;
                 // path lanes: partial sums of the left siblings at depths 1, 2, 3
                 uint64_t X1 = 0;
@@ -273,13 +306,14 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                         double d1[4];
 #pragma unroll
                         for (int m = 0; m < 4; ++m)
-                            d1[m] = r1 ? g_node(c[m], c[m + 4], (uint32_t)(x1 >> (e + 16 * m)) & 1u) : f_minsum(c[m], c[m + 4]);
+                            d1[m] = r1 ? g_node_wbit(c[m], c[m + 4], (uint32_t)(x1 >> (32 * (m >> 1))), (uint32_t)(e + 16 * (m & 1)))
+                                       : f_minsum(c[m], c[m + 4]);
                         double d2[2];
 #pragma unroll
                         for (int s2 = 0; s2 < 2; ++s2)
                             d2[s2] = r2 ? g_node(d1[s2], d1[s2 + 2], (x2 >> (e + 16 * s2)) & 1u) : f_minsum(d1[s2], d1[s2 + 2]);
                         const double d3 = r3 ? g_node(d2[0], d2[1], (x3 >> e) & 1u) : f_minsum(d2[0], d2[1]);
-                        A[fj * Ly::FSTRIDE + Ly::OFF3 + e * LMAX + p] = d3;
+                        A[fj * Ly::FSTRIDE + Ly::OFF3 + Ly::at(16, e, p)] = d3;
                     }
                 } else
 #pragma unroll
@@ -287,28 +321,45 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     const int e = g + G * q;
                     double c[8];
 #pragma unroll
-                    for (int m = 0; m < 8; ++m) c[m] = CH ? Af[e + 16 * m] : chan[e + 16 * m];
+                    for (int m = 0; m < 8; ++m) {
+                        if constexpr (CREG) c[m] = creg[m];  // (G == 16: e == g)
+                        else c[m] = CH ? Af[e + 16 * m] : chan[e + 16 * m];
+                    }
                     double d1l[4];
 #pragma unroll
                     for (int m = 0; m < 4; ++m) d1l[m] = f_minsum(c[m], c[m + 4]);
+                    // each path lane publishes its partial sums once; every lane then reads those of
+                    // the path it works on (one ds_read_b128 instead of four ds_bpermute)
+                    uint4* xs_lds = reinterpret_cast<uint4*>(Af + Ly::OFFX);
+                    if (q == 0 && (r1 || r2 || r3)) {
+                        if (path_lane) xs_lds[g] = make_uint4((uint32_t)X1, (uint32_t)(X1 >> 32), X2, X3);
+                        wave_lds_fence();
+                    }
 #pragma unroll
-                    for (int p = 0; p < LMAX; ++p) {
-                        const int src = gbase + p;
+                    for (int p0 = 0; p0 < LMAX; ++p0) {
+                        // lane e takes path (p0 + e) mod LMAX in step p0: the 16 lanes of a frame
+                        // then store to 16 distinct bank pairs (the same path for every lane put
+                        // the 16 stores on 2 bank pairs: 8-way conflicts)
+                        const int p = (p0 + e) & (LMAX - 1);
                         uint64_t x1 = 0;
                         uint32_t x2 = 0, x3 = 0;
-                        if (r1) x1 = shfl_u64(X1, src);
-                        if (r2) x2 = bperm32(X2, src);
-                        if (r3) x3 = bperm32(X3, src);
+                        if (r1 || r2 || r3) {
+                            const uint4 xv = xs_lds[p];
+                            x1 = ((uint64_t)xv.y << 32) | xv.x;
+                            x2 = xv.z;
+                            x3 = xv.w;
+                        }
                         double d1[4];
 #pragma unroll
                         for (int m = 0; m < 4; ++m)
-                            d1[m] = r1 ? g_node(c[m], c[m + 4], (uint32_t)(x1 >> (e + 16 * m)) & 1u) : d1l[m];
+                            d1[m] = r1 ? g_node_wbit(c[m], c[m + 4], (uint32_t)(x1 >> (32 * (m >> 1))), (uint32_t)(e + 16 * (m & 1)))
+                                       : d1l[m];
                         double d2[2];
 #pragma unroll
                         for (int s2 = 0; s2 < 2; ++s2)
-                            d2[s2] = r2 ? g_node(d1[s2], d1[s2 + 2], (x2 >> (e + 16 * s2)) & 1u) : f_minsum(d1[s2], d1[s2 + 2]);
-                        const double d3 = r3 ? g_node(d2[0], d2[1], (x3 >> e) & 1u) : f_minsum(d2[0], d2[1]);
-                        Af[Ly::OFF3 + e * LMAX + p] = d3;
+                            d2[s2] = r2 ? g_node_wbit(d1[s2], d1[s2 + 2], x2, (uint32_t)(e + 16 * s2)) : f_minsum(d1[s2], d1[s2 + 2]);
+                        const double d3 = r3 ? g_node_wbit(d2[0], d2[1], x3, (uint32_t)e) : f_minsum(d2[0], d2[1]);
+                        Af[Ly::OFF3 + Ly::at(16, e, p)] = d3;
                     }
                 }
                 wave_lds_fence();
@@ -319,7 +370,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 const int w = 1 << (kn - start), lo = phi - w;
                 xs = polar_transform8((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)) & ((1u << w) - 1u));
             }
-            if (!(PSCL_ABLATE & 4) && start <= 6) {
+            if (!(PSCL_ABLATE & 4) && !(APX && (PSCL_APX_ABLATE & 4)) && start <= 6) {
                 // (DPP evaluated by every lane first: inside ?: only the selected lanes would
                 // run it, and a DPP that reads an inactive lane gets 0)
                 const uint32_t tabp = tab;
@@ -336,8 +387,8 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
             }
             // ---- leaf LLRs.  Lanes >= LMAX: the sibling leaf (phi+1) given bit 0 here.
             // (depth 6 was just rewritten into the path's own slot at even phases)
-            const double* par = Af + Ly::OFF6 + (start <= 6 ? cpath : slot_at(tab, 6));
-            const double la = par[0], lb = par[LMAX];
+            const double2 lab = reinterpret_cast<const double2*>(Af + Ly::OFF6)[start <= 6 ? cpath : slot_at(tab, 6)];
+            const double la = lab.x, lb = lab.y;
             const uint32_t xleaf = lastbit;  // u[phi - 1], the left sibling's bit at odd phases
             const double lam = (PSCL_ABLATE & 128) ? la : (path_lane ? ((phi & 1) ? g_node(la, lb, xleaf) : f_minsum(la, lb)) : lb + la);
             // ---- metric tail log1p(exp(-|llr|)) (scl.py:102-105)
@@ -346,7 +397,8 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
             if (pre_ok) {
                 Lt = pscl_asf64(lpre_up);
             } else {
-                Lt = (PSCL_ABLATE & 1) ? lam * 0.5 : (APX ? pscl_softplus_tail_scr(lam) : pscl_softplus_tail_bf(lam, T));
+                Lt = (PSCL_ABLATE & 1) ? lam * 0.5
+                     : (APX ? ((PSCL_APX_ABLATE & 1) ? fabs(lam) * 0x1p-20 : pscl_softplus_tail_scr(lam)) : pscl_softplus_tail_bf(lam, T));
             }
             const bool frozen_even = !is_info && !(phi & 1);
             Lpre = Lt;
@@ -364,12 +416,14 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 // 0..cnt-1 in any order; frozen phases only advance the metrics.  An exactly
                 // zero LLR needs no special case: both children get metric + tail(0) (= the
                 // exact LOGE2 within the tail's bound), a tie the margin tests catch.
-                if (!is_info) {
-                    metric = neg ? mbd : mgd;
+                if (!is_info) {  // bit 0: metric + max(-lam, 0) + tail (any rounding order will do)
+                    metric = metric + (relu_neg(lam) + Lt);
                     lastbit = 0;
                     return;
                 }
-                const double m0 = neg ? mbd : mgd, m1 = neg ? mgd : mbd;  // bit-0 / bit-1 child
+                // better / worse child (any rounding order will do here)
+                const double mg = metric + Lt, mb = mg + fabs(lam);
+                const double m0 = neg ? mb : mg, m1 = neg ? mg : mb;  // bit-0 / bit-1 child
                 const int ncnt = 2 * cnt < L ? 2 * cnt : L;
                 int src;
                 uint32_t b;
@@ -384,20 +438,20 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     // full list: the better children survive when every worse child exceeds the
                     // largest better child by the margin (group max of the high words over
                     // duplicated keys)
-                    uint32_t mx = merge_from_lower<G, LMAX>(hiw(mgd), hiw(mgd), lane);
+                    uint32_t mx = merge_from_lower<G, LMAX>(hiw(mg), hiw(mg), lane);
                     static_for<Ly::LOG_LM>([&](auto SC) {
                         constexpr int S = 1 << decltype(SC)::value;
                         const uint32_t o = grot32c<G, S>(mx, lane);
                         mx = o > mx ? o : mx;
                     });
-                    const uint64_t badm = wmask(near_or_below(mx, hiw(mbd)));
-                    if ((badm & vmask & KPATH) == 0) {
-                        const uint32_t gb = neg ? 1u : 0u;
-                        metric = mgd;
+                    const uint64_t badm = wmask(near_or_below(mx, hiw(mb)));
+                    if ((PSCL_APX_ABLATE & 8) || (badm & vmask & KPATH) == 0) {
+                        // (lam != +-0 here: a zero LLR gives mbd == mgd, never clear of the margin,
+                        // so the sign bit is the better child's bit)
+                        const uint32_t gb = sign_bit(lam);
+                        metric = mg;
                         lastbit = gb;
-                        if (gb) {
-                            if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
-                        }
+                        if (phi < 64) u0 |= (uint64_t)gb << phi; else u1 |= (uint64_t)gb << (phi - 64);
                         ++j;
                         return;
                     }
@@ -428,9 +482,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 if (phi >= 64) u1 = shfl_u64(u1, src);
                 const uint32_t ntab = bperm32(tab, src);
                 tab = merge_from_lower<G, LMAX>(ntab, ntab, lane);
-                if (b) {
-                    if (phi < 64) u0 |= 1ULL << phi; else u1 |= 1ULL << (phi - 64);
-                }
+                if (phi < 64) u0 |= (uint64_t)b << phi; else u1 |= (uint64_t)b << (phi - 64);
                 lastbit = b;
                 cnt = ncnt;
                 ++j;
@@ -618,7 +670,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 for (int m = 16; m < k4; ++m) syn ^= ST[m * 16 + (uint32_t)((ib1 >> (4 * (m - 16))) & 15u)];
             }
         }
-        if constexpr (APX) {
+        if constexpr (APX && !(PSCL_APX_ABLATE & 16)) {
             // the final list order (best = first CRC pass, and its index): rank on the metric,
             // certified by every position 0..cnt-1 claimed once and sorted neighbours apart by
             // the margin.  Upper lanes hold copies, rank among the same keys and push into the
@@ -639,7 +691,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
         }
         // APX: a frame with an uncertain ordering is handed to the exact re-decode
         const bool famb = APX && ((amb >> gbase) & (G == 64 ? ~0ULL : ((1ULL << (G & 63)) - 1))) != 0;
-        if (APX && famb && g == 0 && fvalid) P.amb_list[atomicAdd(P.amb_count, 1)] = f;
+        if (APX && !PSCL_APX_ABLATE && famb && g == 0 && fvalid) P.amb_list[atomicAdd(P.amb_count, 1)] = f;
         const bool active = path_lane && g < cnt && fvalid && !famb;
         const int64_t fo = P.out_by_row ? frow : f;  // output row
         uint32_t pm = (active && syn == 0) ? (1u << rank) : 0u;
@@ -674,7 +726,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 }
                 if (P.flags) P.flags[fo] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
                 if (P.n_paths) P.n_paths[fo] = cnt;
-                if (P.ref)
+                if (P.ref && !(APX && PSCL_APX_ABLATE))  // (ablation timings: wrong frames, no atomics)
                     count_errors(P.counters, ib0, ib1, P.ref[fo * P.W], P.W > 1 ? P.ref[fo * P.W + 1] : 0, P.k_payload,
                                  bpass);
             }

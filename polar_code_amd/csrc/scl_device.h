@@ -63,6 +63,26 @@ __device__ __forceinline__ double g_node(double a, double b, uint32_t c) {
     return b + pscl_asf64(((uint64_t)hi << 32) | (uint32_t)ab);
 }
 
+// g(a, b, c) with c = bit `pos` of the 32-bit word w (pos may differ per lane): the bit is
+// moved to bit 31 and folded into a's sign in one v_bitop3 (a ^ (m & 0x80000000)); no 64-bit
+// shift of the partial-sum word
+__device__ __forceinline__ double g_node_wbit(double a, double b, uint32_t w, uint32_t pos) {
+    const uint64_t ab = pscl_asu64(a);
+    const uint32_t hi = (uint32_t)(ab >> 32) ^ ((w << (31u - pos)) & 0x80000000u);
+    return b + pscl_asf64(((uint64_t)hi << 32) | (uint32_t)ab);
+}
+
+// max(-v, 0): the part of np.logaddexp(0, -v) beyond the shared tail (bit 0 pays |v| when
+// v < 0); one v_max_f64 with the negation as a source modifier (fmax would canonicalise)
+__device__ __forceinline__ double relu_neg(double v) {
+    double d;
+    asm("v_max_f64 %0, -%1, 0" : "=v"(d) : "v"(v));
+    return d;
+}
+
+// bit 31 of the high word of v: 1 for negative v (and -0.0)
+__device__ __forceinline__ uint32_t sign_bit(double v) { return (uint32_t)(pscl_asu64(v) >> 63); }
+
 // Arikan transform of the low w bits of x (in-word, w <= 64): bit j ^= bit j+s for bit s of j
 // clear, for every stage s (stages commute).  Bits >= w must be zero.
 __device__ __forceinline__ uint64_t polar_transform64(uint64_t x) {

@@ -470,7 +470,9 @@ void pscl_decode_layout(pscl_decode_params& P, int hist) {
     const int lmax = pscl_decode_lmax(P.L);
     const int F = 32 / lmax;  // frames per wavefront
     P.fast = (P.N == 128 && P.L <= 8) ? 1 : 0;
-    P.wg_fixed_bytes = PSCL_EXP_TABLE_WORDS * 8 + (P.fast && PSCL_EPI_LDS ? P.epi_words * 8 : 0);
+    // exp table (exact metric tails; the screening launch, P.apx, has none) + scl128 epilogue tables
+    P.wg_fixed_bytes = (P.apx ? 0 : PSCL_EXP_TABLE_WORDS * 8) + (P.fast && PSCL_EPI_LDS ? P.epi_words * 8 : 0);
+    if (P.fast) P.wg_fixed_bytes = (P.wg_fixed_bytes + 255) & ~255;  // frames start on LDS bank 0 (Layout128)
     if (P.fast) {
         P.a_bytes = F * pscl_fast128_fstride(P.L, P.rm_E != 0) * 8;
         const int wb = P.a_bytes + (hist ? F * P.K * P.L * 9 : 0);

@@ -1,6 +1,8 @@
 """Build a variant of the HIP library with extra compile flags (A/B timing, diagnostics).
 
-    python tools/build_variant.py <name> [-DFLAG=V ...]   ->  tools/_variant/lib_<name>.so
+    python tools/build_variant.py <name> [--spec C_L] [-DFLAG=V ...]   ->  tools/_variant/lib_<name>.so
+(--spec C_L: recompile only the scl128_spec instance (code C, list size L) with the flags and
+link it with the product build's other objects in polar_code_amd/_build)
 Time variants with tools/ab_bench.sh; they are never loaded by the product.
 """
 import subprocess
@@ -12,9 +14,20 @@ sys.path.insert(0, str(ROOT))
 from polar_code_amd import build as B  # noqa: E402
 
 name, flags = sys.argv[1], sys.argv[2:]
+spec = None
+if "--spec" in flags:
+    i = flags.index("--spec")
+    spec = flags[i + 1]
+    flags = flags[:i] + flags[i + 2:]
 out = ROOT / "tools" / "_variant"
 objdir = out / f"obj_{name}"
 objdir.mkdir(parents=True, exist_ok=True)
-objs = B.compile_units(B.hip_units(objdir), flags)
+if spec:
+    units = B.hip_units(objdir)
+    mine = [u for u in units if u[2].name == f"scl128_spec_{spec}.o"]
+    objs = B.compile_units(mine, flags)
+    objs += [str(B.PKG / "_build" / u[2].name) for u in units if u[2].name != f"scl128_spec_{spec}.o"]
+else:
+    objs = B.compile_units(B.hip_units(objdir), flags)
 subprocess.check_call([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", *objs, "-o", str(out / f"lib_{name}.so")])
 print(out / f"lib_{name}.so")
