@@ -381,20 +381,21 @@ PSCL_HD double pscl_softplus_tail_bf(double v, const uint64_t* T) {
  * Screening tail for scl128_kernel<..., APX = true>: L = log1p(exp(-x)), x = |v|, to a proven
  * relative error below PSCL_SCR_EPS = 6 * 2^-23 (about 2^-20.4), mostly in fp32:
  *
- *   k = round(x / ln2), r = x - k ln2 (fp64, Cody-Waite: |r| <= ln2/2, error < 2^-55)
- *   u = e^-r = 2^(-r log2 e)             fp32: cvt + mul + v_exp_f32, u in [0.7, 1.42]
+ *   k = round(x log2 e), r2 = k - x log2 e (fp64: one fma with the exact product; |r2| <= 1/2,
+ *                                    error < 2^-42 from the rounded log2 e for x <= 4096)
+ *   u = e^-(x - k ln2) = 2^r2            fp32: cvt + v_exp_f32, u in [0.7, 1.42]
  *   t = u 2^-k = e^-x                    fp32 ldexp (exact while normal; tiny t only feeds s)
  *   log1p(t) = 2 atanh(s), s = t/(2 + t) in [0, 1/3]:
  *   log1p(t) = 2 s P(s^2) = 2^-k * [u * rcp(2 + t) * 2P(s^2)]     (P: 7 terms, fp32 Horner)
  *   L = ldexp((double)q, -k), q = u * rcp(2 + t) * 2P(s^2)
  *
  * Relative error of q, in units of 2^-23 (v_exp_f32 and v_rcp_f32 within 1 ulp, roundings
- * 2^-24 each): u 1.39 (exp 1, r rounding to fp32 0.09, product with log2 e 0.18, constant
- * 0.12), rcp 1 + its argument 0.5 + t's error through 2 + t 0.46, P 1.45 (Horner roundings
- * 0.56, coefficients 0.56, truncation (1/9)^7/15*9/8 = 0.13, s^2 error x dP/dw 0.2), the two
- * products 1: 5.8 < 6.  The final cvt and ldexp are exact (until fp64 underflow, where the
- * exact tail is subnormal too: then the error is at most one ulp of the result).  x is
- * clamped to 4096 (the exact tail is 0 above ~745.2; the clamp keeps k in int range).
+ * 2^-24 each): u 1.2 (exp 1, r2 rounding to fp32 0.18, r2's fp64 error 0.0), rcp 1 + its
+ * argument 0.5 + t's error through 2 + t 0.4, P 1.45 (Horner roundings 0.56, coefficients 0.56,
+ * truncation (1/9)^7/15*9/8 = 0.13, s^2 error x dP/dw 0.2), the two products 1: 5.6 < 6.  The
+ * final cvt and ldexp are exact (until fp64 underflow, where the exact tail is subnormal too:
+ * then the error is at most one ulp of the result).  x is clamped to 4096 (the exact tail is 0
+ * above ~745.2; the clamp keeps k in int range).
  *
  * With positive increments every screening path metric is within PSCL_SCR_EPS + 2^-52 of
  * the exact metric relatively, and the kernel trusts an ordering of two metrics only when
@@ -441,9 +442,8 @@ PSCL_HD double pscl_softplus_tail_scr(double v) {
     const double kd0 = pscl_fma(-x, PSCL_INVLN2, PSCL_EXP_SHIFT); /* low word = -k */
     const int32_t nk = (int32_t)(uint32_t)pscl_asu64(kd0);
     const double kd = kd0 - PSCL_EXP_SHIFT;                      /* -k */
-    double r = pscl_fma(kd, -PSCL_LN2HI, -x);                   /* -x + k ln2 = -r */
-    r = pscl_fma(kd, -PSCL_LN2LO, r);
-    const float u = pscl_exp2_f32((float)r * PSCL_LOG2E_F);     /* e^-r */
+    const double r2 = pscl_fma(-x, PSCL_INVLN2, -kd);            /* k - x log2 e */
+    const float u = pscl_exp2_f32((float)r2);                    /* e^-(x - k ln2) */
     const float t = ldexpf(u, nk);                               /* e^-x */
     const float rc = pscl_rcp_f32(2.0f + t);
     const float s = t * rc;

@@ -335,12 +335,20 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                         if (path_lane) xs_lds[g] = make_uint4((uint32_t)X1, (uint32_t)(X1 >> 32), X2, X3);
                         wave_lds_fence();
                     }
+                    // left-left quarter (phi = 0, 16): depth 2 = f(depth 1) is the same for every path
+                    const bool shared2 = !r1 && !r2;
+                    double d2s[2];
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) d2s[s2] = f_minsum(d1l[s2], d1l[s2 + 2]);
+                    // paths that exist (compiled-in codes know: phi = 0 has one)
+                    const int npaths = kFixedList && cnt < LMAX ? cnt : LMAX;
 #pragma unroll
                     for (int p0 = 0; p0 < LMAX; ++p0) {
+                        if (p0 >= npaths) break;
                         // lane e takes path (p0 + e) mod LMAX in step p0: the 16 lanes of a frame
                         // then store to 16 distinct bank pairs (the same path for every lane put
                         // the 16 stores on 2 bank pairs: 8-way conflicts)
-                        const int p = (p0 + e) & (LMAX - 1);
+                        const int p = npaths == LMAX ? (p0 + e) & (LMAX - 1) : p0;
                         uint64_t x1 = 0;
                         uint32_t x2 = 0, x3 = 0;
                         if (r1 || r2 || r3) {
@@ -357,7 +365,8 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                         double d2[2];
 #pragma unroll
                         for (int s2 = 0; s2 < 2; ++s2)
-                            d2[s2] = r2 ? g_node_wbit(d1[s2], d1[s2 + 2], x2, (uint32_t)(e + 16 * s2)) : f_minsum(d1[s2], d1[s2 + 2]);
+                            d2[s2] = shared2 ? d2s[s2]
+                                     : (r2 ? g_node_wbit(d1[s2], d1[s2 + 2], x2, (uint32_t)(e + 16 * s2)) : f_minsum(d1[s2], d1[s2 + 2]));
                         const double d3 = r3 ? g_node_wbit(d2[0], d2[1], x3, (uint32_t)e) : f_minsum(d2[0], d2[1]);
                         Af[Ly::OFF3 + Ly::at(16, e, p)] = d3;
                     }
