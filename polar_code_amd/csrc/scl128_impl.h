@@ -134,7 +134,7 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 // Timing-only ablations of the screening kernel (tools/build_variant.py --spec 1_8
 // -DPSCL_APX_ABLATE=m); 0 in the product.  1: tail -> |lam| * 2^-20; 2: no depth-1..3
 // recompute; 4: no depth-4..6 steps; 8: full-list info phases always take the fast path;
-// 16: no final-order certification
+// 16: no final-order certification; 32: full-list info phases always rank
 #ifndef PSCL_APX_ABLATE
 #define PSCL_APX_ABLATE 0
 #endif
@@ -454,7 +454,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                         mx = o > mx ? o : mx;
                     });
                     const uint64_t badm = wmask(near_or_below(mx, hiw(mb)));
-                    if ((PSCL_APX_ABLATE & 8) || (badm & vmask & KPATH) == 0) {
+                    if (!(PSCL_APX_ABLATE & 32) && ((PSCL_APX_ABLATE & 8) || (badm & vmask & KPATH) == 0)) {
                         // (lam != +-0 here: a zero LLR gives mbd == mgd, never clear of the margin,
                         // so the sign bit is the better child's bit)
                         const uint32_t gb = sign_bit(lam);
