@@ -53,7 +53,9 @@ extern "C" {
 #define PSCL_EPRUNED -4  /* "All paths pruned during decoding" (cannot happen for valid input) */
 #define PSCL_EUNSUP -5   /* configuration outside what the kernels implement (N, L, CRC degree) */
 
-#define PSCL_MAX_N 128   /* code length N: power of two, 2..128 (every BASELINE config is N=128) */
+#define PSCL_MAX_N 1024  /* code length N: power of two, 2..1024 (N <= 128: the specialised kernels,
+                            every BASELINE config; 256..1024: one wavefront per frame, global scratch;
+                            the device TX chain and DL-SCL loop stop at 128) */
 #define PSCL_MAX_L 32    /* list size M/L: 1..32 (2L candidates fit one 64-lane wavefront) */
 #define PSCL_MAX_CRC 32  /* CRC degree: 1..32 */
 #define PSCL_WORDS(K) (((K) + 63) / 64)

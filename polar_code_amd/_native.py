@@ -24,7 +24,7 @@ PSCL_EDEVICE = -2
 PSCL_ENOMEM = -3
 PSCL_EPRUNED = -4
 PSCL_EUNSUP = -5
-PSCL_MAX_N = 128
+PSCL_MAX_N = 1024
 PSCL_MAX_L = 32
 PSCL_FLAG_CRC_PASS = 0x80
 PSCL_FLAG_IDX_MASK = 0x3F

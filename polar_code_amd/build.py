@@ -23,7 +23,7 @@ LIB = PKG / "libpolar_mi355x.so"
 ARCH = os.environ.get("PSCL_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-HIP_SOURCES = ["scl_kernels.hip", "scl128.hip", "scl128_spec.hip", "dlscl.hip", "capi.cpp"]
+HIP_SOURCES = ["scl_kernels.hip", "scl128.hip", "scl128_spec.hip", "scl_long.hip", "dlscl.hip", "capi.cpp"]
 HIP_DEPS = HIP_SOURCES + ["scl_kernels.h", "scl_device.h", "scl128_impl.h", "glibc_softplus.h", "exp_table.inc"]
 # scl128_spec.hip is compiled once per (information-set code, list size): 8 objects
 SPEC_UNITS = [(c, l) for c in (1, 2) for l in (1, 2, 4, 8)]
@@ -102,7 +102,12 @@ def build_hip(force: bool = False) -> Path:
         return LIB
     objdir = PKG / "_build"
     objdir.mkdir(exist_ok=True)
-    objs = compile_units(hip_units(objdir, hash_=want), [])
+    units = hip_units(objdir, hash_=want)
+    headers = [*CSRC.glob("*.h"), *CSRC.glob("*.inc"), *INCLUDE.glob("*.h")]
+    # the hash enters capi.cpp only; other objects are reused when newer than their inputs
+    todo = [u for u in units if force or u[0].name == "capi.cpp" or _stale(u[2], [u[0], *headers])]
+    compile_units(todo, [])
+    objs = [str(u[2]) for u in units]
     tmp = LIB.with_suffix(".so.tmp")
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", str(tmp)])
     os.replace(tmp, LIB)

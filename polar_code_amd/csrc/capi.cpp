@@ -84,7 +84,9 @@ struct pscl_handle {
     int device = 0;
     int N = 0, n = 0, K = 0, L = 0, W = 1, crc_deg = 0;
     uint64_t crc_poly = 0;
-    uint64_t info_mask[2] = {0, 0};
+    uint64_t info_mask[2] = {0, 0};   // phases 0..127 (the N <= 128 kernels)
+    std::vector<uint64_t> info_words;  // [N/64 or 1] every phase (scl_long.hip)
+    uint64_t* d_info_words = nullptr;
     std::vector<int32_t> info_set;
     std::vector<uint32_t> check_cols;   // [K]
     std::vector<uint32_t> attach_cols;  // [K - deg]
@@ -144,6 +146,7 @@ void fill_decode_params(const pscl_handle* h, pscl_decode_params& P, int hist) {
     P.W = h->W;
     P.info_mask[0] = h->info_mask[0];
     P.info_mask[1] = h->info_mask[1];
+    P.info_words = h->d_info_words;
     P.crc_cols = h->d_check_cols;
     P.info_set = h->d_info_set;
     P.has_crc = h->crc_poly != 0;
@@ -155,8 +158,15 @@ void fill_decode_params(const pscl_handle* h, pscl_decode_params& P, int hist) {
     pscl_decode_layout(P, hist);
 }
 
-int launch_decode(pscl_handle* h, const pscl_decode_params& P, int hist, hipStream_t st = nullptr) {
+int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStream_t st = nullptr) {
     if (!st) st = h->stream;
+    pscl_decode_params P = P0;
+    if (P.long_mode) {  // global scratch of every workgroup in flight (scl_long.hip)
+        void* d_scr;
+        const int rc = ensure(h, 38, (size_t)pscl_decode_grid(P) * (size_t)P.long_block_bytes, &d_scr);
+        if (rc) return rc;
+        P.long_scratch = (unsigned char*)d_scr;
+    }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->timing) {
         while (h->ev_pool.size() < h->ev_used + 2) {
@@ -240,14 +250,16 @@ int pscl_create(pscl_handle** out, int device, int N, const int32_t* info_set, i
     while ((1 << tmp.n) < N) tmp.n++;
     tmp.K = K;
     tmp.L = L;
-    tmp.W = K > 64 ? 2 : 1;
+    tmp.W = K > 64 ? (K + 63) / 64 : 1;
     tmp.crc_poly = crc_poly;
+    tmp.info_words.assign((size_t)(N >= 64 ? N / 64 : 1), 0ULL);
     for (int i = 0; i < K; ++i) {
         int p = info_set[i];
         if (p < 0 || p >= N) return fail(PSCL_EINVAL, "info_set indices out of range");
         uint64_t bit = 1ULL << (p & 63);
-        if (tmp.info_mask[p >> 6] & bit) return fail(PSCL_EUNSUP, "duplicate info_set index %d", p);
-        tmp.info_mask[p >> 6] |= bit;
+        if (tmp.info_words[(size_t)(p >> 6)] & bit) return fail(PSCL_EUNSUP, "duplicate info_set index %d", p);
+        tmp.info_words[(size_t)(p >> 6)] |= bit;
+        if (p < PSCL_FAST_N) tmp.info_mask[p >> 6] |= bit;
         tmp.info_set.push_back(p);
     }
     // The decoder visits info phases in increasing phase order; candidate bit j belongs to
@@ -302,6 +314,8 @@ int pscl_create(pscl_handle** out, int device, int N, const int32_t* info_set, i
     CREATE_TRY(hipMalloc(&h->d_attach_cols, h->attach_cols.size() * 4));
     CREATE_TRY(hipMalloc(&h->d_info_set, (size_t)(K > 0 ? K : 1) * 4));
     CREATE_TRY(hipMalloc(&h->d_exp_table, sizeof(kExpTable)));
+    CREATE_TRY(hipMalloc(&h->d_info_words, h->info_words.size() * 8));
+    CREATE_TRY(hipMemcpy(h->d_info_words, h->info_words.data(), h->info_words.size() * 8, hipMemcpyHostToDevice));
     CREATE_TRY(hipMemcpy(h->d_check_cols, h->check_cols.data(), h->check_cols.size() * 4, hipMemcpyHostToDevice));
     CREATE_TRY(hipMemcpy(h->d_attach_cols, h->attach_cols.data(), h->attach_cols.size() * 4, hipMemcpyHostToDevice));
     if (K > 0) CREATE_TRY(hipMemcpy(h->d_info_set, h->info_set.data(), (size_t)K * 4, hipMemcpyHostToDevice));
@@ -336,7 +350,7 @@ int pscl_create(pscl_handle** out, int device, int N, const int32_t* info_set, i
         CREATE_TRY(hipMalloc(&h->d_epi, epi.size()));
         CREATE_TRY(hipMemcpy(h->d_epi, epi.data(), epi.size(), hipMemcpyHostToDevice));
     }
-    {
+    if (N <= PSCL_FAST_N) {
         // TX tables: encode and CRC attach are GF(2)-linear, so byte-wise tables give them in
         // ceil(K/8) (resp. ceil(kp/8)) lookups per frame
         const int nb = (K + 7) / 8, kp = K - h->crc_deg, nbp = (kp + 7) / 8;
@@ -391,6 +405,7 @@ int pscl_destroy(pscl_handle* h) {
     if (h->d_attach_cols) hipFree(h->d_attach_cols);
     if (h->d_info_set) hipFree(h->d_info_set);
     if (h->d_exp_table) hipFree(h->d_exp_table);
+    if (h->d_info_words) hipFree(h->d_info_words);
     if (h->d_rm_src) hipFree(h->d_rm_src);
     if (h->d_rm_order) hipFree(h->d_rm_order);
     if (h->d_beta) hipFree(h->d_beta);
@@ -458,6 +473,7 @@ int pscl_path_llrs_device(pscl_handle* h, const double* d_llr, int64_t B, const 
     if (B < 0) return fail(PSCL_EINVAL, "B must be >= 0");
     if (B == 0) return PSCL_OK;
     if (!d_llr || !d_bits || !d_out) return fail(PSCL_EINVAL, "d_llr, d_bits and d_out are required");
+    if (h->N > PSCL_FAST_N) return fail(PSCL_EUNSUP, "decision-LLR replay supports N <= %d", PSCL_FAST_N);
     if (B > INT32_MAX) return fail(PSCL_EUNSUP, "B exceeds 2^31-1");
     int rc = set_device(h);
     if (rc) return rc;
@@ -610,6 +626,7 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
     if (B < 0) return fail(PSCL_EINVAL, "B must be >= 0");
     if (B == 0) return PSCL_OK;
     if (!d_llr || !d_best || !d_flags) return fail(PSCL_EINVAL, "d_llr, d_best and d_flags are required");
+    if (h->N > PSCL_FAST_N) return fail(PSCL_EUNSUP, "the device DL-SCL loop supports N <= %d (use the host-ranked form)", PSCL_FAST_N);
     if (d_ref && (!d_counters_scl || !d_counters_dl)) return fail(PSCL_EINVAL, "d_ref given without both counters");
     if (k_payload < 0 || k_payload > h->K) return fail(PSCL_EINVAL, "k_payload out of range");
     const int rounds = h->crc_poly && retries > 0 ? (retries < h->K ? retries : h->K) : 0;
@@ -847,6 +864,7 @@ int pscl_channel_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, doubl
     if (!(rate > 0)) return fail(PSCL_EINVAL, "rate must be positive");
     if (k_payload + h->crc_deg != h->K || k_payload < 0)
         return fail(PSCL_EINVAL, "k_payload (%d) + crc degree (%d) must equal K (%d)", k_payload, h->crc_deg, h->K);
+    if (h->N > PSCL_FAST_N) return fail(PSCL_EUNSUP, "the device TX chain supports N <= %d", PSCL_FAST_N);
     int rc = set_device(h);
     if (rc) return rc;
     pscl_channel_params P;

@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(256) dl_gather_kernel(const uint64_t* __restri
 // one wavefront per entry: leaf LLRs of the entry's path (bits given), written at its info
 // positions.  LDS: two 128-double level buffers per wave.
 __global__ void __launch_bounds__(256) replay_kernel(const pscl_replay_params R, int64_t cap) {
-    __shared__ double lvl[4][2][PSCL_MAX_N];
+    __shared__ double lvl[4][2][PSCL_FAST_N];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t b = (int64_t)blockIdx.x * 4 + wave;
     if (b >= *R.count || b >= cap) return;

@@ -8,6 +8,9 @@
 #include "polar_scl.h"
 
 #define PSCL_MAX_WAVES_PER_WG 4
+// code length of the specialised, DL-SCL replay and TX kernels; longer codes decode in
+// scl_long.hip
+#define PSCL_FAST_N 128
 // 1: the scl128 epilogue tables (u-byte gather, CRC syndrome) are staged in LDS per workgroup;
 // 0: read from global memory
 #ifndef PSCL_EPI_LDS
@@ -54,6 +57,12 @@ struct pscl_decode_params {
     int out_by_row;              // 1: outputs, reference words and counts at LLR row fidx[b]
     int64_t grid_cap;            // 0, or an upper bound on the workgroups of the launch (the
                                  // kernels stride over frames; a d_count launch of few frames)
+    // code lengths above 128 (scl_long.hip): information set as N/64 words, and the global
+    // scratch of one workgroup per frame in flight
+    const uint64_t* info_words;  // [N/64] (device)
+    unsigned char* long_scratch;  // [grid][long_block_bytes]
+    int64_t long_block_bytes;
+    int long_mode;               // 1: N > PSCL_FAST_N, scl_long.hip
 };
 
 // Decision-LLR replay (dlscl.hip): leaf LLRs of a known path, recomputed top-down
@@ -111,6 +120,10 @@ struct pscl_channel_params {
 };
 
 int pscl_decode_lmax(int L);
+// scl_long.hip (N = 256 .. 1024)
+int64_t pscl_long_block_bytes(int N, int L, int K, int hist);
+int64_t pscl_long_grid(int64_t B);
+hipError_t pscl_launch_long(const pscl_decode_params& P, int hist, hipStream_t s);
 // fills P.a_bytes / P.wave_bytes / P.fast for the kernel that will decode this shape
 void pscl_decode_layout(pscl_decode_params& P, int hist);
 int pscl_fast128_fstride(int L, int ch);

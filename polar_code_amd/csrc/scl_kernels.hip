@@ -418,6 +418,7 @@ __global__ void __launch_bounds__(256) channel_kernel(const pscl_channel_params 
 // wavefronts per workgroup: the choice that keeps the most wavefronts resident per CU
 // under the 160 KB LDS budget (each workgroup also holds the 2 KB exp table); 0 if none fits
 int pscl_decode_wpg(const pscl_decode_params& P) {
+    if (P.long_mode) return 1;  // one wavefront per workgroup, state in global scratch
     const int cu_lds = 160 * 1024, tbl = P.wg_fixed_bytes;
     int best = 0, best_res = 0;
     for (int w = 1; w <= PSCL_MAX_WAVES_PER_WG; ++w) {
@@ -460,6 +461,7 @@ int pscl_decode_lmax(int L) {
 }
 
 int64_t pscl_decode_grid(const pscl_decode_params& P) {
+    if (P.long_mode) return pscl_long_grid(P.grid_cap > 0 && P.grid_cap < P.B ? P.grid_cap : P.B);
     const int per_wg = pscl_decode_wpg(P) * (32 / pscl_decode_lmax(P.L));  // frames per workgroup
     int64_t g = (P.B + per_wg - 1) / per_wg;
     const int64_t cap = P.grid_cap > 0 && P.grid_cap < (1 << 20) ? P.grid_cap : (1 << 20);
@@ -468,6 +470,13 @@ int64_t pscl_decode_grid(const pscl_decode_params& P) {
 
 void pscl_decode_layout(pscl_decode_params& P, int hist) {
     const int lmax = pscl_decode_lmax(P.L);
+    P.long_mode = P.N > PSCL_FAST_N ? 1 : 0;
+    if (P.long_mode) {
+        P.fast = 0;
+        P.wg_fixed_bytes = P.wave_bytes = P.a_bytes = 0;
+        P.long_block_bytes = pscl_long_block_bytes(P.N, P.L, P.K, hist);
+        return;
+    }
     const int F = 32 / lmax;  // frames per wavefront
     P.fast = (P.N == 128 && P.L <= 8) ? 1 : 0;
     // exp table (exact metric tails; the screening launch, P.apx, has none) + scl128 epilogue tables
@@ -486,6 +495,7 @@ void pscl_decode_layout(pscl_decode_params& P, int hist) {
 }
 
 hipError_t pscl_launch_decode(const pscl_decode_params& P, int hist, hipStream_t s) {
+    if (P.long_mode) return pscl_launch_long(P, hist, s);
     if (pscl_decode_wpg(P) < 1) return hipErrorInvalidValue;
     const int64_t grid = pscl_decode_grid(P);
     if (P.fast) return pscl_launch_decode128(P, hist, pscl_decode_wpg(P), grid, decode_lds_bytes(P, hist), s);

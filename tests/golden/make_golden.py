@@ -20,6 +20,7 @@ Fixture sets:
   G11 run_ber_sweep rows                                           eval/run_ber_sweep.py
   G12 make_dataset shards (abs_l0, flip_idx, meta)                 train/make_dataset.py:24-121
   G13 train_beta on the G12 shard (CPU, one thread): beta + log      train/train_beta.py:64-161
+  G14 longer codes: decode_scl at N in {256, 512, 1024} (incl. forced bits) and sc_decode at N=256
 """
 from __future__ import annotations
 
@@ -325,6 +326,19 @@ def g13():
     np.savez_compressed(OUT / "g13_train_beta.npz", **d)
 
 
+def g14():
+    """Code lengths above 128 (decode_scl accepts any power of two, scl.py:25-30)."""
+    decode_set("g14_n256", 256, 128, [1, 4, 8], [2.0], 6, seed=140)
+    decode_set("g14_n256_forced", 256, 128, [4], [2.5], 4, seed=141, force_fn=force_prefix_flip)
+    decode_set("g14_n512", 512, 256, [2, 8], [2.0], 3, seed=142)
+    decode_set("g14_n1024", 1024, 512, [4], [2.0], 2, seed=143)
+    info = construct_info_set(256, 128)
+    rng = np.random.default_rng(144)
+    llr = np.stack([rng.normal(1.0, 2.0, 256) for _ in range(8)])
+    bits = np.stack([sc_decode(x, info) for x in llr])
+    np.savez_compressed(OUT / "g14_sc256.npz", info=info, llr=llr, bits=bits)
+
+
 def main():
     if len(sys.argv) > 1:
         for name in sys.argv[1:]:
@@ -350,6 +364,7 @@ def main():
     g11()
     g12()
     g13()
+    g14()
     for p in sorted(OUT.glob("*.npz")):
         print(p.name, p.stat().st_size)
 

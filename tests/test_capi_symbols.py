@@ -42,4 +42,4 @@ def test_argument_errors_map_to_reference_exceptions():
     with pytest.raises(ValueError):
         _native.Decoder(128, list(range(10)), 4, "0x1864CFB")  # K <= CRC degree
     with pytest.raises(NotImplementedError):
-        _native.Decoder(256, list(range(10)), 4, None)
+        _native.Decoder(2048, list(range(10)), 4, None)  # N > PSCL_MAX_N = 1024

@@ -9,7 +9,8 @@ import pytest
 import oracle
 
 DECODE_SETS = ["g4_decode.npz", "g6_forced.npz", "g10_n16.npz", "g10_n32.npz", "g10_n64_nocrc.npz",
-               "g10_k88.npz", "g10_m16.npz", "g10_n8.npz", "g10_n4.npz", "g10_n2.npz"]
+               "g10_k88.npz", "g10_m16.npz", "g10_n8.npz", "g10_n4.npz", "g10_n2.npz",
+               "g14_n256.npz", "g14_n256_forced.npz", "g14_n512.npz", "g14_n1024.npz"]
 
 
 def test_info_sets(golden):
@@ -77,6 +78,12 @@ def test_decode_ties(golden):
 
 def test_sc_decode(golden):
     g = golden("g9_sc.npz")
+    for llr, bits in zip(g["llr"], g["bits"]):
+        np.testing.assert_array_equal(oracle.sc_decode(llr, g["info"]), bits)
+
+
+def test_sc_decode_n256(golden):
+    g = golden("g14_sc256.npz")
     for llr, bits in zip(g["llr"], g["bits"]):
         np.testing.assert_array_equal(oracle.sc_decode(llr, g["info"]), bits)
 

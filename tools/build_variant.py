@@ -22,11 +22,18 @@ if "--spec" in flags:
 out = ROOT / "tools" / "_variant"
 objdir = out / f"obj_{name}"
 objdir.mkdir(parents=True, exist_ok=True)
+unit = None
+if "--unit" in flags:  # recompile one non-spec source (e.g. scl_long) with the flags
+    i = flags.index("--unit")
+    unit = flags[i + 1] + ".o"
+    flags = flags[:i] + flags[i + 2:]
 if spec:
+    unit = f"scl128_spec_{spec}.o"
+if unit:
     units = B.hip_units(objdir)
-    mine = [u for u in units if u[2].name == f"scl128_spec_{spec}.o"]
+    mine = [u for u in units if u[2].name == unit]
     objs = B.compile_units(mine, flags)
-    objs += [str(B.PKG / "_build" / u[2].name) for u in units if u[2].name != f"scl128_spec_{spec}.o"]
+    objs += [str(B.PKG / "_build" / u[2].name) for u in units if u[2].name != unit]
 else:
     objs = B.compile_units(B.hip_units(objdir), flags)
 subprocess.check_call([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", *objs, "-o", str(out / f"lib_{name}.so")])
