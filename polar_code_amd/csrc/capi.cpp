@@ -183,7 +183,7 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
     // forced bits or row indirection requested) run as a screening decode plus an exact
     // re-decode of the frames it could not certify; the two launches count as one decode.
     const bool screen = h->screen && P.fast && !hist && !P.metrics && !P.cands && !P.force && !P.sc_hard && !P.fidx &&
-                        !P.d_count;
+                        !P.d_count && pscl_screening_available(P);
     hipError_t err;
     if (screen) {
         void *d_cnt, *d_list;

@@ -56,6 +56,7 @@ hipError_t launch128(const pscl_decode_params& P, int hist, int wpg, int64_t gri
             default: return pscl_launch_spec_2_8(P, fs, wpg, grid, lds, s);
         }
     }
+    if (P.apx) return hipErrorInvalidValue;  // screening exists for the compiled-in codes only
     if (P.rm_E)
         return fs ? launch128k<LMAX, false, true, true>(P, wpg, grid, lds, s)
                   : launch128k<LMAX, false, true, false>(P, wpg, grid, lds, s);
@@ -65,6 +66,14 @@ hipError_t launch128(const pscl_decode_params& P, int hist, int wpg, int64_t gri
 
 }  // namespace
 
+
+// the launch launch128 makes for a plain decode (no history, no forced bits) has a screening
+// form: a compiled-in code in its own input mode with a full-size list
+int pscl_screening_available(const pscl_decode_params& P) {
+    if (!P.fast || P.force || P.sc_hard || P.L != pscl_decode_lmax(P.L)) return 0;
+    const int code = spec_code(P);
+    return (code == 1 && !P.rm_E) || (code == 2 && P.rm_E);
+}
 
 int pscl_fast128_fstride(int L, int ch) {
     switch (pscl_decode_lmax(L)) {

@@ -127,6 +127,7 @@ hipError_t pscl_launch_long(const pscl_decode_params& P, int hist, hipStream_t s
 // fills P.a_bytes / P.wave_bytes / P.fast for the kernel that will decode this shape
 void pscl_decode_layout(pscl_decode_params& P, int hist);
 int pscl_fast128_fstride(int L, int ch);
+int pscl_screening_available(const pscl_decode_params& P);  // scl128.hip
 hipError_t pscl_launch_decode128(const pscl_decode_params& P, int hist, int wpg, int64_t grid, int lds, hipStream_t s);
 int64_t pscl_decode_grid(const pscl_decode_params& P);
 int pscl_decode_wpg(const pscl_decode_params& P);

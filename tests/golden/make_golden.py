@@ -21,6 +21,7 @@ Fixture sets:
   G12 make_dataset shards (abs_l0, flip_idx, meta)                 train/make_dataset.py:24-121
   G13 train_beta on the G12 shard (CPU, one thread): beta + log      train/train_beta.py:64-161
   G14 longer codes: decode_scl at N in {256, 512, 1024} (incl. forced bits) and sc_decode at N=256
+  G15 decode_with_retries on quantised LLRs (exact |L0| / q ties in the flip ranking)  flip.py:104-108
 """
 from __future__ import annotations
 
@@ -339,6 +340,41 @@ def g14():
     np.savez_compressed(OUT / "g14_sc256.npz", info=info, llr=llr, bits=bits)
 
 
+def g15():
+    """Flip-ranking ties: LLRs quantised to a few levels make many decision LLRs |L0| equal
+    (min-sum picks the same channel magnitudes), so np.argsort's order among equal keys
+    decides the flip.  Also records which SIMD argsort this host's NumPy used."""
+    info = construct_info_set(128, 64)
+    beta4 = np.load(REF / "checkpoints" / "beta_M4.npy")
+    rng = np.random.default_rng(15)
+    frames = []
+    while len(frames) < 48:
+        msg = attach_crc(rng.integers(0, 2, size=40, dtype=np.int8), POLY)
+        llr = llr_awgn(rng, encode(msg), 3.0, 0.5)
+        llr = np.clip(np.round(llr / 3.0), -3, 3) * 3.0  # levels -9 .. 9, step 3
+        base = decode_scl(llr, info, 4, crc=POLY)
+        if not check_crc(base["best_path_bits"], POLY):
+            frames.append(llr)
+    simd = np.__config__.CONFIG["SIMD Extensions"]["found"] if hasattr(np, "__config__") else []
+    d = {"info": info, "beta": beta4, "llr": np.stack(frames), "numpy_simd": np.array(" ".join(map(str, simd))),
+         "numpy_version": np.array(np.__version__)}
+    for tag, beta in (("beta", beta4), ("none", None)):
+        bits, succ, att, tried = [], [], [], []
+        for llr in frames:
+            r = decode_with_retries(llr, info, 4, 8, crc=POLY, beta=beta)
+            bits.append(r["best_path_bits"])
+            succ.append(r["success"])
+            att.append(len(r["attempts"]))
+            t = np.full(8, -1, np.int32)
+            t[: len(r["tried_indices"])] = r["tried_indices"]
+            tried.append(t)
+        d[f"{tag}_bits"] = np.stack(bits)
+        d[f"{tag}_success"] = np.array(succ)
+        d[f"{tag}_attempts"] = np.array(att, np.int32)
+        d[f"{tag}_tried"] = np.stack(tried)
+    np.savez_compressed(OUT / "g15_dl_ties.npz", **d)
+
+
 def main():
     if len(sys.argv) > 1:
         for name in sys.argv[1:]:
@@ -365,6 +401,7 @@ def main():
     g12()
     g13()
     g14()
+    g15()
     for p in sorted(OUT.glob("*.npz")):
         print(p.name, p.stat().st_size)
 

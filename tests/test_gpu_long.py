@@ -72,6 +72,29 @@ def test_long_codes_match_oracle(N, K, M, ebno):
         assert bool(plain["crc_pass"][f]) == oracle.check_crc(c[b], POLY)
 
 
+def test_long_decode_with_retries_matches_oracle():
+    """DL-SCL (flip.py:65-141, beta None) at N = 256: the batched retry loop (forced decodes
+    with decision LLRs on the long-code kernel) against the oracle, frame by frame."""
+    from polar_code_amd.dlscl.flip import decode_with_retries_batch
+
+    N, K, M, retries = 256, 128, 4, 6
+    rng = np.random.default_rng(77)
+    info = construct_info_set(N, K)
+    B = 40
+    msg = attach_crc(rng.integers(0, 2, size=(B, K - 24), dtype=np.int8), POLY)
+    u = np.zeros((B, N), np.int8)
+    u[:, info] = msg
+    nv = 1.0 / (2.0 * K / N * 10 ** (3.5 / 10))
+    llr = 2.0 * ((1.0 - 2.0 * _polar_transform(u)) + rng.normal(0.0, np.sqrt(nv), size=(B, N))) / nv
+    out = decode_with_retries_batch(llr, info, M, retries, crc=POLY)
+    assert np.count_nonzero(out["attempts"] > 1) >= 3  # some frames exercise the retry loop
+    for f in range(B):
+        r = oracle.decode_with_retries(llr[f], info, M, retries, crc=POLY)
+        np.testing.assert_array_equal(out["best_bits"][f], r["bits"], err_msg=f"frame {f}")
+        assert bool(out["success"][f]) == r["success"] and out["attempts"][f] == r["attempts"], f
+        assert [int(t) for t in out["tried"][f] if t >= 0] == r["tried"], f
+
+
 def test_long_device_counters():
     """Device-buffer decode with in-kernel FER/BER counting at N = 512."""
     N, K, M = 512, 256, 4

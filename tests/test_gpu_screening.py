@@ -88,6 +88,31 @@ def test_screening_nr_rate_matched(M):
         np.testing.assert_array_equal(a["best_bits"][f], c[b])
 
 
+@pytest.mark.parametrize("K,E,M", [(64, 256, 4), (64, 100, 8), (88, 0, 8), (60, 0, 4), (64, 0, 3)])
+def test_plain_decode_without_screening_form(K, E, M):
+    """Codes and modes with no compiled-in screening kernel ((128,64) rate matched, (128,88)
+    unmatched, other information sets, L below its power of two) decode exactly: plain
+    outputs equal the oracle's and no screening pass runs."""
+    from polar_code_amd.nr.polar import derate_match_polar, subblock_deinterleave
+
+    rng = np.random.default_rng(7400 + K + E + M)
+    info = construct_info_set(128, K)
+    B = 600
+    llr = (_frames(rng, B, info, 3.0, K=K) if not E
+           else rng.normal(2.0, 3.0, size=(B, E)) * rng.choice([1.0, -1.0], size=(B, E), p=[0.9, 0.1]))
+    dec = _native.Decoder(128, info, M, POLY)
+    if E:
+        dec.set_rate_match(E)
+    a = _plain(dec, llr)
+    assert dec.screening_count() == 0
+    for f in range(0, B, 5):
+        x = subblock_deinterleave(derate_match_polar(llr[f], 128), 128) if E else llr[f]
+        n, c, m, il, b = oracle.decode_scl(x, info, M, crc=POLY)
+        assert a["n_paths"][f] == n and a["best_idx"][f] == b, f
+        np.testing.assert_array_equal(a["best_bits"][f], c[b], err_msg=f"f={f}")
+        assert bool(a["crc_pass"][f]) == oracle.check_crc(c[b], POLY), f
+
+
 def test_screening_device_counters_equal_exact():
     """Device path with in-kernel FER/BER counting (the bench's step): deferred frames are
     counted by the exact re-decode at their own rows, once."""
