@@ -20,6 +20,8 @@
  *   pscl_dlscl_device           <- decode_with_retries dl_scl_polar/dlscl/flip.py:65-141 over
  *                                  a device batch (+ pscl_set_beta: the beta checkpoint)
  *   pscl_path_llrs_device       <- best_path_info_llrs / info_llrs of given paths (scl.py:158,166)
+ *   pscl_simulate               <- one SNR point of run_sweep (run_fer_sweep.py:41-191): TX,
+ *                                  uncoded baseline, SCL + DL-SCL, counters, in one call
  *
  * Conventions
  *   - Plain pointers and sizes only; no torch/HIP types in signatures (streams are void*).
@@ -224,6 +226,17 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
                       const uint64_t* d_ref, int k_payload, int64_t* d_counters_scl, int64_t* d_counters_dl);
 
 /* Device scratch helpers so that non-torch callers can drive the device path. */
+/*
+ * One call per SNR point (the frame loop of run_fer_sweep.py:41-191 for global frames
+ * [frame0, frame0 + B)): pscl_channel_device, the optional uncoded baseline
+ * (pscl_uncoded_device) and SCL + DL-SCL (pscl_dlscl_device, beta from pscl_set_beta) over
+ * chunks of up to 2^20 frames in handle scratch, counted on the device.  Synchronous.
+ *   counters  out, host int64[3][PSCL_NCOUNT]: rows SCL, DL-SCL, uncoded (PSCL_CNT_* layout)
+ * Counts depend only on (seed, stream_id, frame range): shards add up exactly.
+ */
+int pscl_simulate(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
+                  int64_t frame0, int64_t B, int retries, int include_uncoded, int64_t* counters);
+
 int pscl_device_alloc(pscl_handle* h, void** d_ptr, int64_t bytes);
 int pscl_device_free(pscl_handle* h, void* d_ptr);
 int pscl_memcpy_htod(pscl_handle* h, void* d_dst, const void* src, int64_t bytes);

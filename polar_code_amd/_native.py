@@ -39,7 +39,7 @@ EXPORTS = (
     "pscl_decode_device", "pscl_channel_device", "pscl_device_alloc", "pscl_device_free",
     "pscl_memcpy_htod", "pscl_memcpy_dtoh", "pscl_memset_device", "pscl_timing_enable",
     "pscl_timing_read", "pscl_launch_info", "pscl_set_rate_match", "pscl_set_beta", "pscl_dlscl_device",
-    "pscl_path_llrs_device", "pscl_uncoded_device", "pscl_set_screening", "pscl_build_hash",
+    "pscl_path_llrs_device", "pscl_uncoded_device", "pscl_simulate", "pscl_set_screening", "pscl_build_hash",
     "pscl_screening_count", "pscl_softplus_tails_device",
 )
 
@@ -119,6 +119,7 @@ def lib() -> C.CDLL:
         "pscl_set_beta": (C.c_int, [_vp, _vp]),
         "pscl_path_llrs_device": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
         "pscl_uncoded_device": (C.c_int, [_vp, _u64, C.c_uint32, _dbl, C.c_int, _i64, _i64, _vp]),
+        "pscl_simulate": (C.c_int, [_vp, _u64, C.c_uint32, _dbl, _dbl, C.c_int, _i64, _i64, C.c_int, C.c_int, _vp]),
         "pscl_dlscl_device": (C.c_int, [_vp, _vp, _i64, C.c_int, _vp, _vp, _vp, _vp, C.c_int, _vp, C.c_int, _vp,
                                         _vp]),
     }
@@ -326,6 +327,17 @@ class Decoder:
 
     def sync(self) -> None:
         check(lib().pscl_sync(self._h))
+
+    def simulate(self, seed: int, stream_id: int, ebno_db: float, rate: float, k_payload: int, frame0: int, B: int,
+                 retries: int, include_uncoded: bool = False) -> np.ndarray:
+        """One SNR point in one call (pscl_simulate): int64 counters [3, PSCL_NCOUNT], rows
+        SCL, DL-SCL, uncoded."""
+        out = np.zeros((3, PSCL_NCOUNT), np.int64)
+        with self._lock:
+            check(lib().pscl_simulate(self._h, int(seed) & (2**64 - 1), int(stream_id) & 0xFFFFFFFF, float(ebno_db),
+                                      float(rate), int(k_payload), int(frame0), int(B), int(retries),
+                                      int(bool(include_uncoded)), out.ctypes.data))
+        return out
 
     def screening_count(self) -> int:
         """Frames the last screening decode handed to the exact re-decode (synchronizes)."""

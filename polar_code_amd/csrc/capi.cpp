@@ -855,6 +855,43 @@ int pscl_uncoded_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, doubl
     return PSCL_OK;
 }
 
+int pscl_simulate(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
+                  int64_t frame0, int64_t B, int retries, int include_uncoded, int64_t* counters) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    if (!counters) return fail(PSCL_EINVAL, "counters is NULL");
+    if (B < 0 || frame0 < 0) return fail(PSCL_EINVAL, "B and frame0 must be >= 0");
+    memset(counters, 0, sizeof(int64_t) * 3 * PSCL_NCOUNT);
+    if (B == 0) return PSCL_OK;
+    int rc = set_device(h);
+    if (rc) return rc;
+    // chunks of at most 2^20 frames through handle scratch: 8 KB of LLRs per frame in flight
+    const int64_t chunk = B < (1 << 20) ? B : (1 << 20);
+    const int W = h->W, N = h->N;
+    void *d_llr, *d_msg, *d_best, *d_flags, *d_cnt;
+    if ((rc = ensure(h, 30, (size_t)chunk * N * 8, &d_llr))) return rc;
+    if ((rc = ensure(h, 31, (size_t)chunk * W * 8, &d_msg))) return rc;
+    if ((rc = ensure(h, 32, (size_t)chunk * W * 8, &d_best))) return rc;
+    if ((rc = ensure(h, 33, (size_t)chunk, &d_flags))) return rc;
+    if ((rc = ensure(h, 34, sizeof(int64_t) * 3 * PSCL_NCOUNT, &d_cnt))) return rc;
+    int64_t* cs = (int64_t*)d_cnt;
+    HIP_TRY(hipMemsetAsync(d_cnt, 0, sizeof(int64_t) * 3 * PSCL_NCOUNT, h->stream));
+    for (int64_t f = 0; f < B; f += chunk) {
+        const int64_t n = B - f < chunk ? B - f : chunk;
+        if ((rc = pscl_channel_device(h, seed, stream_id, ebno_db, rate, k_payload, frame0 + f, n, (double*)d_llr,
+                                      (uint64_t*)d_msg)))
+            return rc;
+        if (include_uncoded &&
+            (rc = pscl_uncoded_device(h, seed, stream_id, ebno_db, k_payload, frame0 + f, n, cs + 2 * PSCL_NCOUNT)))
+            return rc;
+        if ((rc = pscl_dlscl_device(h, (const double*)d_llr, n, retries, (uint64_t*)d_best, (uint8_t*)d_flags, nullptr,
+                                    nullptr, 0, (const uint64_t*)d_msg, k_payload, cs, cs + PSCL_NCOUNT)))
+            return rc;
+    }
+    HIP_TRY(hipMemcpyAsync(counters, d_cnt, sizeof(int64_t) * 3 * PSCL_NCOUNT, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return PSCL_OK;
+}
+
 int pscl_channel_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
                         int64_t frame0, int64_t B, double* d_llr, uint64_t* d_msg) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");

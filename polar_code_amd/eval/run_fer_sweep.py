@@ -177,57 +177,60 @@ def _buffers(dec, n: int) -> _SweepBuffers:
     return buf
 
 
+def _add_common(c, cs, cu, n, K, payload_bits, include_uncoded):
+    c[C_FRAMES] += n
+    c[C_SCL_ERR] += int(cs[_native.CNT_FRAME_ERR])
+    c[C_SCL_BIT] += int(cs[_native.CNT_BIT_ERR])
+    c[C_BITS] += n * K
+    if include_uncoded:
+        c[C_UNC_ERR] += int(cu[_native.CNT_FRAME_ERR])
+        c[C_UNC_BIT] += int(cu[_native.CNT_BIT_ERR])
+        c[C_BITS_UNC] += n * payload_bits
+
+
 def _philox_block(c, seed, snr_db, frame0, n, info_set, M, crc, retries, beta, device, include_uncoded,
                   payload_bits, engine="device", slot=0):
     """n frames generated on the device; SCL, DL-SCL and the uncoded baseline counted there."""
     cfg = config.get_config()
     dec = _native.get_decoder(cfg.N, info_set, M, crc, device, slot=slot)
+    sid = int(round(snr_db * 10))
+    if engine == "device":  # TX, uncoded baseline, SCL + DL-SCL and counting: one library call
+        dec.set_beta(beta)
+        cs, cd, cu = dec.simulate(seed, sid, snr_db, cfg.K / cfg.N, payload_bits, frame0, n, retries, include_uncoded)
+        c[C_DL_ERR] += int(cd[_native.CNT_FRAME_ERR])
+        c[C_DL_BIT] += int(cd[_native.CNT_BIT_ERR])
+        c[C_DL_WORK] += int(cd[_native.CNT_RETRIES])
+        _add_common(c, cs, cu, n, cfg.K, payload_bits, include_uncoded)
+        return
+    # host engine: the GPU decodes and counts the baseline, flips are ranked with numpy
     W = dec.W
     buf = _buffers(dec, n)
     mem = buf.mem
     nc = _native.PSCL_NCOUNT
-    d_cs, d_cd, d_cu = buf.cnt, buf.cnt + nc * 8, buf.cnt + 2 * nc * 8
+    d_cs, d_cu = buf.cnt, buf.cnt + 2 * nc * 8
     mem.memset(buf.cnt, 0, 3 * nc * 8)
-    sid = int(round(snr_db * 10))
     dec.channel_device(seed, sid, snr_db, cfg.K / cfg.N, payload_bits, frame0, n, buf.llr, buf.msg)
     if include_uncoded:
         dec.uncoded_device(seed, sid, snr_db, payload_bits, frame0, n, d_cu)
-    if engine == "device":
-        dec.dlscl_device(buf.llr, n, retries, beta=beta, d_best=buf.best, d_flags=buf.flags, d_ref=buf.msg,
-                         k_payload=payload_bits, d_counters_scl=d_cs, d_counters_dl=d_cd)
-        cnt = mem.download(buf.cnt, 3 * nc * 8, np.int64).reshape(3, nc)
-        cs, cd, cu = cnt
-        c[C_DL_ERR] += int(cd[_native.CNT_FRAME_ERR])
-        c[C_DL_BIT] += int(cd[_native.CNT_BIT_ERR])
-        c[C_DL_WORK] += int(cd[_native.CNT_RETRIES])
+    dec.decode_device(buf.llr, n, d_best=buf.best, d_flags=buf.flags, d_ref=buf.msg, k_payload=payload_bits,
+                      d_counters=d_cs)
+    cs, _, cu = mem.download(buf.cnt, 3 * nc * 8, np.int64).reshape(3, nc)
+    flags = mem.download(buf.flags, n, np.uint8)
+    fail = np.flatnonzero((flags & _native.PSCL_FLAG_CRC_PASS) == 0)
+    dl_bit = int(cs[_native.CNT_BIT_ERR])
+    if fail.size and retries > 0:
+        llr_all = mem.download(buf.llr, n * cfg.N * 8, np.float64).reshape(n, cfg.N)
+        msg_f = words_to_bits(mem.download(buf.msg, n * W * 8, np.uint64).reshape(n, W)[fail], cfg.K)
+        base_f = words_to_bits(mem.download(buf.best, n * W * 8, np.uint64).reshape(n, W)[fail], cfg.K)
+        dl = decode_with_retries_batch(llr_all[fail], info_set, M, retries, crc=crc, beta=beta, device=device,
+                                       baseline={"best_bits": base_f, "crc_pass": np.zeros(fail.size, bool)})
+        c[C_DL_ERR] += int(np.count_nonzero(~dl["success"]))
+        dl_bit += int(np.count_nonzero(dl["best_bits"] != msg_f)) - int(np.count_nonzero(base_f != msg_f))
+        c[C_DL_WORK] += int((dl["attempts"] - 1).sum())
     else:
-        dec.decode_device(buf.llr, n, d_best=buf.best, d_flags=buf.flags, d_ref=buf.msg, k_payload=payload_bits,
-                          d_counters=d_cs)
-        cnt = mem.download(buf.cnt, 3 * nc * 8, np.int64).reshape(3, nc)
-        cs, cd, cu = cnt
-        flags = mem.download(buf.flags, n, np.uint8)
-        fail = np.flatnonzero((flags & _native.PSCL_FLAG_CRC_PASS) == 0)
-        dl_bit = int(cs[_native.CNT_BIT_ERR])
-        if fail.size and retries > 0:
-            llr_all = mem.download(buf.llr, n * cfg.N * 8, np.float64).reshape(n, cfg.N)
-            msg_f = words_to_bits(mem.download(buf.msg, n * W * 8, np.uint64).reshape(n, W)[fail], cfg.K)
-            base_f = words_to_bits(mem.download(buf.best, n * W * 8, np.uint64).reshape(n, W)[fail], cfg.K)
-            dl = decode_with_retries_batch(llr_all[fail], info_set, M, retries, crc=crc, beta=beta, device=device,
-                                           baseline={"best_bits": base_f, "crc_pass": np.zeros(fail.size, bool)})
-            c[C_DL_ERR] += int(np.count_nonzero(~dl["success"]))
-            dl_bit += int(np.count_nonzero(dl["best_bits"] != msg_f)) - int(np.count_nonzero(base_f != msg_f))
-            c[C_DL_WORK] += int((dl["attempts"] - 1).sum())
-        else:
-            c[C_DL_ERR] += int(fail.size)
-        c[C_DL_BIT] += dl_bit
-    c[C_FRAMES] += n
-    c[C_SCL_ERR] += int(cs[_native.CNT_FRAME_ERR])
-    c[C_SCL_BIT] += int(cs[_native.CNT_BIT_ERR])
-    c[C_BITS] += n * cfg.K
-    if include_uncoded:
-        c[C_UNC_ERR] += int(cu[_native.CNT_FRAME_ERR])
-        c[C_UNC_BIT] += int(cu[_native.CNT_BIT_ERR])
-        c[C_BITS_UNC] += n * payload_bits
+        c[C_DL_ERR] += int(fail.size)
+    c[C_DL_BIT] += dl_bit
+    _add_common(c, cs, cu, n, cfg.K, payload_bits, include_uncoded)
 
 
 def run_sweep(args: argparse.Namespace) -> List[Dict[str, float]]:

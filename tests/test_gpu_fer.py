@@ -8,10 +8,12 @@
 * --rng philox (on-device channel): FER within Monte-Carlo error of the reference.
 """
 import math
+from pathlib import Path
 
 import numpy as np
 import pytest
 
+from polar_code_amd import _native
 from polar_code_amd.dlscl.flip import decode_with_retries, decode_with_retries_batch, decode_with_retries_device
 from polar_code_amd.eval import run_fer_sweep
 
@@ -136,3 +138,31 @@ def test_device_retry_loop_chunked_pipeline(monkeypatch):
     np.testing.assert_array_equal(dev["attempts"], host["attempts"])
     np.testing.assert_array_equal(dev["best_bits"], host["best_bits"])
     assert dev["counters"]["dl"][1] == int((~host["success"]).sum())
+
+
+def test_simulate_one_call_equals_separate_calls():
+    """pscl_simulate (TX + uncoded + SCL + DL-SCL + counters in one call) equals the separate
+    device calls over the same frames, and frame ranges add up exactly."""
+    from polar_code_amd.polar.polar import construct_info_set
+
+    info = construct_info_set(128, 64)
+    dec = _native.Decoder(128, info, 4, "0x1864CFB")
+    beta = np.load(Path(__file__).resolve().parent / "golden" / "beta_M4.npy")
+    dec.set_beta(beta)
+    B, seed, sid, snr = 6000, 11, 40, 4.0
+    one = dec.simulate(seed, sid, snr, 0.5, 40, 0, B, 8, include_uncoded=True)
+    parts = dec.simulate(seed, sid, snr, 0.5, 40, 0, 2500, 8, True) + dec.simulate(seed, sid, snr, 0.5, 40, 2500,
+                                                                                   B - 2500, 8, True)
+    np.testing.assert_array_equal(one, parts)
+    nc = _native.PSCL_NCOUNT
+    with _native.DeviceArena(dec) as mem:
+        d_llr, d_msg = mem.alloc(B * 128 * 8), mem.alloc(B * 8)
+        d_best, d_flags, d_cnt = mem.alloc(B * 8), mem.alloc(B), mem.alloc(3 * nc * 8)
+        mem.memset(d_cnt, 0, 3 * nc * 8)
+        dec.channel_device(seed, sid, snr, 0.5, 40, 0, B, d_llr, d_msg)
+        dec.uncoded_device(seed, sid, snr, 40, 0, B, d_cnt + 2 * nc * 8)
+        dec.dlscl_device(d_llr, B, 8, beta=beta, d_best=d_best, d_flags=d_flags, d_ref=d_msg, k_payload=40,
+                         d_counters_scl=d_cnt, d_counters_dl=d_cnt + nc * 8)
+        sep = mem.download(d_cnt, 3 * nc * 8, np.int64).reshape(3, nc)
+    np.testing.assert_array_equal(one, sep)
+    assert one[0][0] == B and one[1][1] <= one[0][1] and one[2][0] == B

@@ -1,0 +1,67 @@
+"""The reference-side binding (integration/scl_mi355x.py) is a real,
+importable file: loaded here by path exactly as the reference would import it, and held to
+the reference's golden outputs (decode_scl g4/g6, sc_decode g9, decode_with_retries g7)."""
+import importlib.util
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+STUB = Path(__file__).resolve().parent.parent / "integration" / "scl_mi355x.py"
+POLY = "0x1864CFB"
+
+
+@pytest.fixture(scope="module")
+def stub():
+    spec = importlib.util.spec_from_file_location("scl_mi355x", STUB)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_stub_loads_and_validates_without_a_device(stub):
+    assert set(stub.__all__) == {"decode_scl", "sc_decode", "decode_with_retries_batch"}
+    with pytest.raises(ValueError):
+        stub.decode_scl(np.zeros(128), np.arange(64), 0)  # M <= 0 (scl.py:119-120)
+    with pytest.raises(ValueError):
+        stub.decode_scl(np.zeros(128), np.arange(64), 4, force_info_bits=np.zeros(3, np.int8))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["g4_decode.npz", "g6_forced.npz"])
+def test_stub_decode_scl_golden(stub, golden, name):
+    g = golden(name)
+    crc = str(g["crc"]) or None
+    for key in map(str, g["keys"]):
+        M = int(key.split("_")[0][1:])
+        for f in range(0, len(g[key + "_llr"]), 3):
+            force = g[key + "_force"][f] if key + "_force" in g.files else None
+            if force is not None and np.all(force == -1):
+                force = None
+            r = stub.decode_scl(g[key + "_llr"][f], g["info"], M, crc, force_info_bits=force)
+            n = int(g[key + "_npaths"][f])
+            assert len(r["candidates"]) == n
+            np.testing.assert_array_equal(np.stack(r["candidates"]), g[key + "_cands"][f][:n])
+            np.testing.assert_array_equal(np.array(r["metrics"]), g[key + "_metrics"][f][:n])
+            np.testing.assert_array_equal(np.stack(r["info_llrs"]), g[key + "_info_llrs"][f][:n])
+            b = int(g[key + "_best"][f])
+            np.testing.assert_array_equal(r["best_path_bits"], g[key + "_cands"][f][b])
+            np.testing.assert_array_equal(r["best_path_info_llrs"], g[key + "_info_llrs"][f][b])
+
+
+@pytest.mark.gpu
+def test_stub_sc_decode_golden(stub, golden):
+    g = golden("g9_sc.npz")
+    for llr, bits in zip(g["llr"], g["bits"]):
+        np.testing.assert_array_equal(stub.sc_decode(llr, g["info"]), bits)
+
+
+@pytest.mark.gpu
+def test_stub_decode_with_retries_golden(stub, golden):
+    g = golden("g7_flip.npz")
+    for tag, beta in (("beta", g["beta"]), ("none", None)):
+        r = stub.decode_with_retries_batch(g["llr"], g["info"], 4, 8, crc=POLY, beta=beta)
+        np.testing.assert_array_equal(r["best_path_bits"], g[f"{tag}_bits"])
+        np.testing.assert_array_equal(r["success"], g[f"{tag}_success"].astype(bool))
+        np.testing.assert_array_equal(r["attempts"], g[f"{tag}_attempts"])
+        assert r["tried_indices"] == [[int(t) for t in row if t >= 0] for row in g[f"{tag}_tried"]]
