@@ -86,21 +86,35 @@ __device__ __forceinline__ uint64_t seg_transform(uint64_t u0, uint64_t u1, int 
 // of its own frame and the elements e = 2k + h (h = g / LMAX) of the node's W values, so the
 // parent slot comes from the path's own slot table (tabp: upper lanes hold a copy) and no
 // lane reads another's state.  Inputs e and e + W of the parent are one pair (Layout128).
+//
+// Addresses: with e = 2k + h, input pair e of slot s sits at double2 (2k LMAX) + (h LMAX + s)
+// and (depths 4, 5) output element e of slot p at double 4k LMAX + 2 (h LMAX + p) (first half,
+// 2k < W/2) or 2 (2k - W/2) LMAX + 1 + 2 (h LMAX + p): one per-lane base, lb = Af + 2 (h LMAX + p)
+// doubles (= Af + 2g), serves every depth with compile-time offsets (depth 6 writes at 2p + h).
+// Spelled out so the compiler keeps one base register instead of hoisting a dozen per-depth
+// addresses out of the frame loop (register pressure sets the wave count).
 template <int LMAX, bool CH, int D>
-__device__ __forceinline__ void step_depth(double* Af, int g, uint32_t tabp, uint32_t xsp, bool first, bool is_g) {
+__device__ __forceinline__ void step_depth(double* Af, const double* lb, int g, uint32_t tabp, uint32_t xsp, bool first,
+                                           bool is_g) {
     using Ly = Layout128<LMAX, CH>;
     constexpr int LW = kn - D, W = 1 << LW, HW = W / 2;
     constexpr int OFF_OUT = D == 4 ? Ly::OFF4 : (D == 5 ? Ly::OFF5 : Ly::OFF6);
     constexpr int OFF_IN = D == 4 ? Ly::OFF3 : (D == 5 ? Ly::OFF4 : Ly::OFF5);
     const int p = g & (LMAX - 1), h = g >> Ly::LOG_LM;
-    const int ps = first ? slot_at(tabp, D - 1) : p;
-    const double2* par = reinterpret_cast<const double2*>(Af + OFF_IN) + ps;  // pair e of slot s: [e * LMAX + s]
+    // input base: the parent's slot (from the table at the first rewritten depth, else own)
+    const double* in = first ? Af + 2 * (h * LMAX + slot_at(tabp, D - 1)) : lb;
     const uint32_t xh = xsp >> h;
 #pragma unroll
     for (int k = 0; k < HW; ++k) {
-        const int e = 2 * k + h;
-        const double2 ab = par[e * LMAX];
-        Af[OFF_OUT + Ly::at(W, e, p)] = is_g ? g_node(ab.x, ab.y, (xh >> (2 * k)) & 1u) : f_minsum(ab.x, ab.y);
+        const double2 ab = *reinterpret_cast<const double2*>(in + OFF_IN + 4 * k * LMAX);
+        const double v = is_g ? g_node(ab.x, ab.y, (xh >> (2 * k)) & 1u) : f_minsum(ab.x, ab.y);
+        if constexpr (D == 6) {
+            Af[OFF_OUT + 2 * p + h] = v;
+        } else if (2 * k < HW) {
+            const_cast<double*>(lb)[OFF_OUT + 4 * k * LMAX] = v;
+        } else {
+            const_cast<double*>(lb)[OFF_OUT + 2 * (2 * k - HW) * LMAX + 1] = v;
+        }
     }
     wave_lds_fence();
 }
@@ -137,6 +151,11 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 // 16: no final-order certification; 32: full-list info phases always rank
 #ifndef PSCL_APX_ABLATE
 #define PSCL_APX_ABLATE 0
+#endif
+
+// 16-lane frames keep their 8 channel LLRs in registers across the depth-1..3 recomputes
+#ifndef PSCL_CREG
+#define PSCL_CREG 1
 #endif
 
 #ifndef PSCL_WAVES_PER_EU
@@ -213,7 +232,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
         // 16-lane frames (L = 8): lane g's 8 channel LLRs (elements g + 16 m) are the same at
         // all 8 depth-1..3 recomputes: loaded once per frame into registers, so the recomputes
         // wait on no memory (16 VGPRs; the in-place reads cost 25 % of the screening pass)
-        constexpr bool CREG = G == 16;
+        constexpr bool CREG = G == 16 && PSCL_CREG;
         double creg[CREG ? 8 : 1];
         if constexpr (CREG) {
             if (CH) wave_lds_fence();
@@ -383,10 +402,11 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 // (DPP evaluated by every lane first: inside ?: only the selected lanes would
                 // run it, and a DPP that reads an inactive lane gets 0)
                 const uint32_t tabp = tab;
+                const double* lb = Af + 2 * g;
                 const uint32_t xsp = merge_from_lower<G, LMAX>(xs, xs, lane);
-                if (start <= 4) step_depth<LMAX, CH, 4>(Af, g, tabp, xsp, start == 4, start == 4 && phi);
-                if (start <= 5) step_depth<LMAX, CH, 5>(Af, g, tabp, xsp, start == 5, start == 5);
-                if (start <= 6) step_depth<LMAX, CH, 6>(Af, g, tabp, xsp, start == 6, start == 6);
+                if (start <= 4) step_depth<LMAX, CH, 4>(Af, lb, g, tabp, xsp, start == 4, start == 4 && phi);
+                if (start <= 5) step_depth<LMAX, CH, 5>(Af, lb, g, tabp, xsp, start == 5, start == 5);
+                if (start <= 6) step_depth<LMAX, CH, 6>(Af, lb, g, tabp, xsp, start == 6, start == 6);
             }
             if (start <= 6) {  // this path's own slot at every depth rewritten this phase
                 // (same update in the upper lane's copy: cpath is the path of both lanes)
@@ -454,6 +474,17 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                         mx = o > mx ? o : mx;
                     });
                     const uint64_t badm = wmask(near_or_below(mx, hiw(mb)));
+#ifdef PSCL_STATS  // screening full-list info phases by the wave's worst frame: worse children
+                   // within the margin of the largest better child (0, 1, 2, >= 3) -> slots 12..15
+                    if (lane == 0 && P.counters) {
+                        int worst = 0;
+                        for (int fr = 0; fr < F; ++fr) {
+                            const int pc = __builtin_popcountll((badm & vmask & KPATH) >> (fr * G) & ((1ULL << LMAX) - 1));
+                            worst = pc > worst ? pc : worst;
+                        }
+                        atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + 12 + (worst < 3 ? worst : 3), 1ULL);
+                    }
+#endif
                     if (!(PSCL_APX_ABLATE & 32) && ((PSCL_APX_ABLATE & 8) || (badm & vmask & KPATH) == 0)) {
                         // (lam != +-0 here: a zero LLR gives mbd == mgd, never clear of the margin,
                         // so the sign bit is the better child's bit)

@@ -2,7 +2,9 @@
 
     PSCL_LIB_PATH=tools/_variant/lib_stats.so python tools/fastpath_stats.py [L] [ebno]
 Counters (per wavefront): [8] frozen phases, [9] frozen re-ranks skipped, [10] info phases on
-the full ranking path, [11] info phases kept in place.
+the full ranking path, [11] info phases kept in place (exact kernel); [12..15] screening
+full-list info phases by the wave's worst frame: 0, 1, 2, >= 3 worse children within the
+margin of the largest better child.
 """
 import os
 import sys
@@ -30,3 +32,6 @@ torch.cuda.synchronize()
 c = cnt.cpu().tolist()
 print(f"L={L} {ebno} dB: frozen {c[8]} skipped {c[9]} ({c[9] / max(c[8], 1):.1%}); info full {c[10]} "
       f"kept {c[11]} ({c[11] / max(c[10] + c[11], 1):.1%}); FER {c[1] / B:.4f}")
+tot = max(sum(c[12:16]), 1)
+print("screening full-list info phases (waves) by worst frame's near-worse children: " +
+      ", ".join(f"{k}: {c[12 + i]} ({c[12 + i] / tot:.1%})" for i, k in enumerate(["0", "1", "2", ">=3"])))
