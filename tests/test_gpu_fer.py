@@ -119,6 +119,25 @@ def test_philox_fer_matches_reference_statistically(tmp_path):
     assert abs(r["fer_uncoded"] - 0.218) < 0.01
 
 
+def test_config3_grid_sweep(tmp_path):
+    """BASELINE config 3's shape: L=8, 6 SNR points 4.0-6.5 dB, DL-SCL with beta_M8.  The
+    reference publishes only the 5 dB point (results/fer_M8.csv), so the other points are
+    parity unpinned; they are held to the curve's shape: FER falls with SNR, DL-SCL never
+    loses frames against its own SCL baseline, and 5 dB agrees with the reference (|z| < 3)."""
+    rows = run_fer_sweep.run_sweep(run_fer_sweep.build_argparser().parse_args(
+        ["--M", "8", "--frames", "200000", "--snr_lo", "4.0", "--snr_hi", "6.5", "--snr_step", "0.5", "--retries",
+         "8", "--beta", str(GOLDEN / "beta_M8.npy"), "--rng", "philox", "--batch", "200000", "--out_dir",
+         str(tmp_path), "--plot_dir", str(tmp_path), "--no_plot"]))
+    assert [r["snr_db"] for r in rows] == [4.0, 4.5, 5.0, 5.5, 6.0, 6.5]
+    scl = [r["fer_scl"] for r in rows]
+    assert all(a > b for a, b in zip(scl, scl[1:])), scl
+    assert all(r["fer_dl"] <= r["fer_scl"] for r in rows)
+    p, p_ref = rows[2]["fer_scl"], 26 / 2000
+    pp = (p * 200000 + 26) / 202000
+    assert abs((p - p_ref) / math.sqrt(pp * (1 - pp) * (1 / 200000 + 1 / 2000))) < 3
+    assert (tmp_path / "fer_M8.csv").exists()
+
+
 def test_device_retry_loop_chunked_pipeline(monkeypatch):
     """The chunked retry pipeline (retry rounds of chunk c overlapped with the baseline of c+1)
     gives the same per-frame results as the host ranking."""
