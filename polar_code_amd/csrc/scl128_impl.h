@@ -104,17 +104,19 @@ __device__ __forceinline__ void step_depth(double* Af, const double* lb, int g, 
     // input base: the parent's slot (from the table at the first rewritten depth, else own)
     const double* in = first ? Af + 2 * (h * LMAX + slot_at(tabp, D - 1)) : lb;
     const uint32_t xh = xsp >> h;
-#pragma unroll
-    for (int k = 0; k < HW; ++k) {
+    auto node = [&](int k) {  // element e = 2k + h
         const double2 ab = *reinterpret_cast<const double2*>(in + OFF_IN + 4 * k * LMAX);
-        const double v = is_g ? g_node(ab.x, ab.y, (xh >> (2 * k)) & 1u) : f_minsum(ab.x, ab.y);
-        if constexpr (D == 6) {
-            Af[OFF_OUT + 2 * p + h] = v;
-        } else if (2 * k < HW) {
-            const_cast<double*>(lb)[OFF_OUT + 4 * k * LMAX] = v;
-        } else {
-            const_cast<double*>(lb)[OFF_OUT + 2 * (2 * k - HW) * LMAX + 1] = v;
-        }
+        return is_g ? g_node(ab.x, ab.y, (xh >> (2 * k)) & 1u) : f_minsum(ab.x, ab.y);
+    };
+    if constexpr (D == 6) {
+        Af[OFF_OUT + 2 * p + h] = node(0);
+    } else {
+        // the lane owns both members e, e + W/2 of each of its output pairs: one 16-byte store
+        // per pair, the 16 lanes of a frame on 256 contiguous bytes (single-double stores at a
+        // 16-byte stride put lanes g and g + 8 on the same banks)
+#pragma unroll
+        for (int k = 0; k < HW / 2; ++k)
+            *reinterpret_cast<double2*>(const_cast<double*>(lb) + OFF_OUT + 4 * k * LMAX) = make_double2(node(k), node(k + HW / 2));
     }
     wave_lds_fence();
 }
