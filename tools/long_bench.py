@@ -1,0 +1,48 @@
+"""Throughput of the long-code decoder (csrc/scl_long.hip), N = 256..1024, on one GPU.
+
+    python tools/long_bench.py            (GPU box)
+Frames: random BPSK/AWGN codewords of construct_info_set(N, K) + CRC-24 at 2.5 dB, generated
+on the host once and kept resident; each timed step decodes B frames (decode_device, best bits
+and flags only) on the handle's stream, timed with events on that stream.
+"""
+import sys
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+import torch  # noqa: E402
+
+from polar_code_amd import _native  # noqa: E402
+from polar_code_amd.polar.crc import attach_crc  # noqa: E402
+from polar_code_amd.polar.polar import _polar_transform, construct_info_set  # noqa: E402
+
+POLY = "0x1864CFB"
+for N, K, L, B in [(256, 128, 8, 200_000), (512, 256, 8, 100_000), (1024, 512, 8, 50_000), (1024, 512, 32, 20_000)]:
+    rng = np.random.default_rng(N + L)
+    info = construct_info_set(N, K)
+    msg = attach_crc(rng.integers(0, 2, size=(B, K - 24), dtype=np.int8), POLY)
+    u = np.zeros((B, N), np.int8)
+    u[:, info] = msg
+    nv = 1.0 / (2.0 * K / N * 10 ** (2.5 / 10))
+    llr = 2.0 * ((1.0 - 2.0 * _polar_transform(u)) + rng.normal(0.0, np.sqrt(nv), size=(B, N))) / nv
+    dec = _native.Decoder(N, info, L, POLY)
+    stream = torch.cuda.Stream()  # (not the legacy default stream: its handle is 0)
+    dec.set_stream(stream.cuda_stream)
+    d_llr = torch.from_numpy(llr).cuda()
+    best = torch.empty((B, dec.W), dtype=torch.int64, device="cuda")
+    flags = torch.empty(B, dtype=torch.uint8, device="cuda")
+    dec.decode_device(d_llr.data_ptr(), B, d_best=best.data_ptr(), d_flags=flags.data_ptr())
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    steps = 3
+    e0.record(stream)
+    for _ in range(steps):
+        dec.decode_device(d_llr.data_ptr(), B, d_best=best.data_ptr(), d_flags=flags.data_ptr())
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    fer = float(((flags.cpu().numpy() & 0x80) == 0).mean())
+    print(f"N={N} K={K} L={L}: {B / ms * 1e3 / 1e6:.2f} M frames/s ({ms:.2f} ms per {B} frames), "
+          f"input {B * N * 8 / ms / 1e6:.1f} GB/s, FER {fer:.4f}", flush=True)
+    dec.close()
