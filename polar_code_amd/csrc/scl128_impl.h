@@ -421,7 +421,13 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
             const double2 lab = reinterpret_cast<const double2*>(Af + Ly::OFF6)[start <= 6 ? cpath : slot_at(tab, 6)];
             const double la = lab.x, lb = lab.y;
             const uint32_t xleaf = lastbit;  // u[phi - 1], the left sibling's bit at odd phases
-            const double lam = (PSCL_ABLATE & 128) ? la : (path_lane ? ((phi & 1) ? g_node(la, lb, xleaf) : f_minsum(la, lb)) : lb + la);
+            // Upper lanes: the next (odd) leaf given this phase's bit -- bit 0 at frozen phases;
+            // at even information phases of the screening decode, the better child's bit (the
+            // sign of this leaf), which every path keeps whenever the list update below takes
+            // its keep-the-better-children path
+            double lam_up = lb + la;
+            if (APX && is_info && !(phi & 1)) lam_up = g_node(la, lb, sign_bit(f_minsum(la, lb)));
+            const double lam = (PSCL_ABLATE & 128) ? la : (path_lane ? ((phi & 1) ? g_node(la, lb, xleaf) : f_minsum(la, lb)) : lam_up);
             // ---- metric tail log1p(exp(-|llr|)) (scl.py:102-105)
             double Lt;
             const uint64_t lpre_up = from_upper_half64<G, LMAX>(pscl_asu64(Lpre), lane);
@@ -495,6 +501,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                         lastbit = gb;
                         if (phi < 64) u0 |= (uint64_t)gb << phi; else u1 |= (uint64_t)gb << (phi - 64);
                         ++j;
+                        pre_ok = !(phi & 1);  // the upper lanes' tail is the next leaf's (see lam_up)
                         return;
                     }
                     // rank the 2L children on the high words; lane r takes the child ranked r.
