@@ -42,6 +42,11 @@ using namespace pscl;
 constexpr int kN = 128;
 constexpr int kn = 7;
 
+// 16-lane frames keep their 8 channel LLRs in registers across the depth-1..3 recomputes
+#ifndef PSCL_CREG
+#define PSCL_CREG 1
+#endif
+
 // CH: the frame's channel LLRs are staged in LDS (needed when the decode input is rate
 // matched: the de-rate-matched values exist nowhere else); otherwise the depth-1..3
 // recomputes read them straight from the (L2/MALL-resident) input row, which halves the
@@ -52,12 +57,17 @@ struct Layout128 {
     static constexpr int F = 64 / G;
     static constexpr int LOG_G = __builtin_ctz(G);
     static constexpr int LOG_LM = __builtin_ctz(LMAX);
+    // 16-lane frames (L = 8) hold their channel LLRs in registers (creg) from the frame's start:
+    // a staged (CH) channel row is dead once loaded, so depth 3 is laid over it (the first
+    // depth-3 write, at phase 0, follows the register loads) -- 2 KB per frame instead of 3 KB,
+    // 4 waves/SIMD instead of 3 for the rate-matched NR decode
+    static constexpr bool CREG = G == 16 && PSCL_CREG;
     // depth-d nodes (W = 2^(7-d) values per slot) pair-major, [W/2][slot][2]: element e of
     // slot s at ((e mod W/2) * LMAX + s) * 2 + e div W/2, so the two inputs a = e, b = e + W/2
     // of every f/g of the next depth (and of the leaf) are one 16-byte ds_read_b128 (4 LDS
     // cycles per wave, against 8 for the ds_read2_b64 of two separate doubles), and the
     // 16 lanes of a frame, each on its own path, read 256 contiguous bytes
-    static constexpr int OFF3 = CH ? kN : 0;        // [8][LMAX][2]
+    static constexpr int OFF3 = CH && !CREG ? kN : 0;  // [8][LMAX][2]
     static constexpr int OFF4 = OFF3 + 16 * LMAX;   // [4][LMAX][2]
     static constexpr int OFF5 = OFF4 + 8 * LMAX;    // [2][LMAX][2]
     static constexpr int OFF6 = OFF5 + 4 * LMAX;    // [1][LMAX][2]
@@ -155,11 +165,6 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 #define PSCL_APX_ABLATE 0
 #endif
 
-// 16-lane frames keep their 8 channel LLRs in registers across the depth-1..3 recomputes
-#ifndef PSCL_CREG
-#define PSCL_CREG 1
-#endif
-
 #ifndef PSCL_WAVES_PER_EU
 #define PSCL_WAVES_PER_EU 4
 #endif
@@ -234,7 +239,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
         // 16-lane frames (L = 8): lane g's 8 channel LLRs (elements g + 16 m) are the same at
         // all 8 depth-1..3 recomputes: loaded once per frame into registers, so the recomputes
         // wait on no memory (16 VGPRs; the in-place reads cost 25 % of the screening pass)
-        constexpr bool CREG = G == 16 && PSCL_CREG;
+        constexpr bool CREG = Ly::CREG;
         double creg[CREG ? 8 : 1];
         if constexpr (CREG) {
             if (CH) wave_lds_fence();

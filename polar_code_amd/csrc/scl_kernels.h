@@ -122,7 +122,7 @@ struct pscl_channel_params {
 int pscl_decode_lmax(int L);
 // scl_long.hip (N = 256 .. 1024)
 int64_t pscl_long_block_bytes(int N, int L, int K, int hist);
-int64_t pscl_long_grid(int64_t B);
+int64_t pscl_long_grid(int64_t B, int L);
 hipError_t pscl_launch_long(const pscl_decode_params& P, int hist, hipStream_t s);
 // fills P.a_bytes / P.wave_bytes / P.fast for the kernel that will decode this shape
 void pscl_decode_layout(pscl_decode_params& P, int hist);

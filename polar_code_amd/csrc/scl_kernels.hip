@@ -461,7 +461,7 @@ int pscl_decode_lmax(int L) {
 }
 
 int64_t pscl_decode_grid(const pscl_decode_params& P) {
-    if (P.long_mode) return pscl_long_grid(P.grid_cap > 0 && P.grid_cap < P.B ? P.grid_cap : P.B);
+    if (P.long_mode) return pscl_long_grid(P.grid_cap > 0 && P.grid_cap < P.B ? P.grid_cap : P.B, P.L);
     const int per_wg = pscl_decode_wpg(P) * (32 / pscl_decode_lmax(P.L));  // frames per workgroup
     int64_t g = (P.B + per_wg - 1) / per_wg;
     const int64_t cap = P.grid_cap > 0 && P.grid_cap < (1 << 20) ? P.grid_cap : (1 << 20);

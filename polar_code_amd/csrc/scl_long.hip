@@ -336,8 +336,40 @@ int64_t pscl_long_block_bytes(int N, int L, int K, int hist) {
     return (b + 255) & ~(int64_t)255;
 }
 
-int64_t pscl_long_grid(int64_t B) {
-    const int64_t cap = 256 * 16;  // 16 waves per CU on 256 CUs; each strides over frames
+// resident one-wave workgroups per CU for list size bucket LMAX (the smaller of the plain and
+// history instances: one grid size serves both); 16 when the runtime cannot tell (no device)
+template <int LMAX>
+static int long_blocks_per_cu() {
+    int a = 0, b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, reinterpret_cast<const void*>(scl_long_kernel<LMAX, false>), 64, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(scl_long_kernel<LMAX, true>), 64, 0) != hipSuccess)
+        return 16;
+    const int m = a < b ? a : b;
+    return m < 1 ? 1 : (m > 32 ? 32 : m);
+}
+
+int64_t pscl_long_grid(int64_t B, int L) {
+    // one wavefront per frame is latency-bound: fill every resident wave slot (the VGPR count,
+    // ~70 per lane, allows 7 waves per SIMD), each wave striding over frames
+    static int cus = 0, per_cu[6] = {0, 0, 0, 0, 0, 0};
+    if (!cus) {
+        int dev = 0, n = 0;
+        cus = (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+                  ? n
+                  : 256;
+    }
+    const int lmax = pscl_decode_lmax(L), li = __builtin_ctz((unsigned)lmax);
+    if (!per_cu[li]) {
+        switch (lmax) {
+            case 1: per_cu[li] = long_blocks_per_cu<1>(); break;
+            case 2: per_cu[li] = long_blocks_per_cu<2>(); break;
+            case 4: per_cu[li] = long_blocks_per_cu<4>(); break;
+            case 8: per_cu[li] = long_blocks_per_cu<8>(); break;
+            case 16: per_cu[li] = long_blocks_per_cu<16>(); break;
+            default: per_cu[li] = long_blocks_per_cu<32>(); break;
+        }
+    }
+    const int64_t cap = (int64_t)cus * per_cu[li];
     return B < 1 ? 1 : (B < cap ? B : cap);
 }
 
