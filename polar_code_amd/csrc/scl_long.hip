@@ -49,8 +49,21 @@ __device__ __forceinline__ void wave_mem_fence() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// minimum waves per SIMD the register allocation must allow: 8 (64 VGPRs; the plain
+// instances fit without spills, the history ones spill a few words).  Measured on MI355X
+// (tools/long_bench.py): 7 waves/SIMD at the compiler's ~70 VGPRs -> 8 is 10-11 % faster at
+// N = 256..1024, L = 8.  0: the compiler's choice.
+#ifndef PSCL_LONG_WAVES_PER_EU
+#define PSCL_LONG_WAVES_PER_EU 8
+#endif
+#if PSCL_LONG_WAVES_PER_EU
+#define PSCL_LONG_BOUNDS __launch_bounds__(64, PSCL_LONG_WAVES_PER_EU)
+#else
+#define PSCL_LONG_BOUNDS __launch_bounds__(64)
+#endif
+
 template <int LMAX, bool HIST>
-__global__ void __launch_bounds__(64) scl_long_kernel(const pscl_decode_params P) {
+__global__ void PSCL_LONG_BOUNDS scl_long_kernel(const pscl_decode_params P) {
     constexpr int G = 2 * LMAX;  // candidate lanes: path p in lane p, its bit-1 child in lane p + LMAX
     __shared__ uint64_t T[PSCL_EXP_TABLE_WORDS];
     __shared__ uint64_t xsw[LMAX * kMaxXsWords];
@@ -349,8 +362,8 @@ static int long_blocks_per_cu() {
 }
 
 int64_t pscl_long_grid(int64_t B, int L) {
-    // one wavefront per frame is latency-bound: fill every resident wave slot (the VGPR count,
-    // ~70 per lane, allows 7 waves per SIMD), each wave striding over frames
+    // one wavefront per frame is latency-bound: fill every resident wave slot (64 VGPRs per
+    // lane: 8 waves per SIMD), each wave striding over frames
     static int cus = 0, per_cu[6] = {0, 0, 0, 0, 0, 0};
     if (!cus) {
         int dev = 0, n = 0;
