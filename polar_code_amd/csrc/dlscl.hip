@@ -120,10 +120,12 @@ __global__ void __launch_bounds__(256) replay_kernel(const pscl_replay_params R,
     // level d -> d+1: node k' of width w2 at flat position p' = k' w2 + i; its parent's
     // halves are a = lvl_d[(k'>>1) 2 w2 + i], b = a's partner + w2 (polar.py:122-127)
     for (int d = 0; d < R.n; ++d) {
-        const int w2 = N >> (d + 1);
+        // w2 = N >> (d + 1) = 2^lw2: node index and offset by shift and mask (a runtime
+        // integer division here cost more VALU than the f/g work of the whole replay)
+        const int lw2 = R.n - d - 1, w2 = 1 << lw2;
         for (int p2 = lane; p2 < N; p2 += 64) {
-            const int k2 = p2 / w2, i = p2 - k2 * w2;
-            const int pa = (k2 >> 1) * 2 * w2 + i;
+            const int k2 = p2 >> lw2, i = p2 & (w2 - 1);
+            const int pa = ((k2 >> 1) << (lw2 + 1)) + i;
             const double a = cur[pa], bb = cur[pa + w2];
             double v;
             if (!(k2 & 1)) {
