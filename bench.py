@@ -386,7 +386,10 @@ def main():
         host = r["llr0"][: min(B, 1_000_000)].cpu().numpy()
         if E:
             host = host_internal_llrs(host[: min(host.shape[0], 100_000)], N)
-        cpu, ref, n = cpu_baseline(orc, host, info, L, args.cpu_seconds, args.retries, beta)
+        if world == 1:
+            cpu, ref, n = cpu_baseline(orc, host, info, L, args.cpu_seconds, args.retries, beta)
+        else:  # the CPU baseline is an N = 1 figure; the step-0 parity check stays (untimed)
+            ref = orc.run(host, info, L, args.retries, beta)
         par = parity(r["best0"], r["flags0"], ref, K, check_idx=args.retries == 0)
     r.pop("llr0", None)
     torch.cuda.empty_cache()
