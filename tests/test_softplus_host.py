@@ -76,3 +76,26 @@ def test_screening_tail_within_bound_host():
     nrm = ex > 2.0 ** -1000  # normal range (subnormal tails: absolute bound above)
     rel = np.abs(ap - ex)[nrm] / ex[nrm]
     assert rel.max() < SCR_EPS / 2  # typical case: well inside the proven bound
+
+
+def test_screening_polynomial_error_bound():
+    """The atanh polynomial hard-coded in pscl_softplus_tail_scr (glibc_softplus.h) stays within
+    the 0.06-unit (2^-23) approximation error its proof budgets, evaluated exactly (long double)
+    on a dense grid of w = s^2 in [0, 1/9]; guards the coefficients against edits."""
+    import re
+
+    src = (Path(__file__).resolve().parent.parent / "polar_code_amd" / "csrc" / "glibc_softplus.h").read_text()
+    body = src[src.index("PSCL_HD double pscl_softplus_tail_scr"):]
+    body = body[:body.index("const float q")]
+    coef = [float.fromhex(h) for h in re.findall(r"(0x[0-9a-f.]+p-?\d+)f", body)]
+    assert len(coef) == 4 and "2.0f);" in body  # c4, c3, c2, c1; c0 = 2
+    c = [2.0, coef[3], coef[2], coef[1], coef[0]]  # c0..c4
+    w = np.linspace(0.0, 1.0, 200_001, dtype=np.longdouble) / 9
+    exact = np.zeros_like(w)
+    t = np.ones_like(w)
+    for i in range(40):
+        exact += 2 * t / (2 * i + 1)
+        t *= w
+    p = sum(np.longdouble(ci) * w ** i for i, ci in enumerate(c))
+    err = float(np.max(np.abs(p / exact - 1))) / 2.0 ** -23
+    assert err < 0.07, err
