@@ -346,11 +346,70 @@ def extra_configs(args, ctx: Ctx, orc: Oracle | None):
     return out
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: start N fresh rank processes (one per GPU, the
+    same command line) with RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, relay rank 0's output
+    and return non-zero if any rank fails.  The parent never imports torch or touches the GPU
+    (ranks are children, not exec'd replacements)."""
+    import signal
+    import subprocess
+
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PSCL_BENCH_CHILD="1")
+        procs.append(subprocess.Popen([sys.executable, "-u", str(Path(__file__).resolve()), *sys.argv[1:]],
+                                      env=env, stdout=None if r == 0 else subprocess.DEVNULL))
+    rcs = [None] * n
+    try:
+        while any(rc is None for rc in rcs):
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    rcs[i] = p.poll()
+            bad = [i for i, rc in enumerate(rcs) if rc not in (None, 0)]
+            if bad:  # one rank failed: the others would wait in a collective forever
+                for i, p in enumerate(procs):
+                    if rcs[i] is None:
+                        p.send_signal(signal.SIGTERM)
+                for i, p in enumerate(procs):
+                    try:
+                        rcs[i] = p.wait(timeout=30) if rcs[i] is None else rcs[i]
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[i] = p.wait()
+                break
+            time.sleep(0.2)
+    except KeyboardInterrupt:
+        for p in procs:
+            p.kill()
+        raise
+    failed = [(i, rc) for i, rc in enumerate(rcs) if rc != 0]
+    if failed:
+        sys.stderr.write(f"bench.py: rank(s) failed: {failed}\n")
+        return 1
+    return 0
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        raise SystemExit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (one rank per GPU)")
     import torch
 
     # one process per GPU; PSCL_SHARE_GPU=1 lets a rehearsal put several ranks on fewer GPUs

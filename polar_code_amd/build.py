@@ -94,20 +94,50 @@ def _stale(target: Path, deps: list[Path]) -> bool:
     return any(d.stat().st_mtime > t for d in deps)
 
 
+def unit_key(unit, flags: list[str]) -> str:
+    """Content key of one object: target, compiler, every flag (base, unit, extra) and the bytes
+    of its source and of every header it may include.  Stored next to the object
+    (<obj>.key) so an object is reused only when it was built from exactly these inputs
+    (modification times and the shared object directory are not trusted)."""
+    h = hashlib.sha256()
+    h.update("\0".join([ARCH, HIPCC, *BASE_FLAGS, *unit[1], *flags]).encode())
+    headers = sorted([*CSRC.glob("*.h"), *CSRC.glob("*.inc"), *INCLUDE.glob("*.h")])
+    for f in [unit[0], *headers]:
+        h.update(f.name.encode() + b"\0" + f.read_bytes())
+    return h.hexdigest()[:32]
+
+
+def _key_path(obj: Path) -> Path:
+    return obj.with_name(obj.name + ".key")
+
+
+def object_current(unit, flags: list[str]) -> bool:
+    kp = _key_path(unit[2])
+    return unit[2].exists() and kp.exists() and kp.read_text().strip() == unit_key(unit, flags)
+
+
+def compile_keyed(units, flags: list[str], force: bool = False) -> list[str]:
+    """Compile every unit whose key differs from the one recorded with its object."""
+    todo = [u for u in units if force or not object_current(u, flags)]
+    for u in todo:
+        _key_path(u[2]).unlink(missing_ok=True)
+    compile_units(todo, flags)
+    for u in todo:
+        _key_path(u[2]).write_text(unit_key(u, flags) + "\n")
+    return [str(u[2]) for u in units]
+
+
 def build_hip(force: bool = False) -> Path:
     """Rebuild unless the library's embedded hash equals the hash of the sources in the tree
-    (modification times are not trusted: a copied or pushed library may look newer)."""
+    (modification times are not trusted: a copied or pushed library may look newer).  Objects
+    are reused only when their recorded content key (ARCH, flags, source and headers) matches."""
     want = source_hash()
     if not force and library_hash() == want:
         return LIB
-    objdir = PKG / "_build"
-    objdir.mkdir(exist_ok=True)
+    objdir = PKG / "_build" / ARCH
+    objdir.mkdir(parents=True, exist_ok=True)
     units = hip_units(objdir, hash_=want)
-    headers = [*CSRC.glob("*.h"), *CSRC.glob("*.inc"), *INCLUDE.glob("*.h")]
-    # the hash enters capi.cpp only; other objects are reused when newer than their inputs
-    todo = [u for u in units if force or u[0].name == "capi.cpp" or _stale(u[2], [u[0], *headers])]
-    compile_units(todo, [])
-    objs = [str(u[2]) for u in units]
+    objs = compile_keyed(units, [], force)
     tmp = LIB.with_suffix(".so.tmp")
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", str(tmp)])
     os.replace(tmp, LIB)

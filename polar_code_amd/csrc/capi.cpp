@@ -198,9 +198,13 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
         S.amb_count = (int32_t*)d_cnt;
         err = pscl_launch_decode(S, hist, st);
         h->screened = true;
-        // PSCL_DIAG_SCREEN_ONLY=1: timing diagnostics of the screening pass alone (tools/ablate
-        // variants); the deferred frames are then left undecoded
+#ifdef PSCL_APX_ABLATE
+        // PSCL_DIAG_SCREEN_ONLY=1: timing diagnostics of the screening pass alone (variant
+        // builds only, tools/build_variant.py -DPSCL_APX_ABLATE=..); deferred frames stay undecoded
         static const bool screen_only = getenv("PSCL_DIAG_SCREEN_ONLY") && atoi(getenv("PSCL_DIAG_SCREEN_ONLY")) == 1;
+#else
+        constexpr bool screen_only = false;  // the shipped library always re-decodes deferred frames
+#endif
         if (err == hipSuccess && !screen_only) {
             pscl_decode_params X = P;  // exact decode of the listed frames, outputs at their rows
             X.fidx = (const int64_t*)d_list;
@@ -864,7 +868,8 @@ int pscl_simulate(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno
     if (B == 0) return PSCL_OK;
     int rc = set_device(h);
     if (rc) return rc;
-    // chunks of at most 2^20 frames through handle scratch: 8 KB of LLRs per frame in flight
+    // chunks of at most 2^20 frames through handle scratch: N * 8 bytes of LLRs per frame
+    // (1 KiB at N = 128: about 1 GiB per 2^20-frame chunk)
     const int64_t chunk = B < (1 << 20) ? B : (1 << 20);
     const int W = h->W, N = h->N;
     void *d_llr, *d_msg, *d_best, *d_flags, *d_cnt;

@@ -403,12 +403,14 @@ PSCL_HD double pscl_softplus_tail_bf(double v, const uint64_t* T) {
  * then the error is at most one ulp of the result).  x is clamped to 4096 (the exact tail is 0
  * above ~745.2; the clamp keeps k in int range).
  *
- * With positive increments every screening path metric is within PSCL_SCR_EPS + 2^-52 of
- * the exact metric relatively, and the kernel trusts an ordering of two metrics only when
+ * With positive increments every screening path metric is within PSCL_SCR_EPS + N * 2^-53 of
+ * the exact metric relatively (the tail error, plus the fp64 summation of at most N = 128
+ * increments -- the screening kernels exist for N = 128 only -- which the exact metric also
+ * carries, so two such terms enter the comparison), and the kernel trusts an ordering of two metrics only when
  * their high words (sign, exponent, 20 mantissa bits) differ by more than PSCL_SCR_H: then
  * the larger exceeds the smaller by at least PSCL_SCR_H * 2^-21 relatively (one high-word
- * unit is 2^-21..2^-20 of the value), which must beat the 2 * (PSCL_SCR_EPS + 2^-52) the two
- * errors can close -- checked at compile time below.  Tests: tests/test_softplus_host.py
+ * unit is 2^-21..2^-20 of the value), which must beat the 2 * (PSCL_SCR_EPS + 2 * 128 * 2^-53)
+ * the two metrics' errors can close -- checked at compile time below.  Tests: tests/test_softplus_host.py
  * (host form) and tests/test_gpu_screening.py (device form, pscl_softplus_tails_device).
  */
 #define PSCL_SCR_TERMS 5
@@ -420,7 +422,7 @@ PSCL_HD double pscl_softplus_tail_bf(double v, const uint64_t* T) {
 #define PSCL_SCR_H 8
 #endif
 #ifdef __cplusplus
-static_assert(PSCL_SCR_H / 2097152.0 >= 4.0 * (PSCL_SCR_EPS + 2.220446049250313e-16),
+static_assert(PSCL_SCR_H / 2097152.0 >= 4.0 * (PSCL_SCR_EPS + 2.0 * 128.0 * 1.1102230246251565e-16),
               "screening margin PSCL_SCR_H does not cover twice the metric error (with 2x safety)");
 #endif
 #define PSCL_LN2HI 6.93147180369123816490e-01 /* 32 trailing zero bits: k * LN2HI exact */

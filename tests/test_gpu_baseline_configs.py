@@ -1,0 +1,154 @@
+"""GPU: BASELINE.json configs 2, 4 and 5 at their stated size (10^6-frame batches), every frame
+checked against the oracle (C restatement of the reference, test infrastructure only).
+
+Each test generates one 10^6-frame batch on the device with the Philox TX chain
+(pscl_channel_device: payload -> CRC-24 -> polar encode [-> NR interleave/repeat] -> BPSK ->
+AWGN -> LLR), decodes it through the C ABI exactly as bench.py and the sweeps do, copies the
+LLRs back and decodes the same frames with the oracle.  Compared frame by frame: best bits,
+CRC flag and (plain SCL) best candidate index, DL-SCL attempt counts; and the device-side
+FER/BER counters against counts recomputed on the host from the decoded bits.
+
+  config 2  SCL L=4 P(128,64)+CRC24, 10^6 frames at 5 dB        (scl.py:108-209)
+  config 4  DL-SCL L=4, 8 flip retries, beta_M4, 10^6 frames     (flip.py:65-141)
+  config 5  NR (128,88) rate matched to E=256, SCL L=8, 10^6      (scl_nr.py:40-57 front end)
+Configs 1 and 3 are covered by test_gpu_fer.py (config 1's CSV byte-identical to the
+reference's results/fer_M1.csv, config 3's 4.0-6.5 dB grid).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import GOLDEN
+from polar_code_amd import _native
+from polar_code_amd.dlscl.flip import words_to_bits
+from polar_code_amd.nr.polar import derate_match_polar, subblock_deinterleave
+from polar_code_amd.polar.polar import construct_info_set
+
+pytestmark = pytest.mark.gpu
+POLY = "0x1864CFB"
+B = 1_000_000
+EBNO = 5.0
+FRAMES, FRAME_ERR, BIT_ERR, PAY_ERR, PAY_BIT, RETRIES = 0, 1, 2, 3, 4, 5
+
+
+def _nr_internal(llrE: np.ndarray, N: int) -> np.ndarray:
+    """Vectorised scl_nr.py:47-48 front end (derate_match_polar then subblock_deinterleave) for
+    E = 2N; held to the package's per-frame mirrors on the first rows by the caller."""
+    E = llrE.shape[1]
+    assert E == 2 * N
+    avg = (llrE[:, :N] + llrE[:, N:]) / 2.0  # two repeats summed in order, divided by the count
+    nb = N // 32
+    i = np.arange(N)
+    order = (i % 32) * nb + i // 32
+    out = np.empty_like(avg)
+    out[:, order] = avg
+    return out
+
+
+def _batch(dec, mem, L, K, kp, E, seed):
+    n_in = E or 128
+    rate = kp / E if E else K / 128
+    d_llr = mem.alloc(B * n_in * 8)
+    d_msg = mem.alloc(B * dec.W * 8)
+    dec.channel_device(seed, int(EBNO * 10), EBNO, rate, kp, 0, B, d_llr, d_msg)
+    return d_llr, d_msg
+
+
+def _host_counts(bits, msg_bits, ok, kp):
+    err = bits != msg_bits
+    return {FRAMES: bits.shape[0], FRAME_ERR: int(np.count_nonzero(~ok)), BIT_ERR: int(err.sum()),
+            PAY_ERR: int(np.count_nonzero(err[:, :kp].any(axis=1))), PAY_BIT: int(err[:, :kp].sum())}
+
+
+def _check_counters(cnt, host, tag):
+    for k, v in host.items():
+        assert int(cnt[k]) == v, f"{tag}: counter {k} device {int(cnt[k])} host {v}"
+
+
+def _plain_config(L, E, seed):
+    K = 88 if E else 64
+    kp = K - 24
+    info = construct_info_set(128, K)
+    dec = _native.Decoder(128, info, L, POLY)
+    if E:
+        dec.set_rate_match(E)
+    with _native.DeviceArena(dec) as mem:
+        d_llr, d_msg = _batch(dec, mem, L, K, kp, E, seed)
+        d_best, d_flags, d_cnt = mem.alloc(B * dec.W * 8), mem.alloc(B), mem.alloc(8 * 8)
+        mem.memset(d_cnt, 0, 64)
+        dec.decode_device(d_llr, B, d_best=d_best, d_flags=d_flags, d_ref=d_msg, k_payload=kp, d_counters=d_cnt)
+        dec.sync()
+        scr = dec.screening_count()
+        best = mem.download(d_best, B * dec.W * 8, np.uint64).reshape(B, dec.W)
+        flags = mem.download(d_flags, B, np.uint8)
+        cnt = mem.download(d_cnt, 64, np.int64)
+        msg = mem.download(d_msg, B * dec.W * 8, np.uint64).reshape(B, dec.W)
+        llr = mem.download(d_llr, B * (E or 128) * 8, np.float64).reshape(B, E or 128)
+    dec.close()
+    if E:
+        head = np.stack([subblock_deinterleave(derate_match_polar(r, 128), 128) for r in llr[:2000]])
+        llr = _nr_internal(llr, 128)
+        np.testing.assert_array_equal(llr[:2000], head)  # vectorised front end == the mirrors
+    bits_o, ok_o, idx_o = oracle.decode_batch(llr, info, L, POLY, want_idx=True)
+    bits = words_to_bits(best, K)
+    ok = (flags & 0x80) != 0
+    tag = f"L={L} E={E}"
+    bad_bits = np.flatnonzero(np.any(bits != bits_o, axis=1))
+    assert bad_bits.size == 0, f"{tag}: best bits differ from the oracle in {bad_bits.size} frames, first {bad_bits[:5]}"
+    np.testing.assert_array_equal(ok, ok_o, err_msg=f"{tag}: CRC flags")
+    np.testing.assert_array_equal((flags & 0x3F).astype(np.int32), idx_o, err_msg=f"{tag}: best index")
+    _check_counters(cnt, _host_counts(bits, words_to_bits(msg, K), ok, kp), tag)
+    return cnt, scr
+
+
+def test_config2_scl_L4_1e6_frames_vs_oracle():
+    cnt, scr = _plain_config(4, 0, seed=20)
+    fer = cnt[FRAME_ERR] / cnt[FRAMES]
+    # reference results/fer_M4.csv:2: 91/2000 frame errors at 5 dB; z within MC error
+    p0 = 91 / 2000
+    assert abs(fer - p0) < 4 * np.sqrt(p0 * (1 - p0) / 2000), fer
+    assert 0 < scr < B // 20  # the screening pass ran and deferred a few frames to the exact kernel
+    print(f"config 2: FER {fer:.5f}, {scr} frames re-decoded exactly, 0/{B} oracle mismatches")
+
+
+def test_config5_nr_E256_L8_1e6_frames_vs_oracle():
+    cnt, scr = _plain_config(8, 256, seed=50)
+    assert cnt[FRAMES] == B and 0 < scr < B // 20
+    print(f"config 5: payload FER {cnt[PAY_ERR] / B:.6f}, BER {cnt[PAY_BIT] / (B * 64):.3e}, 0/{B} oracle mismatches")
+
+
+def test_config4_dlscl_L4_r8_beta4_1e6_frames_vs_oracle():
+    L, K, kp, R = 4, 64, 40, 8
+    info = construct_info_set(128, K)
+    beta = np.load(GOLDEN / "beta_M4.npy")
+    dec = _native.Decoder(128, info, L, POLY)
+    with _native.DeviceArena(dec) as mem:
+        d_llr, d_msg = _batch(dec, mem, L, K, kp, 0, seed=40)
+        d_best, d_flags, d_att = mem.alloc(B * 8), mem.alloc(B), mem.alloc(B * 4)
+        d_cs, d_cd = mem.alloc(64), mem.alloc(64)
+        mem.memset(d_cs, 0, 64)
+        mem.memset(d_cd, 0, 64)
+        dec.dlscl_device(d_llr, B, R, beta=beta, d_best=d_best, d_flags=d_flags, d_attempts=d_att, d_ref=d_msg,
+                         k_payload=kp, d_counters_scl=d_cs, d_counters_dl=d_cd)
+        dec.sync()
+        best = mem.download(d_best, B * 8, np.uint64).reshape(B, 1)
+        flags = mem.download(d_flags, B, np.uint8)
+        att = mem.download(d_att, B * 4, np.int32)
+        cs, cd = mem.download(d_cs, 64, np.int64), mem.download(d_cd, 64, np.int64)
+        msg = mem.download(d_msg, B * 8, np.uint64).reshape(B, 1)
+        llr = mem.download(d_llr, B * 128 * 8, np.float64).reshape(B, 128)
+    dec.close()
+    bits_o, ok_o, att_o = oracle.dl_batch(llr, info, L, R, POLY, beta)
+    bits = words_to_bits(best, K)
+    ok = (flags & 0x80) != 0
+    bad = np.flatnonzero(np.any(bits != bits_o, axis=1) | (ok != ok_o) | (att != att_o))
+    assert bad.size == 0, f"DL-SCL differs from the oracle in {bad.size} frames, first {bad[:5]}"
+    _check_counters(cd, _host_counts(bits, words_to_bits(msg, K), ok, kp), "DL-SCL")
+    assert int(cd[RETRIES]) == int((att_o - 1).sum())  # one re-decode per flip tried
+    base_fail = int(cs[FRAME_ERR])
+    assert cs[FRAMES] == B and base_fail == int(np.count_nonzero(att_o > 1))  # retried iff the baseline failed
+    # reference results/fer_M4.csv:2: SCL 91/2000, DL-SCL 71/2000 at 5 dB
+    for got, ref in ((base_fail / B, 91 / 2000), (cd[FRAME_ERR] / B, 71 / 2000)):
+        assert abs(got - ref) < 4 * np.sqrt(ref * (1 - ref) / 2000), (got, ref)
+    print(f"config 4: SCL FER {base_fail / B:.5f}, DL-SCL FER {cd[FRAME_ERR] / B:.5f}, "
+          f"{cd[RETRIES] / B:.3f} re-decodes/frame, 0/{B} oracle mismatches")

@@ -74,3 +74,26 @@ def test_bench_world2_counts_every_frame_once():
     assert line[1]["fer"]["frames"] == 4 * B
     for k in ("frame_errors", "ber", "payload_fer", "payload_ber"):
         assert line[1]["fer"][k] == line[2]["fer"][k], k
+
+
+def test_bench_gpus2_launches_its_own_ranks():
+    """`python bench.py --gpus 2` with no launcher environment (what the driver runs) starts two
+    rank processes itself (rank 0 relays its line) and decodes the same global frames as the
+    world-1 run over [0, 4B)."""
+    B = 50_000
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    env.update(PSCL_SHARE_GPU="1", PSCL_DIST_BACKEND="gloo")
+    base = [sys.executable, "bench.py", "--frames", str(B), "--warmup", "1", "--no-cpu-baseline", "--extra", "none"]
+    line = {}
+    for gpus, steps in ((1, 4), (2, 2)):
+        res = subprocess.run(base + ["--steps", str(steps), "--gpus", str(gpus)], cwd=ROOT, env=env,
+                             capture_output=True, text=True, timeout=240)
+        assert res.returncode == 0, (res.stdout + res.stderr)[-3000:]
+        lines = [x for x in res.stdout.splitlines() if x.startswith("{")]
+        assert len(lines) == 1, res.stdout[-2000:]  # one JSON line: rank 0's
+        line[gpus] = json.loads(lines[0])
+    assert line[2]["n_gpus"] == 2 and line[2]["fer"]["frames"] == 2 * B * 2
+    assert line[1]["fer"]["frames"] == 4 * B
+    for k in ("frame_errors", "ber", "payload_fer", "payload_ber"):
+        assert line[1]["fer"][k] == line[2]["fer"][k], k

@@ -47,8 +47,9 @@ def test_port_matches_numpy_logaddexp():
 
 def apx_grid():
     """|v| grid for the screening tail: dense over the decoder's working range, the 708..745
-    range where exp(-|v|) goes subnormal, tiny and huge magnitudes, both signs."""
-    parts = [np.arange(0.0, 40.0, 1e-4), np.arange(708.0, 745.2, 1e-3), 2.0 ** -np.arange(0.0, 80.0, 0.25),
+    40..708 range (k = 58..1021: the fp32 scaling of t underflows and ldexp(q, -k) scales down), the
+    708..745 range where exp(-|v|) goes subnormal, tiny and huge magnitudes, both signs."""
+    parts = [np.arange(0.0, 40.0, 1e-4), np.arange(40.0, 708.0, 1e-2), np.arange(708.0, 745.2, 1e-3), 2.0 ** -np.arange(0.0, 80.0, 0.25),
              np.array([745.13, 745.14, 745.2, 746.0, 800.0, 1e3, 1e6, 2 ** -1074])]
     v = np.concatenate(parts)
     return np.ascontiguousarray(np.concatenate([v, -v[::7]]))

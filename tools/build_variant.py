@@ -29,12 +29,18 @@ if "--unit" in flags:  # recompile one non-spec source (e.g. scl_long) with the 
     flags = flags[:i] + flags[i + 2:]
 if spec:
     unit = f"scl128_spec_{spec}.o"
+# the variant's own build hash (product hash + its flag set) is compiled into its capi.o, so a
+# variant never reports the product's hash (bench.py keys PMC entries by it)
+vhash = B.hashlib.sha256((B.source_hash() + "\0" + " ".join([name, spec or "", *flags])).encode()).hexdigest()[:16]
 if unit:
-    units = B.hip_units(objdir)
-    mine = [u for u in units if u[2].name == unit]
-    objs = B.compile_units(mine, flags)
-    objs += [str(B.PKG / "_build" / u[2].name) for u in units if u[2].name != unit]
+    units = B.hip_units(objdir, hash_=vhash)
+    mine = [u for u in units if u[2].name == unit or u[0].name == "capi.cpp"]
+    objs = B.compile_keyed([u for u in mine if u[0].name != "capi.cpp"], flags)
+    objs += B.compile_keyed([u for u in mine if u[0].name == "capi.cpp"], [])
+    prod = B.PKG / "_build" / B.ARCH
+    rest = [u for u in B.hip_units(prod) if u[2].name != unit and u[0].name != "capi.cpp"]
+    objs += B.compile_keyed(rest, [])  # the product's objects, rebuilt if not current
 else:
-    objs = B.compile_units(B.hip_units(objdir), flags)
+    objs = B.compile_keyed(B.hip_units(objdir, hash_=vhash), flags)
 subprocess.check_call([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", *objs, "-o", str(out / f"lib_{name}.so")])
 print(out / f"lib_{name}.so")
