@@ -4,8 +4,9 @@ as dl_scl_polar/polar/scl_mi355x.py.
 Self-contained: ctypes and NumPy only, no import of polar_code_amd.  It replaces
   dl_scl_polar.polar.scl.decode_scl           (scl.py:108-209)
   dl_scl_polar.polar.polar.sc_decode           (polar.py:130-168)
-and adds a batch form of dl_scl_polar.dlscl.flip.decode_with_retries (flip.py:65-141) whose
-retry loop runs on the GPU.  Return values and exception types follow the reference.
+and adds the batch API the host keeps (SCLDecoder: one call decodes llr[B, N], the
+dl_scl_polar.polar.scl SCLDecoder contract of polar_code_amd/polar/scl.py) and a batch form of
+dl_scl_polar.dlscl.flip.decode_with_retries (flip.py:65-141) whose retry loop runs on the GPU.  Return values and exception types follow the reference.
 
 The library is found through $PSCL_LIB, else next to this repository's package.
 """
@@ -57,12 +58,12 @@ def _crc_value(crc) -> int:
     return int(crc, 16) if isinstance(crc, str) else int(crc)
 
 
-def _handle(N: int, info_set: np.ndarray, M: int, crc):
+def _handle(N: int, info_set: np.ndarray, M: int, crc, device: int = 0):
     info = np.ascontiguousarray(np.asarray(info_set).ravel(), dtype=np.int32)
-    key = (N, info.tobytes(), M, _crc_value(crc))
+    key = (N, info.tobytes(), M, _crc_value(crc), int(device))
     if key not in _handles:
         h = _vp()
-        _check(_lib.pscl_create(C.byref(h), 0, N, info.ctypes.data_as(C.POINTER(_i32)), info.size, M,
+        _check(_lib.pscl_create(C.byref(h), int(device), N, info.ctypes.data_as(C.POINTER(_i32)), info.size, M,
                                 _crc_value(crc)))
         _handles[key] = h
     return _handles[key]
@@ -103,6 +104,57 @@ def sc_decode(llr, info_set):
     bits = np.zeros(info_set.size, np.int8)
     _check(_lib.pscl_sc_decode(h, llr.ctypes.data, 1, bits.ctypes.data))
     return bits
+
+
+class SCLDecoder:
+    """Frame-batched SCL decoder bound to one GPU (scl.py:108-209 over a batch).
+
+    SCLDecoder(N, info_set, L, crc_poly="0x1864CFB", device=0).decode(llr[B, N]) returns a dict
+    with bits [B, K] int8 (each frame's best_path_bits), crc_pass [B] bool, best_idx [B] and
+    n_paths [B]; with metrics / candidates / info_llrs=True also metrics [B, L] (list order),
+    cands [B, L, K] and info_llrs [B, L, K].  forced: None or [B, K] 0/1 (force_info_bits per
+    frame).  One pscl_decode call per batch.
+    """
+
+    def __init__(self, N: int, info_set, L: int, crc_poly="0x1864CFB", device: int = 0):
+        if L <= 0:
+            raise ValueError("List size M must be positive")
+        self.N, self.L, self.device = int(N), int(L), int(device)
+        self.info_set = np.ascontiguousarray(np.asarray(info_set).ravel(), dtype=np.int32)
+        self.K = self.info_set.size
+        self.crc_poly = crc_poly
+        self._h = _handle(self.N, self.info_set, self.L, crc_poly, self.device)
+
+    def decode(self, llr, forced=None, *, metrics: bool = False, candidates: bool = False,
+               info_llrs: bool = False) -> dict:
+        llr = np.ascontiguousarray(np.asarray(llr, dtype=float))
+        if llr.ndim == 1:
+            llr = llr[None, :]
+        if llr.ndim != 2 or llr.shape[1] != self.N:
+            raise ValueError(f"llr must be [B, {self.N}]")
+        B, K, L = llr.shape[0], self.K, self.L
+        if forced is not None:
+            forced = np.ascontiguousarray(np.asarray(forced), dtype=np.int8)
+            if forced.shape != (B, K):
+                raise ValueError("force_info_bits must have length equal to info_set")
+        out = {"n_paths": np.zeros(B, np.int32), "bits": np.zeros((B, K), np.int8),
+               "crc_pass": np.zeros(B, np.uint8), "best_idx": np.zeros(B, np.int32)}
+        if metrics:
+            out["metrics"] = np.full((B, L), np.nan)
+        if candidates:
+            out["cands"] = np.zeros((B, L, K), np.int8)
+        if info_llrs:
+            out["info_llrs"] = np.full((B, L, K), np.nan)
+
+        def p(k):
+            a = out.get(k)
+            return None if a is None else a.ctypes.data
+
+        _check(_lib.pscl_decode(self._h, llr.ctypes.data, B, None if forced is None else forced.ctypes.data,
+                                p("n_paths"), p("bits"), p("crc_pass"), p("best_idx"), p("metrics"), p("cands"),
+                                p("info_llrs")))
+        out["crc_pass"] = out["crc_pass"].astype(bool)
+        return out
 
 
 class _Device:
@@ -169,4 +221,4 @@ def decode_with_retries_batch(llr, info_set, M, retries, *, crc=None, beta=None)
             "tried_indices": [[int(t) for t in row if t >= 0] for row in tried]}
 
 
-__all__ = ["decode_scl", "sc_decode", "decode_with_retries_batch"]
+__all__ = ["decode_scl", "sc_decode", "SCLDecoder", "decode_with_retries_batch"]

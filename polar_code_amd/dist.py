@@ -86,6 +86,37 @@ def allreduce_sum(vec: np.ndarray, ctx: Context | None = None) -> np.ndarray:
     return t.cpu().numpy()
 
 
+def allgather(vec: np.ndarray, ctx: Context | None = None) -> np.ndarray:
+    """[world, len(vec)]: every rank's vector, in rank order (vec[None] when world == 1)."""
+    ctx = ctx or _CTX or Context()
+    v = np.ascontiguousarray(vec)
+    if ctx.world <= 1:
+        return v[None, :].copy()
+    import torch
+    import torch.distributed as dist
+
+    t = torch.as_tensor(v)
+    if ctx.backend == "nccl":
+        t = t.cuda()
+    out = [torch.empty_like(t) for _ in range(ctx.world)]
+    dist.all_gather(out, t)
+    return torch.stack(out).cpu().numpy()
+
+
+def allreduce_min(x: float, ctx: Context | None = None) -> float:
+    ctx = ctx or _CTX or Context()
+    if ctx.world <= 1:
+        return float(x)
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    if ctx.backend == "nccl":
+        t = t.cuda()
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return float(t.item())
+
+
 def allreduce_max(x: float, ctx: Context | None = None) -> float:
     ctx = ctx or _CTX or Context()
     if ctx.world <= 1:

@@ -4,11 +4,22 @@ reference's 3x6 demo base graph) is out of scope.
 
 The reference draws every frame from ONE NumPy stream shared by all SNR points
 (run_ber_sweep.py:230) and stops each point on a data-dependent rule
-(`while bit_errors < err_cap and bits_total < bits_cap`, :127).  Here frames are generated in
-batches from that same stream and decoded in one GPU call; the exact stop frame is found with
-a prefix sum, and if a batch overshoots, the stream is rewound to the batch start and advanced
-by exactly the frames the reference would have drawn -- so the rows (and the stream handed to
-the next SNR point) are identical to the reference's.
+(`while bit_errors < err_cap and bits_total < bits_cap`, :127).  Two channel modes:
+
+  --rng replay  (default) frames generated in batches from that same stream and decoded in one
+                GPU call; the exact stop frame is found with a prefix sum, and if a batch
+                overshoots, the stream is rewound to the batch start and advanced by exactly
+                the frames the reference would have drawn -- so the rows (and the stream handed
+                to the next SNR point) are identical to the reference's.  One process.
+  --rng philox  frames generated on the GPU (pscl_channel_device: payload -> CRC -> polar
+                encode [-> NR interleave/repeat] -> BPSK -> AWGN -> LLR), keyed by (seed, SNR,
+                global frame index), so the rows do not depend on the number of GPUs.  Under
+                torchrun each round of world x --batch frames is split into contiguous global
+                ranges per rank; one all-gather of per-rank partial sums per round, and in the
+                round where the stop rule fires, the first global frame with
+                bit_errors >= err_cap or bits_total >= bits_cap is found exactly (each rank scans
+                its own range from the prefix of the ranks before it; one MIN and one SUM
+                all-reduce), so a sharded sweep writes the same rows as one GPU.
 """
 from __future__ import annotations
 
@@ -20,7 +31,7 @@ from typing import Dict, Iterable, List, Optional
 
 import numpy as np
 
-from .. import _native
+from .. import _native, dist
 from .. import config as global_config
 from ..dlscl.flip import decode_with_retries_batch
 from ..nr.polar.interleaver import subblock_interleave
@@ -158,6 +169,124 @@ def run_scheme(rng, EbN0_dB, args, info_set, scheme: _Scheme, coded_len, payload
     return row
 
 
+def payload_errors_from_words(best: np.ndarray, ref: np.ndarray, K_payload: int) -> np.ndarray:
+    """Per-frame payload bit errors (run_ber_sweep.py:77-82 on bit-packed words): popcount of
+    best ^ ref over the first K_payload bits (bit j in word j >> 6, bit j & 63)."""
+    best = np.asarray(best, np.uint64)
+    ref = np.asarray(ref, np.uint64)
+    W = best.shape[1]
+    mask = np.zeros(W, np.uint64)
+    for w in range(W):
+        nb = min(max(K_payload - 64 * w, 0), 64)
+        mask[w] = np.uint64((1 << nb) - 1) if nb < 64 else np.uint64(0xFFFFFFFFFFFFFFFF)
+    return np.bitwise_count((best ^ ref) & mask).sum(axis=1).astype(np.int64)
+
+
+class PhiloxFrames:
+    """Frames [frame0, frame0 + n) of the on-device Philox stream of one SNR point, decoded on
+    this rank's GPU: returns per-frame payload bit errors and work (flips tried for dl_scl)."""
+
+    def __init__(self, args, info_set, N: int, device: int):
+        a = self.args = args
+        self.N, self.payload_len = N, a.K_payload
+        crc = a.crc_poly if a.K_crc else None
+        if a.scheme == "nr_polar_scl":
+            crc = a.crc_poly  # scl_nr.py: always CRC-protected
+        self.crc = crc
+        if N > _native.PSCL_DEVICE_LOOP_MAX_N:
+            raise NotImplementedError(f"--rng philox: the device TX chain covers N <= {_native.PSCL_DEVICE_LOOP_MAX_N}")
+        E = a.E if a.scheme == "nr_polar_scl" else 0
+        self.dec = _native.Decoder(N, info_set, a.M, crc, device)
+        if E:
+            self.dec.set_rate_match(E)
+        self.n_in = E or N
+        self.beta = np.load(a.beta) if (a.scheme == "dl_scl" and a.beta) else None
+        self.mem = None
+        self.cap = 0
+
+    def _ensure(self, n: int) -> None:
+        if n <= self.cap:
+            return
+        if self.mem is not None:
+            self.mem.__exit__(None, None, None)
+        W = self.dec.W
+        self.mem = _native.DeviceArena(self.dec)
+        self.d_llr = self.mem.alloc(n * self.n_in * 8)
+        self.d_msg = self.mem.alloc(n * W * 8)
+        self.d_best = self.mem.alloc(n * W * 8)
+        self.d_flags = self.mem.alloc(n)
+        self.d_att = self.mem.alloc(n * 4)
+        self.cap = n
+
+    def frames(self, seed: int, EbN0_dB: float, frame0: int, n: int):
+        a, dec = self.args, self.dec
+        if n <= 0:
+            return np.zeros(0, np.int64), np.zeros(0)
+        self._ensure(n)
+        W = dec.W
+        k_tx = self.payload_len  # payload bits; the CRC (if any) follows them
+        dec.channel_device(seed, int(round(EbN0_dB * 10)), EbN0_dB, self.payload_len / a.E, k_tx, frame0, n,
+                           self.d_llr, self.d_msg)
+        work = np.zeros(n)
+        if a.scheme == "dl_scl" and self.crc is not None:
+            dec.dlscl_device(self.d_llr, n, a.retries, beta=self.beta, d_best=self.d_best, d_flags=self.d_flags,
+                             d_attempts=self.d_att)
+            dec.sync()
+            work = (self.mem.download(self.d_att, n * 4, np.int32) - 1).astype(np.float64)
+        else:
+            dec.decode_device(self.d_llr, n, d_best=self.d_best, d_flags=self.d_flags)
+            dec.sync()
+        best = self.mem.download(self.d_best, n * W * 8, np.uint64).reshape(n, W)
+        msg = self.mem.download(self.d_msg, n * W * 8, np.uint64).reshape(n, W)
+        return payload_errors_from_words(best, msg, self.payload_len), work
+
+    def close(self) -> None:
+        if self.mem is not None:
+            self.mem.__exit__(None, None, None)
+            self.mem = None
+        self.dec.close()
+
+
+def run_scheme_philox(source, EbN0_dB, args, coded_len, payload_len, params_label, ctx=None) -> Dict:
+    """One SNR point with frames from the counter-based device stream, sharded over ranks, with
+    the reference's stop rule (run_ber_sweep.py:127) applied at the exact global frame."""
+    ctx = ctx or dist.Context()
+    stats = SimulationStats()
+    frame = 0  # next global frame index of this SNR point
+    while stats.bit_errors < args.err_cap and stats.bits_total < args.bits_cap:
+        left = max(1, math.ceil((args.bits_cap - stats.bits_total) / payload_len))
+        total = int(min(args.batch * ctx.world, left))
+        s, e = dist.shard(total, ctx.rank, ctx.world)
+        bit_err, work = source.frames(args.seed, EbN0_dB, frame + s, e - s)
+        part = np.array([e - s, bit_err.sum(), np.count_nonzero(bit_err), work.sum()], np.float64)
+        parts = dist.allgather(part, ctx)  # [world, 4], rank order
+        err_round = int(parts[:, 1].sum())
+        if stats.bit_errors + err_round < args.err_cap and stats.bits_total + total * payload_len < args.bits_cap:
+            tot = parts.sum(axis=0)
+            n_used, err_used, ferr_used, work_used = int(tot[0]), int(tot[1]), int(tot[2]), float(tot[3])
+        else:  # the stop frame lies in this round: first global frame meeting the rule
+            before = stats.bit_errors + int(parts[: ctx.rank, 1].sum())
+            cum_err = before + np.cumsum(bit_err)
+            cum_bits = stats.bits_total + payload_len * (s + np.arange(1, e - s + 1))
+            hit = np.flatnonzero((cum_err >= args.err_cap) | (cum_bits >= args.bits_cap))
+            cand = s + int(hit[0]) if hit.size else total
+            stop = int(dist.allreduce_min(cand, ctx))  # round-local index of the last frame drawn
+            k = int(np.clip(stop + 1 - s, 0, e - s))
+            mine = np.array([k, bit_err[:k].sum(), np.count_nonzero(bit_err[:k]), work[:k].sum()], np.float64)
+            tot = dist.allreduce_sum(mine, ctx)
+            n_used, err_used, ferr_used, work_used = int(tot[0]), int(tot[1]), int(tot[2]), float(tot[3])
+        stats.bits_total += n_used * payload_len
+        stats.bit_errors += err_used
+        stats.frame_errors += ferr_used
+        stats.work_sum += work_used
+        stats.frames += n_used
+        frame += total
+    row = stats.row()
+    row.update({"scheme": args.scheme, "code": args.scheme, "N_or_E": coded_len, "K_payload": payload_len,
+                "K_crc": args.K_crc, "rate": payload_len / coded_len, "params": params_label, "EbN0_dB": EbN0_dB})
+    return row
+
+
 def parse_args(argv: Optional[Iterable[str]] = None) -> argparse.Namespace:
     parser = argparse.ArgumentParser(description="BER/FER sweep across schemes")
     parser.add_argument("--scheme", required=True, choices=["polar_scl", "dl_scl", "nr_polar_scl", "nr_ldpc"],
@@ -185,7 +314,10 @@ def parse_args(argv: Optional[Iterable[str]] = None) -> argparse.Namespace:
     parser.add_argument("--plot", type=str, help="Optional plot path")
     # engine options (not in the reference)
     parser.add_argument("--batch", type=int, default=4096, help="frames per GPU batch")
-    parser.add_argument("--device", type=int, default=0)
+    parser.add_argument("--device", type=int, default=0, help="GPU (single process; torchrun ranks use LOCAL_RANK)")
+    parser.add_argument("--rng", choices=["replay", "philox"], default="replay",
+                        help="replay: the reference's NumPy stream, exact rows, one process; philox: frames "
+                             "generated on the GPU by global index, sharded over torchrun ranks")
     args = parser.parse_args(list(argv) if argv is not None else None)
     if args.scheme == "dl_scl" and not args.beta:
         raise ValueError("--beta is required for dl_scl scheme")
@@ -206,9 +338,22 @@ def run(args: argparse.Namespace) -> List[Dict[str, float]]:
         params_label = f"M={args.M},retries={args.retries}"
     else:
         params_label = f"M={args.M},ilv={args.ilv_mode}"
-    scheme = _Scheme(args, info_set, N)
+    snrs = np.arange(args.EbN0_lo, args.EbN0_hi + 1e-12, args.EbN0_step)
     rows: List[Dict[str, float]] = []
-    for EbN0_dB in np.arange(args.EbN0_lo, args.EbN0_hi + 1e-12, args.EbN0_step):
+    if args.rng == "philox":
+        ctx = dist.init()
+        source = PhiloxFrames(args, info_set, N, ctx.device if ctx.world > 1 else args.device)
+        try:
+            for EbN0_dB in snrs:
+                rows.append(run_scheme_philox(source, float(EbN0_dB), args, args.E, args.K_payload, params_label, ctx))
+        finally:
+            source.close()
+        return rows
+    if dist.init().world > 1:
+        raise ValueError("--rng replay draws every frame from one NumPy stream (one process); "
+                         "use --rng philox to shard frames over ranks")
+    scheme = _Scheme(args, info_set, N)
+    for EbN0_dB in snrs:
         rows.append(run_scheme(rng, float(EbN0_dB), args, info_set, scheme, args.E, args.K_payload, params_label))
     return rows
 
@@ -254,11 +399,13 @@ def plot_rows(rows: List[Dict[str, float]], path: Path) -> None:
 def main(argv: Optional[Iterable[str]] = None) -> None:
     args = parse_args(argv)
     rows = run(args)
-    out_path = Path(args.out)
-    out_path.parent.mkdir(parents=True, exist_ok=True)
-    write_csv(rows, out_path)
-    if args.plot:
-        plot_rows(rows, Path(args.plot))
+    if dist.init().is_root:
+        out_path = Path(args.out)
+        out_path.parent.mkdir(parents=True, exist_ok=True)
+        write_csv(rows, out_path)
+        if args.plot:
+            plot_rows(rows, Path(args.plot))
+    dist.finalize()
 
 
 if __name__ == "__main__":

@@ -126,3 +126,24 @@ def test_long_device_counters():
     assert cnt[1] == int(np.count_nonzero(~host["crc_pass"]))
     assert cnt[2] == int(np.count_nonzero(host["best_bits"] != msg))
     np.testing.assert_array_equal((flags & 0x80) != 0, host["crc_pass"])
+
+
+@pytest.mark.parametrize("N,E", [(256, 300), (256, 200), (512, 600)])
+def test_long_code_rate_matched_staging(N, E):
+    """The long-code kernel's rate-matched channel staging (de-repetition / de-puncture and
+    sub-block de-interleave fused into the staging, pscl_set_rate_match with N > 128) against the
+    package's host mirrors of scl_nr.py:47-48 plus the oracle, every output bit for bit."""
+    from polar_code_amd.nr.polar import derate_match_polar, subblock_deinterleave
+
+    rng = np.random.default_rng(N + E)
+    K = N // 2
+    info = construct_info_set(N, K)
+    llrE = rng.normal(1.5, 3.0, size=(40, E))
+    llrE[:5] = np.round(llrE[:5])  # integer LLRs: exact metric ties through the front end
+    dec = _native.Decoder(N, info, 4, POLY)
+    dec.set_rate_match(E)
+    out = dec.decode(llrE)
+    internal = np.stack([subblock_deinterleave(derate_match_polar(x, N), N) for x in llrE])
+    for f in range(llrE.shape[0]):
+        n, c, m, il, b = oracle.decode_scl(internal[f], info, 4, crc=POLY)
+        _assert_decode(out, f, n, c, m, il, b, f"N={N} E={E} frame {f}")

@@ -79,3 +79,45 @@ def test_nr_channel_kernel_roundtrip():
     msg = ((msgw[:, :, None] >> np.arange(64, dtype=np.uint64)) & 1).reshape(B, 128)[:, :88].astype(np.int8)
     assert out["crc_pass"].all()
     np.testing.assert_array_equal(out["best_bits"], msg)
+
+
+CFG5 = ["--scheme", "nr_polar_scl", "--K_payload", "64", "--K_crc", "24", "--E", "256", "--N", "128", "--M", "8"]
+
+
+def test_ber_sweep_philox_world2_equals_world1(tmp_path):
+    """BASELINE config 5 through the CLI with device frames: two ranks (gloo, sharing the GPU)
+    write the same rows as one, including the exact stop frame of every SNR point."""
+    from test_gpu_dist import _launch
+
+    argv = ["-m", "polar_code_amd.eval.run_ber_sweep", *CFG5, "--EbN0_lo", "3.0", "--EbN0_hi", "5.0",
+            "--EbN0_step", "1.0", "--err_cap", "4000", "--bits_cap", "3e6", "--batch", "3000", "--rng", "philox"]
+    text = {}
+    for world in (1, 2):
+        out = tmp_path / f"w{world}.csv"
+        _launch(world, argv + ["--out", str(out)])
+        text[world] = out.read_text()
+    assert text[1] == text[2] and text[1].count("\n") == 4
+    rows = [r.split(",") for r in text[1].splitlines()[1:]]
+    # 3 dB stops on err_cap, the cap on bits can stop the others: both rules exercised
+    assert int(rows[0][9]) >= 4000 and all(int(r[8]) <= 3e6 + 64 for r in rows)
+
+
+def test_ber_sweep_philox_matches_replay_statistically(tmp_path):
+    """Device (Philox) frames and the reference's NumPy stream give the same FER/BER at 5 dB
+    within Monte-Carlo error (config 5)."""
+    rows = {}
+    for rng in ("replay", "philox"):
+        out = tmp_path / f"{rng}.csv"
+        rb.main([*CFG5, "--EbN0_lo", "5.0", "--EbN0_hi", "5.0", "--err_cap", "6000", "--bits_cap", "1e7",
+                 "--batch", "8192", "--rng", rng, "--out", str(out)])
+        h, v = out.read_text().splitlines()[:2]
+        rows[rng] = dict(zip(h.split(","), v.split(",")))
+    n = {k: int(r["bits_total"]) // 64 for k, r in rows.items()}
+    p = {k: float(r["fer"]) for k, r in rows.items()}
+    pp = (p["replay"] * n["replay"] + p["philox"] * n["philox"]) / (n["replay"] + n["philox"])
+    z = (p["philox"] - p["replay"]) / np.sqrt(pp * (1 - pp) * (1 / n["replay"] + 1 / n["philox"]))
+    assert abs(z) < 4.5, (rows, z)
+    ber = {k: float(r["ber"]) for k, r in rows.items()}
+    assert 0.6 < ber["philox"] / ber["replay"] < 1.6, rows
+    print(f"config 5 at 5 dB: replay FER {p['replay']:.4f} ({n['replay']} frames), philox FER {p['philox']:.4f} "
+          f"({n['philox']} frames), z = {z:.2f}")

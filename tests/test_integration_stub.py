@@ -20,11 +20,13 @@ def stub():
 
 
 def test_stub_loads_and_validates_without_a_device(stub):
-    assert set(stub.__all__) == {"decode_scl", "sc_decode", "decode_with_retries_batch"}
+    assert set(stub.__all__) == {"decode_scl", "sc_decode", "SCLDecoder", "decode_with_retries_batch"}
     with pytest.raises(ValueError):
         stub.decode_scl(np.zeros(128), np.arange(64), 0)  # M <= 0 (scl.py:119-120)
     with pytest.raises(ValueError):
         stub.decode_scl(np.zeros(128), np.arange(64), 4, force_info_bits=np.zeros(3, np.int8))
+    with pytest.raises(ValueError):
+        stub.SCLDecoder(128, np.arange(64), 0)
 
 
 @pytest.mark.gpu
@@ -47,6 +49,34 @@ def test_stub_decode_scl_golden(stub, golden, name):
             b = int(g[key + "_best"][f])
             np.testing.assert_array_equal(r["best_path_bits"], g[key + "_cands"][f][b])
             np.testing.assert_array_equal(r["best_path_info_llrs"], g[key + "_info_llrs"][f][b])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["g4_decode.npz", "g6_forced.npz"])
+def test_stub_scl_decoder_batch_golden(stub, golden, name):
+    """The batch API (SCLDecoder.decode over every golden frame of a configuration in one call)
+    equals the reference's per-frame decode_scl outputs."""
+    g = golden(name)
+    crc = str(g["crc"]) or None
+    for key in map(str, g["keys"]):
+        M = int(key.split("_")[0][1:])
+        llr = g[key + "_llr"]
+        forced = g[key + "_force"] if key + "_force" in g.files else None
+        if forced is not None and np.all(forced == -1):
+            forced = None
+        if forced is not None and np.any(forced == -1):
+            continue  # per-frame mix of forced / unforced: covered by test_stub_decode_scl_golden
+        r = stub.SCLDecoder(llr.shape[1], g["info"], M, crc).decode(llr, forced, metrics=True, candidates=True,
+                                                                     info_llrs=True)
+        n = g[key + "_npaths"]
+        np.testing.assert_array_equal(r["n_paths"], n)
+        np.testing.assert_array_equal(r["best_idx"], g[key + "_best"])
+        for f in range(llr.shape[0]):
+            k = int(n[f])
+            np.testing.assert_array_equal(r["cands"][f, :k], g[key + "_cands"][f][:k])
+            np.testing.assert_array_equal(r["metrics"][f, :k], g[key + "_metrics"][f][:k])
+            np.testing.assert_array_equal(r["info_llrs"][f, :k], g[key + "_info_llrs"][f][:k])
+            np.testing.assert_array_equal(r["bits"][f], g[key + "_cands"][f][int(g[key + "_best"][f])])
 
 
 @pytest.mark.gpu
