@@ -73,6 +73,8 @@ def compile_units(units, flags: list[str], jobs: int | None = None) -> list[str]
     """Compile the units in parallel (the spec instances take ~40 s each)."""
     from concurrent.futures import ThreadPoolExecutor
 
+    if not units:
+        return []
     base = [HIPCC, f"--offload-arch={ARCH}", *BASE_FLAGS, f"-I{INCLUDE}", f"-I{CSRC}", *flags]
     jobs = jobs or min(len(units), max(1, min(16, os.cpu_count() or 1)))
     with ThreadPoolExecutor(jobs) as ex:

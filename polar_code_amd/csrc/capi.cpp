@@ -530,12 +530,13 @@ int pscl_set_beta(pscl_handle* h, const double* beta) {
 // retry rounds of one chunk on the retry stream (state sized for the largest chunk)
 namespace {
 struct DlState {
-    int64_t* act;
-    int32_t *list0, *list1, *cnt;
-    double* al0;
-    uint64_t *refw, *tried, *force, *ob;
+    int32_t* cnt;     // [1] failing baseline frames of the chunk (dl_compact)
+    int64_t* act;     // [cap] frame index of each entry
+    int32_t* bcnt;    // [rounds + 1][NSEG * CSTRIDE] bucket counters of each round's list
+    int32_t *list0, *list1;  // [NSEG][cap] bucket lists (entry ids), alternating rounds
+    uint64_t *tried, *force, *warm_u, *ob;
     int32_t* nt;
-    int64_t* fidx;
+    double* warm_metric;
     uint8_t* of;
 };
 
@@ -543,81 +544,72 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
                    uint8_t* d_flags, int32_t* d_attempts, int32_t* d_tried, int tried_stride, int64_t* d_cnt_dl,
                    hipStream_t st) {
     const int K = h->K, W = h->W;
-    const size_t a = (size_t)A;
     hipError_t e;
-    HIP_TRY(hipMemsetAsync(S.tried, 0, a * 16, st));
-    HIP_TRY(hipMemsetAsync(S.nt, 0, a * 4, st));
-    // L0 of the baseline's best path (flip.py:97-102), replayed from its bits; the
-    // reference bits are the baseline's best bits
-    pscl_replay_params Rp;
-    memset(&Rp, 0, sizeof(Rp));
-    Rp.llr = d_llr;
-    Rp.N = h->N;
-    Rp.n = h->n;
-    Rp.K = K;
-    Rp.W = W;
-    Rp.rm_E = h->rm_E;
-    Rp.rm_src = h->d_rm_src;
-    Rp.info_mask[0] = h->info_mask[0];
-    Rp.info_mask[1] = h->info_mask[1];
-    Rp.count = S.cnt;
-    Rp.act = S.act;
-    Rp.bits = d_best;
-    Rp.bits_by_row = 1;
-    Rp.out = S.al0;
-    if ((e = pscl_launch_replay(Rp, A, st)) != hipSuccess) return fail(PSCL_EDEVICE, "replay launch: %s", hipGetErrorString(e));
-    if ((e = pscl_launch_dl_gather(d_best, S.act, S.cnt, A, W, S.refw, st)) != hipSuccess)
-        return fail(PSCL_EDEVICE, "dl_gather launch: %s", hipGetErrorString(e));
-    pscl_dl_params D;
-    memset(&D, 0, sizeof(D));
-    D.K = K;
-    D.W = W;
-    D.rounds = rounds;
-    D.act = S.act;
-    D.al0 = S.al0;
-    D.ref = S.refw;
-    D.tried = S.tried;
-    D.ntried = S.nt;
-    D.beta = h->d_beta;
-    D.force = S.force;
-    D.fidx = S.fidx;
-    D.ob = S.ob;
-    D.oflags = S.of;
-    D.best = d_best;
-    D.flags = d_flags;
-    D.attempts = d_attempts;
-    D.tried_out = d_tried;
-    D.tried_stride = tried_stride;
-    D.counters = d_cnt_dl;
+    const size_t bstride = (size_t)PSCL_DL_NSEG * PSCL_DL_CSTRIDE;
+    HIP_TRY(hipMemsetAsync(S.bcnt, 0, (size_t)(rounds + 1) * bstride * 4, st));
+    pscl_post_params Q;
+    memset(&Q, 0, sizeof(Q));
+    Q.llr = d_llr;
+    Q.N = h->N;
+    Q.n = h->n;
+    Q.K = K;
+    Q.W = W;
+    Q.rm_E = h->rm_E;
+    Q.rm_src = h->d_rm_src;
+    Q.info_mask[0] = h->info_mask[0];
+    Q.info_mask[1] = h->info_mask[1];
+    Q.info_set = h->d_info_set;
+    Q.exp_table = h->d_exp_table;
+    Q.rounds = rounds;
+    Q.cap = A;
+    Q.act = S.act;
+    Q.tried = S.tried;
+    Q.ntried = S.nt;
+    Q.beta = h->d_beta;
+    Q.force = S.force;
+    Q.warm_metric = S.warm_metric;
+    Q.warm_u = S.warm_u;
+    Q.ob = S.ob;
+    Q.of = S.of;
+    Q.best = d_best;
+    Q.flags = d_flags;
+    Q.attempts = d_attempts;
+    Q.tried_out = d_tried;
+    Q.tried_stride = tried_stride;
+    Q.counters = d_cnt_dl;
     int32_t* lists[2] = {S.list0, S.list1};
-    // the retry decodes: plain kernel, LLR rows by indirection, forced prefixes
+    // first flips: replay of every baseline best path (flip.py:97-111)
+    Q.init = 1;
+    Q.in_count = S.cnt;
+    Q.out_count = S.bcnt;
+    Q.out_list = lists[0];
+    if ((e = pscl_launch_dl_post(Q, A, st)) != hipSuccess) return fail(PSCL_EDEVICE, "dl_post launch: %s", hipGetErrorString(e));
+    // the retry decodes: entries bucket by bucket, LLR rows by indirection, forced prefixes,
+    // warm-started past them (the compiled-in FS kernels; others decode from phase 0)
     pscl_decode_params H;
     fill_decode_params(h, H, 0);
     H.llr = d_llr;
     H.B = A;
-    H.fidx = D.fidx;
-    H.force = D.force;
+    H.fidx = S.act;
+    H.force = S.force;
     H.best = S.ob;
     H.flags = S.of;
+    H.bcap = A;
+    H.warm_metric = S.warm_metric;
+    H.warm_u = S.warm_u;
     if (pscl_decode_wpg(H) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
-    Rp.bits = S.ob;  // each round's best bits, by list position
-    Rp.bits_by_row = 0;
     int rc;
+    Q.init = 0;
     for (int r = 0; r < rounds; ++r) {  // no host round trips: the counts stay on the device
-        D.n = S.cnt + r;
-        D.list = lists[r & 1];
-        D.next_list = lists[(r + 1) & 1];
-        D.next_count = S.cnt + r + 1;
-        if ((e = pscl_launch_dl_select(D, A, st)) != hipSuccess)
-            return fail(PSCL_EDEVICE, "dl_select launch: %s", hipGetErrorString(e));
-        H.d_count = D.n;
+        H.elist = lists[r & 1];
+        H.bcount = S.bcnt + (size_t)r * bstride;
         if ((rc = launch_decode(h, H, 0, st))) return rc;
-        Rp.count = D.n;
-        Rp.list = D.list;
-        if ((e = pscl_launch_replay(Rp, A, st)) != hipSuccess)
-            return fail(PSCL_EDEVICE, "replay launch: %s", hipGetErrorString(e));
-        if ((e = pscl_launch_dl_update(D, A, st)) != hipSuccess)
-            return fail(PSCL_EDEVICE, "dl_update launch: %s", hipGetErrorString(e));
+        Q.in_count = H.bcount;
+        Q.in_list = lists[r & 1];
+        Q.out_count = S.bcnt + (size_t)(r + 1) * bstride;
+        Q.out_list = lists[(r + 1) & 1];
+        if ((e = pscl_launch_dl_post(Q, A, st)) != hipSuccess)
+            return fail(PSCL_EDEVICE, "dl_post launch: %s", hipGetErrorString(e));
     }
     return PSCL_OK;
 }
@@ -663,29 +655,29 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
         }
         if (!h->h_count) HIP_TRY(hipHostMalloc((void**)&h->h_count, 16, hipHostMallocDefault));
         // everything sized before any work is queued (an allocation synchronizes the device)
-        const size_t c = (size_t)cap;
-        void* q[12];
-        const size_t sz[12] = {(size_t)(rounds + 2) * 4, c * 8, c * 4, c * 4, c * K * 8, c * W * 8,
-                               c * 16, c * 4, c * 2 * W * 8, c * 8, c * W * 8, c};
-        for (int i = 0; i < 12; ++i)
+        const size_t c = (size_t)cap, NS = PSCL_DL_NSEG;
+        void* q[10];
+        const size_t sz[10] = {(size_t)(rounds + 1) * NS * PSCL_DL_CSTRIDE * 4, NS * c * 4, NS * c * 4, c * 16, c * 4,
+                               c * 2 * W * 8, c * NS * 8, c * 16, c * W * 8, c};
+        for (int i = 0; i < 10; ++i)
             if ((rc = ensure(h, 12 + i, sz[i], &q[i]))) return rc;
-        void *q1[3];
-        if ((rc = ensure(h, 27, sz[0], &q1[0])) || (rc = ensure(h, 28, sz[1], &q1[1])) ||
-            (rc = ensure(h, 29, sz[2], &q1[2])))
+        void *pc[2], *pa[2];
+        if ((rc = ensure(h, 22, 4, &pc[0])) || (rc = ensure(h, 23, c * 8, &pa[0])) || (rc = ensure(h, 27, 4, &pc[1])) ||
+            (rc = ensure(h, 28, c * 8, &pa[1])))
             return rc;
-        for (int i = 0; i < 2; ++i) {
-            S[i].cnt = (int32_t*)(i ? q1[0] : q[0]);
-            S[i].act = (int64_t*)(i ? q1[1] : q[1]);
-            S[i].list0 = (int32_t*)(i ? q1[2] : q[2]);
-            S[i].list1 = (int32_t*)q[3];  // the retry state is used by one chunk at a time
-            S[i].al0 = (double*)q[4];
-            S[i].refw = (uint64_t*)q[5];
-            S[i].tried = (uint64_t*)q[6];
-            S[i].nt = (int32_t*)q[7];
-            S[i].force = (uint64_t*)q[8];
-            S[i].fidx = (int64_t*)q[9];
-            S[i].ob = (uint64_t*)q[10];
-            S[i].of = (uint8_t*)q[11];
+        for (int i = 0; i < 2; ++i) {  // the retry state is used by one chunk at a time
+            S[i].cnt = (int32_t*)pc[i];
+            S[i].act = (int64_t*)pa[i];
+            S[i].bcnt = (int32_t*)q[0];
+            S[i].list0 = (int32_t*)q[1];
+            S[i].list1 = (int32_t*)q[2];
+            S[i].tried = (uint64_t*)q[3];
+            S[i].nt = (int32_t*)q[4];
+            S[i].force = (uint64_t*)q[5];
+            S[i].warm_metric = (double*)q[6];
+            S[i].warm_u = (uint64_t*)q[7];
+            S[i].ob = (uint64_t*)q[8];
+            S[i].of = (uint8_t*)q[9];
         }
     }
     auto retries_of = [&](int64_t c) -> int {
@@ -718,8 +710,8 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
         if (rounds > 0) {
             const int p = (int)(c & 1);
             if (c >= 2) HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[p], 0));  // parity buffers free again
-            HIP_TRY(hipMemsetAsync(S[p].cnt, 0, (size_t)(rounds + 2) * 4, s));
-            if ((e = pscl_launch_dl_compact(d_flags + c0, nc, c0, S[p].act, S[p].list0, S[p].cnt, s)) != hipSuccess)
+            HIP_TRY(hipMemsetAsync(S[p].cnt, 0, 4, s));
+            if ((e = pscl_launch_dl_compact(d_flags + c0, nc, c0, S[p].act, nullptr, S[p].cnt, s)) != hipSuccess)
                 return fail(PSCL_EDEVICE, "dl_compact launch: %s", hipGetErrorString(e));
             HIP_TRY(hipMemcpyAsync(h->h_count + p, S[p].cnt, 4, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipEventRecord(h->ev_base[p], s));

@@ -2,15 +2,27 @@
 //
 // The retry loop of decode_with_retries runs over a compacted list of the frames whose
 // baseline SCL best candidate fails the CRC.  Each frame keeps, in an "entry" slot, the
-// state the reference threads through its loop (flip.py:110-136): the reference bits, the
-// decision LLRs L0 of the best path, and the set of tried indices.  One round is
-//   dl_select_kernel  q = |L0| @ beta (or |L0|), flip = argmin over untried (q, index),
-//                     force vector = reference prefix + flipped bit (flip.py:30-34)
-//   decode            the SCL kernel on the live entries (LLR row indirection, forced bits)
-//   replay_kernel     L0 of the attempt's best path (flip.py:127-132), recomputed from its bits
-//   dl_update_kernel  final-attempt bookkeeping, CRC stop rule, compaction of the survivors
-// Frames never leave the GPU.  The live counts stay on the device: every round is enqueued
-// with grids sized for the first round, and waves past the live count exit at once.
+// state the reference threads through its loop (flip.py:110-136): the set of tried indices
+// and the latest attempt's best bits (the reference bits of the next force vector).  A round
+// is two launches:
+//   decode            the SCL kernel on the round's entries (LLR row by indirection, forced
+//                     bits), warm-started past each entry's forced prefix (below)
+//   dl_post_kernel    per entry: replay of the attempt's best path (all leaf LLRs, hence L0,
+//                     flip.py:127-132), final-attempt bookkeeping and the CRC stop rule
+//                     (flip.py:123-136); for the survivors the next flip -- q = |L0| @ beta,
+//                     argmin over untried (q, index) (flip.py:104-111) -- its force vector
+//                     (flip.py:30-34) and the warm-start state of its forced prefix
+// A first post pass over the baseline results (init) selects every entry's first flip.
+// Frames never leave the GPU; the live counts stay on the device.
+//
+// Warm start.  A retry forces the reference bits on info indices [0, idx) and the flipped bit
+// at idx: up to the flipped phase phi* = info_set[idx] the list holds ONE path whose bits are
+// known, so its leaf LLRs are the replayed ones and its metric is their exact increments summed
+// in phase order.  The post pass writes that metric at every 16-phase boundary below phi*
+// (warm_metric[e][k], k <= phi* / 16) and appends the entry to bucket phi* / 16 of the next
+// round's list; the decode kernel maps its frames to entries bucket by bucket and starts each
+// wavefront at phase 16 k of its first frame's bucket (scl128_impl.h), skipping 16 k phases of
+// tree walk, metric tails and list updates per frame -- half the phases on average at 5 dB.
 //
 // Why a replay instead of the decoder's history: the decision LLR of a path at info phase
 // j (scl.py:158,166) is a function of the channel LLRs and the path's own earlier bits only
@@ -67,7 +79,7 @@ __global__ void __launch_bounds__(1024) dl_compact_kernel(const uint8_t* __restr
     if (failing) {
         const int pos = bbase + wcnt[wave] + __popcll(m & ((1ULL << lane) - 1ULL));
         act[pos] = base + f;
-        list[pos] = pos;
+        if (list) list[pos] = pos;
     }
 }
 
@@ -76,53 +88,41 @@ __global__ void __launch_bounds__(256) iota64_kernel(int64_t* out, int64_t n) {
     if (i < n) out[i] = i;
 }
 
-// entry reference bits = the frame's baseline best bits
-__global__ void __launch_bounds__(256) dl_gather_kernel(const uint64_t* __restrict__ best, const int64_t* __restrict__ act,
-                                                        const int32_t* __restrict__ count, int W,
-                                                        uint64_t* __restrict__ ref) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= *count) return;
-    for (int w = 0; w < W; ++w) ref[e * W + w] = best[act[e] * W + w];
+// Channel LLRs p = lane and lane + 64 of a frame row (rate matched: de-rate-matched and
+// de-interleaved on the fly); N <= 128
+__device__ __forceinline__ void load_row(const double* llr_row, int rm_E, const int32_t* rm_src, int N, double& c0,
+                                         double& c1) {
+    const int lane = threadIdx.x & 63;
+    c0 = c1 = 0.0;
+    if (lane < N) c0 = rm_E == 0 ? llr_row[lane] : pscl::nr_stage(llr_row, rm_src[lane], rm_E, N);
+    if (lane + 64 < N) c1 = rm_E == 0 ? llr_row[lane + 64] : pscl::nr_stage(llr_row, rm_src[lane + 64], rm_E, N);
 }
 
-// one wavefront per entry: leaf LLRs of the entry's path (bits given), written at its info
-// positions.  LDS: two 128-double level buffers per wave.
-__global__ void __launch_bounds__(256) replay_kernel(const pscl_replay_params R, int64_t cap) {
-    __shared__ double lvl[4][2][PSCL_FAST_N];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t b = (int64_t)blockIdx.x * 4 + wave;
-    if (b >= *R.count || b >= cap) return;
-    const int N = R.N, K = R.K, W = R.W;
-    const int e = R.list ? R.list[b] : (int)b;
-    const int64_t row = R.act[e];
-    double* cur = lvl[wave][0];
-    double* nxt = lvl[wave][1];
-    for (int p = lane; p < N; p += 64) {
-        if (R.rm_E == 0) cur[p] = R.llr[row * N + p];
-        else cur[p] = pscl::nr_stage(R.llr + row * R.rm_E, R.rm_src[p], R.rm_E, N);
-    }
-    // the path's u: frozen 0, info position p carries bit j = #info positions below p
-    const uint64_t* bw = R.bits + (R.bits_by_row ? row : b) * W;
-    uint64_t u[2] = {0, 0};
-    int jpos[2] = {-1, -1};
+// Leaf LLRs of a path with information bits (b0, b1), top-down through the tree (one
+// wavefront; channel values c0, c1 from load_row; cur, nxt: 128-double LDS buffers).  Returns
+// the buffer holding the N leaves; u[h] = the path's bits u[64 h + lane] (ballots), jpos[h] =
+// info index of phase 64 h + lane (or -1).
+__device__ __forceinline__ double* replay_leaves(double c0, double c1, int N, int n, const uint64_t* info_mask,
+                                                 uint64_t b0, uint64_t b1, double* cur, double* nxt, uint64_t* u,
+                                                 int* jpos) {
+    const int lane = threadIdx.x & 63;
+    if (lane < N) cur[lane] = c0;
+    if (lane + 64 < N) cur[lane + 64] = c1;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int p = lane + 64 * h;
         bool bit = false;
-        if (p < N && ((R.info_mask[h] >> lane) & 1ULL)) {
-            const int j = (h ? __popcll(R.info_mask[0]) : 0) + __popcll(R.info_mask[h] & ((1ULL << lane) - 1ULL));
+        jpos[h] = -1;
+        if (p < N && ((info_mask[h] >> lane) & 1ULL)) {
+            const int j = (h ? __popcll(info_mask[0]) : 0) + __popcll(info_mask[h] & ((1ULL << lane) - 1ULL));
             jpos[h] = j;
-            bit = (bw[j >> 6] >> (j & 63)) & 1ULL;
+            bit = ((j < 64 ? b0 : b1) >> (j & 63)) & 1ULL;
         }
         u[h] = __ballot(bit);
     }
     pscl::wave_lds_fence();
-    // level d -> d+1: node k' of width w2 at flat position p' = k' w2 + i; its parent's
-    // halves are a = lvl_d[(k'>>1) 2 w2 + i], b = a's partner + w2 (polar.py:122-127)
-    for (int d = 0; d < R.n; ++d) {
-        // w2 = N >> (d + 1) = 2^lw2: node index and offset by shift and mask (a runtime
-        // integer division here cost more VALU than the f/g work of the whole replay)
-        const int lw2 = R.n - d - 1, w2 = 1 << lw2;
+    for (int d = 0; d < n; ++d) {
+        const int lw2 = n - d - 1, w2 = 1 << lw2;
         for (int p2 = lane; p2 < N; p2 += 64) {
             const int k2 = p2 >> lw2, i = p2 & (w2 - 1);
             const int pa = ((k2 >> 1) << (lw2 + 1)) + i;
@@ -130,7 +130,7 @@ __global__ void __launch_bounds__(256) replay_kernel(const pscl_replay_params R,
             double v;
             if (!(k2 & 1)) {
                 v = f_minsum(a, bb);
-            } else {  // partial sums of the left sibling u[(k2-1) w2, k2 w2)
+            } else {
                 const int lo = (k2 - 1) * w2;
                 const uint64_t word = u[lo >> 6] >> (lo & 63);
                 const uint64_t chunk = w2 >= 64 ? word : (word & ((1ULL << w2) - 1ULL));
@@ -143,114 +143,273 @@ __global__ void __launch_bounds__(256) replay_kernel(const pscl_replay_params R,
         cur = nxt;
         nxt = t;
     }
-    double* out = R.out + (int64_t)e * K;
+    return cur;
+}
+
+// one wavefront per entry: leaf LLRs of the entry's path (bits given), written at its info
+// positions.  LDS: two 128-double level buffers per wave.
+__global__ void __launch_bounds__(256) replay_kernel(const pscl_replay_params R, int64_t cap) {
+    __shared__ double lvl[4][2][PSCL_FAST_N];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+    if (b >= *R.count || b >= cap) return;
+    const int e = R.list ? R.list[b] : (int)b;
+    const int64_t row = R.act[e];
+    const uint64_t* bw = R.bits + (R.bits_by_row ? row : b) * R.W;
+    uint64_t u[2];
+    int jpos[2];
+    double c0, c1;
+    load_row(R.llr + row * (R.rm_E ? R.rm_E : R.N), R.rm_E, R.rm_src, R.N, c0, c1);
+    const double* cur = replay_leaves(c0, c1, R.N, R.n, R.info_mask, bw[0], R.W > 1 ? bw[1] : 0ULL, lvl[wave][0],
+                                      lvl[wave][1], u, jpos);
+    double* out = R.out + (int64_t)e * R.K;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
         if (jpos[h] >= 0) out[jpos[h]] = cur[lane + 64 * h];
 }
 
-// wavefronts over live entries, beta staged in LDS: choose the flip index, build the force
-// words (persistent grid)
-__global__ void __launch_bounds__(256) dl_select_kernel(const pscl_dl_params D) {
-    extern __shared__ double sbeta[];
-    const int K = D.K, W = D.W;
-    if (D.beta) {
-        for (int i = threadIdx.x; i < K * K; i += blockDim.x) sbeta[i] = D.beta[i];
+// Timing-only ablations of dl_post_kernel (tools/build_variant.py --unit dlscl
+// -DPSCL_POST_ABLATE=m; 0 in the product, results invalid otherwise): 1 no bucket atomics,
+// 2 no warm-start tails, 4 no flip metric (q = |L0|), 8 no serial prefix sums
+#ifndef PSCL_POST_ABLATE
+#define PSCL_POST_ABLATE 0
+#endif
+
+// One post pass of the retry loop (see the header).  Workgroups of 8 wavefronts own
+// contiguous ranges of the pass's entries, one entry per wavefront at a time.  Every
+// wavefront preloads the metadata of its next 32 entries (one lane each: entry id, frame,
+// bits, flags, tried state) and prefetches the next entry's channel row while it replays the
+// current one.  Survivors are staged in LDS and appended to the next round's bucket lists
+// with one global atomic per (workgroup, bucket) per 256 entries: one atomic per entry put
+// ~5k same-address device atomics on each bucket counter (measured: 316 of 467 us of the
+// first pass at L = 4, 5 dB).  The flip metric's beta (when K * K doubles fit) and the exp
+// table of the exact metric tails are staged in LDS once per workgroup.
+constexpr int kPostWaves = 8;
+constexpr int kPostIters = 32;  // entries per wavefront between two flushes
+constexpr int kPostChunk = kPostWaves * kPostIters;
+
+struct PostShared {
+    double lvl[kPostWaves][3][PSCL_FAST_N];
+    uint64_t exp_table[PSCL_EXP_TABLE_WORDS];
+    int32_t st_e[kPostChunk];
+    uint16_t st_pos[kPostChunk];
+    uint8_t st_seg[kPostChunk];
+    int32_t lcnt[PSCL_DL_NSEG];
+    int32_t gbase[PSCL_DL_NSEG];
+    int32_t nst;
+};
+
+__global__ void __launch_bounds__(kPostWaves * 64) dl_post_kernel(const pscl_post_params Q, int beta_lds) {
+    __shared__ PostShared S;
+    extern __shared__ double sbeta[];  // [K][K] when beta_lds
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int N = Q.N, K = Q.K, W = Q.W;
+    for (int i = threadIdx.x; i < PSCL_EXP_TABLE_WORDS; i += blockDim.x) S.exp_table[i] = Q.exp_table[i];
+    if (beta_lds)
+        for (int i = threadIdx.x; i < K * K; i += blockDim.x) sbeta[i] = Q.beta[i];
+    if (threadIdx.x < PSCL_DL_NSEG) S.lcnt[threadIdx.x] = 0;
+    if (threadIdx.x == 0) S.nst = 0;
+    const double* beta = beta_lds ? sbeta : Q.beta;
+    int pre[PSCL_DL_NSEG + 1];
+    int64_t n_in;
+    if (Q.init) {
+        n_in = *Q.in_count;
+    } else {
+        n_in = pscl_bucket_prefix(Q.in_count, Q.cap, pre);
+    }
+    if (n_in > Q.cap) n_in = Q.cap;
+    const int64_t per = (n_in + gridDim.x - 1) / gridDim.x;
+    const int64_t i_begin = (int64_t)blockIdx.x * per;
+    const int64_t i_end = i_begin + per < n_in ? i_begin + per : n_in;
+    unsigned long long decodes = 0;
+    double* cur0 = S.lvl[wave][0];
+    double* cur1 = S.lvl[wave][1];
+    double* al = S.lvl[wave][2];
+    __syncthreads();
+    for (int64_t cbase = i_begin; cbase < i_end; cbase += kPostChunk) {  // workgroup-uniform
+        // metadata of this wavefront's entries of the chunk, lane l = entry cbase + 8 l + wave
+        const int64_t mi = cbase + (int64_t)lane * kPostWaves + wave;
+        const bool mvalid = lane < kPostIters && mi < i_end;
+        int me = 0, mnt = 0;
+        int64_t mf = 0;
+        uint64_t mb0 = 0, mb1 = 0, mt0 = 0, mt1 = 0;
+        uint32_t mfl = 0;
+        if (mvalid) {
+            if (Q.init) {
+                me = (int)mi;
+            } else {
+                const int k = pscl_bucket_of(mi, pre);
+                me = Q.in_list[(int64_t)k * Q.cap + (mi - pre[k])];
+            }
+            mf = Q.act[me];
+            const uint64_t* bw = Q.init ? Q.best + mf * W : Q.ob + (int64_t)me * W;
+            mb0 = bw[0];
+            mb1 = W > 1 ? bw[1] : 0ULL;
+            if (!Q.init) {
+                mfl = Q.of[me];
+                mnt = Q.ntried[me];
+                mt0 = Q.tried[2 * me];
+                mt1 = Q.tried[2 * me + 1];
+            }
+        }
+        const int nit = (int)__builtin_amdgcn_readfirstlane((int)__popcll(__ballot(mvalid)));
+        auto rl64 = [](uint64_t v, int l) {
+            return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+        };
+        // channel row of the first entry; later rows are prefetched one entry ahead
+        double c0 = 0.0, c1 = 0.0;
+        if (nit > 0) load_row(Q.llr + rl64((uint64_t)mf, 0) * (Q.rm_E ? Q.rm_E : N), Q.rm_E, Q.rm_src, N, c0, c1);
+        for (int it = 0; it < nit; ++it) {
+            const int e = __builtin_amdgcn_readlane(me, it);
+            const int64_t f = (int64_t)rl64((uint64_t)mf, it);
+            const uint64_t b0 = rl64(mb0, it), b1 = rl64(mb1, it);
+            const int nt = Q.init ? 0 : __builtin_amdgcn_readlane(mnt, it);
+            double n0 = 0.0, n1 = 0.0;
+            if (it + 1 < nit)
+                load_row(Q.llr + rl64((uint64_t)mf, it + 1) * (Q.rm_E ? Q.rm_E : N), Q.rm_E, Q.rm_src, N, n0, n1);
+            bool more;
+            if (Q.init) {  // baseline failing by construction (dl_compact); nothing tried yet
+                more = Q.rounds > 0;
+            } else {       // the attempt just decoded is the frame's latest (flip.py:123-136)
+                const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)mfl, it);
+                if (lane == 0) {
+                    Q.best[f * W] = b0;
+                    if (W > 1) Q.best[f * W + 1] = b1;
+                    Q.flags[f] = (uint8_t)fl;
+                    if (Q.attempts) Q.attempts[f] = nt + 1;
+                }
+                ++decodes;
+                more = !(fl & PSCL_FLAG_CRC_PASS) && nt < Q.rounds;
+            }
+            if (more) {
+                uint64_t u[2];
+                int jpos[2];
+                double* cur = replay_leaves(c0, c1, N, Q.n, Q.info_mask, b0, b1, cur0, cur1, u, jpos);
+                double* nxt = cur == cur0 ? cur1 : cur0;
+                // |L0|: the path's decision LLRs at the information phases (flip.py:97-102, 127-132)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    if (jpos[h] >= 0) al[jpos[h]] = fabs(cur[lane + 64 * h]);
+                pscl::wave_lds_fence();
+                // next flip: argmin over untried indices of (q, index), q = |L0| @ beta summed
+                // in index order (flip.py:104-108), q = |L0| without beta
+                const uint64_t t0 = Q.init ? 0ULL : rl64(mt0, it), t1 = Q.init ? 0ULL : rl64(mt1, it);
+                uint64_t bk = ~0ULL;
+                int bj = 0x7fffffff;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int j = lane + 64 * h;
+                    if (j < K) {
+                        double q;
+                        if (Q.beta && !(PSCL_POST_ABLATE & 4)) {
+                            q = 0.0;
+                            const double* bc = beta + j;
+#pragma unroll 8
+                            for (int k = 0; k < K; ++k) q = q + al[k] * bc[k * K];
+                        } else {
+                            q = al[j];
+                        }
+                        const bool seen = ((h ? t1 : t0) >> (j & 63)) & 1ULL;
+                        const uint64_t key = seen ? ~0ULL : order_key(q);
+                        if (key < bk) {  // h = 0 visited first: ties keep the lower index
+                            bk = key;
+                            bj = j;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int s = 1; s < 64; s <<= 1) {  // wave argmin of (key, index)
+                    const uint64_t ok = pscl::shfl_u64(bk, lane ^ s);
+                    const int oj = __shfl(bj, lane ^ s);
+                    if (ok < bk || (ok == bk && oj < bj)) {
+                        bk = ok;
+                        bj = oj;
+                    }
+                }
+                const int idx = __builtin_amdgcn_readfirstlane(bj);  // an untried index exists: rounds <= min(retries, K)
+                // flipped phase and its warm-start bucket
+                const uint64_t hit0 = __ballot(jpos[0] == idx), hit1 = __ballot(jpos[1] == idx);
+                const int phis = hit0 ? __builtin_ctzll(hit0) : 64 + __builtin_ctzll(hit1);
+                int seg = phis >> 4;
+                if (seg > PSCL_DL_NSEG - 1) seg = PSCL_DL_NSEG - 1;
+                if (PSCL_POST_ABLATE & 2) seg = 0;
+                // exact metric increments of the forced prefix's leaves (scl.py:102-105, as the
+                // decode kernel forms them: good child metric + L, bad child metric + (|llr| + L),
+                // llr == 0: metric + LOGE2), then summed in phase order
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int p = lane + 64 * h;
+                    if (p < 16 * seg) {
+                        const double lam = cur[p];
+                        const uint32_t bit = (uint32_t)(u[h] >> lane) & 1u;
+                        const double Lt = pscl_softplus_tail_bf(lam, S.exp_table);
+                        const bool good = bit == (lam < 0.0 ? 1u : 0u);
+                        nxt[p] = lam == 0.0 ? PSCL_LOGE2 : (good ? Lt : fabs(lam) + Lt);
+                    }
+                }
+                pscl::wave_lds_fence();
+                if (lane == 0) {
+                    double m = 0.0;
+                    double* wm = Q.warm_metric + (int64_t)e * PSCL_DL_NSEG;
+                    for (int k = 0; k <= seg; ++k) {
+                        wm[k] = m;
+                        if (k < seg && !(PSCL_POST_ABLATE & 8))
+                            for (int q = 0; q < 16; ++q) m = m + nxt[16 * k + q];
+                    }
+                    Q.warm_u[2 * e] = u[0];
+                    Q.warm_u[2 * e + 1] = u[1];
+                    // tried set, flip record
+                    Q.tried[2 * e] = idx < 64 ? (t0 | (1ULL << idx)) : t0;
+                    Q.tried[2 * e + 1] = idx >= 64 ? (t1 | (1ULL << (idx - 64))) : t1;
+                    Q.ntried[e] = nt + 1;
+                    if (Q.tried_out) Q.tried_out[f * Q.tried_stride + nt] = idx;
+                    // _force_vector (flip.py:30-34): bits [0, idx) = reference, bit idx flipped, rest free
+                    uint64_t* fr = Q.force + (int64_t)e * 2 * W;
+                    for (int w = 0; w < W; ++w) {
+                        const int lo = 64 * w;
+                        const int nb = idx - lo + 1;  // bits of this word in [0, idx]
+                        const uint64_t mask = nb <= 0 ? 0ULL : (nb >= 64 ? ~0ULL : ((1ULL << nb) - 1ULL));
+                        uint64_t val = (w ? b1 : b0) & mask;
+                        if (idx >= lo && idx < lo + 64) val ^= 1ULL << (idx - lo);
+                        fr[w] = mask;
+                        fr[W + w] = val;
+                    }
+                    // staged append to bucket seg of the next round (LDS atomics)
+                    const int sl = atomicAdd(&S.nst, 1);
+                    S.st_e[sl] = e;
+                    S.st_seg[sl] = (uint8_t)seg;
+                    S.st_pos[sl] = (uint16_t)atomicAdd(&S.lcnt[seg], 1);
+                }
+                pscl::wave_lds_fence();  // the LDS buffers are rewritten by the next entry
+            }
+            c0 = n0;
+            c1 = n1;
+        }
+        // flush: one global atomic per non-empty bucket, then the staged entries scattered
+        __syncthreads();
+        if (threadIdx.x < PSCL_DL_NSEG) {
+            const int c = S.lcnt[threadIdx.x];
+            int g = 0;
+            if (c) {
+                if (PSCL_POST_ABLATE & 1) g = 0;
+                else g = atomicAdd(Q.out_count + threadIdx.x * PSCL_DL_CSTRIDE, c);
+            }
+            S.gbase[threadIdx.x] = g;
+        }
+        __syncthreads();
+        const int nst = S.nst;
+        for (int x = threadIdx.x; x < nst; x += blockDim.x) {
+            const int sg = S.st_seg[x];
+            Q.out_list[(int64_t)sg * Q.cap + S.gbase[sg] + S.st_pos[x]] = S.st_e[x];
+        }
+        __syncthreads();
+        if (threadIdx.x < PSCL_DL_NSEG) S.lcnt[threadIdx.x] = 0;
+        if (threadIdx.x == 0) S.nst = 0;
         __syncthreads();
     }
-    const int lane = threadIdx.x & 63;
-    const int n = *D.n;
-    for (int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); b < n; b += (int64_t)gridDim.x * 4) {
-        const int e = D.list[b];
-        const double* a = D.al0 + (int64_t)e * K;
-        const uint64_t t0 = D.tried[2 * e], t1 = D.tried[2 * e + 1];
-        uint64_t bk = ~0ULL;
-        int bj = 0x7fffffff;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int j = lane + 64 * h;
-            if (j < K) {
-                double q;
-                if (D.beta) {  // q = abs_l0 @ beta (flip.py:104-106), summed in index order
-                    q = 0.0;
-                    for (int k = 0; k < K; ++k) q = q + fabs(a[k]) * sbeta[k * K + j];
-                } else {
-                    q = fabs(a[j]);  // flip.py:107
-                }
-                const bool seen = ((h ? t1 : t0) >> (j & 63)) & 1ULL;
-                const uint64_t key = seen ? ~0ULL : order_key(q);
-                if (key < bk) {  // h = 0 visited first: ties keep the lower index
-                    bk = key;
-                    bj = j;
-                }
-            }
-        }
-#pragma unroll
-        for (int s = 1; s < 64; s <<= 1) {  // wave argmin of (key, index)
-            const uint64_t ok = pscl::shfl_u64(bk, lane ^ s);
-            const int oj = __shfl(bj, lane ^ s);
-            if (ok < bk || (ok == bk && oj < bj)) {
-                bk = ok;
-                bj = oj;
-            }
-        }
-        if (lane == 0) {
-            const int idx = bj;  // an untried index exists: rounds <= min(retries, K)
-            const int nt = D.ntried[e];
-            const int64_t f = D.act[e];
-            if (idx >= 64) D.tried[2 * e + 1] = t1 | (1ULL << (idx - 64)); else D.tried[2 * e] = t0 | (1ULL << idx);
-            D.ntried[e] = nt + 1;
-            if (D.tried_out) D.tried_out[f * D.tried_stride + nt] = idx;
-            D.fidx[b] = f;
-            // _force_vector (flip.py:30-34): bits [0, idx) = reference, bit idx flipped, rest free
-            const uint64_t* ref = D.ref + (int64_t)e * W;
-            uint64_t* fr = D.force + b * 2 * W;
-            for (int w = 0; w < W; ++w) {
-                const int lo = 64 * w;
-                const int nb = idx - lo + 1;  // bits of this word in [0, idx]
-                const uint64_t mask = nb <= 0 ? 0ULL : (nb >= 64 ? ~0ULL : ((1ULL << nb) - 1ULL));
-                uint64_t val = ref[w] & mask;
-                if (idx >= lo && idx < lo + 64) val ^= 1ULL << (idx - lo);
-                fr[w] = mask;
-                fr[W + w] = val;
-            }
-        }
-    }
-}
-
-// one thread per live entry: record the attempt, stop on CRC pass or retry budget, carry
-// the attempt's best bits into the entry state (flip.py:123-136); survivors appended with
-// one atomic per wavefront
-__global__ void __launch_bounds__(256) dl_update_kernel(const pscl_dl_params D) {
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int n = *D.n;
-    const int lane = threadIdx.x & 63;
-    const int W = D.W;
-    bool more = false;
-    int e = 0;
-    if (b < n) {
-        e = D.list[b];
-        const int64_t f = D.act[e];
-        const uint8_t fl = D.oflags[b];
-        const int nt = D.ntried[e];
-        more = !(fl & PSCL_FLAG_CRC_PASS) && nt < D.rounds;
-        for (int w = 0; w < W; ++w) {
-            const uint64_t v = D.ob[b * W + w];
-            D.best[f * W + w] = v;
-            if (more) D.ref[(int64_t)e * W + w] = v;
-        }
-        D.flags[f] = fl;
-        if (D.attempts) D.attempts[f] = nt + 1;
-    }
-    if (b == 0 && D.counters && n > 0)
-        atomicAdd(reinterpret_cast<unsigned long long*>(D.counters) + PSCL_CNT_RETRIES, (unsigned long long)n);
-    const uint64_t m = __ballot(more);
-    if (!m) return;
-    const int leader = __builtin_ctzll(m);
-    int base = 0;
-    if (lane == leader) base = atomicAdd(D.next_count, __popcll(m));
-    base = __shfl(base, leader);
-    if (more) D.next_list[base + __popcll(m & ((1ULL << lane) - 1ULL))] = e;
+    if (Q.counters && decodes && lane == 0)
+        atomicAdd(reinterpret_cast<unsigned long long*>(Q.counters) + PSCL_CNT_RETRIES, decodes);
 }
 
 // FER/BER statistics of the final results against the transmitted words: wavefront sums,
@@ -302,13 +461,6 @@ hipError_t pscl_launch_iota64(int64_t* out, int64_t n, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t pscl_launch_dl_gather(const uint64_t* best, const int64_t* act, const int32_t* count, int64_t cap, int W,
-                                 uint64_t* ref, hipStream_t s) {
-    if (cap <= 0) return hipSuccess;
-    hipLaunchKernelGGL(dl_gather_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, s, best, act, count, W, ref);
-    return hipGetLastError();
-}
-
 hipError_t pscl_launch_replay(const pscl_replay_params& R, int64_t cap, hipStream_t s) {
     if (cap <= 0) return hipSuccess;
     const int64_t grid = (cap + 3) / 4;
@@ -316,19 +468,14 @@ hipError_t pscl_launch_replay(const pscl_replay_params& R, int64_t cap, hipStrea
     return hipGetLastError();
 }
 
-hipError_t pscl_launch_dl_select(const pscl_dl_params& D, int64_t cap, hipStream_t s) {
-    if (cap <= 0) return hipSuccess;
-    int64_t grid = (cap + 3) / 4;
-    if (grid > 2048) grid = 2048;
-    const int lds = D.beta ? D.K * D.K * 8 : 0;
-    hipLaunchKernelGGL(dl_select_kernel, dim3((unsigned)grid), dim3(256), lds, s, D);
-    return hipGetLastError();
-}
-
-hipError_t pscl_launch_dl_update(const pscl_dl_params& D, int64_t cap, hipStream_t s) {
-    if (cap <= 0) return hipSuccess;
-    const int64_t grid = (cap + 255) / 256;
-    hipLaunchKernelGGL(dl_update_kernel, dim3((unsigned)grid), dim3(256), 0, s, D);
+hipError_t pscl_launch_dl_post(const pscl_post_params& Q, int64_t entries, hipStream_t s) {
+    if (entries <= 0) return hipSuccess;
+    // workgroups of 8 wavefronts, at most two resident per CU (256 CUs)
+    int64_t grid = (entries + kPostWaves * 4 - 1) / (kPostWaves * 4);
+    if (grid > 512) grid = 512;
+    const int beta_lds = Q.beta && (size_t)Q.K * Q.K * 8 <= 32 * 1024;  // (workgroup LDS stays <= 64 KB)
+    const size_t lds = beta_lds ? (size_t)Q.K * Q.K * 8 : 0;
+    hipLaunchKernelGGL(dl_post_kernel, dim3((unsigned)grid), dim3(kPostWaves * 64), lds, s, Q, beta_lds);
     return hipGetLastError();
 }
 

@@ -220,12 +220,28 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
     const uint64_t info0 = CODE ? kSpecInfo[CODE][0] : P.info_mask[0];
     const uint64_t info1 = CODE ? kSpecInfo[CODE][1] : P.info_mask[1];
 
-    // live batch size: P.B, or a device-side count bounded by P.B (DL-SCL retry rounds)
-    const int64_t Bn = P.d_count ? (*P.d_count < P.B ? (int64_t)*P.d_count : P.B) : P.B;
+    // live batch size: P.B, or a device-side count bounded by P.B, or (DL-SCL retry rounds)
+    // the total of the bucket lists
+    int bpre[PSCL_DL_NSEG + 1];
+    const bool elist = FS && P.elist;
+    int64_t Bn = P.d_count ? (*P.d_count < P.B ? (int64_t)*P.d_count : P.B) : P.B;
+    if (elist) {
+        const int64_t tot = pscl_bucket_prefix(P.bcount, P.bcap, bpre);
+        Bn = tot < P.B ? tot : P.B;
+    }
     for (int64_t f0 = ((int64_t)blockIdx.x * wpg + wave) * F; f0 < Bn; f0 += wstride) {
-        const int64_t f = f0 + fl;
-        const bool fvalid = f < Bn;
-        const int64_t frow = P.fidx ? P.fidx[fvalid ? f : f0] : (fvalid ? f : f0);
+        const int64_t fi = f0 + fl;
+        const bool fvalid = fi < Bn;
+        const int64_t fsafe = fvalid ? fi : f0;
+        // f indexes the force words and the outputs: the launch's frame index, or the entry id
+        // of a bucket-list launch (then also the LLR row's index in fidx)
+        int64_t f = fi;
+        int seg0 = 0;  // warm start: first 16-phase segment decoded (wave-uniform)
+        if (elist) {
+            f = pscl_elist_entry(P, fsafe, bpre);
+            seg0 = pscl_bucket_of(f0, bpre);
+        }
+        const int64_t frow = P.fidx ? P.fidx[elist ? f : fsafe] : fsafe;
         const double* chan = P.llr + frow * kN;  // !CH: channel LLRs read in place
         if (CH) {
             if (P.rm_E == 0) {
@@ -260,6 +276,22 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
         double metric = 0.0;
         uint32_t rank = 0;          // list position of this path
         uint64_t u0 = 0, u1 = 0;    // decided bits
+        if constexpr (FS && CODE != 0) {
+            // warm start at phase 16 seg0: the forced prefix [0, 16 seg0) is one path whose
+            // metric and bits the post pass replayed (bit-identical to decoding it here)
+            if (seg0 > 0 && P.warm_metric) {
+                metric = P.warm_metric[f * PSCL_DL_NSEG + seg0];
+                const int lo = 16 * seg0;
+                u0 = P.warm_u[2 * f];
+                u1 = P.warm_u[2 * f + 1];
+                if (lo < 64) {
+                    u0 &= (1ULL << lo) - 1ULL;
+                    u1 = 0;
+                } else {
+                    u1 = lo == 64 ? 0ULL : (u1 & ((1ULL << (lo - 64)) - 1ULL));
+                }
+            }
+        }
         uint32_t lastbit = 0;       // the bit decided at the previous phase
         uint32_t tab = 0;           // LDS slot of depths 3..6 (4 bits each); lanes >= LMAX hold
                                     // a copy of their path's table
@@ -286,6 +318,12 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
             const int start = PT ? kn - __builtin_ctz((unsigned)PT) : ((int)blk ? 3 - __builtin_ctz((unsigned)(int)blk) : 1);
             const uint64_t infow = phi < 64 ? info0 : info1;
             const bool is_info = (infow >> (phi & 63)) & 1;
+            // info index: a compile-time constant with a compiled-in code (warm starts enter
+            // the unrolled phases part way), else the running count
+            const int jq = CODE != 0 ? (phi < 64 ? __builtin_popcountll(info0 & ((1ULL << (phi & 63)) - 1ULL))
+                                                 : __builtin_popcountll(info0) +
+                                                       __builtin_popcountll(info1 & ((1ULL << (phi & 63)) - 1ULL)))
+                                     : j;
             if constexpr (kFixedList) {  // min(2^j, L) paths after j information bits
                 const int jb = phi < 64 ? __builtin_popcountll(info0 & ((1ULL << (phi & 63)) - 1))
                                         : __builtin_popcountll(info0) + __builtin_popcountll(info1 & ((1ULL << (phi & 63)) - 1));
@@ -585,7 +623,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     const uint64_t pv = prev_lane64(mg);
                     const uint64_t top = shfl_u64(mg, gbase + L - 1);
                     bool forced_here = false;
-                    if (FS && force) forced_here = (((j < 64 ? fm0 : fm1) >> (j & 63)) & 1) != 0;
+                    if (FS && force) forced_here = (((jq < 64 ? fm0 : fm1) >> (jq & 63)) & 1) != 0;
                     uint64_t badm = wmask(lam == 0.0) | (wmask(pv > mg) & KGE1) | wmask(mb <= top);
                     if (FS && force) badm |= wmask(forced_here);
                     if (kFixedList) {
@@ -595,8 +633,8 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     }
                     if ((badm & vmask & KPATH & LMASK) == 0) {
                         if (HIST && path_lane && g < L) {
-                            hist_llr[j * L + g] = lam;
-                            hist_par[j * L + g] = (uint8_t)g;
+                            hist_llr[jq * L + g] = lam;
+                            hist_par[jq * L + g] = (uint8_t)g;
                         }
                         metric = pscl_asf64(mg);
                         lastbit = gb;
@@ -629,9 +667,9 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     kval = kval && cbit == (uint32_t)((cbit ? plam : lam) < 0.0);
                     ncnt = cnt;
                 } else if (FS && force) {             // forced bits (scl.py:146-161), per frame
-                    const uint64_t fmw = j < 64 ? fm0 : fm1, fvw = j < 64 ? fv0 : fv1;
-                    if ((fmw >> (j & 63)) & 1) {
-                        kval = kval && cbit == (uint32_t)((fvw >> (j & 63)) & 1);
+                    const uint64_t fmw = jq < 64 ? fm0 : fm1, fvw = jq < 64 ? fv0 : fv1;
+                    if ((fmw >> (jq & 63)) & 1) {
+                        kval = kval && cbit == (uint32_t)((fvw >> (jq & 63)) & 1);
                         ncnt = cnt;
                     }
                 }
@@ -671,8 +709,8 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 if (HIST) {
                     const uint64_t plam_h = shfl_u64(pscl_asu64(lam), ps2);
                     if (g < ncnt && path_lane) {
-                        hist_llr[j * L + g] = pscl_asf64(plam_h);  // decision LLR (scl.py:158,166)
-                        hist_par[j * L + g] = (uint8_t)par_g;
+                        hist_llr[jq * L + g] = pscl_asf64(plam_h);  // decision LLR (scl.py:158,166)
+                        hist_par[jq * L + g] = (uint8_t)par_g;
                     }
                 }
                 metric = pscl_asf64(nm);
@@ -692,7 +730,21 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
         };
         // all 128 phases unrolled with phi a compile-time constant (with CODE != 0 the
         // information set is too: every frozen/info branch and the info index fold away)
-        if constexpr (CODE != 0) {
+        if constexpr (CODE != 0 && FS) {
+            // forced decodes enter at their warm-start segment (seg0 = 0 without one)
+            auto seg = [&](auto SB) { static_for<16>([&](auto TC) { phase(SB, TC); }); };
+            using std::integral_constant;
+            switch (seg0) {
+                case 0: seg(integral_constant<int, 0>{}); [[fallthrough]];
+                case 1: seg(integral_constant<int, 1>{}); [[fallthrough]];
+                case 2: seg(integral_constant<int, 2>{}); [[fallthrough]];
+                case 3: seg(integral_constant<int, 3>{}); [[fallthrough]];
+                case 4: seg(integral_constant<int, 4>{}); [[fallthrough]];
+                case 5: seg(integral_constant<int, 5>{}); [[fallthrough]];
+                case 6: seg(integral_constant<int, 6>{}); [[fallthrough]];
+                default: seg(integral_constant<int, 7>{});
+            }
+        } else if constexpr (CODE != 0) {
             static_for<kN>([&](auto PC) { phase(std::integral_constant<int, (decltype(PC)::value >> 4)>{}, std::integral_constant<int, (decltype(PC)::value & 15)>{}); });
         } else {
             for (int blk = 0; blk < kN / 16; ++blk)

@@ -63,7 +63,46 @@ struct pscl_decode_params {
     unsigned char* long_scratch;  // [grid][long_block_bytes]
     int64_t long_block_bytes;
     int long_mode;               // 1: N > PSCL_FAST_N, scl_long.hip
+    // DL-SCL retry rounds (dlscl.hip): the launch's frames are the entries of PSCL_DL_NSEG
+    // bucket lists (bucket k at elist + k * bcap, bcount[k * PSCL_DL_CSTRIDE] entries), in
+    // bucket order; frame i -> entry e, which indexes fidx (LLR row), force and the outputs.
+    const int32_t* elist;
+    const int32_t* bcount;
+    int64_t bcap;
+    // warm start (FS kernels with a compiled-in code): bucket k holds forced decodes whose
+    // forced prefix covers phases [0, 16 k); a wavefront starts at phase 16 k of its first
+    // frame's bucket with each frame's metric warm_metric[e][k] and bits warm_u[e][0..1]
+    // below 16 k (the forced prefix's single path, replayed exactly by dl_post_kernel)
+    const double* warm_metric;   // [entries][PSCL_DL_NSEG]
+    const uint64_t* warm_u;      // [entries][2]
 };
+
+#define PSCL_DL_NSEG 8     // 16-phase segments of N = 128: warm-start buckets
+#define PSCL_DL_CSTRIDE 16 // int32 stride of the bucket counters (one 64-byte line each)
+
+// frame index i of a bucket-list launch -> entry id (pre: bucket prefix counts, pre[0] = 0)
+__device__ __forceinline__ int pscl_bucket_of(int64_t i, const int* pre) {
+    int k = 0;
+#pragma unroll
+    for (int q = 1; q < PSCL_DL_NSEG; ++q) k += i >= pre[q] ? 1 : 0;
+    return k;
+}
+__device__ __forceinline__ int64_t pscl_elist_entry(const pscl_decode_params& P, int64_t i, const int* pre) {
+    const int k = pscl_bucket_of(i, pre);
+    return P.elist[(int64_t)k * P.bcap + (i - pre[k])];
+}
+// prefix counts of the buckets (wave-uniform loads); returns the total
+__device__ __forceinline__ int64_t pscl_bucket_prefix(const int32_t* bcount, int64_t cap, int* pre) {
+    int acc = 0;
+    pre[0] = 0;
+#pragma unroll
+    for (int k = 0; k < PSCL_DL_NSEG; ++k) {
+        const int c = bcount[k * PSCL_DL_CSTRIDE];
+        acc += c < cap ? c : (int)cap;
+        pre[k + 1] = acc;
+    }
+    return acc;
+}
 
 // Decision-LLR replay (dlscl.hip): leaf LLRs of a known path, recomputed top-down
 struct pscl_replay_params {
@@ -79,28 +118,38 @@ struct pscl_replay_params {
     double* out;                 // [entries][K] decision LLRs (signed), row = entry
 };
 
-// DL-SCL retry rounds (dlscl.hip): entry e = one failing frame's retry state
-struct pscl_dl_params {
-    int K, W;
-    int rounds;                  // min(retries, K): attempt budget per frame (flip.py:111)
-    const int32_t* n;            // live entries this round (device count)
-    const int32_t* list;         // [n] live entry ids
-    int32_t* next_list;          // [A] survivors of this round (dl_update)
-    int32_t* next_count;         // device counter of next_list
-    const int64_t* act;          // [A] frame index of each entry
-    double* al0;                 // [A][K] decision LLRs of the entry's reference path
-    uint64_t* ref;               // [A][W] reference bits
-    uint64_t* tried;             // [A][2] tried-index bit sets
-    int32_t* ntried;             // [A]
-    const double* beta;          // [K][K] fp64 or null (flip.py:104-108)
-    uint64_t* force;             // [n][2][W] force words of this round's decode
-    int64_t* fidx;               // [n] LLR row of this round's decode
-    const uint64_t* ob;          // [n][W] this round's best bits
-    const uint8_t* oflags;       // [n]
+// DL-SCL retry rounds (dlscl.hip, dl_post_kernel): entry e = one failing frame's retry state.
+// One pass per round over the entries just decoded: replay of the attempt's best path (its
+// leaf LLRs), final-attempt bookkeeping and the CRC stop rule, then for the survivors the next
+// flip (q = |L0| @ beta), its force words, the warm-start state of its forced prefix and the
+// append to the next round's bucket list.  init = 1: the first pass, over the baseline.
+struct pscl_post_params {
+    const double* llr;           // channel LLRs [.][N] (or [.][E] with rate matching)
+    int N, n, K, W, rm_E;
+    const int32_t* rm_src;
+    uint64_t info_mask[2];
+    const int32_t* info_set;     // [K] (device)
+    const uint64_t* exp_table;   // glibc exp table (exact metric tails)
+    int rounds;                  // min(retries, K)
+    int init;
+    const int32_t* in_count;     // init: [1] entry count; else bucket counts of this round
+    const int32_t* in_list;      // bucket lists of this round ([NSEG][cap] entry ids)
+    int64_t cap;
+    int32_t* out_count;          // next round's bucket counts (zeroed)
+    int32_t* out_list;           // [NSEG][cap]
+    const int64_t* act;          // [cap] frame index (LLR row) of each entry
+    uint64_t* tried;             // [cap][2] tried-index bit sets
+    int32_t* ntried;             // [cap]
+    const double* beta;          // [K][K] or null
+    uint64_t* force;             // [cap][2][W]
+    double* warm_metric;         // [cap][NSEG]
+    uint64_t* warm_u;            // [cap][2]
+    const uint64_t* ob;          // [cap][W] this round's best bits, by entry
+    const uint8_t* of;           // [cap]
     uint64_t* best;              // [B][W] final best bits (per frame)
     uint8_t* flags;              // [B]
-    int32_t* attempts;           // [B] or null: 1 + flips tried
-    int32_t* tried_out;          // [B][tried_stride] or null: flip indices in order
+    int32_t* attempts;           // [B] or null
+    int32_t* tried_out;          // [B][tried_stride] or null
     int tried_stride;
     int64_t* counters;           // or null: PSCL_CNT_RETRIES += decodes
 };
@@ -137,14 +186,11 @@ hipError_t pscl_launch_channel(const pscl_channel_params& P, hipStream_t s);
 hipError_t pscl_launch_uncoded(const pscl_channel_params& P, int64_t* counters, hipStream_t s);
 hipError_t pscl_launch_dl_compact(const uint8_t* flags, int64_t B, int64_t base, int64_t* act, int32_t* list,
                                   int32_t* count, hipStream_t s);
-hipError_t pscl_launch_dl_select(const pscl_dl_params& D, int64_t cap, hipStream_t s);
-hipError_t pscl_launch_dl_update(const pscl_dl_params& D, int64_t cap, hipStream_t s);
-hipError_t pscl_launch_dl_gather(const uint64_t* best, const int64_t* act, const int32_t* count, int64_t cap, int W,
-                                 uint64_t* ref, hipStream_t s);
 hipError_t pscl_launch_iota64(int64_t* out, int64_t n, hipStream_t s);
 hipError_t pscl_launch_replay(const pscl_replay_params& R, int64_t cap, hipStream_t s);
 hipError_t pscl_launch_softplus_tails(const double* v, int64_t n, const uint64_t* exp_table, double* exact,
                                      double* apx, hipStream_t s);
+hipError_t pscl_launch_dl_post(const pscl_post_params& Q, int64_t entries, hipStream_t s);
 hipError_t pscl_launch_dl_count(const uint64_t* best, const uint8_t* flags, const uint64_t* ref, int64_t B, int W,
                                 int k_payload, int64_t* counters, hipStream_t s);
 

@@ -65,12 +65,21 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
     const int cpath = g & (LMAX - 1);
     const uint32_t cbit = g >= LMAX ? 1u : 0u;
 
-    // live batch size: P.B, or a device-side count bounded by P.B (DL-SCL retry rounds)
-    const int64_t Bn = P.d_count ? (*P.d_count < P.B ? (int64_t)*P.d_count : P.B) : P.B;
+    // live batch size: P.B, or a device-side count bounded by P.B, or (DL-SCL retry rounds)
+    // the total of the bucket lists (no warm start here: every frame decodes from phase 0)
+    int bpre[PSCL_DL_NSEG + 1];
+    int64_t Bn = P.d_count ? (*P.d_count < P.B ? (int64_t)*P.d_count : P.B) : P.B;
+    if (P.elist) {
+        const int64_t tot = pscl_bucket_prefix(P.bcount, P.bcap, bpre);
+        Bn = tot < P.B ? tot : P.B;
+    }
     for (int64_t f0 = ((int64_t)blockIdx.x * wpg + wave) * F; f0 < Bn; f0 += wstride) {
-        const int64_t f = f0 + fl;
-        const bool fvalid = f < Bn;
-        const int64_t frow = P.fidx ? P.fidx[fvalid ? f : f0] : (fvalid ? f : f0);
+        const int64_t fi = f0 + fl;
+        const bool fvalid = fi < Bn;
+        const int64_t fsafe = fvalid ? fi : f0;
+        // f indexes the force words and outputs: the frame index, or a bucket list's entry id
+        const int64_t f = P.elist ? pscl_elist_entry(P, fsafe, bpre) : fi;
+        const int64_t frow = P.fidx ? P.fidx[P.elist ? f : fsafe] : fsafe;
         if (P.rm_E == 0) {  // stage this frame's channel LLRs in LDS (read at every depth-1 use)
             const double* src = P.llr + frow * N;
             for (int x = g; x < N; x += G) Af[x] = src[x];
