@@ -17,7 +17,9 @@ The line also carries
                 library's source hash), the VALU issue bound priced per instruction class;
   extra_configs BASELINE configs 2 (L=4), 4 (DL-SCL L=4 + 8 flips, beta_M4) and 5 (NR
                 E=256 L=8): ms/step, frames/s, FER (z vs the reference's results/fer_M4.csv
-                where one applies) and an oracle parity sample each.
+                where one applies) and an oracle parity sample each; config 3 (L=8 FER sweep
+                4.0-6.5 dB with DL-SCL beta_M8) through run_fer_sweep --rng philox: wall time
+                and frames/s per SNR point, FER z at 5 dB.
 
 Multi-GPU: one process per GPU (torchrun), frames sharded by global frame index, no
 data-path collective; one RCCL all-reduce of the error counters and one of the timings.
@@ -399,6 +401,48 @@ def launch_ranks(n: int) -> int:
     return 0
 
 
+def config3_sweep(args, ctx: Ctx):
+    """BASELINE config 3 through the product path: run_fer_sweep --rng philox (pscl_simulate per
+    SNR point: TX, uncoded baseline, SCL + DL-SCL with beta_M8, counters), L = 8, 4.0-6.5 dB in
+    0.5 dB steps, args.frames frames per GPU per point.  Wall time per point (max over ranks,
+    Python included), frames/s, and the 5 dB FER z-scores against results/fer_M8.csv."""
+    import contextlib
+    import io
+    import tempfile
+
+    from polar_code_amd.eval import run_fer_sweep as rfs
+
+    frames = args.frames * ctx.world
+    beta = str(ROOT / "tests" / "golden" / "beta_M8.npy")
+    pts, total_t = [], 0.0
+    with tempfile.TemporaryDirectory() as td:
+        for snr in np.arange(4.0, 6.5 + 1e-9, 0.5):
+            a = rfs.build_argparser().parse_args(
+                ["--M", "8", "--frames", str(frames), "--snr_lo", f"{snr:g}", "--snr_hi", f"{snr:g}", "--snr_step", "0",
+                 "--retries", "8", "--beta", beta, "--rng", "philox", "--include_uncoded", "--no_plot", "--seed",
+                 str(args.seed), "--out_dir", td, "--plot_dir", td])
+            ctx.barrier()
+            ctx.torch.cuda.synchronize(ctx.dev)
+            t0 = time.perf_counter()
+            with contextlib.redirect_stdout(io.StringIO()):
+                row = rfs.run_sweep(a)[0]
+            ctx.torch.cuda.synchronize(ctx.dev)
+            dt = ctx.max_over_ranks(time.perf_counter() - t0)
+            total_t += dt
+            pt = {"snr_db": float(snr), "wall_s": dt, "frames": frames, "frames_per_s": frames / dt,
+                  "fer_scl": row["fer_scl"], "fer_dl": row["fer_dl"], "fer_uncoded": row["fer_uncoded"],
+                  "avg_retries": row["avg_retries"]}
+            if abs(snr - 5.0) < 1e-9:
+                pt["z_scl_vs_reference"] = fer_z(int(round(row["fer_scl"] * frames)), frames, REF_ERRS[("scl", 8)])
+                pt["z_dl_vs_reference"] = fer_z(int(round(row["fer_dl"] * frames)), frames, REF_ERRS[("dl", 8)])
+            pts.append(pt)
+    return {"workload": "run_fer_sweep --M 8 --retries 8 --beta beta_M8 --rng philox --include_uncoded, "
+                        "4.0-6.5 dB step 0.5 (pscl_simulate per point)",
+            "frames_per_point": frames, "wall_s": total_t, "value": frames * len(pts) / total_t,
+            "unit": "frames/s (SCL + DL-SCL + uncoded per frame, whole sweep)", "points": pts,
+            "reference": "results/fer_M8.csv:2 (5 dB): fer_scl 26/2000, fer_dl 20/2000"}
+
+
 def main():
     args = parse()
     if args.gpus < 1:
@@ -455,6 +499,9 @@ def main():
     extra = None
     if args.extra == "auto" and not E and args.retries == 0 and L == 8:
         extra = extra_configs(args, ctx, orc)
+        sweep = config3_sweep(args, ctx)
+        if rank == 0:
+            extra["config3_sweep_L8"] = sweep
 
     if rank == 0:
         launches, kern_ms = r["launches"], r["kern_ms"]

@@ -121,6 +121,22 @@ __device__ __forceinline__ double* replay_leaves(double c0, double c1, int N, in
         u[h] = __ballot(bit);
     }
     pscl::wave_lds_fence();
+    // Partial sums: the g node k2 (odd) of width w = 2^m takes bit i of the transform of
+    // u[(k2-1) w, k2 w), which is bit (k2-1) w + i of X_m = u after butterfly stages 1, 2, ..,
+    // 2^(m-1) (polar_transform64 stage by stage: the later stages do not mix an aligned w-bit
+    // segment).  The stages are involutions that commute, so X_{m-1} = stage 2^(m-1) of X_m:
+    // one wave-uniform (scalar) stage per level instead of a full transform per element.
+    auto stage = [](uint64_t x, int s) {
+        const uint64_t M = s == 1 ? 0x5555555555555555ULL : s == 2 ? 0x3333333333333333ULL
+                         : s == 4 ? 0x0f0f0f0f0f0f0f0fULL : s == 8 ? 0x00ff00ff00ff00ffULL
+                         : s == 16 ? 0x0000ffff0000ffffULL : 0x00000000ffffffffULL;
+        return x ^ ((x >> s) & M);
+    };
+    uint64_t X0 = u[0], X1 = u[1];
+    for (int m = 1; m < n; ++m) {  // X_{n-1}
+        X0 = stage(X0, 1 << (m - 1));
+        X1 = stage(X1, 1 << (m - 1));
+    }
     for (int d = 0; d < n; ++d) {
         const int lw2 = n - d - 1, w2 = 1 << lw2;
         for (int p2 = lane; p2 < N; p2 += 64) {
@@ -131,10 +147,8 @@ __device__ __forceinline__ double* replay_leaves(double c0, double c1, int N, in
             if (!(k2 & 1)) {
                 v = f_minsum(a, bb);
             } else {
-                const int lo = (k2 - 1) * w2;
-                const uint64_t word = u[lo >> 6] >> (lo & 63);
-                const uint64_t chunk = w2 >= 64 ? word : (word & ((1ULL << w2) - 1ULL));
-                v = g_node(a, bb, (uint32_t)(polar_transform64(chunk) >> i) & 1u);
+                const int q = p2 - w2;  // bit (k2-1) w2 + i of X_lw2
+                v = g_node(a, bb, (uint32_t)(((q >> 6) ? X1 : X0) >> (q & 63)) & 1u);
             }
             nxt[p2] = v;
         }
@@ -142,6 +156,10 @@ __device__ __forceinline__ double* replay_leaves(double c0, double c1, int N, in
         double* t = cur;
         cur = nxt;
         nxt = t;
+        if (lw2 > 0) {
+            X0 = stage(X0, w2 >> 1);
+            X1 = stage(X1, w2 >> 1);
+        }
     }
     return cur;
 }
@@ -184,6 +202,12 @@ __global__ void __launch_bounds__(256) replay_kernel(const pscl_replay_params R,
 // ~5k same-address device atomics on each bucket counter (measured: 316 of 467 us of the
 // first pass at L = 4, 5 dB).  The flip metric's beta (when K * K doubles fit) and the exp
 // table of the exact metric tails are staged in LDS once per workgroup.
+#ifndef PSCL_POST_GRID
+#define PSCL_POST_GRID 512
+#endif
+#ifndef PSCL_POST_BETA_LDS
+#define PSCL_POST_BETA_LDS 1
+#endif
 constexpr int kPostWaves = 8;
 constexpr int kPostIters = 32;  // entries per wavefront between two flushes
 constexpr int kPostChunk = kPostWaves * kPostIters;
@@ -199,11 +223,13 @@ struct PostShared {
     int32_t nst;
 };
 
+// NC, KC: N and K compiled in (128 and 64 / 88: the BASELINE codes) or 0 (from Q)
+template <int NC, int KC>
 __global__ void __launch_bounds__(kPostWaves * 64) dl_post_kernel(const pscl_post_params Q, int beta_lds) {
     __shared__ PostShared S;
     extern __shared__ double sbeta[];  // [K][K] when beta_lds
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int N = Q.N, K = Q.K, W = Q.W;
+    const int N = NC ? NC : Q.N, K = KC ? KC : Q.K, W = KC ? (KC + 63) / 64 : Q.W, n = NC ? 7 : Q.n;
     for (int i = threadIdx.x; i < PSCL_EXP_TABLE_WORDS; i += blockDim.x) S.exp_table[i] = Q.exp_table[i];
     if (beta_lds)
         for (int i = threadIdx.x; i < K * K; i += blockDim.x) sbeta[i] = Q.beta[i];
@@ -285,7 +311,7 @@ __global__ void __launch_bounds__(kPostWaves * 64) dl_post_kernel(const pscl_pos
             if (more) {
                 uint64_t u[2];
                 int jpos[2];
-                double* cur = replay_leaves(c0, c1, N, Q.n, Q.info_mask, b0, b1, cur0, cur1, u, jpos);
+                double* cur = replay_leaves(c0, c1, N, n, Q.info_mask, b0, b1, cur0, cur1, u, jpos);
                 double* nxt = cur == cur0 ? cur1 : cur0;
                 // |L0|: the path's decision LLRs at the information phases (flip.py:97-102, 127-132)
 #pragma unroll
@@ -472,10 +498,16 @@ hipError_t pscl_launch_dl_post(const pscl_post_params& Q, int64_t entries, hipSt
     if (entries <= 0) return hipSuccess;
     // workgroups of 8 wavefronts, at most two resident per CU (256 CUs)
     int64_t grid = (entries + kPostWaves * 4 - 1) / (kPostWaves * 4);
-    if (grid > 512) grid = 512;
-    const int beta_lds = Q.beta && (size_t)Q.K * Q.K * 8 <= 32 * 1024;  // (workgroup LDS stays <= 64 KB)
+    if (grid > PSCL_POST_GRID) grid = PSCL_POST_GRID;
+    const int beta_lds = PSCL_POST_BETA_LDS && Q.beta && (size_t)Q.K * Q.K * 8 <= 32 * 1024;  // (LDS <= 64 KB)
     const size_t lds = beta_lds ? (size_t)Q.K * Q.K * 8 : 0;
-    hipLaunchKernelGGL(dl_post_kernel, dim3((unsigned)grid), dim3(kPostWaves * 64), lds, s, Q, beta_lds);
+    const dim3 g((unsigned)grid), b(kPostWaves * 64);
+    if (Q.N == 128 && Q.K == 64)
+        hipLaunchKernelGGL((dl_post_kernel<128, 64>), g, b, lds, s, Q, beta_lds);
+    else if (Q.N == 128 && Q.K == 88)
+        hipLaunchKernelGGL((dl_post_kernel<128, 88>), g, b, lds, s, Q, beta_lds);
+    else
+        hipLaunchKernelGGL((dl_post_kernel<0, 0>), g, b, lds, s, Q, beta_lds);
     return hipGetLastError();
 }
 
