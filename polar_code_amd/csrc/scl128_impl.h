@@ -165,6 +165,10 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 #define PSCL_APX_ABLATE 0
 #endif
 
+#ifndef PSCL_LEAF_BLEND
+#define PSCL_LEAF_BLEND 0
+#endif
+
 #ifndef PSCL_WAVES_PER_EU
 #define PSCL_WAVES_PER_EU 4
 #endif
@@ -204,7 +208,10 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
     // with a compiled-in information set and no forced bits the list is full-size (launches
     // with L != LMAX take the CODE 0 kernels) and its length at every phase is known
     constexpr bool kFixedList = CODE != 0 && !FS;
-    const int K = P.K, L = kFixedList ? LMAX : P.L;
+    // K and the word count W are compile-time constants with a compiled-in code (the epilogue's
+    // syndrome lookups then unroll with immediate LDS offsets)
+    const int K = CODE ? kSpecK[CODE] : P.K, L = kFixedList ? LMAX : P.L;
+    const int PW = CODE ? (kSpecK[CODE] + 63) / 64 : P.W;
     unsigned char* wbase = smem + P.wg_fixed_bytes + (size_t)wave * P.wave_bytes;
     double* A = reinterpret_cast<double*>(wbase);
     double* Af = A + fl * Ly::FSTRIDE;
@@ -264,12 +271,12 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
         }
         uint64_t fm0 = 0, fm1 = 0, fv0 = 0, fv1 = 0;
         if (FS && force && fvalid) {
-            const uint64_t* fr = force + f * 2 * P.W;
+            const uint64_t* fr = force + f * 2 * PW;
             fm0 = fr[0];
-            fv0 = fr[P.W];
-            if (P.W > 1) {
+            fv0 = fr[PW];
+            if (PW > 1) {
                 fm1 = fr[1];
-                fv1 = fr[P.W + 1];
+                fv1 = fr[PW + 1];
             }
         }
         wave_lds_fence();
@@ -391,7 +398,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     }
                     double d1l[4];
 #pragma unroll
-                    for (int m = 0; m < 4; ++m) d1l[m] = f_minsum(c[m], c[m + 4]);
+                    for (int m = 0; m < 4; ++m) d1l[m] = r1 ? 0.0 : f_minsum(c[m], c[m + 4]);  // (r1: g nodes below)
                     // each path lane publishes its partial sums once; every lane then reads those of
                     // the path it works on (one ds_read_b128 instead of four ds_bpermute)
                     uint4* xs_lds = reinterpret_cast<uint4*>(Af + Ly::OFFX);
@@ -403,7 +410,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     const bool shared2 = !r1 && !r2;
                     double d2s[2];
 #pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2) d2s[s2] = f_minsum(d1l[s2], d1l[s2 + 2]);
+                    for (int s2 = 0; s2 < 2; ++s2) d2s[s2] = shared2 ? f_minsum(d1l[s2], d1l[s2 + 2]) : 0.0;
                     // paths that exist (compiled-in codes know: phi = 0 has one)
                     const int npaths = kFixedList && cnt < LMAX ? cnt : LMAX;
 #pragma unroll
@@ -468,9 +475,24 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
             // at even information phases of the screening decode, the better child's bit (the
             // sign of this leaf), which every path keeps whenever the list update below takes
             // its keep-the-better-children path
+#if PSCL_LEAF_BLEND
+            // branch-free: every lane evaluates both forms and keeps its own by a bit blend (a
+            // ternary on path_lane around the f asm becomes a divergent branch)
+            double lam;
+            if (phi & 1) {  // path lanes g(u[phi-1]), upper lanes g(0): one g with a per-lane bit
+                lam = g_node(la, lb, path_lane ? xleaf : 0u);
+            } else {
+                const double fv = f_minsum(la, lb);
+                const double up = (APX && is_info) ? g_node(la, lb, sign_bit(fv)) : lb + la;
+                const uint64_t m = path_lane ? ~0ULL : 0ULL;
+                lam = pscl_asf64((pscl_asu64(fv) & m) | (pscl_asu64(up) & ~m));
+            }
+            if (PSCL_ABLATE & 128) lam = la;
+#else
             double lam_up = lb + la;
             if (APX && is_info && !(phi & 1)) lam_up = g_node(la, lb, sign_bit(f_minsum(la, lb)));
             const double lam = (PSCL_ABLATE & 128) ? la : (path_lane ? ((phi & 1) ? g_node(la, lb, xleaf) : f_minsum(la, lb)) : lam_up);
+#endif
             // ---- metric tail log1p(exp(-|llr|)) (scl.py:102-105)
             double Lt;
             const uint64_t lpre_up = from_upper_half64<G, LMAX>(pscl_asu64(Lpre), lane);
@@ -807,8 +829,8 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
             const int64_t row = fo * L + rank;
             if (P.metrics) P.metrics[row] = metric;
             if (P.cands) {
-                P.cands[row * P.W] = ib0;
-                if (P.W > 1) P.cands[row * P.W + 1] = ib1;
+                P.cands[row * PW] = ib0;
+                if (PW > 1) P.cands[row * PW + 1] = ib1;
             }
             if (HIST && P.info_llrs) {
                 int cur = g;
@@ -827,13 +849,13 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     }
                 }
                 if (P.best) {
-                    P.best[fo * P.W] = ib0;
-                    if (P.W > 1) P.best[fo * P.W + 1] = ib1;
+                    P.best[fo * PW] = ib0;
+                    if (PW > 1) P.best[fo * PW + 1] = ib1;
                 }
                 if (P.flags) P.flags[fo] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
                 if (P.n_paths) P.n_paths[fo] = cnt;
                 if (P.ref && !(APX && PSCL_APX_ABLATE))  // (ablation timings: wrong frames, no atomics)
-                    count_errors(P.counters, ib0, ib1, P.ref[fo * P.W], P.W > 1 ? P.ref[fo * P.W + 1] : 0, P.k_payload,
+                    count_errors(P.counters, ib0, ib1, P.ref[fo * PW], PW > 1 ? P.ref[fo * PW + 1] : 0, P.k_payload,
                                  bpass);
             }
         }
