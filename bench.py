@@ -416,6 +416,13 @@ def config3_sweep(args, ctx: Ctx):
     beta = str(ROOT / "tests" / "golden" / "beta_M8.npy")
     pts, total_t = [], 0.0
     with tempfile.TemporaryDirectory() as td:
+        # untimed warm-up point (handles, device buffers, beta upload) at a different seed
+        a = rfs.build_argparser().parse_args(
+            ["--M", "8", "--frames", str(min(frames, 65536)), "--snr_lo", "4", "--snr_hi", "4", "--snr_step", "0",
+             "--retries", "8", "--beta", beta, "--rng", "philox", "--include_uncoded", "--no_plot", "--seed",
+             str(args.seed + 1), "--out_dir", td, "--plot_dir", td])
+        with contextlib.redirect_stdout(io.StringIO()):
+            rfs.run_sweep(a)
         for snr in np.arange(4.0, 6.5 + 1e-9, 0.5):
             a = rfs.build_argparser().parse_args(
                 ["--M", "8", "--frames", str(frames), "--snr_lo", f"{snr:g}", "--snr_hi", f"{snr:g}", "--snr_step", "0",

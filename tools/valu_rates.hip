@@ -77,6 +77,30 @@ __global__ void __launch_bounds__(1024) stream_kernel(uint64_t* out, uint32_t se
 #define OP(x, y) asm volatile("v_sub_co_u32_dpp %1, vcc, %2, %2 row_ror:5 row_mask:0xf bank_mask:0xf\n\tv_addc_co_u32 %0, vcc, 0, %0, vcc" : "+v"(x), "=&v"(tmp) : "v"(y) : "vcc");
                 BLOCK8(OP)
 #undef OP
+            } else if constexpr (CLS == 16) {  // v_add_u32 in the VOP3 (8-byte) encoding
+#define OP(x, y) asm volatile("v_add_u32_e64 %0, %0, %1" : "+v"(x) : "v"(y));
+                BLOCK8(OP)
+#undef OP
+            } else if constexpr (CLS == 17) {  // v_add_u32 followed by s_nop 0 (counted: the VALU only)
+#define OP(x, y) asm volatile("v_add_u32 %0, %0, %1\n\ts_nop 0" : "+v"(x) : "v"(y));
+                BLOCK8(OP)
+#undef OP
+            } else if constexpr (CLS == 18) {  // v_add_u32 with a 32-bit literal (8 bytes)
+#define OP(x, y) asm volatile("v_add_u32 %0, 0x12345, %0" : "+v"(x));
+                BLOCK8(OP)
+#undef OP
+            } else if constexpr (CLS == 19) {  // v_cndmask_b32 with VCC (VOP2, 4 bytes)
+#define OP(x, y) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(x) : "v"(y));
+                BLOCK8(OP)
+#undef OP
+            } else if constexpr (CLS == 20) {  // v_add_u32 followed by s_waitcnt lgkmcnt(0) (nothing outstanding)
+#define OP(x, y) asm volatile("v_add_u32 %0, %0, %1\n\ts_waitcnt lgkmcnt(0)" : "+v"(x) : "v"(y));
+                BLOCK8(OP)
+#undef OP
+            } else if constexpr (CLS == 21) {  // v_add_u32 followed by an independent s_add_u32 (SALU)
+#define OP(x, y) asm volatile("v_add_u32 %0, %0, %1\n\ts_add_u32 s44, s44, 1" : "+v"(x) : "v"(y) : "s44", "scc");
+                BLOCK8(OP)
+#undef OP
             } else if constexpr (CLS == 12) {  // v_xor_b32 (the f/g sign work)
 #define OP(x, y) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x) : "v"(y));
                 BLOCK8(OP)
@@ -110,7 +134,9 @@ __global__ void __launch_bounds__(1024) stream_kernel(uint64_t* out, uint32_t se
 static const char* kName[] = {"v_add_u32",     "v_cndmask_b32", "v_mov_b32_dpp", "v_add_f64",   "v_fma_f64",
                               "v_min_f64|.|",  "v_fma_f32",     "v_exp_f32",     "v_rcp_f32",   "v_cvt_f32_f64",
                               "v_ldexp_f64",   "sub_co_dpp+addc (2 instr)", "v_xor_b32", "v_lshrrev_b64",
-                              "v_cvt_f64_f32", "v_cmp_gt_u32"};
+                              "v_cvt_f64_f32", "v_cmp_gt_u32", "v_add_u32_e64 (VOP3)", "v_add_u32 + s_nop 0",
+                              "v_add_u32 literal", "v_cndmask_b32 vcc (VOP2)", "v_add_u32 + s_waitcnt",
+                              "v_add_u32 + s_add_u32"};
 
 template <int CLS>
 void run(uint64_t* d, uint64_t* h, int cus) {
@@ -172,6 +198,12 @@ int main() {
     run<9>(d, h, cus);
     run<14>(d, h, cus);
     run<10>(d, h, cus);
+    run<16>(d, h, cus);
+    run<18>(d, h, cus);
+    run<19>(d, h, cus);
+    run<17>(d, h, cus);
+    run<20>(d, h, cus);
+    run<21>(d, h, cus);
     hipFree(d);
     free(h);
     return 0;
