@@ -193,15 +193,18 @@ __global__ void __launch_bounds__(256) replay_kernel(const pscl_replay_params R,
 #define PSCL_POST_ABLATE 0
 #endif
 
-// One post pass of the retry loop (see the header).  Workgroups of 8 wavefronts own
-// contiguous ranges of the pass's entries, one entry per wavefront at a time.  Every
-// wavefront preloads the metadata of its next 32 entries (one lane each: entry id, frame,
-// bits, flags, tried state) and prefetches the next entry's channel row while it replays the
-// current one.  Survivors are staged in LDS and appended to the next round's bucket lists
-// with one global atomic per (workgroup, bucket) per 256 entries: one atomic per entry put
+// One post pass of the retry loop (see the header).  Each wavefront works on two entries at
+// a time, one per 32-lane half (4 tree elements and up to 4 flip candidates per lane), so a
+// workgroup keeps twice the entries in flight that one entry per wavefront allowed (the pass
+// is latency-bound: LDS round trips of the replay levels, the flip metric's sums, the serial
+// prefix sums).  Workgroups of 8 wavefronts own contiguous ranges of the pass's entries; every
+// wavefront preloads the metadata of its next 64 entries (one lane each: entry id, frame,
+// bits, flags, tried state) and prefetches the next pair's channel rows while it replays the
+// current pair.  Survivors are staged in LDS and appended to the next round's bucket lists
+// with one global atomic per (workgroup, bucket) per 512 entries: one atomic per entry put
 // ~5k same-address device atomics on each bucket counter (measured: 316 of 467 us of the
-// first pass at L = 4, 5 dB).  The flip metric's beta (when K * K doubles fit) and the exp
-// table of the exact metric tails are staged in LDS once per workgroup.
+// first pass at L = 4, 5 dB).  beta (when K * K doubles fit) and the exp table of the exact
+// metric tails are staged in LDS once per workgroup.
 #ifndef PSCL_POST_GRID
 #define PSCL_POST_GRID 512
 #endif
@@ -209,11 +212,11 @@ __global__ void __launch_bounds__(256) replay_kernel(const pscl_replay_params R,
 #define PSCL_POST_BETA_LDS 1
 #endif
 constexpr int kPostWaves = 8;
-constexpr int kPostIters = 32;  // entries per wavefront between two flushes
-constexpr int kPostChunk = kPostWaves * kPostIters;
+constexpr int kPostIters = 32;                          // entry pairs per wavefront between flushes
+constexpr int kPostChunk = kPostWaves * 2 * kPostIters;  // entries per workgroup between flushes
 
 struct PostShared {
-    double lvl[kPostWaves][3][PSCL_FAST_N];
+    double lvl[kPostWaves][2][2][PSCL_FAST_N];  // [wave][half][buffer][element]
     uint64_t exp_table[PSCL_EXP_TABLE_WORDS];
     int32_t st_e[kPostChunk];
     uint16_t st_pos[kPostChunk];
@@ -223,12 +226,27 @@ struct PostShared {
     int32_t nst;
 };
 
+// Channel LLRs p = hl + 32 m (m = 0..3) of a frame row, N <= 128
+__device__ __forceinline__ void load_row4(const double* row, int rm_E, const int32_t* rm_src, int N, int hl, double* c) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int p = hl + 32 * m;
+        c[m] = p < N ? (rm_E == 0 ? row[p] : pscl::nr_stage(row, rm_src[p], rm_E, N)) : 0.0;
+    }
+}
+
+// per-half broadcast of lane l's value (ds_bpermute; l differs between the halves)
+__device__ __forceinline__ uint64_t bcast64(uint64_t v, int l) {
+    return ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), l) << 32) | (uint32_t)__shfl((int)(uint32_t)v, l);
+}
+
 // NC, KC: N and K compiled in (128 and 64 / 88: the BASELINE codes) or 0 (from Q)
 template <int NC, int KC>
-__global__ void __launch_bounds__(kPostWaves * 64) dl_post_kernel(const pscl_post_params Q, int beta_lds) {
+__global__ void __launch_bounds__(kPostWaves * 64) __attribute__((amdgpu_waves_per_eu(4))) dl_post_kernel(const pscl_post_params Q, int beta_lds) {
     __shared__ PostShared S;
     extern __shared__ double sbeta[];  // [K][K] when beta_lds
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int hs = lane >> 5, hl = lane & 31, hb = lane & 32;  // half, lane in half, half's first lane
     const int N = NC ? NC : Q.N, K = KC ? KC : Q.K, W = KC ? (KC + 63) / 64 : Q.W, n = NC ? 7 : Q.n;
     for (int i = threadIdx.x; i < PSCL_EXP_TABLE_WORDS; i += blockDim.x) S.exp_table[i] = Q.exp_table[i];
     if (beta_lds)
@@ -236,6 +254,8 @@ __global__ void __launch_bounds__(kPostWaves * 64) dl_post_kernel(const pscl_pos
     if (threadIdx.x < PSCL_DL_NSEG) S.lcnt[threadIdx.x] = 0;
     if (threadIdx.x == 0) S.nst = 0;
     const double* beta = beta_lds ? sbeta : Q.beta;
+    const uint64_t info0 = Q.info_mask[0], info1 = Q.info_mask[1];
+    const int ninfo0 = __popcll(info0);
     int pre[PSCL_DL_NSEG + 1];
     int64_t n_in;
     if (Q.init) {
@@ -248,14 +268,25 @@ __global__ void __launch_bounds__(kPostWaves * 64) dl_post_kernel(const pscl_pos
     const int64_t i_begin = (int64_t)blockIdx.x * per;
     const int64_t i_end = i_begin + per < n_in ? i_begin + per : n_in;
     unsigned long long decodes = 0;
-    double* cur0 = S.lvl[wave][0];
-    double* cur1 = S.lvl[wave][1];
-    double* al = S.lvl[wave][2];
+    double* buf0 = S.lvl[wave][hs][0];
+    double* buf1 = S.lvl[wave][hs][1];
+    // info index of each of the lane's tree positions p = hl + 32 m (-1: frozen or beyond N)
+    int jpos[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int p = hl + 32 * m;
+        const uint64_t w = p < 64 ? info0 : info1;
+        const bool inf = p < N && ((w >> (p & 63)) & 1ULL);
+        jpos[m] = inf ? (p < 64 ? __popcll(info0 & ((1ULL << p) - 1ULL))
+                                : ninfo0 + __popcll(info1 & ((1ULL << (p - 64)) - 1ULL)))
+                      : -1;
+    }
     __syncthreads();
     for (int64_t cbase = i_begin; cbase < i_end; cbase += kPostChunk) {  // workgroup-uniform
-        // metadata of this wavefront's entries of the chunk, lane l = entry cbase + 8 l + wave
+        // metadata of this wavefront's entries of the chunk, lane l = entry cbase + 8 l + wave;
+        // half s takes lane 2 it + s at iteration it
         const int64_t mi = cbase + (int64_t)lane * kPostWaves + wave;
-        const bool mvalid = lane < kPostIters && mi < i_end;
+        const bool mvalid = mi < i_end;
         int me = 0, mnt = 0;
         int64_t mf = 0;
         uint64_t mb0 = 0, mb1 = 0, mt0 = 0, mt1 = 0;
@@ -278,113 +309,175 @@ __global__ void __launch_bounds__(kPostWaves * 64) dl_post_kernel(const pscl_pos
                 mt1 = Q.tried[2 * me + 1];
             }
         }
-        const int nit = (int)__builtin_amdgcn_readfirstlane((int)__popcll(__ballot(mvalid)));
-        auto rl64 = [](uint64_t v, int l) {
-            return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
-                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-        };
-        // channel row of the first entry; later rows are prefetched one entry ahead
-        double c0 = 0.0, c1 = 0.0;
-        if (nit > 0) load_row(Q.llr + rl64((uint64_t)mf, 0) * (Q.rm_E ? Q.rm_E : N), Q.rm_E, Q.rm_src, N, c0, c1);
-        for (int it = 0; it < nit; ++it) {
-            const int e = __builtin_amdgcn_readlane(me, it);
-            const int64_t f = (int64_t)rl64((uint64_t)mf, it);
-            const uint64_t b0 = rl64(mb0, it), b1 = rl64(mb1, it);
-            const int nt = Q.init ? 0 : __builtin_amdgcn_readlane(mnt, it);
-            double n0 = 0.0, n1 = 0.0;
-            if (it + 1 < nit)
-                load_row(Q.llr + rl64((uint64_t)mf, it + 1) * (Q.rm_E ? Q.rm_E : N), Q.rm_E, Q.rm_src, N, n0, n1);
+        const int nval = (int)__builtin_amdgcn_readfirstlane((int)__popcll(__ballot(mvalid)));  // lanes 0..nval-1
+        const int npair = (nval + 1) >> 1;
+        // channel rows of the first pair; later pairs' rows are prefetched one pair ahead
+        double c[4], cn[4];
+        load_row4(Q.llr + (int64_t)bcast64((uint64_t)mf, hs) * (Q.rm_E ? Q.rm_E : N), Q.rm_E, Q.rm_src, N, hl, c);
+        for (int it = 0; it < npair; ++it) {
+            const int src = 2 * it + hs;  // this half's metadata lane
+            const bool valid = src < nval;
+            const int e = __shfl(me, src);
+            const int64_t f = (int64_t)bcast64((uint64_t)mf, src);
+            const uint64_t b0 = bcast64(mb0, src), b1 = bcast64(mb1, src);
+            const int nt = Q.init ? 0 : __shfl(mnt, src);
+            if (it + 1 < npair)
+                load_row4(Q.llr + (int64_t)bcast64((uint64_t)mf, src + 2 < nval ? src + 2 : 0) * (Q.rm_E ? Q.rm_E : N),
+                          Q.rm_E, Q.rm_src, N, hl, cn);
             bool more;
             if (Q.init) {  // baseline failing by construction (dl_compact); nothing tried yet
-                more = Q.rounds > 0;
+                more = valid && Q.rounds > 0;
             } else {       // the attempt just decoded is the frame's latest (flip.py:123-136)
-                const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)mfl, it);
-                if (lane == 0) {
+                const uint32_t fl = (uint32_t)__shfl((int)mfl, src);
+                if (valid && hl == 0) {
                     Q.best[f * W] = b0;
                     if (W > 1) Q.best[f * W + 1] = b1;
                     Q.flags[f] = (uint8_t)fl;
                     if (Q.attempts) Q.attempts[f] = nt + 1;
                 }
-                ++decodes;
-                more = !(fl & PSCL_FLAG_CRC_PASS) && nt < Q.rounds;
+                if (valid && hl == 0) ++decodes;
+                more = valid && !(fl & PSCL_FLAG_CRC_PASS) && nt < Q.rounds;
             }
-            if (more) {
-                uint64_t u[2];
-                int jpos[2];
-                double* cur = replay_leaves(c0, c1, N, n, Q.info_mask, b0, b1, cur0, cur1, u, jpos);
-                double* nxt = cur == cur0 ? cur1 : cur0;
-                // |L0|: the path's decision LLRs at the information phases (flip.py:97-102, 127-132)
+            if (__ballot(more)) {  // (wave-uniform: both halves run the steps below; a half with
+                                   // nothing to do computes on its own buffers and writes nothing)
+                // ---- replay: the leaves of the attempt's best path, level by level
+                uint64_t u0 = 0, u1 = 0;  // the path's bits u[0..63], u[64..127] (this half's)
 #pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (jpos[h] >= 0) al[jpos[h]] = fabs(cur[lane + 64 * h]);
+                for (int m = 0; m < 4; ++m) {
+                    const int j = jpos[m];
+                    const bool bit = j >= 0 && (((j < 64 ? b0 : b1) >> (j & 63)) & 1ULL);
+                    const uint64_t bm = __ballot(bit) >> hb;
+                    const uint64_t part = bm & 0xffffffffULL;
+                    if (m == 0) u0 |= part;
+                    if (m == 1) u0 |= part << 32;
+                    if (m == 2) u1 |= part;
+                    if (m == 3) u1 |= part << 32;
+                }
+                double* cur = buf0;
+                double* nxt = buf1;
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    if (hl + 32 * m < N) cur[hl + 32 * m] = c[m];
                 pscl::wave_lds_fence();
-                // next flip: argmin over untried indices of (q, index), q = |L0| @ beta summed
-                // in index order (flip.py:104-108), q = |L0| without beta
-                const uint64_t t0 = Q.init ? 0ULL : rl64(mt0, it), t1 = Q.init ? 0ULL : rl64(mt1, it);
+                // partial sums of level lw2 from X_lw2 = u after butterfly stages 1..2^(lw2-1)
+                // (see replay_leaves)
+                auto stage = [](uint64_t x, int st) {
+                    const uint64_t M = st == 1 ? 0x5555555555555555ULL : st == 2 ? 0x3333333333333333ULL
+                                     : st == 4 ? 0x0f0f0f0f0f0f0f0fULL : st == 8 ? 0x00ff00ff00ff00ffULL
+                                     : st == 16 ? 0x0000ffff0000ffffULL : 0x00000000ffffffffULL;
+                    return x ^ ((x >> st) & M);
+                };
+                uint64_t X0 = u0, X1 = u1;
+                for (int mm = 1; mm < n; ++mm) {
+                    X0 = stage(X0, 1 << (mm - 1));
+                    X1 = stage(X1, 1 << (mm - 1));
+                }
+                for (int d = 0; d < n; ++d) {
+                    const int lw2 = n - d - 1, w2 = 1 << lw2;
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        const int p2 = hl + 32 * m;
+                        if (p2 < N) {
+                            const int k2 = p2 >> lw2, i = p2 & (w2 - 1);
+                            const int pa = ((k2 >> 1) << (lw2 + 1)) + i;
+                            const double a = cur[pa], bb = cur[pa + w2];
+                            const int q = (p2 - w2) & 127;  // bit (k2-1) w2 + i of X_lw2 (odd k2)
+                            const double gv = g_node(a, bb, (uint32_t)(((q >> 6) ? X1 : X0) >> (q & 63)) & 1u);
+                            const double fv = f_minsum(a, bb);
+                            const uint64_t msk = (k2 & 1) ? ~0ULL : 0ULL;
+                            nxt[p2] = pscl_asf64((pscl_asu64(gv) & msk) | (pscl_asu64(fv) & ~msk));
+                        }
+                    }
+                    pscl::wave_lds_fence();
+                    double* t = cur;
+                    cur = nxt;
+                    nxt = t;
+                    if (lw2 > 0) {
+                        X0 = stage(X0, w2 >> 1);
+                        X1 = stage(X1, w2 >> 1);
+                    }
+                }
+                // ---- |L0| at the information phases (flip.py:97-102, 127-132), in nxt
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    if (jpos[m] >= 0) nxt[jpos[m]] = fabs(cur[hl + 32 * m]);
+                pscl::wave_lds_fence();
+                // ---- next flip: argmin over untried (q, index), q = |L0| @ beta summed in
+                // index order (flip.py:104-108), q = |L0| without beta
+                const uint64_t t0 = Q.init ? 0ULL : bcast64(mt0, src), t1 = Q.init ? 0ULL : bcast64(mt1, src);
                 uint64_t bk = ~0ULL;
                 int bj = 0x7fffffff;
+                // candidates j = hl + 32 m; their sums advance together (one |L0_k| read serves
+                // all, and the dependent adds of the chains interleave)
+                constexpr int MC = KC ? (KC + 31) / 32 : 4;
+                double qv[MC];
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int j = lane + 64 * h;
+                for (int m = 0; m < MC; ++m) qv[m] = 0.0;
+                if (Q.beta && !(PSCL_POST_ABLATE & 4)) {
+                    const double* bc = beta + hl;
+#pragma unroll 4
+                    for (int k = 0; k < K; ++k) {
+                        const double ak = nxt[k];
+#pragma unroll
+                        for (int m = 0; m < MC; ++m)
+                            if (hl + 32 * m < K) qv[m] = qv[m] + ak * bc[k * K + 32 * m];
+                    }
+                } else {
+#pragma unroll
+                    for (int m = 0; m < MC; ++m) qv[m] = hl + 32 * m < K ? nxt[hl + 32 * m] : 0.0;
+                }
+#pragma unroll
+                for (int m = 0; m < MC; ++m) {
+                    const int j = hl + 32 * m;
                     if (j < K) {
-                        double q;
-                        if (Q.beta && !(PSCL_POST_ABLATE & 4)) {
-                            q = 0.0;
-                            const double* bc = beta + j;
-#pragma unroll 8
-                            for (int k = 0; k < K; ++k) q = q + al[k] * bc[k * K];
-                        } else {
-                            q = al[j];
-                        }
-                        const bool seen = ((h ? t1 : t0) >> (j & 63)) & 1ULL;
-                        const uint64_t key = seen ? ~0ULL : order_key(q);
-                        if (key < bk) {  // h = 0 visited first: ties keep the lower index
+                        const bool seen = ((j < 64 ? t0 : t1) >> (j & 63)) & 1ULL;
+                        const uint64_t key = seen ? ~0ULL : order_key(qv[m]);
+                        if (key < bk) {  // lower m first: ties keep the lower index
                             bk = key;
                             bj = j;
                         }
                     }
                 }
 #pragma unroll
-                for (int s = 1; s < 64; s <<= 1) {  // wave argmin of (key, index)
-                    const uint64_t ok = pscl::shfl_u64(bk, lane ^ s);
-                    const int oj = __shfl(bj, lane ^ s);
+                for (int sft = 1; sft < 32; sft <<= 1) {  // argmin of (key, index) within the half
+                    const uint64_t ok = pscl::shfl_u64(bk, lane ^ sft);
+                    const int oj = __shfl(bj, lane ^ sft);
                     if (ok < bk || (ok == bk && oj < bj)) {
                         bk = ok;
                         bj = oj;
                     }
                 }
-                const int idx = __builtin_amdgcn_readfirstlane(bj);  // an untried index exists: rounds <= min(retries, K)
-                // flipped phase and its warm-start bucket
-                const uint64_t hit0 = __ballot(jpos[0] == idx), hit1 = __ballot(jpos[1] == idx);
-                const int phis = hit0 ? __builtin_ctzll(hit0) : 64 + __builtin_ctzll(hit1);
+                const int idx = bj;  // (half-uniform) an untried index exists: rounds <= min(retries, K)
+                const int phis = Q.info_set[idx < K ? idx : 0];
                 int seg = phis >> 4;
                 if (seg > PSCL_DL_NSEG - 1) seg = PSCL_DL_NSEG - 1;
                 if (PSCL_POST_ABLATE & 2) seg = 0;
-                // exact metric increments of the forced prefix's leaves (scl.py:102-105, as the
-                // decode kernel forms them: good child metric + L, bad child metric + (|llr| + L),
-                // llr == 0: metric + LOGE2), then summed in phase order
+                pscl::wave_lds_fence();  // (the select's reads of nxt before the tails overwrite it)
+                // ---- exact metric increments of the forced prefix's leaves (scl.py:102-105, as
+                // the decode kernel forms them: good child metric + L, bad child metric +
+                // (|llr| + L), llr == 0: metric + LOGE2), then summed in phase order
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int p = lane + 64 * h;
+                for (int m = 0; m < 4; ++m) {
+                    const int p = hl + 32 * m;
                     if (p < 16 * seg) {
-                        const double lam = cur[p];
-                        const uint32_t bit = (uint32_t)(u[h] >> lane) & 1u;
+                        const double lam = cur[p];  // (the leaves stay in cur)
+                        const uint32_t bit = (uint32_t)(((p < 64 ? u0 : u1) >> (p & 63)) & 1ULL);
                         const double Lt = pscl_softplus_tail_bf(lam, S.exp_table);
                         const bool good = bit == (lam < 0.0 ? 1u : 0u);
                         nxt[p] = lam == 0.0 ? PSCL_LOGE2 : (good ? Lt : fabs(lam) + Lt);
                     }
                 }
                 pscl::wave_lds_fence();
-                if (lane == 0) {
-                    double m = 0.0;
+                if (more && hl == 0) {
+                    double mt = 0.0;
                     double* wm = Q.warm_metric + (int64_t)e * PSCL_DL_NSEG;
                     for (int k = 0; k <= seg; ++k) {
-                        wm[k] = m;
+                        wm[k] = mt;
                         if (k < seg && !(PSCL_POST_ABLATE & 8))
-                            for (int q = 0; q < 16; ++q) m = m + nxt[16 * k + q];
+                            for (int qq = 0; qq < 16; ++qq) mt = mt + nxt[16 * k + qq];
                     }
-                    Q.warm_u[2 * e] = u[0];
-                    Q.warm_u[2 * e + 1] = u[1];
+                    Q.warm_u[2 * e] = u0;
+                    Q.warm_u[2 * e + 1] = u1;
                     // tried set, flip record
                     Q.tried[2 * e] = idx < 64 ? (t0 | (1ULL << idx)) : t0;
                     Q.tried[2 * e + 1] = idx >= 64 ? (t1 | (1ULL << (idx - 64))) : t1;
@@ -407,19 +500,19 @@ __global__ void __launch_bounds__(kPostWaves * 64) dl_post_kernel(const pscl_pos
                     S.st_seg[sl] = (uint8_t)seg;
                     S.st_pos[sl] = (uint16_t)atomicAdd(&S.lcnt[seg], 1);
                 }
-                pscl::wave_lds_fence();  // the LDS buffers are rewritten by the next entry
+                pscl::wave_lds_fence();  // the LDS buffers are rewritten by the next pair
             }
-            c0 = n0;
-            c1 = n1;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) c[m] = cn[m];
         }
         // flush: one global atomic per non-empty bucket, then the staged entries scattered
         __syncthreads();
         if (threadIdx.x < PSCL_DL_NSEG) {
-            const int c = S.lcnt[threadIdx.x];
+            const int cc = S.lcnt[threadIdx.x];
             int g = 0;
-            if (c) {
+            if (cc) {
                 if (PSCL_POST_ABLATE & 1) g = 0;
-                else g = atomicAdd(Q.out_count + threadIdx.x * PSCL_DL_CSTRIDE, c);
+                else g = atomicAdd(Q.out_count + threadIdx.x * PSCL_DL_CSTRIDE, cc);
             }
             S.gbase[threadIdx.x] = g;
         }
@@ -434,7 +527,7 @@ __global__ void __launch_bounds__(kPostWaves * 64) dl_post_kernel(const pscl_pos
         if (threadIdx.x == 0) S.nst = 0;
         __syncthreads();
     }
-    if (Q.counters && decodes && lane == 0)
+    if (Q.counters && decodes)
         atomicAdd(reinterpret_cast<unsigned long long*>(Q.counters) + PSCL_CNT_RETRIES, decodes);
 }
 
@@ -496,8 +589,8 @@ hipError_t pscl_launch_replay(const pscl_replay_params& R, int64_t cap, hipStrea
 
 hipError_t pscl_launch_dl_post(const pscl_post_params& Q, int64_t entries, hipStream_t s) {
     if (entries <= 0) return hipSuccess;
-    // workgroups of 8 wavefronts, at most two resident per CU (256 CUs)
-    int64_t grid = (entries + kPostWaves * 4 - 1) / (kPostWaves * 4);
+    // workgroups of 8 wavefronts (16 entries in flight), at most two resident per CU
+    int64_t grid = (entries + kPostWaves * 8 - 1) / (kPostWaves * 8);
     if (grid > PSCL_POST_GRID) grid = PSCL_POST_GRID;
     const int beta_lds = PSCL_POST_BETA_LDS && Q.beta && (size_t)Q.K * Q.K * 8 <= 32 * 1024;  // (LDS <= 64 KB)
     const size_t lds = beta_lds ? (size_t)Q.K * Q.K * 8 : 0;
