@@ -99,9 +99,9 @@ struct pscl_handle {
     int rm_E = 0;                     // NR rate matching (0 = off)
     int32_t* d_rm_src = nullptr;      // [N] de-interleave gather index
     int32_t* d_rm_order = nullptr;    // [N] interleaver order
-    DevBuf scratch[40];
-    hipStream_t retry_stream = nullptr;  // DL-SCL retry rounds, overlapped with baseline decodes
-    hipEvent_t ev_base[2] = {nullptr, nullptr}, ev_retry[2] = {nullptr, nullptr};
+    DevBuf scratch[64];
+    hipStream_t retry_stream[2] = {nullptr, nullptr};  // DL-SCL retry chains of the two chunk parities
+    hipEvent_t ev_base[2] = {nullptr, nullptr}, ev_retry[2] = {nullptr, nullptr}, ev_join = nullptr;
     int32_t* h_count = nullptr;          // pinned: failing-frame counts of the two chunk parities
     double* d_beta = nullptr;         // [K][K] DL-SCL flip metric (null = |L0|)
     uint64_t* d_epi = nullptr;        // scl128 epilogue tables (gather + syndrome)
@@ -416,13 +416,16 @@ int pscl_destroy(pscl_handle* h) {
     if (h->d_epi) hipFree(h->d_epi);
     if (h->d_xtab) hipFree(h->d_xtab);
     if (h->d_crctab) hipFree(h->d_crctab);
-    if (h->retry_stream) hipStreamSynchronize(h->retry_stream);
+    for (int i = 0; i < 2; ++i)
+        if (h->retry_stream[i]) hipStreamSynchronize(h->retry_stream[i]);
     for (int i = 0; i < 2; ++i) {
         if (h->ev_base[i]) hipEventDestroy(h->ev_base[i]);
         if (h->ev_retry[i]) hipEventDestroy(h->ev_retry[i]);
     }
+    if (h->ev_join) hipEventDestroy(h->ev_join);
     if (h->h_count) hipHostFree(h->h_count);
-    if (h->retry_stream) hipStreamDestroy(h->retry_stream);
+    for (int i = 0; i < 2; ++i)
+        if (h->retry_stream[i]) hipStreamDestroy(h->retry_stream[i]);
     if (h->own_stream) hipStreamDestroy(h->own_stream);
     delete h;
     return PSCL_OK;
@@ -530,8 +533,7 @@ int pscl_set_beta(pscl_handle* h, const double* beta) {
 // retry rounds of one chunk on the retry stream (state sized for the largest chunk)
 namespace {
 struct DlState {
-    int32_t* cnt;     // [1] failing baseline frames of the chunk (dl_compact)
-    int64_t* act;     // [cap] frame index of each entry
+    int64_t* act;     // [cap] frame index of each entry (a slice of the chunk's dl_compact output)
     int32_t* bcnt;    // [rounds + 1][NSEG * CSTRIDE] bucket counters of each round's list
     int32_t *list0, *list1;  // [NSEG][cap] bucket lists (entry ids), alternating rounds
     uint64_t *tried, *force, *warm_u, *ob;
@@ -580,7 +582,7 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     int32_t* lists[2] = {S.list0, S.list1};
     // first flips: replay of every baseline best path (flip.py:97-111)
     Q.init = 1;
-    Q.in_count = S.cnt;
+    Q.in_count = nullptr;
     Q.out_count = S.bcnt;
     Q.out_list = lists[0];
     if ((e = pscl_launch_dl_post(Q, A, st)) != hipSuccess) return fail(PSCL_EDEVICE, "dl_post launch: %s", hipGetErrorString(e));
@@ -636,38 +638,51 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
     hipError_t e;
     if (d_attempts) HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)d_attempts, 1, (size_t)B, s));
     if (d_tried) HIP_TRY(hipMemsetAsync(d_tried, 0xff, (size_t)B * tried_stride * 4, s));
-    // Chunks (PSCL_DL_CHUNKS, default 1): the retry rounds of chunk c run on the retry stream
-    // while the main stream decodes chunk c + 1.  Measured on MI355X (L=4, 1e6 frames, 5 dB):
-    // 1 chunk 9.7 ms, 2 10.4, 4 12.9 -- the rounds are latency-bound and every chunk adds its
-    // own chain of min(retries, K) rounds on the retry stream, so overlap does not pay here.
+    // Chunks (PSCL_DL_CHUNKS, default 1): the baseline decodes run in order on the handle's
+    // stream; the retry entries of chunk c are split over two chains, each on its own retry
+    // stream with its own state, so the two chains' rounds overlap each other (and chunk c + 1's
+    // baseline decode).  A round is latency-bound (a few 10^4 entries per launch), so a second
+    // concurrent chain fills what one leaves idle.  PSCL_DL_SPLIT (1 or 2, default 2) sets the
+    // chains per chunk; chunks below 2 * kMinSplit failing frames keep one chain.
     int64_t nch = 1;
+    int nsplit = 2;
     if (rounds > 0 && getenv("PSCL_DL_CHUNKS")) {  // tuning override
         const long v = atol(getenv("PSCL_DL_CHUNKS"));
         if (v >= 1 && v <= 64) nch = v;
     }
+    if (rounds > 0 && getenv("PSCL_DL_SPLIT")) {  // tuning override
+        const long v = atol(getenv("PSCL_DL_SPLIT"));
+        if (v >= 1 && v <= 2) nsplit = (int)v;
+    }
+    constexpr int kMinSplit = 2048;
     const int64_t cap = (B + nch - 1) / nch;
-    DlState S[2];
+    DlState S[2];              // chain state (S[k] on retry stream k)
+    int32_t* cnt[2] = {};      // failing-frame count of the two chunk parities
+    int64_t* act[2] = {};      // their frame indices
     if (rounds > 0) {
-        if (!h->retry_stream) HIP_TRY(hipStreamCreateWithFlags(&h->retry_stream, hipStreamNonBlocking));
+        for (int i = 0; i < 2; ++i)
+            if (!h->retry_stream[i]) HIP_TRY(hipStreamCreateWithFlags(&h->retry_stream[i], hipStreamNonBlocking));
         for (int i = 0; i < 2; ++i) {
             if (!h->ev_base[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_base[i], hipEventDisableTiming));
             if (!h->ev_retry[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_retry[i], hipEventDisableTiming));
         }
+        if (!h->ev_join) HIP_TRY(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
         if (!h->h_count) HIP_TRY(hipHostMalloc((void**)&h->h_count, 16, hipHostMallocDefault));
         // everything sized before any work is queued (an allocation synchronizes the device)
-        const size_t c = (size_t)cap, NS = PSCL_DL_NSEG;
-        void* q[10];
-        const size_t sz[10] = {(size_t)(rounds + 1) * NS * PSCL_DL_CSTRIDE * 4, NS * c * 4, NS * c * 4, c * 16, c * 4,
-                               c * 2 * W * 8, c * NS * 8, c * 16, c * W * 8, c};
-        for (int i = 0; i < 10; ++i)
-            if ((rc = ensure(h, 12 + i, sz[i], &q[i]))) return rc;
-        void *pc[2], *pa[2];
-        if ((rc = ensure(h, 22, 4, &pc[0])) || (rc = ensure(h, 23, c * 8, &pa[0])) || (rc = ensure(h, 27, 4, &pc[1])) ||
-            (rc = ensure(h, 28, c * 8, &pa[1])))
-            return rc;
-        for (int i = 0; i < 2; ++i) {  // the retry state is used by one chunk at a time
-            S[i].cnt = (int32_t*)pc[i];
-            S[i].act = (int64_t*)pa[i];
+        const size_t NS = PSCL_DL_NSEG;
+        for (int i = 0; i < (nch >= 2 ? 2 : 1); ++i) {
+            void *pc, *pa;
+            if ((rc = ensure(h, 22 + 5 * i, 4, &pc)) || (rc = ensure(h, 23 + 5 * i, (size_t)cap * 8, &pa))) return rc;
+            cnt[i] = (int32_t*)pc;
+            act[i] = (int64_t*)pa;
+        }
+        for (int i = 0; i < nsplit; ++i) {  // chain i handles at most cap - cap / 2 entries when split
+            const size_t c = (size_t)(nsplit == 2 ? cap - cap / 2 : cap);
+            const size_t sz[10] = {(size_t)(rounds + 1) * NS * PSCL_DL_CSTRIDE * 4, NS * c * 4, NS * c * 4, c * 16, c * 4,
+                                   c * 2 * W * 8, c * NS * 8, c * 16, c * W * 8, c};
+            void* q[10];
+            for (int k = 0; k < 10; ++k)
+                if ((rc = ensure(h, (i ? 40 : 12) + k, sz[k], &q[k]))) return rc;
             S[i].bcnt = (int32_t*)q[0];
             S[i].list0 = (int32_t*)q[1];
             S[i].list1 = (int32_t*)q[2];
@@ -684,13 +699,21 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
         const int p = (int)(c & 1);
         HIP_TRY(hipEventSynchronize(h->ev_base[p]));
         const int A = h->h_count[p];
-        if (A > 0) {
-            HIP_TRY(hipStreamWaitEvent(h->retry_stream, h->ev_base[p], 0));
-            int r2 = dl_retry_chunk(h, S[p], A, rounds, d_llr, d_best, d_flags, d_attempts, d_tried, tried_stride,
-                                    d_ref ? d_counters_dl : nullptr, h->retry_stream);
+        const int parts = (nsplit == 2 && A >= 2 * kMinSplit) ? 2 : 1;
+        const int A0 = parts == 2 ? A - A / 2 : A;
+        for (int k = 0; k < parts && A > 0; ++k) {
+            HIP_TRY(hipStreamWaitEvent(h->retry_stream[k], h->ev_base[p], 0));
+            DlState T = S[k];
+            T.act = act[p] + (k ? A0 : 0);
+            int r2 = dl_retry_chunk(h, T, k ? A - A0 : A0, rounds, d_llr, d_best, d_flags, d_attempts, d_tried,
+                                    tried_stride, d_ref ? d_counters_dl : nullptr, h->retry_stream[k]);
             if (r2) return r2;
         }
-        HIP_TRY(hipEventRecord(h->ev_retry[p], h->retry_stream));
+        if (parts == 2) {  // both chains done before the parity's indices are reused
+            HIP_TRY(hipEventRecord(h->ev_join, h->retry_stream[1]));
+            HIP_TRY(hipStreamWaitEvent(h->retry_stream[0], h->ev_join, 0));
+        }
+        HIP_TRY(hipEventRecord(h->ev_retry[p], h->retry_stream[0]));
         return PSCL_OK;
     };
     for (int64_t c = 0; c < nch; ++c) {
@@ -709,19 +732,18 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
         if ((rc = launch_decode(h, P, 0))) return rc;
         if (rounds > 0) {
             const int p = (int)(c & 1);
-            if (c >= 2) HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[p], 0));  // parity buffers free again
-            HIP_TRY(hipMemsetAsync(S[p].cnt, 0, 4, s));
-            if ((e = pscl_launch_dl_compact(d_flags + c0, nc, c0, S[p].act, nullptr, S[p].cnt, s)) != hipSuccess)
+            if (c >= 2) HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[p], 0));  // the parity's indices free again
+            HIP_TRY(hipMemsetAsync(cnt[p], 0, 4, s));
+            if ((e = pscl_launch_dl_compact(d_flags + c0, nc, c0, act[p], nullptr, cnt[p], s)) != hipSuccess)
                 return fail(PSCL_EDEVICE, "dl_compact launch: %s", hipGetErrorString(e));
-            HIP_TRY(hipMemcpyAsync(h->h_count + p, S[p].cnt, 4, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(h->h_count + p, cnt[p], 4, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipEventRecord(h->ev_base[p], s));
             if (c >= 1 && (rc = retries_of(c - 1))) return rc;
         }
     }
     if (rounds > 0) {
         if ((rc = retries_of(nch - 1))) return rc;
-        HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[(nch - 1) & 1], 0));
-        if (nch >= 2) HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[(nch - 2) & 1], 0));
+        HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[(nch - 1) & 1], 0));  // chains run in order on stream 0
     }
     if (d_ref) {
         e = pscl_launch_dl_count(d_best, d_flags, d_ref, B, W, k_payload, d_counters_dl, s);

@@ -259,7 +259,7 @@ __global__ void __launch_bounds__(kPostWaves * 64) __attribute__((amdgpu_waves_p
     int pre[PSCL_DL_NSEG + 1];
     int64_t n_in;
     if (Q.init) {
-        n_in = *Q.in_count;
+        n_in = Q.cap;  // the entries are act[0, cap)
     } else {
         n_in = pscl_bucket_prefix(Q.in_count, Q.cap, pre);
     }

@@ -132,7 +132,7 @@ struct pscl_post_params {
     const uint64_t* exp_table;   // glibc exp table (exact metric tails)
     int rounds;                  // min(retries, K)
     int init;
-    const int32_t* in_count;     // init: [1] entry count; else bucket counts of this round
+    const int32_t* in_count;     // bucket counts of this round (init: unused, cap entries)
     const int32_t* in_list;      // bucket lists of this round ([NSEG][cap] entry ids)
     int64_t cap;
     int32_t* out_count;          // next round's bucket counts (zeroed)

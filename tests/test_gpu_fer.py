@@ -159,6 +159,31 @@ def test_device_retry_loop_chunked_pipeline(monkeypatch):
     assert dev["counters"]["dl"][1] == int((~host["success"]).sum())
 
 
+@pytest.mark.parametrize("chunks,split", [("1", "2"), ("2", "2"), ("1", "1")])
+def test_device_retry_loop_split_chains(monkeypatch, chunks, split):
+    """Two concurrent retry chains per chunk (each on its own stream, >= 4096 failing frames)
+    give the same per-frame results as the host ranking."""
+    from polar_code_amd.polar.polar import construct_info_set, encode
+    from polar_code_amd.polar.crc import attach_crc
+
+    monkeypatch.setenv("PSCL_DL_CHUNKS", chunks)
+    monkeypatch.setenv("PSCL_DL_SPLIT", split)
+    rng = np.random.default_rng(78)
+    B = 24000
+    info = construct_info_set(128, 64)
+    msg = attach_crc(rng.integers(0, 2, size=(B, 40), dtype=np.int8), "0x1864CFB")
+    var = 1.0 / (2.0 * 0.5 * 10 ** (1.0 / 10))
+    llr = 2.0 * ((1.0 - 2.0 * encode(msg)) + rng.normal(0, math.sqrt(var), size=(B, 128))) / var
+    beta = np.load(GOLDEN / "beta_M4.npy")
+    dev = decode_with_retries_device(llr, info, 4, 8, crc="0x1864CFB", beta=beta, msg=msg)
+    host = decode_with_retries_batch(llr, info, 4, 8, crc="0x1864CFB", beta=beta)
+    assert (dev["attempts"] > 1).sum() >= 4096 * int(chunks) + 1000  # every chunk splits
+    np.testing.assert_array_equal(dev["tried"], host["tried"])
+    np.testing.assert_array_equal(dev["attempts"], host["attempts"])
+    np.testing.assert_array_equal(dev["best_bits"], host["best_bits"])
+    assert dev["counters"]["dl"][1] == int((~host["success"]).sum())
+
+
 def test_simulate_one_call_equals_separate_calls():
     """pscl_simulate (TX + uncoded + SCL + DL-SCL + counters in one call) equals the separate
     device calls over the same frames, and frame ranges add up exactly."""
