@@ -25,7 +25,7 @@ PSCL_ENOMEM = -3
 PSCL_EPRUNED = -4
 PSCL_EUNSUP = -5
 PSCL_MAX_N = 1024
-PSCL_DEVICE_LOOP_MAX_N = 128  # device TX chain, decision-LLR replay and DL-SCL loop (capi.cpp)
+PSCL_REPLAY_MAX_N = 128  # pscl_path_llrs_device (decision-LLR replay); TX, decode and the DL-SCL loop take any N
 PSCL_MAX_L = 32
 PSCL_FLAG_CRC_PASS = 0x80
 PSCL_FLAG_IDX_MASK = 0x3F

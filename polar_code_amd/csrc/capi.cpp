@@ -158,12 +158,14 @@ void fill_decode_params(const pscl_handle* h, pscl_decode_params& P, int hist) {
     pscl_decode_layout(P, hist);
 }
 
-int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStream_t st = nullptr) {
+// scr_slot: the scratch buffer of a long-code decode (decodes that may run concurrently on
+// different streams need different slots)
+int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStream_t st = nullptr, int scr_slot = 38) {
     if (!st) st = h->stream;
     pscl_decode_params P = P0;
     if (P.long_mode) {  // global scratch of every workgroup in flight (scl_long.hip)
         void* d_scr;
-        const int rc = ensure(h, 38, (size_t)pscl_decode_grid(P) * (size_t)P.long_block_bytes, &d_scr);
+        const int rc = ensure(h, scr_slot, (size_t)pscl_decode_grid(P) * (size_t)P.long_block_bytes, &d_scr);
         if (rc) return rc;
         P.long_scratch = (unsigned char*)d_scr;
     }
@@ -354,14 +356,17 @@ int pscl_create(pscl_handle** out, int device, int N, const int32_t* info_set, i
         CREATE_TRY(hipMalloc(&h->d_epi, epi.size()));
         CREATE_TRY(hipMemcpy(h->d_epi, epi.data(), epi.size(), hipMemcpyHostToDevice));
     }
-    if (N <= PSCL_FAST_N) {
+    {
         // TX tables: encode and CRC attach are GF(2)-linear, so byte-wise tables give them in
-        // ceil(K/8) (resp. ceil(kp/8)) lookups per frame
+        // ceil(K/8) (resp. ceil(kp/8)) lookups per frame.  Codeword words per entry: 2 for
+        // N <= 128 (channel_kernel), N / 64 for the long codes (channel_long_kernel).
         const int nb = (K + 7) / 8, kp = K - h->crc_deg, nbp = (kp + 7) / 8;
-        std::vector<uint64_t> xt((size_t)(nb > 0 ? nb : 1) * 256 * 2, 0);
+        const int XW = N <= PSCL_FAST_N ? 2 : N / 64;
+        std::vector<uint64_t> xt((size_t)(nb > 0 ? nb : 1) * 256 * XW, 0);
+        std::vector<uint64_t> u(XW);
         for (int k = 0; k < nb; ++k)
             for (int v = 0; v < 256; ++v) {
-                uint64_t u[2] = {0, 0};
+                std::fill(u.begin(), u.end(), 0ULL);
                 for (int t = 0; t < 8; ++t) {
                     const int q = 8 * k + t;
                     if (q < K && ((v >> t) & 1)) {
@@ -369,16 +374,17 @@ int pscl_create(pscl_handle** out, int device, int N, const int32_t* info_set, i
                         u[pos >> 6] |= 1ULL << (pos & 63);
                     }
                 }
-                for (int w = 0; w < 2; ++w)  // in-word Arikan stages (polar.py:17-29)
+                for (int w = 0; w < XW; ++w)  // in-word Arikan stages (polar.py:17-29)
                     for (int st = 1; st < 64; st <<= 1) {
                         uint64_t m = 0;
                         for (int b = 0; b < 64; ++b)
                             if (!(b & st)) m |= 1ULL << b;
                         u[w] ^= (u[w] >> st) & m;
                     }
-                if (h->N > 64) u[0] ^= u[1];
-                xt[((size_t)k * 256 + v) * 2] = u[0];
-                xt[((size_t)k * 256 + v) * 2 + 1] = u[1];
+                for (int sw = 1; 64 * sw < N; sw <<= 1)  // stages of 64 bits and more: whole words
+                    for (int w = 0; w < XW; ++w)
+                        if (!(w & sw) && w + sw < XW) u[w] ^= u[w + sw];
+                for (int w = 0; w < XW; ++w) xt[((size_t)k * 256 + v) * XW + w] = u[w];
             }
         std::vector<uint32_t> ct((size_t)(nbp > 0 ? nbp : 1) * 256, 0);
         for (int k = 0; k < nbp; ++k)
@@ -615,6 +621,85 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     }
     return PSCL_OK;
 }
+
+// long codes (N > PSCL_FAST_N): dense entry state, ping-ponged between passes; the retry
+// decodes' workgroup scratch has its own slot (they may overlap the next chunk's baseline)
+constexpr int kLongRetryScratch = 62;
+struct DlLongState {
+    int64_t* act1;              // the second entry-frame array (the first is the compaction's)
+    uint64_t *tried[2], *ob, *force;
+    int32_t *nt[2], *cnt;       // cnt: [rounds + 2] entries of each pass
+    uint8_t* of;
+    double* l0;
+};
+
+// The retry chain of a chunk's A failing frames (act0/cnt0: dl_compact's output) for the long
+// codes: the failing frames decoded again with decision-LLR history (the baseline's L0,
+// flip.py:97-102; same best bits), a first post pass, then per round a HIST decode of the live
+// entries (forced bits, LLR rows by indirection, the live count on the device) and a post pass.
+int dl_retry_long(pscl_handle* h, const DlLongState& S, int64_t* act0, const int32_t* cnt0, int A, int rounds,
+                  const double* d_llr, uint64_t* d_best, uint8_t* d_flags, int32_t* d_attempts, int32_t* d_tried,
+                  int tried_stride, int64_t* d_cnt_dl, hipStream_t st) {
+    hipError_t e;
+    int rc;
+    HIP_TRY(hipMemsetAsync(S.cnt, 0, (size_t)(rounds + 2) * 4, st));
+    pscl_decode_params H;
+    fill_decode_params(h, H, 1);
+    H.llr = d_llr;
+    H.B = A;
+    H.fidx = act0;
+    H.d_count = cnt0;
+    H.best = S.ob;
+    H.flags = S.of;
+    H.best_info_llrs = S.l0;
+    if ((rc = launch_decode(h, H, 1, st, kLongRetryScratch))) return rc;
+    pscl_post_long_params Q;
+    memset(&Q, 0, sizeof(Q));
+    Q.K = h->K;
+    Q.W = h->W;
+    Q.rounds = rounds;
+    Q.cap = A;
+    Q.ob = S.ob;
+    Q.of = S.of;
+    Q.l0 = S.l0;
+    Q.force = S.force;
+    Q.beta = h->d_beta;
+    Q.best = d_best;
+    Q.flags = d_flags;
+    Q.attempts = d_attempts;
+    Q.tried_out = d_tried;
+    Q.tried_stride = tried_stride;
+    Q.counters = d_cnt_dl;
+    int64_t* acts[2] = {act0, S.act1};
+    Q.init = 1;
+    Q.in_count = cnt0;
+    Q.out_count = S.cnt + 1;
+    Q.act_in = act0;
+    Q.act_out = S.act1;
+    Q.tried_w_out = S.tried[1];
+    Q.nt_out = S.nt[1];
+    if ((e = pscl_launch_dl_post_long(Q, st)) != hipSuccess)
+        return fail(PSCL_EDEVICE, "dl_post_long launch: %s", hipGetErrorString(e));
+    Q.init = 0;
+    for (int r = 0; r < rounds; ++r) {  // pass r + 1 reads state set (r + 1) & 1
+        const int c = (r + 1) & 1;
+        H.fidx = acts[c];
+        H.d_count = S.cnt + r + 1;
+        H.force = S.force;
+        if ((rc = launch_decode(h, H, 1, st, kLongRetryScratch))) return rc;
+        Q.in_count = S.cnt + r + 1;
+        Q.out_count = S.cnt + r + 2;
+        Q.act_in = acts[c];
+        Q.act_out = acts[c ^ 1];
+        Q.tried_in = S.tried[c];
+        Q.tried_w_out = S.tried[c ^ 1];
+        Q.nt_in = S.nt[c];
+        Q.nt_out = S.nt[c ^ 1];
+        if ((e = pscl_launch_dl_post_long(Q, st)) != hipSuccess)
+            return fail(PSCL_EDEVICE, "dl_post_long launch: %s", hipGetErrorString(e));
+    }
+    return PSCL_OK;
+}
 }  // namespace
 
 int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retries, uint64_t* d_best, uint8_t* d_flags,
@@ -624,7 +709,6 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
     if (B < 0) return fail(PSCL_EINVAL, "B must be >= 0");
     if (B == 0) return PSCL_OK;
     if (!d_llr || !d_best || !d_flags) return fail(PSCL_EINVAL, "d_llr, d_best and d_flags are required");
-    if (h->N > PSCL_FAST_N) return fail(PSCL_EUNSUP, "the device DL-SCL loop supports N <= %d (use the host-ranked form)", PSCL_FAST_N);
     if (d_ref && (!d_counters_scl || !d_counters_dl)) return fail(PSCL_EINVAL, "d_ref given without both counters");
     if (k_payload < 0 || k_payload > h->K) return fail(PSCL_EINVAL, "k_payload out of range");
     const int rounds = h->crc_poly && retries > 0 ? (retries < h->K ? retries : h->K) : 0;
@@ -657,6 +741,7 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
     constexpr int kMinSplit = 2048;
     const int64_t cap = (B + nch - 1) / nch;
     DlState S[2];              // chain state (S[k] on retry stream k)
+    DlLongState LS = {};       // (long codes)
     int32_t* cnt[2] = {};      // failing-frame count of the two chunk parities
     int64_t* act[2] = {};      // their frame indices
     if (rounds > 0) {
@@ -675,6 +760,31 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
             if ((rc = ensure(h, 22 + 5 * i, 4, &pc)) || (rc = ensure(h, 23 + 5 * i, (size_t)cap * 8, &pa))) return rc;
             cnt[i] = (int32_t*)pc;
             act[i] = (int64_t*)pa;
+        }
+        if (h->N > PSCL_FAST_N) {  // long codes: one chain, dense state (dl_retry_long)
+            const size_t c = (size_t)cap;
+            const size_t sz[10] = {c * 8, c * W * 8, c * W * 8, c * W * 8, c * 2 * W * 8, c * 4, c * 4,
+                                   (size_t)(rounds + 2) * 4, c, c * K * 8};
+            void* q[10];
+            for (int k = 0; k < 10; ++k)
+                if ((rc = ensure(h, 52 + k, sz[k], &q[k]))) return rc;
+            LS.act1 = (int64_t*)q[0];
+            LS.tried[0] = (uint64_t*)q[1];
+            LS.tried[1] = (uint64_t*)q[2];
+            LS.ob = (uint64_t*)q[3];
+            LS.force = (uint64_t*)q[4];
+            LS.nt[0] = (int32_t*)q[5];
+            LS.nt[1] = (int32_t*)q[6];
+            LS.cnt = (int32_t*)q[7];
+            LS.of = (uint8_t*)q[8];
+            LS.l0 = (double*)q[9];
+            nsplit = 0;
+            pscl_decode_params H;  // the retry decodes' scratch, sized before any work is queued
+            fill_decode_params(h, H, 1);
+            H.B = cap;
+            void* d_scr;
+            if ((rc = ensure(h, kLongRetryScratch, (size_t)pscl_decode_grid(H) * (size_t)H.long_block_bytes, &d_scr)))
+                return rc;
         }
         for (int i = 0; i < nsplit; ++i) {  // chain i handles at most cap - cap / 2 entries when split
             const size_t c = (size_t)(nsplit == 2 ? cap - cap / 2 : cap);
@@ -699,6 +809,16 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
         const int p = (int)(c & 1);
         HIP_TRY(hipEventSynchronize(h->ev_base[p]));
         const int A = h->h_count[p];
+        if (h->N > PSCL_FAST_N) {
+            if (A > 0) {
+                HIP_TRY(hipStreamWaitEvent(h->retry_stream[0], h->ev_base[p], 0));
+                int r2 = dl_retry_long(h, LS, act[p], cnt[p], A, rounds, d_llr, d_best, d_flags, d_attempts, d_tried,
+                                       tried_stride, d_ref ? d_counters_dl : nullptr, h->retry_stream[0]);
+                if (r2) return r2;
+            }
+            HIP_TRY(hipEventRecord(h->ev_retry[p], h->retry_stream[0]));
+            return PSCL_OK;
+        }
         const int parts = (nsplit == 2 && A >= 2 * kMinSplit) ? 2 : 1;
         const int A0 = parts == 2 ? A - A / 2 : A;
         for (int k = 0; k < parts && A > 0; ++k) {
@@ -855,7 +975,7 @@ int pscl_uncoded_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, doubl
     if (B < 0 || frame0 < 0) return fail(PSCL_EINVAL, "B and frame0 must be >= 0");
     if (B == 0) return PSCL_OK;
     if (!d_counters) return fail(PSCL_EINVAL, "d_counters is NULL");
-    if (k_payload < 0 || k_payload > 128) return fail(PSCL_EINVAL, "k_payload out of range");
+    if (k_payload < 0 || k_payload > PSCL_MAX_N) return fail(PSCL_EINVAL, "k_payload out of range");
     int rc = set_device(h);
     if (rc) return rc;
     pscl_channel_params P;
@@ -920,7 +1040,6 @@ int pscl_channel_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, doubl
     if (!(rate > 0)) return fail(PSCL_EINVAL, "rate must be positive");
     if (k_payload + h->crc_deg != h->K || k_payload < 0)
         return fail(PSCL_EINVAL, "k_payload (%d) + crc degree (%d) must equal K (%d)", k_payload, h->crc_deg, h->K);
-    if (h->N > PSCL_FAST_N) return fail(PSCL_EUNSUP, "the device TX chain supports N <= %d", PSCL_FAST_N);
     int rc = set_device(h);
     if (rc) return rc;
     pscl_channel_params P;

@@ -531,6 +531,92 @@ __global__ void __launch_bounds__(kPostWaves * 64) __attribute__((amdgpu_waves_p
         atomicAdd(reinterpret_cast<unsigned long long*>(Q.counters) + PSCL_CNT_RETRIES, decodes);
 }
 
+// Post pass of the long codes (N > PSCL_FAST_N): one wavefront per entry, no replay -- the
+// retry decodes run the HIST kernel, so the attempt's best-path decision LLRs (L0, scl.py:158,
+// 166) arrive with it.  Per entry: final-attempt bookkeeping and the CRC stop rule
+// (flip.py:123-136); for the survivors the next flip (q = |L0| @ beta summed in index order,
+// argmin over untried (q, index), flip.py:104-111), its force words (flip.py:30-34), and the
+// entry's state moved to a dense slot of the next pass (one atomic per wavefront).  The long
+// kernel decodes every phase, so there is no warm start.
+__global__ void __launch_bounds__(256) dl_post_long_kernel(const pscl_post_long_params Q) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int K = Q.K, W = Q.W;
+    const int64_t n_in = *Q.in_count < Q.cap ? (int64_t)*Q.in_count : Q.cap;
+    const int64_t wstride = (int64_t)gridDim.x * (blockDim.x >> 6);
+    unsigned long long decodes = 0;
+    for (int64_t e = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave; e < n_in; e += wstride) {  // wave-uniform
+        const int64_t f = Q.act_in[e];
+        const int nt = Q.init ? 0 : Q.nt_in[e];
+        const uint8_t fl = Q.of[e];
+        const uint64_t* bw = Q.ob + e * W;
+        bool more;
+        if (Q.init) {  // baseline failing by construction (dl_compact); its results stay
+            more = Q.rounds > 0;
+        } else {       // the attempt just decoded is the frame's latest
+            for (int w = lane; w < W; w += 64) Q.best[f * W + w] = bw[w];
+            if (lane == 0) {
+                Q.flags[f] = fl;
+                if (Q.attempts) Q.attempts[f] = nt + 1;
+            }
+            ++decodes;
+            more = !(fl & PSCL_FLAG_CRC_PASS) && nt < Q.rounds;
+        }
+        if (!more) continue;
+        // next flip: candidates j = lane + 64 m, q_j summed over k in index order
+        const double* a = Q.l0 + e * K;
+        uint64_t bk = ~0ULL;
+        int bj = 0x7fffffff;
+        for (int j0 = 0; j0 < K; j0 += 64) {
+            const int j = j0 + lane;
+            double q = 0.0;
+            if (j < K) {
+                if (Q.beta) {
+                    for (int k = 0; k < K; ++k) q = q + fabs(a[k]) * Q.beta[(int64_t)k * K + j];
+                } else {
+                    q = fabs(a[j]);
+                }
+                const bool seen = !Q.init && ((Q.tried_in[e * W + (j >> 6)] >> (j & 63)) & 1ULL);
+                const uint64_t key = seen ? ~0ULL : order_key(q);
+                if (key < bk) {  // lower j first: ties keep the lower index
+                    bk = key;
+                    bj = j;
+                }
+            }
+        }
+#pragma unroll
+        for (int sft = 1; sft < 64; sft <<= 1) {  // wave argmin of (key, index)
+            const uint64_t ok = pscl::shfl_u64(bk, lane ^ sft);
+            const int oj = __shfl(bj, lane ^ sft);
+            if (ok < bk || (ok == bk && oj < bj)) {
+                bk = ok;
+                bj = oj;
+            }
+        }
+        const int idx = bj;  // an untried index exists: rounds <= min(retries, K)
+        int slot = 0;
+        if (lane == 0) slot = atomicAdd(Q.out_count, 1);
+        const int64_t e2 = __shfl(slot, 0);
+        if (lane == 0) {
+            Q.act_out[e2] = f;
+            Q.nt_out[e2] = nt + 1;
+            if (Q.tried_out) Q.tried_out[f * Q.tried_stride + nt] = idx;
+        }
+        for (int w = lane; w < W; w += 64) {
+            const uint64_t t = Q.init ? 0ULL : Q.tried_in[e * W + w];
+            Q.tried_w_out[e2 * W + w] = (idx >> 6) == w ? (t | (1ULL << (idx & 63))) : t;
+            // _force_vector (flip.py:30-34): bits [0, idx) = reference, bit idx flipped, rest free
+            const int lo = 64 * w, nb = idx - lo + 1;
+            const uint64_t mask = nb <= 0 ? 0ULL : (nb >= 64 ? ~0ULL : ((1ULL << nb) - 1ULL));
+            uint64_t val = bw[w] & mask;
+            if (idx >= lo && idx < lo + 64) val ^= 1ULL << (idx - lo);
+            Q.force[e2 * 2 * W + w] = mask;
+            Q.force[e2 * 2 * W + W + w] = val;
+        }
+    }
+    if (Q.counters && lane == 0 && decodes)
+        atomicAdd(reinterpret_cast<unsigned long long*>(Q.counters) + PSCL_CNT_RETRIES, decodes);
+}
+
 // FER/BER statistics of the final results against the transmitted words: wavefront sums,
 // then one atomic per counter per 1024-thread block
 __global__ void __launch_bounds__(1024) dl_count_kernel(const uint64_t* __restrict__ best, const uint8_t* __restrict__ flags,
@@ -543,14 +629,14 @@ __global__ void __launch_bounds__(1024) dl_count_kernel(const uint64_t* __restri
     if (f == 0) atomicAdd(C + PSCL_CNT_FRAMES, (unsigned long long)B);
     int v[4] = {0, 0, 0, 0};  // frame errors, bit errors, payload frame errors, payload bit errors
     if (f < B) {
-        const uint64_t d0 = best[f * W] ^ ref[f * W];
-        const uint64_t d1 = W > 1 ? best[f * W + 1] ^ ref[f * W + 1] : 0ULL;
-        const int kp = k_payload;
-        const uint64_t pm0 = kp >= 64 ? ~0ULL : ((1ULL << kp) - 1);
-        const uint64_t pm1 = kp >= 128 ? ~0ULL : (kp > 64 ? ((1ULL << (kp - 64)) - 1) : 0ULL);
         v[0] = (flags[f] & PSCL_FLAG_CRC_PASS) ? 0 : 1;
-        v[1] = __popcll(d0) + __popcll(d1);
-        v[3] = __popcll(d0 & pm0) + __popcll(d1 & pm1);
+        for (int w = 0; w < W; ++w) {  // payload = the first k_payload information bits
+            const uint64_t d = best[f * W + w] ^ ref[f * W + w];
+            const int kp = k_payload - 64 * w;
+            const uint64_t pm = kp >= 64 ? ~0ULL : (kp > 0 ? ((1ULL << kp) - 1) : 0ULL);
+            v[1] += __popcll(d);
+            v[3] += __popcll(d & pm);
+        }
         v[2] = v[3] ? 1 : 0;
     }
 #pragma unroll
@@ -567,6 +653,14 @@ __global__ void __launch_bounds__(1024) dl_count_kernel(const uint64_t* __restri
 }
 
 }  // namespace
+
+hipError_t pscl_launch_dl_post_long(const pscl_post_long_params& Q, hipStream_t s) {
+    if (Q.cap <= 0) return hipSuccess;
+    int64_t grid = (Q.cap + 3) / 4;  // one wavefront per entry, the live count read on the device
+    if (grid > 2048) grid = 2048;
+    hipLaunchKernelGGL(dl_post_long_kernel, dim3((unsigned)grid), dim3(256), 0, s, Q);
+    return hipGetLastError();
+}
 
 hipError_t pscl_launch_dl_compact(const uint8_t* flags, int64_t B, int64_t base, int64_t* act, int32_t* list,
                                   int32_t* count, hipStream_t s) {

@@ -154,6 +154,33 @@ struct pscl_post_params {
     int64_t* counters;           // or null: PSCL_CNT_RETRIES += decodes
 };
 
+// DL-SCL post pass of the long codes (N > PSCL_FAST_N, dlscl.hip dl_post_long_kernel): the
+// retry decodes run the HIST long kernel, whose best-path decision LLRs are the attempt's L0;
+// survivors are compacted into the next round's dense state (no buckets, no warm start).
+struct pscl_post_long_params {
+    int K, W, rounds, init;
+    int64_t cap;                 // entries the state arrays hold
+    const int32_t* in_count;     // [1] entries of this pass
+    int32_t* out_count;          // [1] entries of the next pass (zeroed before the pass)
+    const int64_t* act_in;       // [cap] frame of each entry
+    int64_t* act_out;
+    const uint64_t* tried_in;    // [cap][W] tried flip indices (null at init: none)
+    uint64_t* tried_w_out;
+    const int32_t* nt_in;        // [cap] flips tried (null at init)
+    int32_t* nt_out;
+    const uint64_t* ob;          // [cap][W] the attempt's best bits, by entry
+    const uint8_t* of;           // [cap] its flags
+    const double* l0;            // [cap][K] its best path's decision LLRs
+    uint64_t* force;             // [cap][2W] force words of the next pass, by new entry
+    const double* beta;          // [K][K] or null (q = |L0|)
+    uint64_t* best;              // [B][W] final best bits (per frame)
+    uint8_t* flags;              // [B]
+    int32_t* attempts;           // [B] or null
+    int32_t* tried_out;          // [B][tried_stride] or null
+    int tried_stride;
+    int64_t* counters;           // or null: PSCL_CNT_RETRIES += decodes
+};
+
 struct pscl_channel_params {
     uint64_t seed;
     uint32_t stream_id;
@@ -191,6 +218,7 @@ hipError_t pscl_launch_replay(const pscl_replay_params& R, int64_t cap, hipStrea
 hipError_t pscl_launch_softplus_tails(const double* v, int64_t n, const uint64_t* exp_table, double* exact,
                                      double* apx, hipStream_t s);
 hipError_t pscl_launch_dl_post(const pscl_post_params& Q, int64_t entries, hipStream_t s);
+hipError_t pscl_launch_dl_post_long(const pscl_post_long_params& Q, hipStream_t s);
 hipError_t pscl_launch_dl_count(const uint64_t* best, const uint8_t* flags, const uint64_t* ref, int64_t B, int W,
                                 int k_payload, int64_t* counters, hipStream_t s);
 

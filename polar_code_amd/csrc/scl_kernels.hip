@@ -521,6 +521,73 @@ hipError_t pscl_launch_decode(const pscl_decode_params& P, int hist, hipStream_t
 int pscl_decode_lds(const pscl_decode_params& P, int hist) { return decode_lds_bytes(P, hist); }
 
 // uncoded BPSK baseline: one frame per lane, kp payload symbols, errors reduced per block
+// TX chain of the long codes (N > PSCL_FAST_N): one wavefront per frame, lane w holds word w
+// of the message (w < W) and of the codeword (w < N / 64).  Same stream as channel_kernel:
+// payload bits 128 j .. 128 j + 127 from the Philox block (frame, 0xffffffff - j) (j = 0 is
+// channel_kernel's block), symbol noise from the blocks (frame, lane + 64 q).
+__global__ void __launch_bounds__(256) channel_long_kernel(const pscl_channel_params P) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t k0 = (uint32_t)P.seed, k1 = (uint32_t)(P.seed >> 32) ^ (P.stream_id * 0x85EBCA6Bu);
+    const int E = P.rm_E ? P.rm_E : P.N;
+    const int kp = P.k_payload, W = P.W, NW = P.N >> 6;
+    const int nb = (P.K + 7) >> 3, nbp = (kp + 7) >> 3;
+    for (int64_t idx = (int64_t)blockIdx.x * 4 + wave; idx < P.B; idx += (int64_t)gridDim.x * 4) {  // wave-uniform
+        const uint64_t fr = (uint64_t)(P.frame0 + idx);
+        // payload word `lane`, masked to kp bits
+        uint64_t m = 0;
+        if (lane < W) {
+            const u32x4 rb = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), 0xffffffffu - (uint32_t)(lane >> 1), 0u},
+                                        k0, k1);
+            m = (lane & 1) ? (((uint64_t)rb.w << 32) | rb.z) : (((uint64_t)rb.y << 32) | rb.x);
+            const int nbits = kp - 64 * lane;
+            m = nbits >= 64 ? m : (nbits > 0 ? (m & ((1ULL << nbits) - 1)) : 0ULL);
+        }
+        // attach_cols (crc.py:19-37): the remainder of the payload bytes, XOR-reduced over lanes
+        uint32_t rem = 0;
+        if (lane < W)
+            for (int t = 0; t < 8; ++t) {
+                const int k = 8 * lane + t;
+                if (k < nbp) rem ^= P.crctab[k * 256 + (uint32_t)((m >> (8 * t)) & 255u)];
+            }
+        for (int sft = 1; sft < 64; sft <<= 1) rem ^= (uint32_t)__shfl_xor((int)rem, sft);
+        if (P.crc_deg) {
+            const int w0 = kp >> 6, o = kp & 63;
+            if (lane == w0) m |= (uint64_t)rem << o;
+            if (lane == w0 + 1 && o + P.crc_deg > 64) m |= (uint64_t)rem >> (64 - o);
+        }
+        // codeword x = u G (polar.py:17-29,106-119): one table row per message byte
+        uint64_t x = 0;
+        for (int k = 0; k < nb; ++k) {
+            const uint64_t mw = pscl::shfl_u64(m, k >> 3);
+            const uint32_t v = (uint32_t)((mw >> (8 * (k & 7))) & 255u);
+            if (lane < NW) x ^= P.xtab[((size_t)k * 256 + v) * NW + lane];
+        }
+        if (P.msg && lane < W) P.msg[idx * W + lane] = m;
+        double* row = P.llr + idx * E;
+        for (int q = 0; q * 128 < E; ++q) {
+            const u32x4 rn = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), (uint32_t)(lane + 64 * q), 0u}, k0, k1);
+            const uint64_t a = ((uint64_t)rn.y << 32) | rn.x, bb = ((uint64_t)rn.w << 32) | rn.z;
+            const double uu1 = ((double)(a >> 11) + 1.0) * 0x1p-53;  // (0, 1]
+            const double uu2 = (double)(bb >> 11) * 0x1p-53;         // [0, 1)
+            const double rad = sqrt(-2.0 * log(uu1));
+            double sn, cs;
+            sincospi(2.0 * uu2, &sn, &cs);
+            const double z[2] = {rad * cs, rad * sn};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int p = lane + 64 * h + 128 * q;
+                const int pos = p < E ? (P.rm_E ? P.rm_order[p % P.N] : p) : 0;
+                const uint64_t xw = pscl::shfl_u64(x, pos >> 6);  // (every lane takes part)
+                if (p < E) {
+                    const double sym = ((xw >> (pos & 63)) & 1) ? -1.0 : 1.0;
+                    const double received = sym + P.sigma * z[h];
+                    row[p] = 2.0 * received / P.noise_var;
+                }
+            }
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) uncoded_kernel(const pscl_channel_params P, int64_t* counters) {
     __shared__ long long part[4][2];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -530,9 +597,14 @@ __global__ void __launch_bounds__(256) uncoded_kernel(const pscl_channel_params 
     int ferr = 0, berr = 0;
     if (idx < P.B) {
         const uint64_t fr = (uint64_t)(P.frame0 + idx);
-        const u32x4 rb = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), 0xffffffffu, 0u}, k0, k1);
-        const uint64_t r0 = ((uint64_t)rb.y << 32) | rb.x, r1 = ((uint64_t)rb.w << 32) | rb.z;
+        u32x4 rb = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), 0xffffffffu, 0u}, k0, k1);
+        uint64_t r0 = ((uint64_t)rb.y << 32) | rb.x, r1 = ((uint64_t)rb.w << 32) | rb.z;
         for (int c = 0; 2 * c < kp; ++c) {
+            if (c && (c & 63) == 0) {  // payload bits 128 j.. (long codes): Philox block (frame, 0xffffffff - j)
+                rb = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), 0xffffffffu - (uint32_t)(c >> 6), 0u}, k0, k1);
+                r0 = ((uint64_t)rb.y << 32) | rb.x;
+                r1 = ((uint64_t)rb.w << 32) | rb.z;
+            }
             const u32x4 rn = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), 0x40000000u + (uint32_t)c, 0u}, k0, k1);
             const uint64_t a = ((uint64_t)rn.y << 32) | rn.x, bb = ((uint64_t)rn.w << 32) | rn.z;
             const double uu1 = ((double)(a >> 11) + 1.0) * 0x1p-53;
@@ -545,7 +617,7 @@ __global__ void __launch_bounds__(256) uncoded_kernel(const pscl_channel_params 
             for (int h = 0; h < 2; ++h) {
                 const int q = 2 * c + h;
                 if (q < kp) {
-                    const int bit = (int)(((q < 64 ? r0 : r1) >> (q & 63)) & 1ULL);
+                    const int bit = (int)((((q & 127) < 64 ? r0 : r1) >> (q & 63)) & 1ULL);
                     const double y = (bit ? -1.0 : 1.0) + P.sigma * z[h];
                     berr += ((2.0 * y / P.noise_var) < 0.0 ? 1 : 0) != bit;
                 }
@@ -600,6 +672,12 @@ hipError_t pscl_launch_channel(const pscl_channel_params& P, hipStream_t s) {
     int64_t grid = (P.B + 255) / 256;
     if (grid > (1 << 20)) grid = 1 << 20;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(channel_kernel, dim3((unsigned)grid), dim3(256), 0, s, P);
+    if (P.N > PSCL_FAST_N) {  // one wavefront per frame
+        int64_t g = (P.B + 3) / 4;
+        if (g > (1 << 16)) g = 1 << 16;
+        hipLaunchKernelGGL(channel_long_kernel, dim3((unsigned)g), dim3(256), 0, s, P);
+    } else {
+        hipLaunchKernelGGL(channel_kernel, dim3((unsigned)grid), dim3(256), 0, s, P);
+    }
     return hipGetLastError();
 }

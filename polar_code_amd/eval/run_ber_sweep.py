@@ -193,8 +193,6 @@ class PhiloxFrames:
         if a.scheme == "nr_polar_scl":
             crc = a.crc_poly  # scl_nr.py: always CRC-protected
         self.crc = crc
-        if N > _native.PSCL_DEVICE_LOOP_MAX_N:
-            raise NotImplementedError(f"--rng philox: the device TX chain covers N <= {_native.PSCL_DEVICE_LOOP_MAX_N}")
         E = a.E if a.scheme == "nr_polar_scl" else 0
         self.dec = _native.Decoder(N, info_set, a.M, crc, device)
         if E:

@@ -253,10 +253,8 @@ def run_sweep(args: argparse.Namespace) -> List[Dict[str, float]]:
             stream = ReplayStream(args.seed, float(snr_db), payload_bits, cfg.crc_poly, args.include_uncoded)
             for b0, b1 in blocks:
                 payload, msg, llr, llr_unc = stream.take(b0, b1)
-                # the device DL-SCL loop covers N <= 128; longer codes rank flips on the host
-                engine = args.dl_engine if cfg.N <= _native.PSCL_DEVICE_LOOP_MAX_N else "host"
                 _count_block(c, msg, llr, payload, llr_unc, info_set, args.M, cfg.crc_poly, args.retries, beta, device,
-                             engine)
+                             args.dl_engine)
         else:
             # batches in flight on `--streams` handles (own HIP streams), one host thread each:
             # one batch's TX and DL-SCL retry chain overlap another's decode; counts add exactly

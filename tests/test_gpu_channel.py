@@ -2,7 +2,8 @@
 
 Payload bits, CRC, codeword and message words must match exactly; LLRs agree to ~1e-12
 (the host uses libm log/sin/cos, the device the ROCm device library).  Covers plain N=128,
-short codes, K > 64 (two message words) and NR rate matching (repetition and puncturing).
+short codes, K > 64 (two message words), NR rate matching (repetition and puncturing) and the
+long codes (N = 256..1024: channel_long_kernel, payloads beyond one Philox block).
 """
 import numpy as np
 import pytest
@@ -30,17 +31,25 @@ def philox4x32(c, k0, k1):
     return c0, c1, c2, c3
 
 
+def host_payload(k0, k1, lo, hi, kp):
+    """Payload bits 128 j .. 128 j + 127 from the Philox block (frame, 0xffffffff - j)."""
+    pay = np.zeros((lo.size, kp), np.int8)
+    for j in range((kp + 127) // 128):
+        c2 = np.full(lo.size, 0xFFFFFFFF - j, np.uint64)
+        x, y, z, w = philox4x32((lo, hi, c2, np.zeros(lo.size, np.uint64)), k0, k1)
+        r0, r1 = (y << np.uint64(32)) | x, (w << np.uint64(32)) | z
+        for q in range(128 * j, min(kp, 128 * j + 128)):
+            word = r0 if (q & 127) < 64 else r1
+            pay[:, q] = ((word >> np.uint64(q & 63)) & np.uint64(1)).astype(np.int8)
+    return pay
+
+
 def host_stream(seed, stream_id, frame0, B, N, info, K, kp, crc, ebno_db, rate, E=0, order=None):
     k0 = seed & 0xFFFFFFFF
     k1 = ((seed >> 32) ^ ((stream_id * 0x85EBCA6B) & 0xFFFFFFFF)) & 0xFFFFFFFF
     fr = np.arange(frame0, frame0 + B, dtype=np.uint64)
     lo, hi = fr & M32, fr >> np.uint64(32)
-    x, y, z, w = philox4x32((lo, hi, np.full(B, 0xFFFFFFFF, np.uint64), np.zeros(B, np.uint64)), k0, k1)
-    r0, r1 = (y << np.uint64(32)) | x, (w << np.uint64(32)) | z
-    pay = np.zeros((B, kp), np.int8)
-    for q in range(kp):
-        word = r0 if q < 64 else r1
-        pay[:, q] = ((word >> np.uint64(q & 63)) & np.uint64(1)).astype(np.int8)
+    pay = host_payload(k0, k1, lo, hi, kp)
     msg = attach_crc(pay, crc) if crc else pay
     u = np.zeros((B, N), np.int8)
     u[:, info] = msg
@@ -79,7 +88,9 @@ def _encode(u):
 
 @pytest.mark.parametrize("N,K,crc,E", [(128, 64, "0x1864CFB", 0), (64, 40, "0x1864CFB", 0), (32, 16, None, 0),
                                        (128, 88, "0x1864CFB", 0), (128, 64, "0x1864CFB", 300),
-                                       (128, 64, "0x1864CFB", 100)])
+                                       (128, 64, "0x1864CFB", 100), (256, 128, "0x1864CFB", 0),
+                                       (512, 300, "0x1864CFB", 0), (1024, 512, None, 0),
+                                       (256, 100, "0x1864CFB", 300), (512, 256, "0x1864CFB", 400)])
 def test_channel_stream(N, K, crc, E):
     info = construct_info_set(N, K)
     dec = _native.Decoder(N, info, 2, crc)
@@ -102,3 +113,41 @@ def test_channel_stream(N, K, crc, E):
     got = ((words[:, :, None] >> np.arange(64, dtype=np.uint64)) & np.uint64(1)).reshape(B, -1)[:, :K]
     np.testing.assert_array_equal(got.astype(np.int8), msg)
     np.testing.assert_allclose(llr, ref, rtol=1e-11, atol=1e-11)
+
+
+@pytest.mark.parametrize("kp", [40, 200])
+def test_uncoded_stream(kp):
+    """The uncoded BPSK baseline (run_fer_sweep.py:111-121) counts the errors of the same
+    payload bits as the TX chain with its own noise blocks (frame, 0x40000000 + c)."""
+    info = construct_info_set(256, kp)
+    dec = _native.Decoder(256, info, 2, None)
+    B, frame0, seed, sid, ebno = 3000, 77, 0x5EED, 9, 1.0
+    nc = _native.PSCL_NCOUNT
+    with _native.DeviceArena(dec) as mem:
+        d_cnt = mem.alloc(nc * 8)
+        mem.memset(d_cnt, 0, nc * 8)
+        dec.uncoded_device(seed, sid, ebno, kp, frame0, B, d_cnt)
+        cnt = mem.download(d_cnt, nc * 8, np.int64)
+    k0 = seed & 0xFFFFFFFF
+    k1 = ((seed >> 32) ^ ((sid * 0x85EBCA6B) & 0xFFFFFFFF)) & 0xFFFFFFFF
+    fr = np.arange(frame0, frame0 + B, dtype=np.uint64)
+    lo, hi = fr & M32, fr >> np.uint64(32)
+    pay = host_payload(k0, k1, lo, hi, kp)
+    nvar = 1.0 / (2.0 * 10 ** (ebno / 10.0))
+    err = np.zeros((B, kp), bool)
+    for c in range((kp + 1) // 2):
+        c2 = np.full(B, 0x40000000 + c, np.uint64)
+        cx, cy, cz, cw2 = philox4x32((lo, hi, c2, np.zeros(B, np.uint64)), k0, k1)
+        a, bb = (cy << np.uint64(32)) | cx, (cw2 << np.uint64(32)) | cz
+        u1 = ((a >> np.uint64(11)).astype(np.float64) + 1.0) * 2.0 ** -53
+        u2 = (bb >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+        rad = np.sqrt(-2.0 * np.log(u1))
+        zz = (rad * np.cos(2 * np.pi * u2), rad * np.sin(2 * np.pi * u2))
+        for h in range(2):
+            q = 2 * c + h
+            if q < kp:
+                y = (1.0 - 2.0 * pay[:, q]) + np.sqrt(nvar) * zz[h]
+                err[:, q] = (2.0 * y / nvar < 0.0) != (pay[:, q] == 1)
+    assert cnt[_native.CNT_FRAMES] == B
+    assert cnt[_native.CNT_FRAME_ERR] == int(err.any(axis=1).sum())
+    assert cnt[_native.CNT_BIT_ERR] == int(err.sum())

@@ -95,6 +95,41 @@ def test_long_decode_with_retries_matches_oracle():
         assert [int(t) for t in out["tried"][f] if t >= 0] == r["tried"], f
 
 
+@pytest.mark.parametrize("N,K,M,retries,use_beta,snr,chunks", [(256, 128, 4, 6, False, 2.0, "1"),
+                                                             (256, 128, 8, 4, True, 1.5, "2"),
+                                                             (512, 256, 4, 3, False, 1.25, "1")])
+def test_long_device_retry_loop(monkeypatch, N, K, M, retries, use_beta, snr, chunks):
+    """The device DL-SCL loop at N > 128 (HIST long-kernel retry decodes, dense per-round state)
+    equals the host-ranked batch form frame by frame (bits, CRC, attempts, tried indices) and
+    the oracle on a sample; in-kernel counters match the host's counts."""
+    from polar_code_amd.dlscl.flip import decode_with_retries_batch, decode_with_retries_device
+
+    monkeypatch.setenv("PSCL_DL_CHUNKS", chunks)
+    rng = np.random.default_rng(N + K + M)
+    info = construct_info_set(N, K)
+    B = 600
+    msg = attach_crc(rng.integers(0, 2, size=(B, K - 24), dtype=np.int8), POLY)
+    u = np.zeros((B, N), np.int8)
+    u[:, info] = msg
+    nv = 1.0 / (2.0 * K / N * 10 ** (snr / 10))
+    llr = 2.0 * ((1.0 - 2.0 * _polar_transform(u)) + rng.normal(0.0, np.sqrt(nv), size=(B, N))) / nv
+    beta = rng.random((K, K)).astype(np.float32) if use_beta else None  # (the reference stores beta in fp32)
+    dev = decode_with_retries_device(llr, info, M, retries, crc=POLY, beta=beta, msg=msg)
+    host = decode_with_retries_batch(llr, info, M, retries, crc=POLY, beta=beta)
+    assert np.count_nonzero(host["attempts"] > 1) >= 50  # the retry loop is exercised
+    for k in ("best_bits", "success", "attempts", "tried"):
+        np.testing.assert_array_equal(dev[k], host[k], err_msg=k)
+    cd = dev["counters"]["dl"]
+    assert cd[_native.CNT_FRAME_ERR] == int(np.count_nonzero(~host["success"]))
+    assert cd[_native.CNT_BIT_ERR] == int(np.count_nonzero(host["best_bits"] != msg))
+    assert cd[_native.CNT_RETRIES] == int((host["attempts"] - 1).sum())
+    for f in range(0, B, 40):  # the reference loop (oracle) on a sample
+        r = oracle.decode_with_retries(llr[f], info, M, retries, crc=POLY, beta=beta)
+        np.testing.assert_array_equal(dev["best_bits"][f], r["bits"], err_msg=f"frame {f}")
+        assert dev["attempts"][f] == r["attempts"], f
+        assert [int(t) for t in dev["tried"][f] if t >= 0] == r["tried"], f
+
+
 def test_long_device_counters():
     """Device-buffer decode with in-kernel FER/BER counting at N = 512."""
     N, K, M = 512, 256, 4

@@ -104,25 +104,32 @@ def test_ber_sweep_philox_world2_equals_world1(tmp_path):
     assert errs[0] >= 4000 and all(b <= 1e5 + 64 for b in bits) and bits[-1] >= 1e5 and errs[-1] < 4000
 
 
-def test_ber_sweep_philox_matches_replay_statistically(tmp_path):
-    """Device (Philox) frames and the reference's NumPy stream give the same FER/BER at 5 dB
-    within Monte-Carlo error (config 5)."""
+# a long code through the same CLI: N = 256 (long-code kernels, channel_long_kernel, the
+# long-code DL-SCL-free NR decode), E = 300 (repetition)
+CFG_LONG = ["--scheme", "nr_polar_scl", "--K_payload", "100", "--K_crc", "24", "--E", "300", "--N", "256", "--M", "4"]
+
+
+@pytest.mark.parametrize("cfg,snr,err_cap,bits_cap,batch", [(CFG5, "5.0", "6000", "1e7", "8192"),
+                                                            (CFG_LONG, "3.5", "3000", "2e6", "4096")])
+def test_ber_sweep_philox_matches_replay_statistically(tmp_path, cfg, snr, err_cap, bits_cap, batch):
+    """Device (Philox) frames and the reference's NumPy stream give the same FER/BER within
+    Monte-Carlo error (config 5 at 5 dB; an N = 256 NR code)."""
     rows = {}
     for rng in ("replay", "philox"):
         out = tmp_path / f"{rng}.csv"
-        rb.main([*CFG5, "--EbN0_lo", "5.0", "--EbN0_hi", "5.0", "--err_cap", "6000", "--bits_cap", "1e7",
-                 "--batch", "8192", "--rng", rng, "--out", str(out)])
+        rb.main([*cfg, "--EbN0_lo", snr, "--EbN0_hi", snr, "--err_cap", err_cap, "--bits_cap", bits_cap,
+                 "--batch", batch, "--rng", rng, "--out", str(out)])
         h, v = out.read_text().splitlines()[:2]
         hv = h.split(",")
         vv = v.split(",")
         vv = vv[:6] + [",".join(vv[6:len(vv) - 6])] + vv[len(vv) - 6:]  # params holds a comma
         rows[rng] = dict(zip(hv, vv))
-    n = {k: int(r["bits_total"]) // 64 for k, r in rows.items()}
+    n = {k: int(r["bits_total"]) // int(cfg[cfg.index("--K_payload") + 1]) for k, r in rows.items()}
     p = {k: float(r["fer"]) for k, r in rows.items()}
     pp = (p["replay"] * n["replay"] + p["philox"] * n["philox"]) / (n["replay"] + n["philox"])
     z = (p["philox"] - p["replay"]) / np.sqrt(pp * (1 - pp) * (1 / n["replay"] + 1 / n["philox"]))
     assert abs(z) < 4.5, (rows, z)
     ber = {k: float(r["ber"]) for k, r in rows.items()}
     assert 0.6 < ber["philox"] / ber["replay"] < 1.6, rows
-    print(f"config 5 at 5 dB: replay FER {p['replay']:.4f} ({n['replay']} frames), philox FER {p['philox']:.4f} "
+    print(f"{cfg[-5:]} at {snr} dB: replay FER {p['replay']:.4f} ({n['replay']} frames), philox FER {p['philox']:.4f} "
           f"({n['philox']} frames), z = {z:.2f}")
