@@ -57,7 +57,7 @@ extern "C" {
 
 #define PSCL_MAX_N 1024  /* code length N: power of two, 2..1024 (N <= 128: the specialised kernels,
                             every BASELINE config; 256..1024: one wavefront per frame, global scratch;
-                            the device TX chain and DL-SCL loop stop at 128) */
+                            the decision-LLR replay pscl_path_llrs_device stops at 128) */
 #define PSCL_MAX_L 32    /* list size M/L: 1..32 (2L candidates fit one 64-lane wavefront) */
 #define PSCL_MAX_CRC 32  /* CRC degree: 1..32 */
 #define PSCL_WORDS(K) (((K) + 63) / 64)

@@ -6,7 +6,13 @@ code's waterfall (the reference's construction, design SNR 2.5 dB: oracle FER at
 for N = 256 at 4 dB, 0.32 for N = 512 at 5 dB, 0.42 for N = 1024 at 6 dB), generated on the
 host once and kept resident; each timed step decodes B frames (decode_device, best bits
 and flags only) on the handle's stream, timed with events on that stream.
+
+    python tools/long_bench.py --dl       (the long-code DL-SCL loop and TX chain instead)
+DL-SCL (8 flips, no beta) on device-resident frames: the device loop (pscl_dlscl_device, HIST
+long-kernel retry decodes) against the host-ranked form (decode_with_retries_batch: GPU decodes
+from host buffers, numpy ranking), and the device TX chain (pscl_channel_device).
 """
+import time
 import sys
 from pathlib import Path
 
@@ -20,6 +26,58 @@ from polar_code_amd.polar.crc import attach_crc  # noqa: E402
 from polar_code_amd.polar.polar import _polar_transform, construct_info_set  # noqa: E402
 
 POLY = "0x1864CFB"
+
+
+def dl_bench():
+    from polar_code_amd.dlscl.flip import decode_with_retries_batch
+
+    for N, K, L, B, snr in [(256, 128, 4, 50_000, 3.5), (512, 256, 4, 20_000, 4.0)]:
+        rng = np.random.default_rng(N + L)
+        info = construct_info_set(N, K)
+        msg = attach_crc(rng.integers(0, 2, size=(B, K - 24), dtype=np.int8), POLY)
+        u = np.zeros((B, N), np.int8)
+        u[:, info] = msg
+        nv = 1.0 / (2.0 * K / N * 10 ** (snr / 10))
+        llr = 2.0 * ((1.0 - 2.0 * _polar_transform(u)) + rng.normal(0.0, np.sqrt(nv), size=(B, N))) / nv
+        dec = _native.Decoder(N, info, L, POLY)
+        stream = torch.cuda.Stream()
+        dec.set_stream(stream.cuda_stream)
+        d_llr = torch.from_numpy(llr).cuda()
+        W = dec.W
+        best = torch.empty((B, W), dtype=torch.int64, device="cuda")
+        flags = torch.empty(B, dtype=torch.uint8, device="cuda")
+        att = torch.empty(B, dtype=torch.int32, device="cuda")
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for rep in range(2):  # (the first call sizes the state)
+            e0.record(stream)
+            dec.dlscl_device(d_llr.data_ptr(), B, 8, d_best=best.data_ptr(), d_flags=flags.data_ptr(),
+                             d_attempts=att.data_ptr())
+            e1.record(stream)
+            torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        a = att.cpu().numpy()
+        t0 = time.perf_counter()
+        host = decode_with_retries_batch(llr, info, L, 8, crc=POLY)
+        hs = time.perf_counter() - t0
+        same = bool((host["attempts"] == a).all())
+        d_msg = torch.empty((B, W), dtype=torch.int64, device="cuda")
+        dec.channel_device(1, 35, snr, K / N, K - 24, 0, B, d_llr.data_ptr(), d_msg.data_ptr())
+        torch.cuda.synchronize()
+        e0.record(stream)
+        dec.channel_device(1, 35, snr, K / N, K - 24, 0, B, d_llr.data_ptr(), d_msg.data_ptr())
+        e1.record(stream)
+        torch.cuda.synchronize()
+        tx = e0.elapsed_time(e1)
+        print(f"N={N} K={K} L={L} {snr:g} dB, {B} frames: DL-SCL device loop {B / ms * 1e3 / 1e6:.3f} M frames/s "
+              f"({ms:.1f} ms; {int((a > 1).sum())} frames retried, {int(a.sum() - B)} re-decodes); host-ranked "
+              f"form {B / hs / 1e6:.3f} M frames/s ({hs * 1e3:.0f} ms), attempts equal: {same}; TX chain "
+              f"{B / tx * 1e3 / 1e6:.1f} M frames/s", flush=True)
+        dec.close()
+
+
+if "--dl" in sys.argv:
+    dl_bench()
+    sys.exit(0)
 for N, K, L, B, snr in [(256, 128, 8, 200_000, 4.0), (512, 256, 8, 100_000, 5.0), (1024, 512, 8, 50_000, 6.0),
                         (1024, 512, 32, 20_000, 6.0)]:
     rng = np.random.default_rng(N + L)
