@@ -546,6 +546,7 @@ struct DlState {
     int32_t* nt;
     double* warm_metric;
     uint8_t* of;
+    int32_t *dcnt, *dlist;   // screening retry decodes: deferred entries ([NSEG * CSTRIDE] counts, [cap])
 };
 
 int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const double* d_llr, uint64_t* d_best,
@@ -607,11 +608,38 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     H.warm_u = S.warm_u;
     if (pscl_decode_wpg(H) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
     int rc;
+    // screening retry decodes (PSCL_DL_SCREEN=1, measured below): the forced-bit screening
+    // instance, then the exact decode of the entries it could not certify (one bucket, no
+    // warm start), outputs at their entries
+    const bool dl_screen = getenv("PSCL_DL_SCREEN") && atoi(getenv("PSCL_DL_SCREEN")) == 1;
+    const bool scr = dl_screen && h->screen && S.dcnt && pscl_screening_fs_available(H);
+    pscl_decode_params HA, HX;
+    if (scr) {
+        HA = H;
+        HA.apx = 1;
+        pscl_decode_layout(HA, 0);  // (no exp table in LDS)
+        HA.amb_elist = S.dlist;
+        HA.amb_count = S.dcnt;
+        HX = H;
+        HX.elist = S.dlist;
+        HX.bcount = S.dcnt;
+        HX.grid_cap = (int64_t)256 * 16 / (pscl_decode_wpg(HX) > 0 ? pscl_decode_wpg(HX) : 1);
+    }
     Q.init = 0;
     for (int r = 0; r < rounds; ++r) {  // no host round trips: the counts stay on the device
         H.elist = lists[r & 1];
         H.bcount = S.bcnt + (size_t)r * bstride;
-        if ((rc = launch_decode(h, H, 0, st))) return rc;
+        if (scr) {
+            HIP_TRY(hipMemsetAsync(S.dcnt, 0, bstride * 4, st));
+            HA.elist = H.elist;
+            HA.bcount = H.bcount;
+            if ((e = pscl_launch_decode(HA, 0, st)) != hipSuccess)
+                return fail(PSCL_EDEVICE, "screening retry decode: %s", hipGetErrorString(e));
+            if ((e = pscl_launch_decode(HX, 0, st)) != hipSuccess)
+                return fail(PSCL_EDEVICE, "exact retry re-decode: %s", hipGetErrorString(e));
+        } else if ((rc = launch_decode(h, H, 0, st))) {
+            return rc;
+        }
         Q.in_count = H.bcount;
         Q.in_list = lists[r & 1];
         Q.out_count = S.bcnt + (size_t)(r + 1) * bstride;
@@ -788,11 +816,13 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
         }
         for (int i = 0; i < nsplit; ++i) {  // chain i handles at most cap - cap / 2 entries when split
             const size_t c = (size_t)(nsplit == 2 ? cap - cap / 2 : cap);
-            const size_t sz[10] = {(size_t)(rounds + 1) * NS * PSCL_DL_CSTRIDE * 4, NS * c * 4, NS * c * 4, c * 16, c * 4,
-                                   c * 2 * W * 8, c * NS * 8, c * 16, c * W * 8, c};
-            void* q[10];
-            for (int k = 0; k < 10; ++k)
-                if ((rc = ensure(h, (i ? 40 : 12) + k, sz[k], &q[k]))) return rc;
+            const size_t sz[12] = {(size_t)(rounds + 1) * NS * PSCL_DL_CSTRIDE * 4, NS * c * 4, NS * c * 4, c * 16, c * 4,
+                                   c * 2 * W * 8, c * NS * 8, c * 16, c * W * 8, c, NS * PSCL_DL_CSTRIDE * 4, c * 4};
+            void* q[12];
+            for (int k = 0; k < 12; ++k)  // (slots: set 0 12..21 and 8..9, set 1 40..51)
+                if ((rc = ensure(h, k < 10 ? (i ? 40 : 12) + k : (i ? 50 : 8) + k - 10, sz[k], &q[k]))) return rc;
+            S[i].dcnt = (int32_t*)q[10];
+            S[i].dlist = (int32_t*)q[11];
             S[i].bcnt = (int32_t*)q[0];
             S[i].list0 = (int32_t*)q[1];
             S[i].list1 = (int32_t*)q[2];

@@ -69,6 +69,11 @@ hipError_t launch128(const pscl_decode_params& P, int hist, int wpg, int64_t gri
 
 // the launch launch128 makes for a plain decode (no history, no forced bits) has a screening
 // form: a compiled-in code in its own input mode with a full-size list
+int pscl_screening_fs_available(const pscl_decode_params& P) {
+    if (!P.fast || P.sc_hard || P.rm_E || P.L != pscl_decode_lmax(P.L) || P.L < 4) return 0;
+    return spec_code(P) == 1;
+}
+
 int pscl_screening_available(const pscl_decode_params& P) {
     if (!P.fast || P.force || P.sc_hard || P.L != pscl_decode_lmax(P.L)) return 0;
     const int code = spec_code(P);

@@ -526,11 +526,28 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 // better / worse child (any rounding order will do here)
                 const double mg = metric + Lt, mb = mg + fabs(lam);
                 const double m0 = neg ? mb : mg, m1 = neg ? mg : mb;  // bit-0 / bit-1 child
-                const int ncnt = 2 * cnt < L ? 2 * cnt : L;
+                int ncnt = 2 * cnt < L ? 2 * cnt : L;
                 int src;
                 uint32_t b;
                 uint64_t nm;
-                if (2 * cnt <= L) {
+                // forced bits (FS: the DL-SCL retry decodes, scl.py:146-161): a force vector
+                // fixes a prefix of the information bits, so a forced frame holds one path and
+                // takes the forced child -- no ordering decision (frames of a wavefront may be
+                // forced or free at a phase: cnt and the branches below are per frame)
+                bool forced_here = false;
+                uint32_t fbit = 0;
+                if constexpr (FS) {
+                    if (force) {
+                        forced_here = (((jq < 64 ? fm0 : fm1) >> (jq & 63)) & 1) != 0;
+                        fbit = (uint32_t)(((jq < 64 ? fv0 : fv1) >> (jq & 63)) & 1);
+                    }
+                }
+                if (FS && forced_here) {
+                    src = lane;
+                    b = fbit;
+                    nm = pscl_asu64(b ? m1 : m0);
+                    ncnt = cnt;
+                } else if (2 * cnt <= L) {
                     // every child survives: bit 0 stays in lane p, bit 1 goes to lane cnt + p
                     src = gbase + (g & (cnt - 1));
                     b = (g & cnt) ? 1u : 0u;
@@ -566,7 +583,9 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                         lastbit = gb;
                         if (phi < 64) u0 |= (uint64_t)gb << phi; else u1 |= (uint64_t)gb << (phi - 64);
                         ++j;
-                        pre_ok = !(phi & 1);  // the upper lanes' tail is the next leaf's (see lam_up)
+                        // the upper lanes' tail is the next leaf's (see lam_up); not with forced
+                        // bits, where the frames of a wavefront may take other branches here
+                        pre_ok = !FS && !(phi & 1);
                         return;
                     }
                     // rank the 2L children on the high words; lane r takes the child ranked r.
@@ -819,7 +838,11 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
         }
         // APX: a frame with an uncertain ordering is handed to the exact re-decode
         const bool famb = APX && ((amb >> gbase) & (G == 64 ? ~0ULL : ((1ULL << (G & 63)) - 1))) != 0;
-        if (APX && !PSCL_APX_ABLATE && famb && g == 0 && fvalid) P.amb_list[atomicAdd(P.amb_count, 1)] = f;
+        if (APX && !PSCL_APX_ABLATE && famb && g == 0 && fvalid) {
+            const int slot = atomicAdd(P.amb_count, 1);
+            if (FS && P.amb_elist) P.amb_elist[slot] = (int32_t)f;
+            else P.amb_list[slot] = f;
+        }
         const bool active = path_lane && g < cnt && fvalid && !famb;
         const int64_t fo = P.out_by_row ? frow : f;  // output row
         uint32_t pm = (active && syn == 0) ? (1u << rank) : 0u;

@@ -17,9 +17,14 @@
 // (128,64) decodes read plain channel rows; (128,88) is the NR code, decoded rate matched
 hipError_t PSCL_SPEC_FN(const pscl_decode_params& P, bool fs, int wpg, int64_t grid, int lds, hipStream_t s) {
     constexpr bool CH = PSCL_SPEC_CODE == 2;
-    if (P.apx && !fs)  // screening decode (plain decodes only)
+    if (P.apx && !fs)  // screening decode (plain decodes)
         hipLaunchKernelGGL((scl128_kernel<PSCL_SPEC_LMAX, false, CH, false, PSCL_SPEC_CODE, true>), dim3((unsigned)grid),
                            dim3(wpg * 64), lds, s, P);
+#if PSCL_SPEC_CODE == 1 && PSCL_SPEC_LMAX >= 4
+    else if (P.apx && fs)  // screening decode with forced bits (the DL-SCL retry rounds)
+        hipLaunchKernelGGL((scl128_kernel<PSCL_SPEC_LMAX, false, CH, true, PSCL_SPEC_CODE, true>), dim3((unsigned)grid),
+                           dim3(wpg * 64), lds, s, P);
+#endif
     else if (fs)
         hipLaunchKernelGGL((scl128_kernel<PSCL_SPEC_LMAX, false, CH, true, PSCL_SPEC_CODE>), dim3((unsigned)grid),
                            dim3(wpg * 64), lds, s, P);

@@ -54,6 +54,7 @@ struct pscl_decode_params {
     int apx;
     int64_t* amb_list;           // [B] frame indices to re-decode exactly
     int32_t* amb_count;
+    int32_t* amb_elist;          // or (bucket-list launches): [B] entry ids, appended instead
     int out_by_row;              // 1: outputs, reference words and counts at LLR row fidx[b]
     int64_t grid_cap;            // 0, or an upper bound on the workgroups of the launch (the
                                  // kernels stride over frames; a d_count launch of few frames)
@@ -204,6 +205,7 @@ hipError_t pscl_launch_long(const pscl_decode_params& P, int hist, hipStream_t s
 void pscl_decode_layout(pscl_decode_params& P, int hist);
 int pscl_fast128_fstride(int L, int ch);
 int pscl_screening_available(const pscl_decode_params& P);  // scl128.hip
+int pscl_screening_fs_available(const pscl_decode_params& P);  // forced-bit screening (DL-SCL retries)
 hipError_t pscl_launch_decode128(const pscl_decode_params& P, int hist, int wpg, int64_t grid, int lds, hipStream_t s);
 int64_t pscl_decode_grid(const pscl_decode_params& P);
 int pscl_decode_wpg(const pscl_decode_params& P);

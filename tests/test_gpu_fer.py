@@ -71,11 +71,16 @@ def test_device_retry_loop_golden(golden):
         assert cd[5] == int((g[f"{tag}_attempts"] - 1).sum())
 
 
-@pytest.mark.parametrize("M,retries,ebno", [(4, 8, 3.0), (8, 8, 3.5), (2, 3, 3.0), (1, 70, 4.0)])
-def test_device_retry_loop_equals_host_ranking(M, retries, ebno):
-    """Device retry loop == numpy-ranked retries, frame by frame (3000 frames, ~30% failing)."""
+@pytest.mark.parametrize("M,retries,ebno,screen", [(4, 8, 3.0, "0"), (8, 8, 3.5, "0"), (2, 3, 3.0, "0"), (1, 70, 4.0, "0"),
+                                                   (4, 8, 2.0, "1"), (8, 8, 2.5, "1")])
+def test_device_retry_loop_equals_host_ranking(monkeypatch, M, retries, ebno, screen):
+    """Device retry loop == numpy-ranked retries, frame by frame (3000 frames, ~30% failing);
+    screen = 1: the retry decodes on the forced-bit screening instance plus the exact decode of
+    the entries it defers (PSCL_DL_SCREEN=1)."""
     from polar_code_amd.polar.polar import construct_info_set, encode
     from polar_code_amd.polar.crc import attach_crc
+
+    monkeypatch.setenv("PSCL_DL_SCREEN", screen)
 
     rng = np.random.default_rng(M * 100 + retries)
     info = construct_info_set(128, 64)
