@@ -101,6 +101,8 @@ struct pscl_handle {
     int32_t* d_rm_order = nullptr;    // [N] interleaver order
     DevBuf scratch[64];
     hipStream_t retry_stream[2] = {nullptr, nullptr};  // DL-SCL retry chains of the two chunk parities
+    hipStream_t side_stream[2] = {nullptr, nullptr};   // their deferred-entry work (PSCL_DL_SCREEN)
+    hipEvent_t ev_scr[2] = {nullptr, nullptr}, ev_def[2] = {nullptr, nullptr};
     hipEvent_t ev_base[2] = {nullptr, nullptr}, ev_retry[2] = {nullptr, nullptr}, ev_join = nullptr;
     int32_t* h_count = nullptr;          // pinned: failing-frame counts of the two chunk parities
     double* d_beta = nullptr;         // [K][K] DL-SCL flip metric (null = |L0|)
@@ -430,8 +432,13 @@ int pscl_destroy(pscl_handle* h) {
     }
     if (h->ev_join) hipEventDestroy(h->ev_join);
     if (h->h_count) hipHostFree(h->h_count);
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i) {
+        if (h->side_stream[i]) hipStreamSynchronize(h->side_stream[i]);
         if (h->retry_stream[i]) hipStreamDestroy(h->retry_stream[i]);
+        if (h->side_stream[i]) hipStreamDestroy(h->side_stream[i]);
+        if (h->ev_scr[i]) hipEventDestroy(h->ev_scr[i]);
+        if (h->ev_def[i]) hipEventDestroy(h->ev_def[i]);
+    }
     if (h->own_stream) hipStreamDestroy(h->own_stream);
     delete h;
     return PSCL_OK;
@@ -546,12 +553,14 @@ struct DlState {
     int32_t* nt;
     double* warm_metric;
     uint8_t* of;
-    int32_t *dcnt, *dlist;   // screening retry decodes: deferred entries ([NSEG * CSTRIDE] counts, [cap])
+    int32_t *dcnt, *dlist;   // screening retry decodes: deferred entries ([NSEG * CSTRIDE] counts, [NSEG][cap])
+    uint64_t* ob2;           // [cap][W] and [cap]: their exact decode's outputs (the main post pass reads
+    uint8_t* of2;            //   `of` concurrently, where the deferred mark must stay)
 };
 
 int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const double* d_llr, uint64_t* d_best,
                    uint8_t* d_flags, int32_t* d_attempts, int32_t* d_tried, int tried_stride, int64_t* d_cnt_dl,
-                   hipStream_t st) {
+                   hipStream_t st, hipStream_t side, hipEvent_t ev_s, hipEvent_t ev_d) {
     const int K = h->K, W = h->W;
     hipError_t e;
     const size_t bstride = (size_t)PSCL_DL_NSEG * PSCL_DL_CSTRIDE;
@@ -608,12 +617,15 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     H.warm_u = S.warm_u;
     if (pscl_decode_wpg(H) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
     int rc;
-    // screening retry decodes (PSCL_DL_SCREEN=1, measured below): the forced-bit screening
-    // instance, then the exact decode of the entries it could not certify (one bucket, no
-    // warm start), outputs at their entries
+    // screening retry decodes (PSCL_DL_SCREEN=1, measured in DESIGN.md §5.1b): the forced-bit
+    // screening instance decodes the round's entries and files the ones it cannot certify in
+    // bucket lists of their own (flags PSCL_DL_DEFERRED, which the post pass skips); on the side
+    // stream the exact kernel decodes those (warm-started, as every retry decode) and a second
+    // post pass handles them, overlapping the main post pass
     const bool dl_screen = getenv("PSCL_DL_SCREEN") && atoi(getenv("PSCL_DL_SCREEN")) == 1;
-    const bool scr = dl_screen && h->screen && S.dcnt && pscl_screening_fs_available(H);
+    const bool scr = dl_screen && h->screen && S.dcnt && S.ob2 && side && pscl_screening_fs_available(H);
     pscl_decode_params HA, HX;
+    pscl_post_params QD;
     if (scr) {
         HA = H;
         HA.apx = 1;
@@ -623,20 +635,36 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
         HX = H;
         HX.elist = S.dlist;
         HX.bcount = S.dcnt;
+        HX.best = S.ob2;
+        HX.flags = S.of2;
         HX.grid_cap = (int64_t)256 * 16 / (pscl_decode_wpg(HX) > 0 ? pscl_decode_wpg(HX) : 1);
+        QD = Q;
+        QD.init = 0;
+        QD.in_count = S.dcnt;
+        QD.in_list = S.dlist;
+        QD.ob = S.ob2;
+        QD.of = S.of2;
     }
     Q.init = 0;
     for (int r = 0; r < rounds; ++r) {  // no host round trips: the counts stay on the device
         H.elist = lists[r & 1];
         H.bcount = S.bcnt + (size_t)r * bstride;
         if (scr) {
+            if (r > 0) HIP_TRY(hipStreamWaitEvent(st, ev_d, 0));  // the previous round's deferred entries
             HIP_TRY(hipMemsetAsync(S.dcnt, 0, bstride * 4, st));
             HA.elist = H.elist;
             HA.bcount = H.bcount;
             if ((e = pscl_launch_decode(HA, 0, st)) != hipSuccess)
                 return fail(PSCL_EDEVICE, "screening retry decode: %s", hipGetErrorString(e));
-            if ((e = pscl_launch_decode(HX, 0, st)) != hipSuccess)
+            HIP_TRY(hipEventRecord(ev_s, st));
+            HIP_TRY(hipStreamWaitEvent(side, ev_s, 0));
+            if ((e = pscl_launch_decode(HX, 0, side)) != hipSuccess)
                 return fail(PSCL_EDEVICE, "exact retry re-decode: %s", hipGetErrorString(e));
+            QD.out_count = S.bcnt + (size_t)(r + 1) * bstride;
+            QD.out_list = lists[(r + 1) & 1];
+            if ((e = pscl_launch_dl_post(QD, A, side)) != hipSuccess)
+                return fail(PSCL_EDEVICE, "dl_post launch: %s", hipGetErrorString(e));
+            HIP_TRY(hipEventRecord(ev_d, side));
         } else if ((rc = launch_decode(h, H, 0, st))) {
             return rc;
         }
@@ -647,6 +675,7 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
         if ((e = pscl_launch_dl_post(Q, A, st)) != hipSuccess)
             return fail(PSCL_EDEVICE, "dl_post launch: %s", hipGetErrorString(e));
     }
+    if (scr && rounds > 0) HIP_TRY(hipStreamWaitEvent(st, ev_d, 0));
     return PSCL_OK;
 }
 
@@ -780,6 +809,11 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
             if (!h->ev_retry[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_retry[i], hipEventDisableTiming));
         }
         if (!h->ev_join) HIP_TRY(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+        for (int i = 0; i < 2; ++i) {
+            if (!h->side_stream[i]) HIP_TRY(hipStreamCreateWithFlags(&h->side_stream[i], hipStreamNonBlocking));
+            if (!h->ev_scr[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_scr[i], hipEventDisableTiming));
+            if (!h->ev_def[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_def[i], hipEventDisableTiming));
+        }
         if (!h->h_count) HIP_TRY(hipHostMalloc((void**)&h->h_count, 16, hipHostMallocDefault));
         // everything sized before any work is queued (an allocation synchronizes the device)
         const size_t NS = PSCL_DL_NSEG;
@@ -814,15 +848,22 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
             if ((rc = ensure(h, kLongRetryScratch, (size_t)pscl_decode_grid(H) * (size_t)H.long_block_bytes, &d_scr)))
                 return rc;
         }
-        for (int i = 0; i < nsplit; ++i) {  // chain i handles at most cap - cap / 2 entries when split
-            const size_t c = (size_t)(nsplit == 2 ? cap - cap / 2 : cap);
-            const size_t sz[12] = {(size_t)(rounds + 1) * NS * PSCL_DL_CSTRIDE * 4, NS * c * 4, NS * c * 4, c * 16, c * 4,
-                                   c * 2 * W * 8, c * NS * 8, c * 16, c * W * 8, c, NS * PSCL_DL_CSTRIDE * 4, c * 4};
-            void* q[12];
-            for (int k = 0; k < 12; ++k)  // (slots: set 0 12..21 and 8..9, set 1 40..51)
-                if ((rc = ensure(h, k < 10 ? (i ? 40 : 12) + k : (i ? 50 : 8) + k - 10, sz[k], &q[k]))) return rc;
+        for (int i = 0; i < nsplit; ++i) {
+            // chain 0 takes every entry of a call that does not split (fewer than 2 kMinSplit
+            // failing frames, which may still exceed half the chunk); chain 1 at most half
+            const size_t c = (size_t)(i == 0 ? cap : cap - cap / 2);
+            const size_t sz[14] = {(size_t)(rounds + 1) * NS * PSCL_DL_CSTRIDE * 4, NS * c * 4, NS * c * 4, c * 16, c * 4,
+                                   c * 2 * W * 8, c * NS * 8, c * 16, c * W * 8, c, NS * PSCL_DL_CSTRIDE * 4, NS * c * 4,
+                                   c * W * 8, c};
+            static const int slot[2][14] = {{12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 8, 9, 10, 11},
+                                            {40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 24, 29}};
+            void* q[14];
+            for (int k = 0; k < 14; ++k)
+                if ((rc = ensure(h, slot[i][k], sz[k], &q[k]))) return rc;
             S[i].dcnt = (int32_t*)q[10];
             S[i].dlist = (int32_t*)q[11];
+            S[i].ob2 = (uint64_t*)q[12];
+            S[i].of2 = (uint8_t*)q[13];
             S[i].bcnt = (int32_t*)q[0];
             S[i].list0 = (int32_t*)q[1];
             S[i].list1 = (int32_t*)q[2];
@@ -852,11 +893,15 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
         const int parts = (nsplit == 2 && A >= 2 * kMinSplit) ? 2 : 1;
         const int A0 = parts == 2 ? A - A / 2 : A;
         for (int k = 0; k < parts && A > 0; ++k) {
+            const int64_t nk = k ? A - A0 : A0, capk = k ? cap - cap / 2 : cap;  // (state sized above)
+            if (nk > capk) return fail(PSCL_EDEVICE, "retry chain %d: %lld entries exceed its state (%lld)", k,
+                                       (long long)nk, (long long)capk);
             HIP_TRY(hipStreamWaitEvent(h->retry_stream[k], h->ev_base[p], 0));
             DlState T = S[k];
             T.act = act[p] + (k ? A0 : 0);
             int r2 = dl_retry_chunk(h, T, k ? A - A0 : A0, rounds, d_llr, d_best, d_flags, d_attempts, d_tried,
-                                    tried_stride, d_ref ? d_counters_dl : nullptr, h->retry_stream[k]);
+                                    tried_stride, d_ref ? d_counters_dl : nullptr, h->retry_stream[k],
+                                    h->side_stream[k], h->ev_scr[k], h->ev_def[k]);
             if (r2) return r2;
         }
         if (parts == 2) {  // both chains done before the parity's indices are reused

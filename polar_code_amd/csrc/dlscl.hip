@@ -316,7 +316,7 @@ __global__ void __launch_bounds__(kPostWaves * 64) __attribute__((amdgpu_waves_p
         load_row4(Q.llr + (int64_t)bcast64((uint64_t)mf, hs) * (Q.rm_E ? Q.rm_E : N), Q.rm_E, Q.rm_src, N, hl, c);
         for (int it = 0; it < npair; ++it) {
             const int src = 2 * it + hs;  // this half's metadata lane
-            const bool valid = src < nval;
+            bool valid = src < nval;
             const int e = __shfl(me, src);
             const int64_t f = (int64_t)bcast64((uint64_t)mf, src);
             const uint64_t b0 = bcast64(mb0, src), b1 = bcast64(mb1, src);
@@ -329,6 +329,8 @@ __global__ void __launch_bounds__(kPostWaves * 64) __attribute__((amdgpu_waves_p
                 more = valid && Q.rounds > 0;
             } else {       // the attempt just decoded is the frame's latest (flip.py:123-136)
                 const uint32_t fl = (uint32_t)__shfl((int)mfl, src);
+                // (deferred by the screening retry decode: its exact decode and post pass follow)
+                if (fl == PSCL_DL_DEFERRED) valid = false;
                 if (valid && hl == 0) {
                     Q.best[f * W] = b0;
                     if (W > 1) Q.best[f * W + 1] = b1;

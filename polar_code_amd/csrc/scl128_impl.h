@@ -839,9 +839,14 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
         // APX: a frame with an uncertain ordering is handed to the exact re-decode
         const bool famb = APX && ((amb >> gbase) & (G == 64 ? ~0ULL : ((1ULL << (G & 63)) - 1))) != 0;
         if (APX && !PSCL_APX_ABLATE && famb && g == 0 && fvalid) {
-            const int slot = atomicAdd(P.amb_count, 1);
-            if (FS && P.amb_elist) P.amb_elist[slot] = (int32_t)f;
-            else P.amb_list[slot] = f;
+            if (FS && P.amb_elist) {  // DL-SCL retry round: into the entry's bucket, flagged deferred
+                const int fseg = pscl_bucket_of(fsafe, bpre);
+                const int slot = atomicAdd(P.amb_count + fseg * PSCL_DL_CSTRIDE, 1);
+                P.amb_elist[(int64_t)fseg * P.bcap + slot] = (int32_t)f;
+                P.flags[f] = PSCL_DL_DEFERRED;
+            } else {
+                P.amb_list[atomicAdd(P.amb_count, 1)] = f;
+            }
         }
         const bool active = path_lane && g < cnt && fvalid && !famb;
         const int64_t fo = P.out_by_row ? frow : f;  // output row

@@ -54,7 +54,8 @@ struct pscl_decode_params {
     int apx;
     int64_t* amb_list;           // [B] frame indices to re-decode exactly
     int32_t* amb_count;
-    int32_t* amb_elist;          // or (bucket-list launches): [B] entry ids, appended instead
+    int32_t* amb_elist;          // or (bucket-list launches): [NSEG][bcap] entry ids by bucket, appended
+                                 // instead (amb_count then [NSEG * CSTRIDE]); their flags PSCL_DL_DEFERRED
     int out_by_row;              // 1: outputs, reference words and counts at LLR row fidx[b]
     int64_t grid_cap;            // 0, or an upper bound on the workgroups of the launch (the
                                  // kernels stride over frames; a d_count launch of few frames)
@@ -80,6 +81,7 @@ struct pscl_decode_params {
 
 #define PSCL_DL_NSEG 8     // 16-phase segments of N = 128: warm-start buckets
 #define PSCL_DL_CSTRIDE 16 // int32 stride of the bucket counters (one 64-byte line each)
+#define PSCL_DL_DEFERRED 0xFF  /* flags of a retry entry the screening decode deferred (no valid flags value) */
 
 // frame index i of a bucket-list launch -> entry id (pre: bucket prefix counts, pre[0] = 0)
 __device__ __forceinline__ int pscl_bucket_of(int64_t i, const int* pre) {
