@@ -71,8 +71,9 @@ def test_device_retry_loop_golden(golden):
         assert cd[5] == int((g[f"{tag}_attempts"] - 1).sum())
 
 
+# (1.5 dB: most frames fail, more than half of the chunk goes to one retry chain)
 @pytest.mark.parametrize("M,retries,ebno,screen", [(4, 8, 3.0, "0"), (8, 8, 3.5, "0"), (2, 3, 3.0, "0"), (1, 70, 4.0, "0"),
-                                                   (4, 8, 2.0, "1"), (8, 8, 2.5, "1")])
+                                                   (4, 8, 1.5, "0"), (4, 8, 2.0, "1"), (8, 8, 2.5, "1")])
 def test_device_retry_loop_equals_host_ranking(monkeypatch, M, retries, ebno, screen):
     """Device retry loop == numpy-ranked retries, frame by frame (3000 frames, ~30% failing);
     screen = 1: the retry decodes on the forced-bit screening instance plus the exact decode of
@@ -91,7 +92,7 @@ def test_device_retry_loop_equals_host_ranking(monkeypatch, M, retries, ebno, sc
     for b in (beta, None):
         dev = decode_with_retries_device(llr, info, M, retries, crc="0x1864CFB", beta=b)
         host = decode_with_retries_batch(llr, info, M, retries, crc="0x1864CFB", beta=b)
-        assert 0.05 < (~dev["base_pass"]).mean() < 0.9
+        assert 0.05 < (~dev["base_pass"]).mean() < (0.97 if ebno < 2 else 0.9)
         np.testing.assert_array_equal(dev["tried"], host["tried"])
         np.testing.assert_array_equal(dev["attempts"], host["attempts"])
         np.testing.assert_array_equal(dev["best_bits"], host["best_bits"])
