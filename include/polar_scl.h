@@ -259,6 +259,23 @@ int pscl_set_screening(pscl_handle* h, int enable);
 int pscl_screening_count(pscl_handle* h, int64_t* count);
 
 /*
+ * Pipelined plain decodes (throughput mode; the reference's run_sweep frame loop,
+ * run_fer_sweep.py:41-191, over a stream of independent batches).  With enable = 1 a plain
+ * pscl_decode_device that takes the screening path leaves its exact re-decode of the deferred
+ * frames on a second stream, where it overlaps the caller's next decode: when the call returns,
+ * that re-decode is not yet ordered into the handle's stream.  Its input rows, output rows and
+ * counters stay in use until pscl_join, pscl_sync, any other entry point on the handle (each
+ * orders the pending re-decodes into the handle's stream first) or the second following
+ * pipelined decode.  Consecutive pipelined decodes must not write the same output buffers.
+ * Results are bit-identical to the non-pipelined form.  enable = 0 (default) restores
+ * stream-ordered completion.  Timing (pscl_timing_*) of a pipelined decode covers its
+ * screening launch only.
+ */
+int pscl_set_pipelined(pscl_handle* h, int enable);
+/* Order the pending pipelined re-decodes into the handle's stream (no host wait). */
+int pscl_join(pscl_handle* h);
+
+/*
  * Diagnostic: the metric tail log1p(exp(-|v|)) (scl.py:102-105) of n device values, evaluated
  * as the decode kernels do -- d_exact by the bit-exact glibc port, d_apx by the screening
  * decode's bounded-error form.  Device buffers, handle stream.

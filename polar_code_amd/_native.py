@@ -40,7 +40,7 @@ EXPORTS = (
     "pscl_memcpy_htod", "pscl_memcpy_dtoh", "pscl_memset_device", "pscl_timing_enable",
     "pscl_timing_read", "pscl_launch_info", "pscl_set_rate_match", "pscl_set_beta", "pscl_dlscl_device",
     "pscl_path_llrs_device", "pscl_uncoded_device", "pscl_simulate", "pscl_set_screening", "pscl_build_hash",
-    "pscl_screening_count", "pscl_softplus_tails_device",
+    "pscl_screening_count", "pscl_softplus_tails_device", "pscl_set_pipelined", "pscl_join",
 )
 
 _vp, _i32, _i64, _u64, _dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
@@ -95,6 +95,8 @@ def lib() -> C.CDLL:
         "pscl_abi_version": (C.c_int, []),
         "pscl_build_hash": (C.c_char_p, []),
         "pscl_screening_count": (C.c_int, [_vp, P(_i64)]),
+        "pscl_set_pipelined": (C.c_int, [_vp, C.c_int]),
+        "pscl_join": (C.c_int, [_vp]),
         "pscl_softplus_tails_device": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
         "pscl_device_count": (C.c_int, []),
         "pscl_create": (C.c_int, [P(_vp), C.c_int, C.c_int, P(_i32), C.c_int, C.c_int, _u64]),
@@ -353,6 +355,15 @@ class Decoder:
             mem.upload(d_v, v)
             check(lib().pscl_softplus_tails_device(self._h, d_v, v.size, d_e, d_a))
             return mem.download(d_e, v.nbytes, np.float64), mem.download(d_a, v.nbytes, np.float64)
+
+    def set_pipelined(self, on: bool = True) -> None:
+        """Throughput mode for streams of plain decodes (include/polar_scl.h): a screening
+        decode's exact re-decode overlaps the next decode; join() / sync() order it back."""
+        check(lib().pscl_set_pipelined(self._h, 1 if on else 0))
+
+    def join(self) -> None:
+        """Order pending pipelined re-decodes into the handle's stream (no host wait)."""
+        check(lib().pscl_join(self._h))
 
     def set_screening(self, on: bool = True) -> None:
         """Screening decode for plain decodes (default on; include/polar_scl.h)."""

@@ -112,17 +112,38 @@ struct pscl_handle {
     int epi_words = 0;
     bool timing = false;
     bool screen = true;               // screening decode for plain decodes (pscl_set_screening)
-    bool screened = false;            // a screening decode ran (scratch 36 holds its count)
+    bool screened = false;            // a screening decode ran (scratch screened_slot holds its count)
+    int screened_slot = 36;
+    // pipelined plain decodes (pscl_set_pipelined): a screening decode's exact re-decode runs on
+    // pipe_stream and overlaps the caller's next decode; the two alternate scratch parities
+    // (deferred-frame count + list: slots 36/37 and 54/55), and every other entry point, and
+    // pscl_join, order the pending re-decodes back into the handle's stream
+    bool pipelined = false;
+    hipStream_t pipe_stream = nullptr;
+    hipEvent_t ev_pscr[2] = {nullptr, nullptr}, ev_px[2] = {nullptr, nullptr};
+    bool px_pending[2] = {false, false};
+    int pipe_par = 0;
+    // pipelined pscl_dlscl_device: a call's retry chains (and its DL counters) stay on the retry
+    // streams and overlap the next call's baseline decode; the calls alternate the compaction
+    // parity (act/cnt), ev_dl[p] marks the end of parity p's chains
+    hipEvent_t ev_dl[2] = {nullptr, nullptr};
+    bool dl_pending[2] = {false, false};
+    int dl_par = 0;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
 };
 
 namespace {
 
+void quiesce(pscl_handle* h);
+
 int ensure(pscl_handle* h, int slot, size_t bytes, void** out) {
     DevBuf& b = h->scratch[slot];
     if (b.n < bytes) {
-        if (b.p) hipFree(b.p);
+        if (b.p) {
+            quiesce(h);  // (pipelined work may still read it)
+            hipFree(b.p);
+        }
         b.p = nullptr;
         b.n = 0;
         size_t want = bytes + bytes / 2;  // geometric growth: varying batch sizes settle quickly
@@ -137,6 +158,47 @@ int ensure(pscl_handle* h, int slot, size_t bytes, void** out) {
 int set_device(pscl_handle* h) {
     HIP_TRY(hipSetDevice(h->device));
     return PSCL_OK;
+}
+
+// the handle's stream waits for the pending pipelined work (no host wait): what = 1 the plain
+// decodes' re-decodes, 2 the DL-SCL retry chains, 3 both
+int join_pipe(pscl_handle* h, int what = 3) {
+    for (int p = 0; p < 2; ++p) {
+        if ((what & 1) && h->px_pending[p]) {
+            HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_px[p], 0));
+            h->px_pending[p] = false;
+        }
+        if ((what & 2) && h->dl_pending[p]) {
+            HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_dl[p], 0));
+            h->dl_pending[p] = false;
+        }
+    }
+    return PSCL_OK;
+}
+
+// every stream the handle's pipelined work may still run on, drained (before a scratch buffer is
+// freed and regrown)
+void quiesce(pscl_handle* h) {
+    if (h->pipe_stream) hipStreamSynchronize(h->pipe_stream);
+    for (int i = 0; i < 2; ++i) {
+        if (h->retry_stream[i]) hipStreamSynchronize(h->retry_stream[i]);
+        if (h->side_stream[i]) hipStreamSynchronize(h->side_stream[i]);
+    }
+}
+
+// a stream of the highest priority: latency-bound chains (retry rounds, deferred re-decodes)
+// take workgroup slots ahead of a concurrent throughput-bound baseline decode
+hipError_t create_priority_stream(hipStream_t* s) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+    static const bool plain = getenv("PSCL_PRIO") && atoi(getenv("PSCL_PRIO")) == 0;  // tuning override
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, plain ? least : greatest);
+}
+
+// entry points other than a pipelined plain decode: device, then the pending re-decodes
+int enter(pscl_handle* h) {
+    const int rc = set_device(h);
+    return rc ? rc : join_pipe(h);
 }
 
 void fill_decode_params(const pscl_handle* h, pscl_decode_params& P, int hist) {
@@ -162,7 +224,9 @@ void fill_decode_params(const pscl_handle* h, pscl_decode_params& P, int hist) {
 
 // scr_slot: the scratch buffer of a long-code decode (decodes that may run concurrently on
 // different streams need different slots)
-int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStream_t st = nullptr, int scr_slot = 38) {
+// pipe: the caller is a plain pscl_decode_device on a pipelined handle (see pscl_handle)
+int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStream_t st = nullptr, int scr_slot = 38,
+                  bool pipe = false) {
     if (!st) st = h->stream;
     pscl_decode_params P = P0;
     if (P.long_mode) {  // global scratch of every workgroup in flight (scl_long.hip)
@@ -189,11 +253,33 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
     const bool screen = h->screen && P.fast && !hist && !P.metrics && !P.cands && !P.force && !P.sc_hard && !P.fidx &&
                         !P.d_count && pscl_screening_available(P);
     hipError_t err;
+    if (!(screen && pipe)) {
+        const int rc = join_pipe(h, 1);
+        if (rc) return rc;
+    }
     if (screen) {
         void *d_cnt, *d_list;
         int rc;
-        if ((rc = ensure(h, 36, 4, &d_cnt))) return rc;
-        if ((rc = ensure(h, 37, (size_t)P.B * 8, &d_list))) return rc;
+        // pipelined: parity p's list may still be read by the re-decode two calls back
+        const int p = pipe ? h->pipe_par : 0;
+        const int s_cnt = p ? 54 : 36, s_list = p ? 55 : 37;
+        if (pipe) {
+            if (!h->pipe_stream) {
+                HIP_TRY(create_priority_stream(&h->pipe_stream));
+                for (int i = 0; i < 2; ++i) {
+                    HIP_TRY(hipEventCreateWithFlags(&h->ev_pscr[i], hipEventDisableTiming));
+                    HIP_TRY(hipEventCreateWithFlags(&h->ev_px[i], hipEventDisableTiming));
+                }
+            }
+            if (h->px_pending[p]) {
+                if (h->scratch[s_list].n < (size_t)P.B * 8) HIP_TRY(hipEventSynchronize(h->ev_px[p]));  // (regrown)
+                HIP_TRY(hipStreamWaitEvent(st, h->ev_px[p], 0));
+                h->px_pending[p] = false;
+            }
+            h->pipe_par ^= 1;
+        }
+        if ((rc = ensure(h, s_cnt, 4, &d_cnt))) return rc;
+        if ((rc = ensure(h, s_list, (size_t)P.B * 8, &d_list))) return rc;
         HIP_TRY(hipMemsetAsync(d_cnt, 0, 4, st));
         pscl_decode_params S = P;
         S.apx = 1;
@@ -202,6 +288,7 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
         S.amb_count = (int32_t*)d_cnt;
         err = pscl_launch_decode(S, hist, st);
         h->screened = true;
+        h->screened_slot = s_cnt;
 #ifdef PSCL_APX_ABLATE
         // PSCL_DIAG_SCREEN_ONLY=1: timing diagnostics of the screening pass alone (variant
         // builds only, tools/build_variant.py -DPSCL_APX_ABLATE=..); deferred frames stay undecoded
@@ -217,6 +304,18 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
             // few frames: one resident set of workgroups (4 waves/SIMD on 256 CUs), striding
             // over the listed frames, instead of a grid sized for the whole batch
             X.grid_cap = (int64_t)256 * 16 / (pscl_decode_wpg(X) > 0 ? pscl_decode_wpg(X) : 1);
+            if (pipe) {
+                // the re-decode overlaps the caller's next decode; the timed interval is the
+                // screening launch alone
+                if (h->timing) HIP_TRY(hipEventRecord(e1, st));
+                HIP_TRY(hipEventRecord(h->ev_pscr[p], st));
+                HIP_TRY(hipStreamWaitEvent(h->pipe_stream, h->ev_pscr[p], 0));
+                err = pscl_launch_decode(X, hist, h->pipe_stream);
+                if (err != hipSuccess) return fail(PSCL_EDEVICE, "decode kernel launch: %s", hipGetErrorString(err));
+                HIP_TRY(hipEventRecord(h->ev_px[p], h->pipe_stream));
+                h->px_pending[p] = true;
+                return PSCL_OK;
+            }
             err = pscl_launch_decode(X, hist, st);
         }
     } else {
@@ -410,6 +509,7 @@ int pscl_destroy(pscl_handle* h) {
     if (!h) return PSCL_OK;
     hipSetDevice(h->device);
     if (h->own_stream) hipStreamSynchronize(h->own_stream);
+    if (h->pipe_stream) hipStreamSynchronize(h->pipe_stream);
     for (auto& b : h->scratch)
         if (b.p) hipFree(b.p);
     for (auto e : h->ev_pool) hipEventDestroy(e);
@@ -439,6 +539,12 @@ int pscl_destroy(pscl_handle* h) {
         if (h->ev_scr[i]) hipEventDestroy(h->ev_scr[i]);
         if (h->ev_def[i]) hipEventDestroy(h->ev_def[i]);
     }
+    for (int i = 0; i < 2; ++i) {
+        if (h->ev_dl[i]) hipEventDestroy(h->ev_dl[i]);
+        if (h->ev_pscr[i]) hipEventDestroy(h->ev_pscr[i]);
+        if (h->ev_px[i]) hipEventDestroy(h->ev_px[i]);
+    }
+    if (h->pipe_stream) hipStreamDestroy(h->pipe_stream);
     if (h->own_stream) hipStreamDestroy(h->own_stream);
     delete h;
     return PSCL_OK;
@@ -446,6 +552,8 @@ int pscl_destroy(pscl_handle* h) {
 
 int pscl_set_stream(pscl_handle* h, void* s) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    int rc = join_pipe(h);  // pending re-decodes ordered before the old stream's later work
+    if (rc) return rc;
     h->stream = s ? (hipStream_t)s : h->own_stream;
     return PSCL_OK;
 }
@@ -455,6 +563,8 @@ void* pscl_get_stream(pscl_handle* h) { return h ? (void*)h->stream : nullptr; }
 int pscl_sync(pscl_handle* h) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
     HIP_TRY(hipSetDevice(h->device));
+    int rc = join_pipe(h);
+    if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(h->stream));
     return PSCL_OK;
 }
@@ -485,7 +595,24 @@ int pscl_decode_device(pscl_handle* h, const double* d_llr, int64_t B, const uin
     P.k_payload = k_payload;
     P.counters = d_counters;
     if (pscl_decode_wpg(P) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
-    return launch_decode(h, P, hist);
+    if (!h->pipelined && (rc = join_pipe(h))) return rc;
+    return launch_decode(h, P, hist, nullptr, 38, h->pipelined);
+}
+
+int pscl_join(pscl_handle* h) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    int rc = set_device(h);
+    if (rc) return rc;
+    return join_pipe(h);
+}
+
+int pscl_set_pipelined(pscl_handle* h, int enable) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    int rc = set_device(h);
+    if (rc) return rc;
+    if ((rc = join_pipe(h))) return rc;
+    h->pipelined = enable != 0;
+    return PSCL_OK;
 }
 
 int pscl_path_llrs_device(pscl_handle* h, const double* d_llr, int64_t B, const uint64_t* d_bits, double* d_out) {
@@ -495,7 +622,7 @@ int pscl_path_llrs_device(pscl_handle* h, const double* d_llr, int64_t B, const 
     if (!d_llr || !d_bits || !d_out) return fail(PSCL_EINVAL, "d_llr, d_bits and d_out are required");
     if (h->N > PSCL_FAST_N) return fail(PSCL_EUNSUP, "decision-LLR replay supports N <= %d", PSCL_FAST_N);
     if (B > INT32_MAX) return fail(PSCL_EUNSUP, "B exceeds 2^31-1");
-    int rc = set_device(h);
+    int rc = enter(h);
     if (rc) return rc;
     void *d_cnt, *d_rows;
     if ((rc = ensure(h, 25, 8, &d_cnt))) return rc;
@@ -528,7 +655,7 @@ int pscl_path_llrs_device(pscl_handle* h, const double* d_llr, int64_t B, const 
 
 int pscl_set_beta(pscl_handle* h, const double* beta) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
-    int rc = set_device(h);
+    int rc = enter(h);
     if (rc) return rc;
     if (!beta) {
         if (h->d_beta) HIP_TRY(hipFree(h->d_beta));
@@ -773,6 +900,18 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
     if (B > INT32_MAX) return fail(PSCL_EUNSUP, "B exceeds 2^31-1");
     int rc = set_device(h);
     if (rc) return rc;
+    // pipelined (pscl_set_pipelined, one chunk): this call's retry chains are left running on the
+    // retry streams, where they overlap the next call's baseline decode
+    const bool dl_pipe = h->pipelined && rounds > 0 && !getenv("PSCL_DL_CHUNKS");
+    if ((rc = join_pipe(h, dl_pipe ? 1 : 3))) return rc;
+    const int pbase = dl_pipe ? h->dl_par : 0;  // compaction parity of chunk 0
+    if (dl_pipe && h->dl_pending[pbase]) {
+        // the chains of the call two back (same parity) may still read their compaction output and
+        // write their call's outputs: they end before this call starts (the contract of
+        // pscl_set_pipelined: a call's buffers are free again at the second following call)
+        HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_dl[pbase], 0));
+        h->dl_pending[pbase] = false;
+    }
     const int K = h->K, W = h->W;
     const int64_t row = h->rm_E ? h->rm_E : h->N;
     hipStream_t s = h->stream;
@@ -803,21 +942,23 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
     int64_t* act[2] = {};      // their frame indices
     if (rounds > 0) {
         for (int i = 0; i < 2; ++i)
-            if (!h->retry_stream[i]) HIP_TRY(hipStreamCreateWithFlags(&h->retry_stream[i], hipStreamNonBlocking));
+            if (!h->retry_stream[i]) HIP_TRY(create_priority_stream(&h->retry_stream[i]));
         for (int i = 0; i < 2; ++i) {
             if (!h->ev_base[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_base[i], hipEventDisableTiming));
             if (!h->ev_retry[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_retry[i], hipEventDisableTiming));
         }
         if (!h->ev_join) HIP_TRY(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+        for (int i = 0; i < 2; ++i)
+            if (!h->ev_dl[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_dl[i], hipEventDisableTiming));
         for (int i = 0; i < 2; ++i) {
-            if (!h->side_stream[i]) HIP_TRY(hipStreamCreateWithFlags(&h->side_stream[i], hipStreamNonBlocking));
+            if (!h->side_stream[i]) HIP_TRY(create_priority_stream(&h->side_stream[i]));
             if (!h->ev_scr[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_scr[i], hipEventDisableTiming));
             if (!h->ev_def[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_def[i], hipEventDisableTiming));
         }
         if (!h->h_count) HIP_TRY(hipHostMalloc((void**)&h->h_count, 16, hipHostMallocDefault));
         // everything sized before any work is queued (an allocation synchronizes the device)
         const size_t NS = PSCL_DL_NSEG;
-        for (int i = 0; i < (nch >= 2 ? 2 : 1); ++i) {
+        for (int i = 0; i < (nch >= 2 || dl_pipe ? 2 : 1); ++i) {
             void *pc, *pa;
             if ((rc = ensure(h, 22 + 5 * i, 4, &pc)) || (rc = ensure(h, 23 + 5 * i, (size_t)cap * 8, &pa))) return rc;
             cnt[i] = (int32_t*)pc;
@@ -877,7 +1018,7 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
         }
     }
     auto retries_of = [&](int64_t c) -> int {
-        const int p = (int)(c & 1);
+        const int p = (int)((c + pbase) & 1);
         HIP_TRY(hipEventSynchronize(h->ev_base[p]));
         const int A = h->h_count[p];
         if (h->N > PSCL_FAST_N) {
@@ -926,7 +1067,7 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
         if (pscl_decode_wpg(P) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
         if ((rc = launch_decode(h, P, 0))) return rc;
         if (rounds > 0) {
-            const int p = (int)(c & 1);
+            const int p = (int)((c + pbase) & 1);
             if (c >= 2) HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[p], 0));  // the parity's indices free again
             HIP_TRY(hipMemsetAsync(cnt[p], 0, 4, s));
             if ((e = pscl_launch_dl_compact(d_flags + c0, nc, c0, act[p], nullptr, cnt[p], s)) != hipSuccess)
@@ -938,7 +1079,18 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
     }
     if (rounds > 0) {
         if ((rc = retries_of(nch - 1))) return rc;
-        HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[(nch - 1) & 1], 0));  // chains run in order on stream 0
+        if (dl_pipe) {  // the DL counters follow the chains on retry stream 0; pscl_join orders them back
+            const int p = pbase;
+            if (d_ref) {
+                e = pscl_launch_dl_count(d_best, d_flags, d_ref, B, W, k_payload, d_counters_dl, h->retry_stream[0]);
+                if (e != hipSuccess) return fail(PSCL_EDEVICE, "dl_count launch: %s", hipGetErrorString(e));
+            }
+            HIP_TRY(hipEventRecord(h->ev_dl[p], h->retry_stream[0]));
+            h->dl_pending[p] = true;
+            h->dl_par ^= 1;
+            return PSCL_OK;
+        }
+        HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[(nch - 1 + pbase) & 1], 0));  // chains run in order on stream 0
     }
     if (d_ref) {
         e = pscl_launch_dl_count(d_best, d_flags, d_ref, B, W, k_payload, d_counters_dl, s);
@@ -971,7 +1123,7 @@ static int decode_host(pscl_handle* h, const double* llr, int64_t B, const int8_
             }
         }
     }
-    int rc = set_device(h);
+    int rc = enter(h);
     if (rc) return rc;
     void *d_llr, *d_force = nullptr, *d_np, *d_best, *d_flags, *d_met = nullptr, *d_cands = nullptr, *d_illr = nullptr;
     const size_t sz_llr = (size_t)B * (h->rm_E ? h->rm_E : N) * 8;
@@ -1051,7 +1203,7 @@ int pscl_uncoded_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, doubl
     if (B == 0) return PSCL_OK;
     if (!d_counters) return fail(PSCL_EINVAL, "d_counters is NULL");
     if (k_payload < 0 || k_payload > PSCL_MAX_N) return fail(PSCL_EINVAL, "k_payload out of range");
-    int rc = set_device(h);
+    int rc = enter(h);
     if (rc) return rc;
     pscl_channel_params P;
     memset(&P, 0, sizeof(P));
@@ -1075,7 +1227,7 @@ int pscl_simulate(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno
     if (B < 0 || frame0 < 0) return fail(PSCL_EINVAL, "B and frame0 must be >= 0");
     memset(counters, 0, sizeof(int64_t) * 3 * PSCL_NCOUNT);
     if (B == 0) return PSCL_OK;
-    int rc = set_device(h);
+    int rc = enter(h);
     if (rc) return rc;
     // chunks of at most 2^20 frames through handle scratch: N * 8 bytes of LLRs per frame
     // (1 KiB at N = 128: about 1 GiB per 2^20-frame chunk)
@@ -1115,7 +1267,7 @@ int pscl_channel_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, doubl
     if (!(rate > 0)) return fail(PSCL_EINVAL, "rate must be positive");
     if (k_payload + h->crc_deg != h->K || k_payload < 0)
         return fail(PSCL_EINVAL, "k_payload (%d) + crc degree (%d) must equal K (%d)", k_payload, h->crc_deg, h->K);
-    int rc = set_device(h);
+    int rc = enter(h);
     if (rc) return rc;
     pscl_channel_params P;
     memset(&P, 0, sizeof(P));
@@ -1157,7 +1309,7 @@ int pscl_set_rate_match(pscl_handle* h, int E) {
     const int nb = (N + 31) / 32;
     for (int k = 0; k < N; ++k) order[(size_t)k] = N >= 32 ? (k % 32) * nb + k / 32 : k;
     for (int k = 0; k < N; ++k) src[(size_t)order[(size_t)k]] = k;
-    int rc = set_device(h);
+    int rc = enter(h);
     if (rc) return rc;
     if (!h->d_rm_src) HIP_TRY(hipMalloc(&h->d_rm_src, (size_t)N * 4));
     if (!h->d_rm_order) HIP_TRY(hipMalloc(&h->d_rm_order, (size_t)N * 4));
@@ -1169,7 +1321,7 @@ int pscl_set_rate_match(pscl_handle* h, int E) {
 
 int pscl_device_alloc(pscl_handle* h, void** d_ptr, int64_t bytes) {
     if (!h || !d_ptr || bytes < 0) return fail(PSCL_EINVAL, "bad arguments");
-    int rc = set_device(h);
+    int rc = enter(h);
     if (rc) return rc;
     HIP_TRY(hipMalloc(d_ptr, (size_t)(bytes > 0 ? bytes : 1)));
     return PSCL_OK;
@@ -1177,12 +1329,15 @@ int pscl_device_alloc(pscl_handle* h, void** d_ptr, int64_t bytes) {
 
 int pscl_device_free(pscl_handle* h, void* d_ptr) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    if (h->pipe_stream) HIP_TRY(hipStreamSynchronize(h->pipe_stream));  // (a pending re-decode's buffers)
     if (d_ptr) HIP_TRY(hipFree(d_ptr));
     return PSCL_OK;
 }
 
 int pscl_memcpy_htod(pscl_handle* h, void* d_dst, const void* src, int64_t bytes) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    int rc = enter(h);
+    if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(d_dst, src, (size_t)bytes, hipMemcpyHostToDevice, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     return PSCL_OK;
@@ -1190,6 +1345,8 @@ int pscl_memcpy_htod(pscl_handle* h, void* d_dst, const void* src, int64_t bytes
 
 int pscl_memcpy_dtoh(pscl_handle* h, void* dst, const void* d_src, int64_t bytes) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    int rc = enter(h);
+    if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(dst, d_src, (size_t)bytes, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     return PSCL_OK;
@@ -1197,6 +1354,8 @@ int pscl_memcpy_dtoh(pscl_handle* h, void* dst, const void* d_src, int64_t bytes
 
 int pscl_memset_device(pscl_handle* h, void* d_dst, int value, int64_t bytes) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    int rc = enter(h);
+    if (rc) return rc;
     HIP_TRY(hipMemsetAsync(d_dst, value, (size_t)bytes, h->stream));
     return PSCL_OK;
 }
@@ -1210,11 +1369,12 @@ int pscl_set_screening(pscl_handle* h, int enable) {
 int pscl_screening_count(pscl_handle* h, int64_t* count) {
     if (!h || !count) return fail(PSCL_EINVAL, "bad arguments");
     *count = 0;
-    if (!h->screened || !h->scratch[36].p) return PSCL_OK;
-    HIP_TRY(hipSetDevice(h->device));
+    if (!h->screened || !h->scratch[h->screened_slot].p) return PSCL_OK;
+    int rc = enter(h);
+    if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(h->stream));
     int32_t c = 0;
-    HIP_TRY(hipMemcpy(&c, h->scratch[36].p, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&c, h->scratch[h->screened_slot].p, 4, hipMemcpyDeviceToHost));
     *count = c;
     return PSCL_OK;
 }
@@ -1224,7 +1384,7 @@ int pscl_softplus_tails_device(pscl_handle* h, const double* d_v, int64_t n, dou
     if (n < 0) return fail(PSCL_EINVAL, "n must be >= 0");
     if (n == 0) return PSCL_OK;
     if (!d_v || !d_exact || !d_apx) return fail(PSCL_EINVAL, "d_v, d_exact and d_apx are required");
-    int rc = set_device(h);
+    int rc = enter(h);
     if (rc) return rc;
     hipError_t e = pscl_launch_softplus_tails(d_v, n, h->d_exp_table, d_exact, d_apx, h->stream);
     if (e != hipSuccess) return fail(PSCL_EDEVICE, "softplus tails launch: %s", hipGetErrorString(e));
@@ -1240,6 +1400,8 @@ int pscl_timing_enable(pscl_handle* h, int enable) {
 
 int pscl_timing_read(pscl_handle* h, int64_t* launches, double* total_ms) {
     if (!h || !launches || !total_ms) return fail(PSCL_EINVAL, "bad arguments");
+    int rc = enter(h);
+    if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(h->stream));
     double tot = 0.0;
     for (size_t i = 0; i + 1 < h->ev_used; i += 2) {

@@ -31,6 +31,7 @@
 // values at ~1/15 of a decode, and the decode itself keeps the occupancy of the plain kernel.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "polar_scl.h"
 #include "scl_device.h"
@@ -687,7 +688,9 @@ hipError_t pscl_launch_dl_post(const pscl_post_params& Q, int64_t entries, hipSt
     if (entries <= 0) return hipSuccess;
     // workgroups of 8 wavefronts (16 entries in flight), at most two resident per CU
     int64_t grid = (entries + kPostWaves * 8 - 1) / (kPostWaves * 8);
-    if (grid > PSCL_POST_GRID) grid = PSCL_POST_GRID;
+    static const int64_t cap_env = getenv("PSCL_POST_GRID") ? atol(getenv("PSCL_POST_GRID")) : 0;  // tuning override
+    const int64_t gcap = cap_env >= 16 && cap_env <= 4096 ? cap_env : PSCL_POST_GRID;
+    if (grid > gcap) grid = gcap;
     const int beta_lds = PSCL_POST_BETA_LDS && Q.beta && (size_t)Q.K * Q.K * 8 <= 32 * 1024;  // (LDS <= 64 KB)
     const size_t lds = beta_lds ? (size_t)Q.K * Q.K * 8 : 0;
     const dim3 g((unsigned)grid), b(kPostWaves * 64);

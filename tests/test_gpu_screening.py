@@ -140,6 +140,43 @@ def test_screening_device_counters_equal_exact():
     assert out[True][2][0] == B
 
 
+@pytest.mark.parametrize("M", [4, 8])
+def test_pipelined_decodes_equal_stream_ordered(M):
+    """pscl_set_pipelined: a stream of plain decodes whose exact re-decodes overlap the next
+    call (alternate output buffers, as bench.py steps), then join: every batch's best bits and
+    flags, and the accumulated counters, equal the stream-ordered decodes'; an entry point other
+    than a pipelined decode (memcpy) orders the pending re-decodes first."""
+    info = construct_info_set(128, 64)
+    B, nb = 60_000, 5
+    res = {}
+    for pipe in (True, False):
+        dec = _native.Decoder(128, info, M, POLY)
+        dec.set_pipelined(pipe)
+        with _native.DeviceArena(dec) as mem:
+            d_llr = [mem.alloc(B * 128 * 8) for _ in range(nb)]
+            d_msg = [mem.alloc(B * 8) for _ in range(nb)]
+            d_out = [(mem.alloc(B * 8), mem.alloc(B)) for _ in range(nb)]
+            d_cnt = mem.alloc(8 * 8)
+            mem.memset(d_cnt, 0, 64)
+            for i in range(nb):
+                dec.channel_device(11, 30 + i, 1.5 + 0.5 * i, 0.5, 40, i * B, B, d_llr[i], d_msg[i])
+            # ties in the last batch: many deferred frames
+            llr = mem.download(d_llr[nb - 1], B * 128 * 8, np.float64).reshape(B, 128)
+            mem.upload(d_llr[nb - 1], np.round(llr / 4.0))
+            for i in range(nb):
+                dec.decode_device(d_llr[i], B, d_best=d_out[i][0], d_flags=d_out[i][1], d_ref=d_msg[i],
+                                  k_payload=40, d_counters=d_cnt)
+            res[pipe] = ([(mem.download(b, B * 8, np.uint64), mem.download(f, B, np.uint8)) for b, f in d_out],
+                         mem.download(d_cnt, 64, np.int64))
+            assert dec.screening_count() > 0
+        dec.close()
+    for i in range(nb):
+        np.testing.assert_array_equal(res[True][0][i][0], res[False][0][i][0], err_msg=f"best, batch {i}")
+        np.testing.assert_array_equal(res[True][0][i][1], res[False][0][i][1], err_msg=f"flags, batch {i}")
+    np.testing.assert_array_equal(res[True][1], res[False][1], err_msg="counters")
+    assert res[True][1][0] == nb * B
+
+
 @pytest.mark.parametrize("M", [1, 2, 4, 8])
 def test_screening_boundary_ties_every_frame(M):
     """Crafted worst cases for the screening pass: exactly zero leaf LLRs (every child pays
