@@ -277,6 +277,7 @@ def run_workload(ctx: Ctx, *, L: int, E: int, retries: int, beta, B: int, steps:
 
     for i in range(warmup):
         step(i % nbuf)
+    dec.join()  # (pipelined: the last warmup call's retry rounds, enqueued and finished here)
     torch.cuda.synchronize(dev)
     counters.zero_()
     counters_dl.zero_()
@@ -286,6 +287,7 @@ def run_workload(ctx: Ctx, *, L: int, E: int, retries: int, beta, B: int, steps:
     t0 = time.perf_counter()
     for i in range(steps):
         step(i % nbuf)
+    dec.join()  # the last step's pending work (pipelined: its retry rounds) inside the timed region
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     ctx.barrier()

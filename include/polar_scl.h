@@ -267,6 +267,9 @@ int pscl_screening_count(pscl_handle* h, int64_t* count);
  * counters stay in use until pscl_join, pscl_sync, any other entry point on the handle (each
  * orders the pending re-decodes into the handle's stream first) or the second following
  * pipelined decode.  Consecutive pipelined decodes must not write the same output buffers.
+ * pscl_dlscl_device (one chunk) likewise: a pipelined call enqueues its baseline decode, then the
+ * previous pipelined call's retry rounds and DL counters (on high-priority streams, beside this
+ * call's baseline), and leaves its own rounds to the next call or the join.
  * Results are bit-identical to the non-pipelined form.  enable = 0 (default) restores
  * stream-ordered completion.  Timing (pscl_timing_*) of a pipelined decode covers its
  * screening launch only.

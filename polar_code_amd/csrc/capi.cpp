@@ -80,6 +80,24 @@ struct DevBuf {
 
 }  // namespace
 
+// the arguments of a pscl_dlscl_device call (kept for a pipelined call's deferred chains)
+struct pscl_dl_call {
+    const double* d_llr = nullptr;
+    int64_t B = 0;
+    int rounds = 0;
+    uint64_t* d_best = nullptr;
+    uint8_t* d_flags = nullptr;
+    int32_t* d_attempts = nullptr;
+    int32_t* d_tried = nullptr;
+    int tried_stride = 0;
+    const uint64_t* d_ref = nullptr;
+    int k_payload = 0;
+    int64_t* d_counters_dl = nullptr;
+    int64_t nch = 1, cap = 0;
+    int nsplit = 2, pbase = 0;
+    bool pipe = false;
+};
+
 struct pscl_handle {
     int device = 0;
     int N = 0, n = 0, K = 0, L = 0, W = 1, crc_deg = 0;
@@ -129,6 +147,8 @@ struct pscl_handle {
     hipEvent_t ev_dl[2] = {nullptr, nullptr};
     bool dl_pending[2] = {false, false};
     int dl_par = 0;
+    pscl_dl_call dl_defer;            // the last pipelined call, its chains not yet enqueued
+    bool dl_defer_valid = false;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
 };
@@ -162,7 +182,13 @@ int set_device(pscl_handle* h) {
 
 // the handle's stream waits for the pending pipelined work (no host wait): what = 1 the plain
 // decodes' re-decodes, 2 the DL-SCL retry chains, 3 both
+int dl_enqueue_deferred(pscl_handle* h);
+
 int join_pipe(pscl_handle* h, int what = 3) {
+    if (what & 2) {  // a pipelined DL-SCL call's chains, enqueued first
+        const int rc = dl_enqueue_deferred(h);
+        if (rc) return rc;
+    }
     for (int p = 0; p < 2; ++p) {
         if ((what & 1) && h->px_pending[p]) {
             HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_px[p], 0));
@@ -186,13 +212,15 @@ void quiesce(pscl_handle* h) {
     }
 }
 
-// a stream of the highest priority: latency-bound chains (retry rounds, deferred re-decodes)
-// take workgroup slots ahead of a concurrent throughput-bound baseline decode
-hipError_t create_priority_stream(hipStream_t* s) {
+// a side stream; on a pipelined handle of the highest priority: latency-bound chains (retry
+// rounds, deferred re-decodes) take workgroup slots ahead of the next call's throughput-bound
+// baseline decode (measured, config 4 pipelined: 3.55 ms against 4.0 at equal priority).  Not
+// otherwise: the FER sweep's two concurrent handles lose from it (4.0 dB point 16.6 -> 25.8 ms)
+hipError_t create_priority_stream(pscl_handle* h, hipStream_t* s) {
     int least = 0, greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = least = 0;
     static const bool plain = getenv("PSCL_PRIO") && atoi(getenv("PSCL_PRIO")) == 0;  // tuning override
-    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, plain ? least : greatest);
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, h->pipelined && !plain ? greatest : least);
 }
 
 // entry points other than a pipelined plain decode: device, then the pending re-decodes
@@ -265,7 +293,7 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
         const int s_cnt = p ? 54 : 36, s_list = p ? 55 : 37;
         if (pipe) {
             if (!h->pipe_stream) {
-                HIP_TRY(create_priority_stream(&h->pipe_stream));
+                HIP_TRY(create_priority_stream(h, &h->pipe_stream));
                 for (int i = 0; i < 2; ++i) {
                     HIP_TRY(hipEventCreateWithFlags(&h->ev_pscr[i], hipEventDisableTiming));
                     HIP_TRY(hipEventCreateWithFlags(&h->ev_px[i], hipEventDisableTiming));
@@ -508,6 +536,8 @@ int pscl_create(pscl_handle** out, int device, int N, const int32_t* info_set, i
 int pscl_destroy(pscl_handle* h) {
     if (!h) return PSCL_OK;
     hipSetDevice(h->device);
+    if (h->dl_defer_valid) dl_enqueue_deferred(h);  // (a pipelined call's chains complete before the buffers go)
+    quiesce(h);
     if (h->own_stream) hipStreamSynchronize(h->own_stream);
     if (h->pipe_stream) hipStreamSynchronize(h->pipe_stream);
     for (auto& b : h->scratch)
@@ -687,7 +717,7 @@ struct DlState {
 
 int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const double* d_llr, uint64_t* d_best,
                    uint8_t* d_flags, int32_t* d_attempts, int32_t* d_tried, int tried_stride, int64_t* d_cnt_dl,
-                   hipStream_t st, hipStream_t side, hipEvent_t ev_s, hipEvent_t ev_d) {
+                   hipStream_t st, hipStream_t side, hipEvent_t ev_s, hipEvent_t ev_d, bool narrow) {
     const int K = h->K, W = h->W;
     hipError_t e;
     const size_t bstride = (size_t)PSCL_DL_NSEG * PSCL_DL_CSTRIDE;
@@ -706,6 +736,7 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     Q.info_set = h->d_info_set;
     Q.exp_table = h->d_exp_table;
     Q.rounds = rounds;
+    Q.narrow = narrow ? 1 : 0;  // (pipelined calls: beside the next call's baseline)
     Q.cap = A;
     Q.act = S.act;
     Q.tried = S.tried;
@@ -886,6 +917,159 @@ int dl_retry_long(pscl_handle* h, const DlLongState& S, int64_t* act0, const int
 }
 }  // namespace
 
+namespace {
+constexpr int kMinSplit = 2048;
+
+// the retry chains' state (scratch slots), sized by dl_setup
+struct DlBufs {
+    DlState S[2];         // chain state (S[k] on retry stream k)
+    DlLongState LS = {};  // (long codes)
+    int32_t* cnt[2] = {};  // failing-frame count of the two compaction parities
+    int64_t* act[2] = {};  // their frame indices
+};
+
+// streams, events and scratch of a DL-SCL call (everything sized before any work is queued:
+// an allocation synchronizes the device)
+int dl_setup(pscl_handle* h, const pscl_dl_call& a, DlBufs& b) {
+    int rc;
+    const int K = h->K, W = h->W, rounds = a.rounds;
+    const int64_t cap = a.cap;
+    for (int i = 0; i < 2; ++i)
+        if (!h->retry_stream[i]) HIP_TRY(create_priority_stream(h, &h->retry_stream[i]));
+    for (int i = 0; i < 2; ++i) {
+        if (!h->ev_base[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_base[i], hipEventDisableTiming));
+        if (!h->ev_retry[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_retry[i], hipEventDisableTiming));
+        if (!h->ev_dl[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_dl[i], hipEventDisableTiming));
+        if (!h->side_stream[i]) HIP_TRY(create_priority_stream(h, &h->side_stream[i]));
+        if (!h->ev_scr[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_scr[i], hipEventDisableTiming));
+        if (!h->ev_def[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_def[i], hipEventDisableTiming));
+    }
+    if (!h->ev_join) HIP_TRY(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+    if (!h->h_count) HIP_TRY(hipHostMalloc((void**)&h->h_count, 16, hipHostMallocDefault));
+    const size_t NS = PSCL_DL_NSEG;
+    for (int i = 0; i < (a.nch >= 2 || a.pipe ? 2 : 1); ++i) {
+        void *pc, *pa;
+        if ((rc = ensure(h, 22 + 5 * i, 4, &pc)) || (rc = ensure(h, 23 + 5 * i, (size_t)cap * 8, &pa))) return rc;
+        b.cnt[i] = (int32_t*)pc;
+        b.act[i] = (int64_t*)pa;
+    }
+    if (h->N > PSCL_FAST_N) {  // long codes: one chain, dense state (dl_retry_long)
+        const size_t c = (size_t)cap;
+        const size_t sz[10] = {c * 8, c * W * 8, c * W * 8, c * W * 8, c * 2 * W * 8, c * 4, c * 4,
+                               (size_t)(rounds + 2) * 4, c, c * K * 8};
+        void* q[10];
+        for (int k = 0; k < 10; ++k)
+            if ((rc = ensure(h, 52 + k, sz[k], &q[k]))) return rc;
+        b.LS.act1 = (int64_t*)q[0];
+        b.LS.tried[0] = (uint64_t*)q[1];
+        b.LS.tried[1] = (uint64_t*)q[2];
+        b.LS.ob = (uint64_t*)q[3];
+        b.LS.force = (uint64_t*)q[4];
+        b.LS.nt[0] = (int32_t*)q[5];
+        b.LS.nt[1] = (int32_t*)q[6];
+        b.LS.cnt = (int32_t*)q[7];
+        b.LS.of = (uint8_t*)q[8];
+        b.LS.l0 = (double*)q[9];
+        pscl_decode_params H;  // the retry decodes' scratch
+        fill_decode_params(h, H, 1);
+        H.B = cap;
+        void* d_scr;
+        if ((rc = ensure(h, kLongRetryScratch, (size_t)pscl_decode_grid(H) * (size_t)H.long_block_bytes, &d_scr)))
+            return rc;
+    }
+    for (int i = 0; i < a.nsplit; ++i) {
+        // chain 0 takes every entry of a call that does not split (fewer than 2 kMinSplit
+        // failing frames, which may still exceed half the chunk); chain 1 at most half
+        const size_t c = (size_t)(i == 0 ? cap : cap - cap / 2);
+        const size_t sz[14] = {(size_t)(rounds + 1) * NS * PSCL_DL_CSTRIDE * 4, NS * c * 4, NS * c * 4, c * 16, c * 4,
+                               c * 2 * W * 8, c * NS * 8, c * 16, c * W * 8, c, NS * PSCL_DL_CSTRIDE * 4, NS * c * 4,
+                               c * W * 8, c};
+        static const int slot[2][14] = {{12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 8, 9, 10, 11},
+                                        {40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 24, 29}};
+        void* q[14];
+        for (int k = 0; k < 14; ++k)
+            if ((rc = ensure(h, slot[i][k], sz[k], &q[k]))) return rc;
+        b.S[i].dcnt = (int32_t*)q[10];
+        b.S[i].dlist = (int32_t*)q[11];
+        b.S[i].ob2 = (uint64_t*)q[12];
+        b.S[i].of2 = (uint8_t*)q[13];
+        b.S[i].bcnt = (int32_t*)q[0];
+        b.S[i].list0 = (int32_t*)q[1];
+        b.S[i].list1 = (int32_t*)q[2];
+        b.S[i].tried = (uint64_t*)q[3];
+        b.S[i].nt = (int32_t*)q[4];
+        b.S[i].force = (uint64_t*)q[5];
+        b.S[i].warm_metric = (double*)q[6];
+        b.S[i].warm_u = (uint64_t*)q[7];
+        b.S[i].ob = (uint64_t*)q[8];
+        b.S[i].of = (uint8_t*)q[9];
+    }
+    return PSCL_OK;
+}
+
+// the retry chains of chunk c (compaction parity p): the host reads the chunk's failing count
+// (waiting for its baseline) and enqueues the rounds on the retry streams; ev_retry[p] marks
+// their end on retry stream 0
+int dl_chain(pscl_handle* h, const pscl_dl_call& a, const DlBufs& b, int64_t c) {
+    const int p = (int)((c + a.pbase) & 1);
+    const int64_t cap = a.cap;
+    HIP_TRY(hipEventSynchronize(h->ev_base[p]));
+    const int A = h->h_count[p];
+    int64_t* d_cdl = a.d_ref ? a.d_counters_dl : nullptr;
+    if (h->N > PSCL_FAST_N) {
+        if (A > 0) {
+            HIP_TRY(hipStreamWaitEvent(h->retry_stream[0], h->ev_base[p], 0));
+            int r2 = dl_retry_long(h, b.LS, b.act[p], b.cnt[p], A, a.rounds, a.d_llr, a.d_best, a.d_flags, a.d_attempts,
+                                   a.d_tried, a.tried_stride, d_cdl, h->retry_stream[0]);
+            if (r2) return r2;
+        }
+        HIP_TRY(hipEventRecord(h->ev_retry[p], h->retry_stream[0]));
+        return PSCL_OK;
+    }
+    const int parts = (a.nsplit == 2 && A >= 2 * kMinSplit) ? 2 : 1;
+    const int A0 = parts == 2 ? A - A / 2 : A;
+    for (int k = 0; k < parts && A > 0; ++k) {
+        const int64_t nk = k ? A - A0 : A0, capk = k ? cap - cap / 2 : cap;  // (state sized by dl_setup)
+        if (nk > capk)
+            return fail(PSCL_EDEVICE, "retry chain %d: %lld entries exceed its state (%lld)", k, (long long)nk,
+                        (long long)capk);
+        HIP_TRY(hipStreamWaitEvent(h->retry_stream[k], h->ev_base[p], 0));
+        DlState T = b.S[k];
+        T.act = b.act[p] + (k ? A0 : 0);
+        int r2 = dl_retry_chunk(h, T, k ? A - A0 : A0, a.rounds, a.d_llr, a.d_best, a.d_flags, a.d_attempts,
+                                a.d_tried, a.tried_stride, d_cdl, h->retry_stream[k], h->side_stream[k], h->ev_scr[k],
+                                h->ev_def[k], a.pipe);
+        if (r2) return r2;
+    }
+    if (parts == 2) {  // both chains done before the parity's indices are reused
+        HIP_TRY(hipEventRecord(h->ev_join, h->retry_stream[1]));
+        HIP_TRY(hipStreamWaitEvent(h->retry_stream[0], h->ev_join, 0));
+    }
+    HIP_TRY(hipEventRecord(h->ev_retry[p], h->retry_stream[0]));
+    return PSCL_OK;
+}
+
+// a pipelined call's retry chains and DL counters, enqueued on the retry streams (ev_dl marks
+// their end; join_pipe orders it into the handle's stream)
+int dl_enqueue_deferred(pscl_handle* h) {
+    if (!h->dl_defer_valid) return PSCL_OK;
+    h->dl_defer_valid = false;
+    const pscl_dl_call a = h->dl_defer;
+    DlBufs b;
+    int rc = dl_setup(h, a, b);  // (the sizes of the call's own setup: no allocation)
+    if (rc) return rc;
+    if ((rc = dl_chain(h, a, b, 0))) return rc;
+    if (a.d_ref) {
+        hipError_t e = pscl_launch_dl_count(a.d_best, a.d_flags, a.d_ref, a.B, h->W, a.k_payload, a.d_counters_dl,
+                                            h->retry_stream[0]);
+        if (e != hipSuccess) return fail(PSCL_EDEVICE, "dl_count launch: %s", hipGetErrorString(e));
+    }
+    HIP_TRY(hipEventRecord(h->ev_dl[a.pbase], h->retry_stream[0]));
+    h->dl_pending[a.pbase] = true;
+    return PSCL_OK;
+}
+}  // namespace
+
 int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retries, uint64_t* d_best, uint8_t* d_flags,
                       int32_t* d_attempts, int32_t* d_tried, int tried_stride, const uint64_t* d_ref, int k_payload,
                       int64_t* d_counters_scl, int64_t* d_counters_dl) {
@@ -900,158 +1084,64 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
     if (B > INT32_MAX) return fail(PSCL_EUNSUP, "B exceeds 2^31-1");
     int rc = set_device(h);
     if (rc) return rc;
-    // pipelined (pscl_set_pipelined, one chunk): this call's retry chains are left running on the
-    // retry streams, where they overlap the next call's baseline decode
-    const bool dl_pipe = h->pipelined && rounds > 0 && !getenv("PSCL_DL_CHUNKS");
-    if ((rc = join_pipe(h, dl_pipe ? 1 : 3))) return rc;
-    const int pbase = dl_pipe ? h->dl_par : 0;  // compaction parity of chunk 0
-    if (dl_pipe && h->dl_pending[pbase]) {
-        // the chains of the call two back (same parity) may still read their compaction output and
-        // write their call's outputs: they end before this call starts (the contract of
-        // pscl_set_pipelined: a call's buffers are free again at the second following call)
-        HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_dl[pbase], 0));
-        h->dl_pending[pbase] = false;
-    }
-    const int K = h->K, W = h->W;
-    const int64_t row = h->rm_E ? h->rm_E : h->N;
-    hipStream_t s = h->stream;
-    hipError_t e;
-    if (d_attempts) HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)d_attempts, 1, (size_t)B, s));
-    if (d_tried) HIP_TRY(hipMemsetAsync(d_tried, 0xff, (size_t)B * tried_stride * 4, s));
+    pscl_dl_call a;
+    a.d_llr = d_llr;
+    a.B = B;
+    a.rounds = rounds;
+    a.d_best = d_best;
+    a.d_flags = d_flags;
+    a.d_attempts = d_attempts;
+    a.d_tried = d_tried;
+    a.tried_stride = tried_stride;
+    a.d_ref = d_ref;
+    a.k_payload = k_payload;
+    a.d_counters_dl = d_counters_dl;
     // Chunks (PSCL_DL_CHUNKS, default 1): the baseline decodes run in order on the handle's
     // stream; the retry entries of chunk c are split over two chains, each on its own retry
     // stream with its own state, so the two chains' rounds overlap each other (and chunk c + 1's
     // baseline decode).  A round is latency-bound (a few 10^4 entries per launch), so a second
     // concurrent chain fills what one leaves idle.  PSCL_DL_SPLIT (1 or 2, default 2) sets the
     // chains per chunk; chunks below 2 * kMinSplit failing frames keep one chain.
-    int64_t nch = 1;
-    int nsplit = 2;
+    a.nch = 1;
+    a.nsplit = h->N > PSCL_FAST_N ? 0 : 2;
     if (rounds > 0 && getenv("PSCL_DL_CHUNKS")) {  // tuning override
         const long v = atol(getenv("PSCL_DL_CHUNKS"));
-        if (v >= 1 && v <= 64) nch = v;
+        if (v >= 1 && v <= 64) a.nch = v;
     }
-    if (rounds > 0 && getenv("PSCL_DL_SPLIT")) {  // tuning override
+    if (rounds > 0 && h->N <= PSCL_FAST_N && getenv("PSCL_DL_SPLIT")) {  // tuning override
         const long v = atol(getenv("PSCL_DL_SPLIT"));
-        if (v >= 1 && v <= 2) nsplit = (int)v;
+        if (v >= 1 && v <= 2) a.nsplit = (int)v;
     }
-    constexpr int kMinSplit = 2048;
-    const int64_t cap = (B + nch - 1) / nch;
-    DlState S[2];              // chain state (S[k] on retry stream k)
-    DlLongState LS = {};       // (long codes)
-    int32_t* cnt[2] = {};      // failing-frame count of the two chunk parities
-    int64_t* act[2] = {};      // their frame indices
-    if (rounds > 0) {
-        for (int i = 0; i < 2; ++i)
-            if (!h->retry_stream[i]) HIP_TRY(create_priority_stream(&h->retry_stream[i]));
-        for (int i = 0; i < 2; ++i) {
-            if (!h->ev_base[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_base[i], hipEventDisableTiming));
-            if (!h->ev_retry[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_retry[i], hipEventDisableTiming));
-        }
-        if (!h->ev_join) HIP_TRY(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
-        for (int i = 0; i < 2; ++i)
-            if (!h->ev_dl[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_dl[i], hipEventDisableTiming));
-        for (int i = 0; i < 2; ++i) {
-            if (!h->side_stream[i]) HIP_TRY(create_priority_stream(&h->side_stream[i]));
-            if (!h->ev_scr[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_scr[i], hipEventDisableTiming));
-            if (!h->ev_def[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_def[i], hipEventDisableTiming));
-        }
-        if (!h->h_count) HIP_TRY(hipHostMalloc((void**)&h->h_count, 16, hipHostMallocDefault));
-        // everything sized before any work is queued (an allocation synchronizes the device)
-        const size_t NS = PSCL_DL_NSEG;
-        for (int i = 0; i < (nch >= 2 || dl_pipe ? 2 : 1); ++i) {
-            void *pc, *pa;
-            if ((rc = ensure(h, 22 + 5 * i, 4, &pc)) || (rc = ensure(h, 23 + 5 * i, (size_t)cap * 8, &pa))) return rc;
-            cnt[i] = (int32_t*)pc;
-            act[i] = (int64_t*)pa;
-        }
-        if (h->N > PSCL_FAST_N) {  // long codes: one chain, dense state (dl_retry_long)
-            const size_t c = (size_t)cap;
-            const size_t sz[10] = {c * 8, c * W * 8, c * W * 8, c * W * 8, c * 2 * W * 8, c * 4, c * 4,
-                                   (size_t)(rounds + 2) * 4, c, c * K * 8};
-            void* q[10];
-            for (int k = 0; k < 10; ++k)
-                if ((rc = ensure(h, 52 + k, sz[k], &q[k]))) return rc;
-            LS.act1 = (int64_t*)q[0];
-            LS.tried[0] = (uint64_t*)q[1];
-            LS.tried[1] = (uint64_t*)q[2];
-            LS.ob = (uint64_t*)q[3];
-            LS.force = (uint64_t*)q[4];
-            LS.nt[0] = (int32_t*)q[5];
-            LS.nt[1] = (int32_t*)q[6];
-            LS.cnt = (int32_t*)q[7];
-            LS.of = (uint8_t*)q[8];
-            LS.l0 = (double*)q[9];
-            nsplit = 0;
-            pscl_decode_params H;  // the retry decodes' scratch, sized before any work is queued
-            fill_decode_params(h, H, 1);
-            H.B = cap;
-            void* d_scr;
-            if ((rc = ensure(h, kLongRetryScratch, (size_t)pscl_decode_grid(H) * (size_t)H.long_block_bytes, &d_scr)))
-                return rc;
-        }
-        for (int i = 0; i < nsplit; ++i) {
-            // chain 0 takes every entry of a call that does not split (fewer than 2 kMinSplit
-            // failing frames, which may still exceed half the chunk); chain 1 at most half
-            const size_t c = (size_t)(i == 0 ? cap : cap - cap / 2);
-            const size_t sz[14] = {(size_t)(rounds + 1) * NS * PSCL_DL_CSTRIDE * 4, NS * c * 4, NS * c * 4, c * 16, c * 4,
-                                   c * 2 * W * 8, c * NS * 8, c * 16, c * W * 8, c, NS * PSCL_DL_CSTRIDE * 4, NS * c * 4,
-                                   c * W * 8, c};
-            static const int slot[2][14] = {{12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 8, 9, 10, 11},
-                                            {40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 24, 29}};
-            void* q[14];
-            for (int k = 0; k < 14; ++k)
-                if ((rc = ensure(h, slot[i][k], sz[k], &q[k]))) return rc;
-            S[i].dcnt = (int32_t*)q[10];
-            S[i].dlist = (int32_t*)q[11];
-            S[i].ob2 = (uint64_t*)q[12];
-            S[i].of2 = (uint8_t*)q[13];
-            S[i].bcnt = (int32_t*)q[0];
-            S[i].list0 = (int32_t*)q[1];
-            S[i].list1 = (int32_t*)q[2];
-            S[i].tried = (uint64_t*)q[3];
-            S[i].nt = (int32_t*)q[4];
-            S[i].force = (uint64_t*)q[5];
-            S[i].warm_metric = (double*)q[6];
-            S[i].warm_u = (uint64_t*)q[7];
-            S[i].ob = (uint64_t*)q[8];
-            S[i].of = (uint8_t*)q[9];
-        }
+    a.cap = (B + a.nch - 1) / a.nch;
+    // Pipelined (pscl_set_pipelined, one chunk): the call enqueues its baseline, then the retry
+    // chains of the PREVIOUS pipelined call (whose baseline has ended or is about to: the host
+    // waits only for that one), and leaves its own chains to the next call or join -- so the
+    // handle's stream holds back-to-back baselines and the chains (high-priority streams) run
+    // beside them, the host never waiting for the baseline it has just enqueued.
+    a.pipe = h->pipelined && rounds > 0 && a.nch == 1;
+    if (h->dl_defer_valid &&
+        (!a.pipe || h->dl_defer.B != B || h->dl_defer.rounds != rounds || h->dl_defer.nsplit != a.nsplit)) {
+        // (a different shape: the pending chains first, their state sized as they were)
+        if ((rc = dl_enqueue_deferred(h))) return rc;
     }
-    auto retries_of = [&](int64_t c) -> int {
-        const int p = (int)((c + pbase) & 1);
-        HIP_TRY(hipEventSynchronize(h->ev_base[p]));
-        const int A = h->h_count[p];
-        if (h->N > PSCL_FAST_N) {
-            if (A > 0) {
-                HIP_TRY(hipStreamWaitEvent(h->retry_stream[0], h->ev_base[p], 0));
-                int r2 = dl_retry_long(h, LS, act[p], cnt[p], A, rounds, d_llr, d_best, d_flags, d_attempts, d_tried,
-                                       tried_stride, d_ref ? d_counters_dl : nullptr, h->retry_stream[0]);
-                if (r2) return r2;
-            }
-            HIP_TRY(hipEventRecord(h->ev_retry[p], h->retry_stream[0]));
-            return PSCL_OK;
-        }
-        const int parts = (nsplit == 2 && A >= 2 * kMinSplit) ? 2 : 1;
-        const int A0 = parts == 2 ? A - A / 2 : A;
-        for (int k = 0; k < parts && A > 0; ++k) {
-            const int64_t nk = k ? A - A0 : A0, capk = k ? cap - cap / 2 : cap;  // (state sized above)
-            if (nk > capk) return fail(PSCL_EDEVICE, "retry chain %d: %lld entries exceed its state (%lld)", k,
-                                       (long long)nk, (long long)capk);
-            HIP_TRY(hipStreamWaitEvent(h->retry_stream[k], h->ev_base[p], 0));
-            DlState T = S[k];
-            T.act = act[p] + (k ? A0 : 0);
-            int r2 = dl_retry_chunk(h, T, k ? A - A0 : A0, rounds, d_llr, d_best, d_flags, d_attempts, d_tried,
-                                    tried_stride, d_ref ? d_counters_dl : nullptr, h->retry_stream[k],
-                                    h->side_stream[k], h->ev_scr[k], h->ev_def[k]);
-            if (r2) return r2;
-        }
-        if (parts == 2) {  // both chains done before the parity's indices are reused
-            HIP_TRY(hipEventRecord(h->ev_join, h->retry_stream[1]));
-            HIP_TRY(hipStreamWaitEvent(h->retry_stream[0], h->ev_join, 0));
-        }
-        HIP_TRY(hipEventRecord(h->ev_retry[p], h->retry_stream[0]));
-        return PSCL_OK;
-    };
+    if ((rc = join_pipe(h, a.pipe ? 1 : 3))) return rc;
+    a.pbase = a.pipe ? h->dl_par : 0;  // compaction parity of chunk 0
+    if (a.pipe && h->dl_pending[a.pbase]) {
+        // the chains of the call two back (same parity) may still read their compaction output and
+        // write their call's outputs: they end before this call starts (the contract of
+        // pscl_set_pipelined: a call's buffers are free again at the second following call)
+        HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_dl[a.pbase], 0));
+        h->dl_pending[a.pbase] = false;
+    }
+    const int W = h->W;
+    const int64_t row = h->rm_E ? h->rm_E : h->N;
+    const int64_t nch = a.nch, cap = a.cap;
+    hipStream_t s = h->stream;
+    hipError_t e;
+    if (d_attempts) HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)d_attempts, 1, (size_t)B, s));
+    if (d_tried) HIP_TRY(hipMemsetAsync(d_tried, 0xff, (size_t)B * tried_stride * 4, s));
+    DlBufs bufs;
+    if (rounds > 0 && (rc = dl_setup(h, a, bufs))) return rc;
     for (int64_t c = 0; c < nch; ++c) {
         const int64_t c0 = c * cap, nc = (B - c0) < cap ? (B - c0) : cap;
         // baseline SCL (flip.py:79-80) of chunk c
@@ -1067,30 +1157,28 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
         if (pscl_decode_wpg(P) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
         if ((rc = launch_decode(h, P, 0))) return rc;
         if (rounds > 0) {
-            const int p = (int)((c + pbase) & 1);
+            const int p = (int)((c + a.pbase) & 1);
             if (c >= 2) HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[p], 0));  // the parity's indices free again
-            HIP_TRY(hipMemsetAsync(cnt[p], 0, 4, s));
-            if ((e = pscl_launch_dl_compact(d_flags + c0, nc, c0, act[p], nullptr, cnt[p], s)) != hipSuccess)
+            HIP_TRY(hipMemsetAsync(bufs.cnt[p], 0, 4, s));
+            if ((e = pscl_launch_dl_compact(d_flags + c0, nc, c0, bufs.act[p], nullptr, bufs.cnt[p], s)) != hipSuccess)
                 return fail(PSCL_EDEVICE, "dl_compact launch: %s", hipGetErrorString(e));
-            HIP_TRY(hipMemcpyAsync(h->h_count + p, cnt[p], 4, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(h->h_count + p, bufs.cnt[p], 4, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipEventRecord(h->ev_base[p], s));
-            if (c >= 1 && (rc = retries_of(c - 1))) return rc;
+            if (c >= 1 && (rc = dl_chain(h, a, bufs, c - 1))) return rc;
         }
     }
+    if (a.pipe) {
+        // the previous call's chains now (its baseline precedes this call's on the stream), this
+        // call's at the next call or join
+        if ((rc = dl_enqueue_deferred(h))) return rc;
+        h->dl_defer = a;
+        h->dl_defer_valid = true;
+        h->dl_par ^= 1;
+        return PSCL_OK;
+    }
     if (rounds > 0) {
-        if ((rc = retries_of(nch - 1))) return rc;
-        if (dl_pipe) {  // the DL counters follow the chains on retry stream 0; pscl_join orders them back
-            const int p = pbase;
-            if (d_ref) {
-                e = pscl_launch_dl_count(d_best, d_flags, d_ref, B, W, k_payload, d_counters_dl, h->retry_stream[0]);
-                if (e != hipSuccess) return fail(PSCL_EDEVICE, "dl_count launch: %s", hipGetErrorString(e));
-            }
-            HIP_TRY(hipEventRecord(h->ev_dl[p], h->retry_stream[0]));
-            h->dl_pending[p] = true;
-            h->dl_par ^= 1;
-            return PSCL_OK;
-        }
-        HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[(nch - 1 + pbase) & 1], 0));  // chains run in order on stream 0
+        if ((rc = dl_chain(h, a, bufs, nch - 1))) return rc;
+        HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[(nch - 1 + a.pbase) & 1], 0));  // chains run in order on stream 0
     }
     if (d_ref) {
         e = pscl_launch_dl_count(d_best, d_flags, d_ref, B, W, k_payload, d_counters_dl, s);

@@ -198,30 +198,37 @@ __global__ void __launch_bounds__(256) replay_kernel(const pscl_replay_params R,
 // a time, one per 32-lane half (4 tree elements and up to 4 flip candidates per lane), so a
 // workgroup keeps twice the entries in flight that one entry per wavefront allowed (the pass
 // is latency-bound: LDS round trips of the replay levels, the flip metric's sums, the serial
-// prefix sums).  Workgroups of 8 wavefronts own contiguous ranges of the pass's entries; every
+// prefix sums).  Workgroups of 4 wavefronts own contiguous ranges of the pass's entries; every
 // wavefront preloads the metadata of its next 64 entries (one lane each: entry id, frame,
 // bits, flags, tried state) and prefetches the next pair's channel rows while it replays the
 // current pair.  Survivors are staged in LDS and appended to the next round's bucket lists
 // with one global atomic per (workgroup, bucket) per 512 entries: one atomic per entry put
 // ~5k same-address device atomics on each bucket counter (measured: 316 of 467 us of the
-// first pass at L = 4, 5 dB).  beta (when K * K doubles fit) and the exp table of the exact
-// metric tails are staged in LDS once per workgroup.
+// first pass at L = 4, 5 dB).  The exp table of the exact metric tails is staged in LDS once
+// per workgroup, and beta (when K * K doubles fit) too.  Pipelined DL-SCL calls
+// (pscl_set_pipelined, Q.narrow) take a narrow form instead: workgroups of 4 wavefronts with beta
+// read through L2 (~20 KB of LDS against ~70 KB), which fit beside the next call's baseline decode
+// running concurrently -- a post pass that needs 70 KB of free LDS on one CU waits for that
+// baseline to end (measured, config 4 pipelined: 3.86-3.93 -> 3.54-3.58 ms per step; 8
+// wavefronts with beta through L2 4.10, 4 with beta staged 3.91).  Alone on the GPU the wide
+// form is the faster one (the FER sweep's 4.0 dB point: 16.6 against 34 ms).
 #ifndef PSCL_POST_GRID
 #define PSCL_POST_GRID 512
 #endif
 #ifndef PSCL_POST_BETA_LDS
 #define PSCL_POST_BETA_LDS 1
 #endif
-constexpr int kPostWaves = 8;
-constexpr int kPostIters = 32;                          // entry pairs per wavefront between flushes
-constexpr int kPostChunk = kPostWaves * 2 * kPostIters;  // entries per workgroup between flushes
+constexpr int kPostWavesWide = 8, kPostWavesNarrow = 4;
+constexpr int kPostIters = 32;  // entry pairs per wavefront between flushes
 
+template <int PW>
 struct PostShared {
-    double lvl[kPostWaves][2][2][PSCL_FAST_N];  // [wave][half][buffer][element]
+    static constexpr int kChunk = PW * 2 * kPostIters;  // entries per workgroup between flushes
+    double lvl[PW][2][2][PSCL_FAST_N];  // [wave][half][buffer][element]
     uint64_t exp_table[PSCL_EXP_TABLE_WORDS];
-    int32_t st_e[kPostChunk];
-    uint16_t st_pos[kPostChunk];
-    uint8_t st_seg[kPostChunk];
+    int32_t st_e[kChunk];
+    uint16_t st_pos[kChunk];
+    uint8_t st_seg[kChunk];
     int32_t lcnt[PSCL_DL_NSEG];
     int32_t gbase[PSCL_DL_NSEG];
     int32_t nst;
@@ -242,9 +249,10 @@ __device__ __forceinline__ uint64_t bcast64(uint64_t v, int l) {
 }
 
 // NC, KC: N and K compiled in (128 and 64 / 88: the BASELINE codes) or 0 (from Q)
-template <int NC, int KC>
-__global__ void __launch_bounds__(kPostWaves * 64) __attribute__((amdgpu_waves_per_eu(4))) dl_post_kernel(const pscl_post_params Q, int beta_lds) {
-    __shared__ PostShared S;
+template <int NC, int KC, int PW>
+__global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(4))) dl_post_kernel(const pscl_post_params Q, int beta_lds) {
+    constexpr int kPostWaves = PW, kPostChunk = PostShared<PW>::kChunk;
+    __shared__ PostShared<PW> S;
     extern __shared__ double sbeta[];  // [K][K] when beta_lds
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int hs = lane >> 5, hl = lane & 31, hb = lane & 32;  // half, lane in half, half's first lane
@@ -686,20 +694,29 @@ hipError_t pscl_launch_replay(const pscl_replay_params& R, int64_t cap, hipStrea
 
 hipError_t pscl_launch_dl_post(const pscl_post_params& Q, int64_t entries, hipStream_t s) {
     if (entries <= 0) return hipSuccess;
-    // workgroups of 8 wavefronts (16 entries in flight), at most two resident per CU
-    int64_t grid = (entries + kPostWaves * 8 - 1) / (kPostWaves * 8);
+    // workgroups of PW wavefronts (2 PW entries in flight)
+    const int PW = Q.narrow ? kPostWavesNarrow : kPostWavesWide;
+    int64_t grid = (entries + PW * 8 - 1) / (PW * 8);
     static const int64_t cap_env = getenv("PSCL_POST_GRID") ? atol(getenv("PSCL_POST_GRID")) : 0;  // tuning override
     const int64_t gcap = cap_env >= 16 && cap_env <= 4096 ? cap_env : PSCL_POST_GRID;
     if (grid > gcap) grid = gcap;
-    const int beta_lds = PSCL_POST_BETA_LDS && Q.beta && (size_t)Q.K * Q.K * 8 <= 32 * 1024;  // (LDS <= 64 KB)
+    const int beta_lds = PSCL_POST_BETA_LDS && !Q.narrow && Q.beta && (size_t)Q.K * Q.K * 8 <= 32 * 1024;  // (LDS <= 64 KB)
     const size_t lds = beta_lds ? (size_t)Q.K * Q.K * 8 : 0;
-    const dim3 g((unsigned)grid), b(kPostWaves * 64);
-    if (Q.N == 128 && Q.K == 64)
-        hipLaunchKernelGGL((dl_post_kernel<128, 64>), g, b, lds, s, Q, beta_lds);
-    else if (Q.N == 128 && Q.K == 88)
-        hipLaunchKernelGGL((dl_post_kernel<128, 88>), g, b, lds, s, Q, beta_lds);
-    else
-        hipLaunchKernelGGL((dl_post_kernel<0, 0>), g, b, lds, s, Q, beta_lds);
+    const dim3 g((unsigned)grid), b(PW * 64);
+    if (Q.narrow) {
+        if (Q.N == 128 && Q.K == 64)
+            hipLaunchKernelGGL((dl_post_kernel<128, 64, kPostWavesNarrow>), g, b, lds, s, Q, beta_lds);
+        else if (Q.N == 128 && Q.K == 88)
+            hipLaunchKernelGGL((dl_post_kernel<128, 88, kPostWavesNarrow>), g, b, lds, s, Q, beta_lds);
+        else
+            hipLaunchKernelGGL((dl_post_kernel<0, 0, kPostWavesNarrow>), g, b, lds, s, Q, beta_lds);
+    } else if (Q.N == 128 && Q.K == 64) {
+        hipLaunchKernelGGL((dl_post_kernel<128, 64, kPostWavesWide>), g, b, lds, s, Q, beta_lds);
+    } else if (Q.N == 128 && Q.K == 88) {
+        hipLaunchKernelGGL((dl_post_kernel<128, 88, kPostWavesWide>), g, b, lds, s, Q, beta_lds);
+    } else {
+        hipLaunchKernelGGL((dl_post_kernel<0, 0, kPostWavesWide>), g, b, lds, s, Q, beta_lds);
+    }
     return hipGetLastError();
 }
 

@@ -134,6 +134,7 @@ struct pscl_post_params {
     const int32_t* info_set;     // [K] (device)
     const uint64_t* exp_table;   // glibc exp table (exact metric tails)
     int rounds;                  // min(retries, K)
+    int narrow;                  // small workgroups, beta through L2 (pipelined calls, dl_post_kernel)
     int init;
     const int32_t* in_count;     // bucket counts of this round (init: unused, cap entries)
     const int32_t* in_list;      // bucket lists of this round ([NSEG][cap] entry ids)

@@ -21,6 +21,7 @@
 // key (metric, previous list position).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "glibc_softplus.h"
 #include "scl_device.h"
@@ -430,7 +431,10 @@ int pscl_decode_wpg(const pscl_decode_params& P) {
     if (P.long_mode) return 1;  // one wavefront per workgroup, state in global scratch
     const int cu_lds = 160 * 1024, tbl = P.wg_fixed_bytes;
     int best = 0, best_res = 0;
-    for (int w = 1; w <= PSCL_MAX_WAVES_PER_WG; ++w) {
+    // DL-SCL retry rounds (bucket-list launches): workgroup size cap (tuning override)
+    static const int retry_cap = getenv("PSCL_RETRY_WPG") ? atoi(getenv("PSCL_RETRY_WPG")) : 0;
+    const int wmax = P.elist && retry_cap >= 1 && retry_cap < PSCL_MAX_WAVES_PER_WG ? retry_cap : PSCL_MAX_WAVES_PER_WG;
+    for (int w = 1; w <= wmax; ++w) {
         const int wg = tbl + w * P.wave_bytes;
         if (wg > cu_lds) break;
         int res = (cu_lds / wg) * w;
