@@ -74,7 +74,7 @@ def parse():
                          "decoder de-rate-matches in its channel staging")
     ap.add_argument("--extra", choices=["auto", "none"], default="auto",
                     help="auto: also time BASELINE configs 2, 4, 5 (extra_configs) after the headline")
-    ap.add_argument("--extra-steps", type=int, default=5)
+    ap.add_argument("--extra-steps", type=int, default=10)
     ap.add_argument("--extra-parity", type=int, default=50_000, help="oracle parity frames per extra config")
     return ap.parse_args()
 
