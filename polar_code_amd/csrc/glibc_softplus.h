@@ -401,7 +401,9 @@ PSCL_HD double pscl_softplus_tail_bf(double v, const uint64_t* T) {
  * 0.62, s^2 error x dP/dw 0.2), the two products 1: 5.0 < 6.  The
  * final cvt and ldexp are exact (until fp64 underflow, where the exact tail is subnormal too:
  * then the error is at most one ulp of the result).  x is clamped to 4096 (the exact tail is 0
- * above ~745.2; the clamp keeps k in int range).
+ * above ~745.2; the clamp keeps k in int range) -- or, in pscl_softplus_tail_scr_nc, not
+ * clamped by a caller that guarantees |v| < 2^30 (the L = 8 screening kernel: channel LLRs
+ * below 2^22, larger or NaN frames deferred).
  *
  * With positive increments every screening path metric is within PSCL_SCR_EPS + N * 2^-53 of
  * the exact metric relatively (the tail error, plus the fp64 summation of at most N = 128
@@ -448,8 +450,12 @@ __device__ __forceinline__ double pscl_ldexp_f64(double a, int e) { return __bui
 #define pscl_ldexp_f64(a, e) ldexp((a), (e))
 #endif
 
-PSCL_HD double pscl_softplus_tail_scr(double v) {
-    const double x = pscl_absmin(v, 4096.0);
+/* the screening tail of x = |v| without the clamp: valid while k = round(x log2 e) fits the
+ * 32-bit exponent arithmetic, i.e. |v| < 2^30 (the result is then the clamped form's: both are
+ * 0 above 745.2).  The decode kernel that uses it defers every frame with a channel LLR of
+ * magnitude >= 2^22 (or NaN), which bounds every tree LLR by 128 * 2^22 = 2^29 */
+PSCL_HD double pscl_softplus_tail_scr_nc(double v) {
+    const double x = fabs(v);
     const double kd0 = pscl_fma(-x, PSCL_INVLN2, PSCL_EXP_SHIFT); /* low word = -k */
     const int32_t nk = (int32_t)(uint32_t)pscl_asu64(kd0);
     const double kd = kd0 - PSCL_EXP_SHIFT;                      /* -k */
@@ -467,6 +473,8 @@ PSCL_HD double pscl_softplus_tail_scr(double v) {
     const float q = (u * rc) * p;
     return pscl_ldexp_f64((double)q, nk);
 }
+
+PSCL_HD double pscl_softplus_tail_scr(double v) { return pscl_softplus_tail_scr_nc(pscl_absmin(v, 4096.0)); }
 
 /* L = log1p(exp(-|v|)), the part of logaddexp(0, +-v) shared by both bit hypotheses. */
 PSCL_HD double pscl_softplus_tail(double v, const uint64_t* T) {

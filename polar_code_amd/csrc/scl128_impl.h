@@ -169,6 +169,11 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 #define PSCL_LEAF_BLEND 0
 #endif
 
+// L = 8 screening: the metric tail without the |v| clamp, frames with channel LLRs >= 2^22 deferred
+#ifndef PSCL_TAIL_NC
+#define PSCL_TAIL_NC 1
+#endif
+
 #ifndef PSCL_WAVES_PER_EU
 #define PSCL_WAVES_PER_EU 4
 #endif
@@ -312,6 +317,15 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
         constexpr uint64_t KPATH = group_prefix_mask<G>(LMAX), KGE1 = ~group_prefix_mask<G>(1);
         const uint64_t LMASK = group_prefix_mask<G>(L);
         uint64_t amb = 0;  // APX: lanes that saw an ordering closer than the margin
+        if constexpr (APX && Ly::CREG && PSCL_TAIL_NC) {
+            // the clamp-free screening tail (pscl_softplus_tail_scr_nc) needs every tree LLR below
+            // 2^30 in magnitude: a frame with a channel LLR of magnitude >= 2^22, or a NaN, goes
+            // to the exact re-decode (|tree LLR| <= sum of the 128 channel magnitudes)
+            double mx = fabs(creg[0]);
+#pragma unroll
+            for (int m = 1; m < 8; ++m) mx = fmax(mx, fabs(creg[m]));
+            amb = wmask(!(mx < 0x1p22) || creg[0] != creg[0]);
+        }
         // high words of two metrics (non-negative doubles: the words order like the values):
         // b - a <= margin, a < b not certain
         auto near_or_below = [](uint32_t a, uint32_t b) { return (int32_t)(b - a) <= (int32_t)PSCL_SCR_H; };
@@ -500,7 +514,9 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 Lt = pscl_asf64(lpre_up);
             } else {
                 Lt = (PSCL_ABLATE & 1) ? lam * 0.5
-                     : (APX ? ((PSCL_APX_ABLATE & 1) ? fabs(lam) * 0x1p-20 : pscl_softplus_tail_scr(lam)) : pscl_softplus_tail_bf(lam, T));
+                     : (APX ? ((PSCL_APX_ABLATE & 1) ? fabs(lam) * 0x1p-20
+                                                       : (Ly::CREG && PSCL_TAIL_NC ? pscl_softplus_tail_scr_nc(lam) : pscl_softplus_tail_scr(lam)))
+                            : pscl_softplus_tail_bf(lam, T));
             }
             const bool frozen_even = !is_info && !(phi & 1);
             Lpre = Lt;
