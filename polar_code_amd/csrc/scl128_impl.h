@@ -317,14 +317,18 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
         constexpr uint64_t KPATH = group_prefix_mask<G>(LMAX), KGE1 = ~group_prefix_mask<G>(1);
         const uint64_t LMASK = group_prefix_mask<G>(L);
         uint64_t amb = 0;  // APX: lanes that saw an ordering closer than the margin
-        if constexpr (APX && Ly::CREG && PSCL_TAIL_NC) {
-            // the clamp-free screening tail (pscl_softplus_tail_scr_nc) needs every tree LLR below
-            // 2^30 in magnitude: a frame with a channel LLR of magnitude >= 2^22, or a NaN, goes
-            // to the exact re-decode (|tree LLR| <= sum of the 128 channel magnitudes)
-            double mx = fabs(creg[0]);
+        // the clamp-free screening tail (pscl_softplus_tail_scr_nc, L >= 4) needs every tree LLR
+        // below 2^30 in magnitude, and |tree LLR| <= the sum of the frame's 128 channel
+        // magnitudes: each lane sums the magnitudes of the channel LLRs it holds (16 or 8 lanes
+        // of a frame cover all 128), and a frame where a lane's sum reaches 2^25 -- or is NaN
+        // (the sum propagates it) -- goes to the exact re-decode.  L = 8: the lane's 8 registers
+        // here; L = 4: its 16 values at the phase-0 recompute
+        constexpr bool kTailNC = APX && PSCL_TAIL_NC && LMAX >= 4;
+        if constexpr (kTailNC && Ly::CREG) {
+            double cs = fabs(creg[0]);
 #pragma unroll
-            for (int m = 1; m < 8; ++m) mx = fmax(mx, fabs(creg[m]));
-            amb = wmask(!(mx < 0x1p22) || creg[0] != creg[0]);
+            for (int m = 1; m < 8; ++m) cs = cs + fabs(creg[m]);
+            amb = wmask(!(cs < 0x1p25));
         }
         // high words of two metrics (non-negative doubles: the words order like the values):
         // b - a <= margin, a < b not certain
@@ -409,6 +413,14 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     for (int m = 0; m < 8; ++m) {
                         if constexpr (CREG) c[m] = creg[m];  // (G == 16: e == g)
                         else c[m] = CH ? Af[e + 16 * m] : chan[e + 16 * m];
+                    }
+                    if constexpr (kTailNC && !CREG) {  // (the check above, at phase 0)
+                        if (phi == 0) {
+                            double cs = fabs(c[0]);
+#pragma unroll
+                            for (int m = 1; m < 8; ++m) cs = cs + fabs(c[m]);
+                            amb |= wmask(!(cs < 0x1p24));  // (two such sums per lane at G = 8)
+                        }
                     }
                     double d1l[4];
 #pragma unroll
@@ -515,7 +527,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
             } else {
                 Lt = (PSCL_ABLATE & 1) ? lam * 0.5
                      : (APX ? ((PSCL_APX_ABLATE & 1) ? fabs(lam) * 0x1p-20
-                                                       : (Ly::CREG && PSCL_TAIL_NC ? pscl_softplus_tail_scr_nc(lam) : pscl_softplus_tail_scr(lam)))
+                                                       : (kTailNC ? pscl_softplus_tail_scr_nc(lam) : pscl_softplus_tail_scr(lam)))
                             : pscl_softplus_tail_bf(lam, T));
             }
             const bool frozen_even = !is_info && !(phi & 1);

@@ -140,23 +140,25 @@ def test_screening_device_counters_equal_exact():
     assert out[True][2][0] == B
 
 
-def test_screening_huge_llrs_deferred():
-    """L = 8: the screening tail runs without its |v| clamp (pscl_softplus_tail_scr_nc), valid
-    while every tree LLR stays below 2^30, so a frame with a channel LLR of magnitude >= 2^22 is
-    handed to the exact kernel: results equal the exact decode's and the oracle's."""
-    rng = np.random.default_rng(7400)
+@pytest.mark.parametrize("M", [4, 8])
+def test_screening_huge_llrs_deferred(M):
+    """L >= 4: the screening tail runs without its |v| clamp (pscl_softplus_tail_scr_nc), valid
+    while every tree LLR stays below 2^30, so a frame whose channel magnitudes sum to 2^25 or more
+    over one lane's share is handed to the exact kernel: results equal the exact decode's and the
+    oracle's."""
+    rng = np.random.default_rng(7400 + M)
     info = construct_info_set(128, 64)
     B = 4000
     llr = _frames(rng, B, info, 4.0)
     big = np.arange(0, B, 9)
     vals = np.array([2.0 ** 22, -(2.0 ** 22), 1e7, -3e9, 1e15, 2.0 ** 22 - 1.0])
     llr[big, rng.integers(0, 128, size=big.size)] = vals[np.arange(big.size) % vals.size]
-    scr, ex = _pair(128, info, 8)
+    scr, ex = _pair(128, info, M)
     a = _plain(scr, llr)
     _assert_same(a, _plain(ex, llr), "huge LLRs")
-    assert scr.screening_count() >= int(np.sum(np.abs(llr).max(axis=1) >= 2.0 ** 22))
+    assert scr.screening_count() >= int(np.sum(np.abs(llr).max(axis=1) >= 2.0 ** 25))
     for f in big[::5]:
-        n, c, m, il, b = oracle.decode_scl(llr[f], info, 8, crc=POLY)
+        n, c, m, il, b = oracle.decode_scl(llr[f], info, M, crc=POLY)
         assert a["n_paths"][f] == n and a["best_idx"][f] == b, f
         np.testing.assert_array_equal(a["best_bits"][f], c[b], err_msg=f"f={f}")
 
