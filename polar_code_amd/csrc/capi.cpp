@@ -117,7 +117,7 @@ struct pscl_handle {
     int rm_E = 0;                     // NR rate matching (0 = off)
     int32_t* d_rm_src = nullptr;      // [N] de-interleave gather index
     int32_t* d_rm_order = nullptr;    // [N] interleaver order
-    DevBuf scratch[64];
+    DevBuf scratch[80];
     hipStream_t retry_stream[2] = {nullptr, nullptr};  // DL-SCL retry chains of the two chunk parities
     hipStream_t side_stream[2] = {nullptr, nullptr};   // their deferred-entry work (PSCL_DL_SCREEN)
     hipEvent_t ev_scr[2] = {nullptr, nullptr}, ev_def[2] = {nullptr, nullptr};
@@ -134,7 +134,7 @@ struct pscl_handle {
     int screened_slot = 36;
     // pipelined plain decodes (pscl_set_pipelined): a screening decode's exact re-decode runs on
     // pipe_stream and overlaps the caller's next decode; the two alternate scratch parities
-    // (deferred-frame count + list: slots 36/37 and 54/55), and every other entry point, and
+    // (deferred-frame count + list: slots 36/37 and 64/65), and every other entry point, and
     // pscl_join, order the pending re-decodes back into the handle's stream
     bool pipelined = false;
     hipStream_t pipe_stream = nullptr;
@@ -290,7 +290,7 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
         int rc;
         // pipelined: parity p's list may still be read by the re-decode two calls back
         const int p = pipe ? h->pipe_par : 0;
-        const int s_cnt = p ? 54 : 36, s_list = p ? 55 : 37;
+        const int s_cnt = p ? 64 : 36, s_list = p ? 65 : 37;
         if (pipe) {
             if (!h->pipe_stream) {
                 HIP_TRY(create_priority_stream(h, &h->pipe_stream));
