@@ -404,9 +404,6 @@ __device__ __forceinline__ double nr_stage(const double* src, int k, int E, int 
         s = s + src[reps * N + k];
         ++cnt;
     }
-    // a power-of-two count (E = 2N, 4N, ...: every BASELINE repetition) divides exactly by an
-    // exponent shift -- the same correctly rounded quotient without the fp64 division sequence
-    if ((cnt & (cnt - 1)) == 0) return __builtin_amdgcn_ldexp(s, -__builtin_ctz((unsigned)cnt));
     return s / (double)cnt;
 }
 
