@@ -141,7 +141,7 @@ def run_scheme(rng, EbN0_dB, args, info_set, scheme: _Scheme, coded_len, payload
     sym_len = scheme.encode(np.zeros(payload_len, np.int8)).shape[-1]  # symbols per frame
     while stats.bit_errors < args.err_cap and stats.bits_total < args.bits_cap:
         left = max(1, math.ceil((args.bits_cap - stats.bits_total) / payload_len))
-        B = int(min(args.batch, left))
+        B = int(min(args.batch or 4096, left))
         state = rng.bit_generator.state
         payload = np.empty((B, payload_len), np.int8)
         noise = np.empty((B, sym_len))
@@ -253,7 +253,10 @@ def run_scheme_philox(source, EbN0_dB, args, coded_len, payload_len, params_labe
     frame = 0  # next global frame index of this SNR point
     while stats.bit_errors < args.err_cap and stats.bits_total < args.bits_cap:
         left = max(1, math.ceil((args.bits_cap - stats.bits_total) / payload_len))
-        total = int(min(args.batch * ctx.world, left))
+        # philox: 2^16 frames per GPU per round by default -- a round's fixed cost (launches, the
+        # all-gather, the host copy of per-frame errors) outweighs decoding a few thousand frames,
+        # and the stop frame is exact whatever the round size (rows identical at any batch)
+        total = int(min((args.batch or (1 << 16)) * ctx.world, left))
         s, e = dist.shard(total, ctx.rank, ctx.world)
         bit_err, work = source.frames(args.seed, EbN0_dB, frame + s, e - s)
         part = np.array([e - s, bit_err.sum(), np.count_nonzero(bit_err), work.sum()], np.float64)
@@ -311,7 +314,8 @@ def parse_args(argv: Optional[Iterable[str]] = None) -> argparse.Namespace:
     parser.add_argument("--out", type=str, required=True, help="CSV output path")
     parser.add_argument("--plot", type=str, help="Optional plot path")
     # engine options (not in the reference)
-    parser.add_argument("--batch", type=int, default=4096, help="frames per GPU batch")
+    parser.add_argument("--batch", type=int, default=None,
+                        help="frames per GPU batch (default 4096 with --rng replay, 2^16 with philox)")
     parser.add_argument("--device", type=int, default=0, help="GPU (single process; torchrun ranks use LOCAL_RANK)")
     parser.add_argument("--rng", choices=["replay", "philox"], default="replay",
                         help="replay: the reference's NumPy stream, exact rows, one process; philox: frames "
