@@ -231,6 +231,49 @@ def test_pipelined_dlscl_calls_equal_stream_ordered(L):
     assert c[0][0] == nb * B and c[1][1] <= c[0][1] and (res[True][0][0][2] > 1).sum() > 1000
 
 
+@pytest.mark.parametrize("N,K,E,L", [(128, 88, 256, 8), (256, 128, 0, 4)])
+def test_pipelined_dlscl_rate_matched_and_long(N, K, E, L):
+    """Pipelined DL-SCL calls on the NR (128,88) code rate matched to E = 256 (config 5's code)
+    and on a long code (N = 256: HIST retry decodes, dense per-pass state on one chain): four
+    calls on two alternating output buffers equal the stream-ordered calls (bits, flags,
+    attempts of the last two calls; SCL/DL counters of all four)."""
+    from polar_code_amd.polar.polar import construct_info_set
+
+    info = construct_info_set(N, K)
+    kp, n_in = K - 24, (E or N)
+    B, nb, nc = 6000, 4, _native.PSCL_NCOUNT
+    res = {}
+    for pipe in (True, False):
+        dec = _native.Decoder(N, info, L, "0x1864CFB")
+        if E:
+            dec.set_rate_match(E)
+        dec.set_pipelined(pipe)
+        with _native.DeviceArena(dec) as mem:
+            d_llr = [mem.alloc(B * n_in * 8) for _ in range(nb)]
+            d_msg = [mem.alloc(B * 16) for _ in range(nb)]
+            d_out = [(mem.alloc(B * 16), mem.alloc(B), mem.alloc(B * 4)) for _ in range(2)]
+            d_cnt = mem.alloc(2 * nc * 8)
+            mem.memset(d_cnt, 0, 2 * nc * 8)
+            rate = kp / E if E else K / N
+            for i in range(nb):
+                dec.channel_device(9, 70 + i, 1.0 + 0.5 * i, rate, kp, i * B, B, d_llr[i], d_msg[i])
+            for i in range(nb):
+                o = d_out[i & 1]
+                dec.dlscl_device(d_llr[i], B, 8, d_best=o[0], d_flags=o[1], d_attempts=o[2], d_ref=d_msg[i],
+                                 k_payload=kp, d_counters_scl=d_cnt, d_counters_dl=d_cnt + nc * 8)
+            dec.join()
+            res[pipe] = ([(mem.download(b, B * 16, np.uint64), mem.download(f, B, np.uint8),
+                           mem.download(a, B * 4, np.int32)) for b, f, a in d_out],
+                         mem.download(d_cnt, 2 * nc * 8, np.int64).reshape(2, nc))
+        dec.close()
+    for i in range(2):
+        for k, name in enumerate(("best", "flags", "attempts")):
+            np.testing.assert_array_equal(res[True][0][i][k], res[False][0][i][k], err_msg=f"{name}, buffer {i}")
+    np.testing.assert_array_equal(res[True][1], res[False][1], err_msg="counters")
+    c = res[True][1]
+    assert c[0][0] == nb * B and c[1][5] > 100  # retries ran
+
+
 def test_simulate_one_call_equals_separate_calls():
     """pscl_simulate (TX + uncoded + SCL + DL-SCL + counters in one call) equals the separate
     device calls over the same frames, and frame ranges add up exactly."""
