@@ -169,7 +169,8 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 #define PSCL_LEAF_BLEND 0
 #endif
 
-// L = 8 screening: the metric tail without the |v| clamp, frames with channel LLRs >= 2^22 deferred
+// L >= 4 screening: the metric tail without the |v| clamp; frames whose channel magnitudes could
+// push a tree LLR to 2^30 are deferred (the check at the frame's start, below)
 #ifndef PSCL_TAIL_NC
 #define PSCL_TAIL_NC 1
 #endif
