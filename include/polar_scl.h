@@ -238,6 +238,8 @@ int pscl_simulate(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno
                   int64_t frame0, int64_t B, int retries, int include_uncoded, int64_t* counters);
 
 int pscl_device_alloc(pscl_handle* h, void** d_ptr, int64_t bytes);
+/* (pscl_device_free first orders and completes the handle's pending pipelined work, which may
+ * still use the buffer) */
 int pscl_device_free(pscl_handle* h, void* d_ptr);
 int pscl_memcpy_htod(pscl_handle* h, void* d_dst, const void* src, int64_t bytes);
 int pscl_memcpy_dtoh(pscl_handle* h, void* dst, const void* d_src, int64_t bytes);
@@ -275,8 +277,31 @@ int pscl_screening_count(pscl_handle* h, int64_t* count);
  * screening launch only.
  */
 int pscl_set_pipelined(pscl_handle* h, int enable);
-/* Order the pending pipelined re-decodes into the handle's stream (no host wait). */
+/* Order the pending pipelined re-decodes into the handle's stream (no host wait on the plain
+ * decodes' re-decodes; a pending pipelined DL-SCL call's chains are enqueued here, which waits for
+ * that call's baseline decode on the host to read its failing-frame count). */
 int pscl_join(pscl_handle* h);
+
+/*
+ * Tuning and test knobs of one handle (value 0 restores the default, which is the measured best
+ * schedule).  The library reads no environment variables: a knob changes only
+ * the handle it is set on, never a result (every schedule is bit-identical).  Pending pipelined
+ * work is ordered first.  PSCL_EINVAL for an unknown knob or a value out of range.
+ *   PSCL_TUNE_DL_SCREEN     1: DL-SCL retry decodes on the forced-bit screening instance
+ *   PSCL_TUNE_DL_CHUNKS     1..64: baseline chunks of a DL-SCL call (default 1)
+ *   PSCL_TUNE_DL_SPLIT      1..2: retry chains per chunk (default 2)
+ *   PSCL_TUNE_SIDE_PRIORITY 1: a pipelined handle's side streams at normal priority (default high)
+ *   PSCL_TUNE_POST_GRID     16..4096: workgroup cap of the DL-SCL post pass (default 512)
+ *   PSCL_TUNE_RETRY_WPG     1..4: wavefronts per workgroup of the retry decodes (default: by LDS)
+ */
+#define PSCL_TUNE_DL_SCREEN 1
+#define PSCL_TUNE_DL_CHUNKS 2
+#define PSCL_TUNE_DL_SPLIT 3
+#define PSCL_TUNE_SIDE_PRIORITY 4
+#define PSCL_TUNE_POST_GRID 5
+#define PSCL_TUNE_RETRY_WPG 6
+#define PSCL_TUNE_COUNT 7
+int pscl_set_tuning(pscl_handle* h, int knob, int64_t value);
 
 /*
  * Diagnostic: the metric tail log1p(exp(-|v|)) (scl.py:102-105) of n device values, evaluated
@@ -284,6 +309,14 @@ int pscl_join(pscl_handle* h);
  * decode's bounded-error form.  Device buffers, handle stream.
  */
 int pscl_softplus_tails_device(pscl_handle* h, const double* d_v, int64_t n, double* d_exact, double* d_apx);
+
+/*
+ * Diagnostic (the screening margin's proof obligation): the absolute error of the screening
+ * metric tail against the bit-exact glibc port for every fp32 bit pattern x32 in [lo, hi].
+ * d_out[2] (device, zeroed by the caller): d_out[0] = fp64 bits of the largest error, d_out[1]
+ * = (its high word << 32) | the x32 bit pattern of the largest error.  Handle stream.
+ */
+int pscl_tail_abs_scan_device(pscl_handle* h, uint32_t lo, uint32_t hi, uint64_t* d_out);
 
 /*
  * Kernel timing with HIP events recorded on the launch stream around every decode kernel

@@ -112,8 +112,8 @@ class SCLDecoder:
     SCLDecoder(N, info_set, L, crc_poly="0x1864CFB", device=0).decode(llr[B, N]) returns a dict
     with bits [B, K] int8 (each frame's best_path_bits), crc_pass [B] bool, best_idx [B] and
     n_paths [B]; with metrics / candidates / info_llrs=True also metrics [B, L] (list order),
-    cands [B, L, K] and info_llrs [B, L, K].  forced: None or [B, K] 0/1 (force_info_bits per
-    frame).  One pscl_decode call per batch.
+    cands [B, L, K] and info_llrs [B, L, K].  forced: None or [B, K] int8 in {-1, 0, 1}
+    (force_info_bits per frame: -1 free, 0/1 forced, scl.py:131-133).  One pscl_decode call per batch.
     """
 
     def __init__(self, N: int, info_set, L: int, crc_poly="0x1864CFB", device: int = 0):

@@ -41,7 +41,11 @@ EXPORTS = (
     "pscl_timing_read", "pscl_launch_info", "pscl_set_rate_match", "pscl_set_beta", "pscl_dlscl_device",
     "pscl_path_llrs_device", "pscl_uncoded_device", "pscl_simulate", "pscl_set_screening", "pscl_build_hash",
     "pscl_screening_count", "pscl_softplus_tails_device", "pscl_set_pipelined", "pscl_join",
+    "pscl_tail_abs_scan_device", "pscl_set_tuning",
 )
+
+# pscl_set_tuning knobs (include/polar_scl.h)
+TUNE = {"dl_screen": 1, "dl_chunks": 2, "dl_split": 3, "side_priority": 4, "post_grid": 5, "retry_wpg": 6}
 
 _vp, _i32, _i64, _u64, _dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
 
@@ -98,6 +102,8 @@ def lib() -> C.CDLL:
         "pscl_set_pipelined": (C.c_int, [_vp, C.c_int]),
         "pscl_join": (C.c_int, [_vp]),
         "pscl_softplus_tails_device": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
+        "pscl_tail_abs_scan_device": (C.c_int, [_vp, C.c_uint32, C.c_uint32, _vp]),
+        "pscl_set_tuning": (C.c_int, [_vp, C.c_int, _i64]),
         "pscl_device_count": (C.c_int, []),
         "pscl_create": (C.c_int, [P(_vp), C.c_int, C.c_int, P(_i32), C.c_int, C.c_int, _u64]),
         "pscl_destroy": (C.c_int, [_vp]),
@@ -356,14 +362,36 @@ class Decoder:
             check(lib().pscl_softplus_tails_device(self._h, d_v, v.size, d_e, d_a))
             return mem.download(d_e, v.nbytes, np.float64), mem.download(d_a, v.nbytes, np.float64)
 
+    def tail_abs_scan(self, lo: int = 0, hi: int = 0x7F800000):
+        """Largest |screening tail - exact tail| over the fp32 bit patterns [lo, hi] and the x32
+        where it occurs (pscl_tail_abs_scan_device; the default range is every x32 >= 0)."""
+        with DeviceArena(self) as mem:
+            d = mem.alloc(16)
+            mem.memset(d, 0, 16)
+            check(lib().pscl_tail_abs_scan_device(self._h, int(lo), int(hi), d))
+            out = mem.download(d, 16, np.uint64)
+        err = float(out[:1].view(np.float64)[0])
+        x32 = float(np.array([int(out[1]) & 0xFFFFFFFF], np.uint32).view(np.float32)[0])
+        return err, x32
+
     def set_pipelined(self, on: bool = True) -> None:
         """Throughput mode for streams of plain decodes (include/polar_scl.h): a screening
         decode's exact re-decode overlaps the next decode; join() / sync() order it back."""
         check(lib().pscl_set_pipelined(self._h, 1 if on else 0))
 
     def join(self) -> None:
-        """Order pending pipelined re-decodes into the handle's stream (no host wait)."""
+        """Order pending pipelined work into the handle's stream: the plain decodes' re-decodes
+        without a host wait; a pending pipelined DL-SCL call's chains are enqueued here, which
+        waits on the host for that call's baseline decode (its failing-frame count)."""
         check(lib().pscl_join(self._h))
+
+    def set_tuning(self, **knobs) -> None:
+        """Schedule knobs of this handle (pscl_set_tuning; 0 = default): dl_screen, dl_chunks,
+        dl_split, side_priority, post_grid, retry_wpg.  Results never depend on them."""
+        for k, v in knobs.items():
+            if k not in TUNE:
+                raise ValueError(f"unknown tuning knob {k!r}")
+            check(lib().pscl_set_tuning(self._h, TUNE[k], int(v)))
 
     def set_screening(self, on: bool = True) -> None:
         """Screening decode for plain decodes (default on; include/polar_scl.h)."""

@@ -119,7 +119,7 @@ struct pscl_handle {
     int32_t* d_rm_order = nullptr;    // [N] interleaver order
     DevBuf scratch[80];
     hipStream_t retry_stream[2] = {nullptr, nullptr};  // DL-SCL retry chains of the two chunk parities
-    hipStream_t side_stream[2] = {nullptr, nullptr};   // their deferred-entry work (PSCL_DL_SCREEN)
+    hipStream_t side_stream[2] = {nullptr, nullptr};   // their deferred-entry work (PSCL_TUNE_DL_SCREEN)
     hipEvent_t ev_scr[2] = {nullptr, nullptr}, ev_def[2] = {nullptr, nullptr};
     hipEvent_t ev_base[2] = {nullptr, nullptr}, ev_retry[2] = {nullptr, nullptr}, ev_join = nullptr;
     int32_t* h_count = nullptr;          // pinned: failing-frame counts of the two chunk parities
@@ -151,6 +151,7 @@ struct pscl_handle {
     bool dl_defer_valid = false;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
+    int64_t tune[PSCL_TUNE_COUNT] = {};  // pscl_set_tuning knobs (0 = the default schedule)
 };
 
 namespace {
@@ -212,6 +213,19 @@ void quiesce(pscl_handle* h) {
     }
 }
 
+// destroy the side streams (after draining them) so the next use creates them with the priority
+// the handle's current mode asks for (create_priority_stream)
+void drop_side_streams(pscl_handle* h) {
+    quiesce(h);
+    if (h->pipe_stream) hipStreamDestroy(h->pipe_stream);
+    h->pipe_stream = nullptr;
+    for (int i = 0; i < 2; ++i) {
+        if (h->retry_stream[i]) hipStreamDestroy(h->retry_stream[i]);
+        if (h->side_stream[i]) hipStreamDestroy(h->side_stream[i]);
+        h->retry_stream[i] = h->side_stream[i] = nullptr;
+    }
+}
+
 // a side stream; on a pipelined handle of the highest priority: latency-bound chains (retry
 // rounds, deferred re-decodes) take workgroup slots ahead of the next call's throughput-bound
 // baseline decode (measured, config 4 pipelined: 3.55 ms against 4.0 at equal priority).  Not
@@ -219,7 +233,7 @@ void quiesce(pscl_handle* h) {
 hipError_t create_priority_stream(pscl_handle* h, hipStream_t* s) {
     int least = 0, greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = least = 0;
-    static const bool plain = getenv("PSCL_PRIO") && atoi(getenv("PSCL_PRIO")) == 0;  // tuning override
+    const bool plain = h->tune[PSCL_TUNE_SIDE_PRIORITY] == 1;  // (tuning knob: normal priority)
     return hipStreamCreateWithPriority(s, hipStreamNonBlocking, h->pipelined && !plain ? greatest : least);
 }
 
@@ -641,7 +655,22 @@ int pscl_set_pipelined(pscl_handle* h, int enable) {
     int rc = set_device(h);
     if (rc) return rc;
     if ((rc = join_pipe(h))) return rc;
+    if (h->pipelined != (enable != 0)) drop_side_streams(h);
     h->pipelined = enable != 0;
+    return PSCL_OK;
+}
+
+int pscl_set_tuning(pscl_handle* h, int knob, int64_t value) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    static const int64_t lim[PSCL_TUNE_COUNT][2] = {{0, 0}, {0, 1}, {0, 64}, {0, 2}, {0, 1}, {0, 4096}, {0, PSCL_MAX_WAVES_PER_WG}};
+    if (knob < 1 || knob >= PSCL_TUNE_COUNT) return fail(PSCL_EINVAL, "unknown tuning knob %d", knob);
+    if (value < lim[knob][0] || value > lim[knob][1] || (knob == PSCL_TUNE_POST_GRID && value && value < 16))
+        return fail(PSCL_EINVAL, "tuning knob %d: value %lld out of range", knob, (long long)value);
+    int rc = set_device(h);
+    if (rc) return rc;
+    if ((rc = join_pipe(h))) return rc;  // (pending work ran under the old schedule)
+    if (knob == PSCL_TUNE_SIDE_PRIORITY && h->tune[knob] != value) drop_side_streams(h);
+    h->tune[knob] = value;
     return PSCL_OK;
 }
 
@@ -737,6 +766,7 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     Q.exp_table = h->d_exp_table;
     Q.rounds = rounds;
     Q.narrow = narrow ? 1 : 0;  // (pipelined calls: beside the next call's baseline)
+    Q.grid_cap = h->tune[PSCL_TUNE_POST_GRID];
     Q.cap = A;
     Q.act = S.act;
     Q.tried = S.tried;
@@ -773,14 +803,15 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     H.bcap = A;
     H.warm_metric = S.warm_metric;
     H.warm_u = S.warm_u;
+    H.wpg_cap = (int)h->tune[PSCL_TUNE_RETRY_WPG];
     if (pscl_decode_wpg(H) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
     int rc;
-    // screening retry decodes (PSCL_DL_SCREEN=1, measured in DESIGN.md §5.1b): the forced-bit
+    // screening retry decodes (tuning knob PSCL_TUNE_DL_SCREEN = 1, measured in DESIGN.md §5.1b): the forced-bit
     // screening instance decodes the round's entries and files the ones it cannot certify in
     // bucket lists of their own (flags PSCL_DL_DEFERRED, which the post pass skips); on the side
     // stream the exact kernel decodes those (warm-started, as every retry decode) and a second
     // post pass handles them, overlapping the main post pass
-    const bool dl_screen = getenv("PSCL_DL_SCREEN") && atoi(getenv("PSCL_DL_SCREEN")) == 1;
+    const bool dl_screen = h->tune[PSCL_TUNE_DL_SCREEN] == 1;
     const bool scr = dl_screen && h->screen && S.dcnt && S.ob2 && side && pscl_screening_fs_available(H);
     pscl_decode_params HA, HX;
     pscl_post_params QD;
@@ -1096,22 +1127,16 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
     a.d_ref = d_ref;
     a.k_payload = k_payload;
     a.d_counters_dl = d_counters_dl;
-    // Chunks (PSCL_DL_CHUNKS, default 1): the baseline decodes run in order on the handle's
+    // Chunks (tuning knob PSCL_TUNE_DL_CHUNKS, default 1): the baseline decodes run in order on the handle's
     // stream; the retry entries of chunk c are split over two chains, each on its own retry
     // stream with its own state, so the two chains' rounds overlap each other (and chunk c + 1's
     // baseline decode).  A round is latency-bound (a few 10^4 entries per launch), so a second
-    // concurrent chain fills what one leaves idle.  PSCL_DL_SPLIT (1 or 2, default 2) sets the
+    // concurrent chain fills what one leaves idle.  PSCL_TUNE_DL_SPLIT (1 or 2, default 2) sets the
     // chains per chunk; chunks below 2 * kMinSplit failing frames keep one chain.
     a.nch = 1;
     a.nsplit = h->N > PSCL_FAST_N ? 0 : 2;
-    if (rounds > 0 && getenv("PSCL_DL_CHUNKS")) {  // tuning override
-        const long v = atol(getenv("PSCL_DL_CHUNKS"));
-        if (v >= 1 && v <= 64) a.nch = v;
-    }
-    if (rounds > 0 && h->N <= PSCL_FAST_N && getenv("PSCL_DL_SPLIT")) {  // tuning override
-        const long v = atol(getenv("PSCL_DL_SPLIT"));
-        if (v >= 1 && v <= 2) a.nsplit = (int)v;
-    }
+    if (rounds > 0 && h->tune[PSCL_TUNE_DL_CHUNKS]) a.nch = h->tune[PSCL_TUNE_DL_CHUNKS];
+    if (rounds > 0 && h->N <= PSCL_FAST_N && h->tune[PSCL_TUNE_DL_SPLIT]) a.nsplit = (int)h->tune[PSCL_TUNE_DL_SPLIT];
     a.cap = (B + a.nch - 1) / a.nch;
     // Pipelined (pscl_set_pipelined, one chunk): the call enqueues its baseline, then the retry
     // chains of the PREVIOUS pipelined call (whose baseline has ended or is about to: the host
@@ -1417,7 +1442,12 @@ int pscl_device_alloc(pscl_handle* h, void** d_ptr, int64_t bytes) {
 
 int pscl_device_free(pscl_handle* h, void* d_ptr) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
-    if (h->pipe_stream) HIP_TRY(hipStreamSynchronize(h->pipe_stream));  // (a pending re-decode's buffers)
+    // pending pipelined work may still read or write the buffer (a deferred DL-SCL call's chains
+    // hold its LLR, output, reference and counter pointers): enqueue it, then drain every stream
+    int rc = enter(h);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    quiesce(h);
     if (d_ptr) HIP_TRY(hipFree(d_ptr));
     return PSCL_OK;
 }
@@ -1476,6 +1506,17 @@ int pscl_softplus_tails_device(pscl_handle* h, const double* d_v, int64_t n, dou
     if (rc) return rc;
     hipError_t e = pscl_launch_softplus_tails(d_v, n, h->d_exp_table, d_exact, d_apx, h->stream);
     if (e != hipSuccess) return fail(PSCL_EDEVICE, "softplus tails launch: %s", hipGetErrorString(e));
+    return PSCL_OK;
+}
+
+int pscl_tail_abs_scan_device(pscl_handle* h, uint32_t lo, uint32_t hi, uint64_t* d_out) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    if (!d_out) return fail(PSCL_EINVAL, "d_out is required");
+    if (lo > hi) return fail(PSCL_EINVAL, "lo > hi");
+    int rc = enter(h);
+    if (rc) return rc;
+    hipError_t e = pscl_launch_tail_abs_scan(lo, hi, h->d_exp_table, reinterpret_cast<unsigned long long*>(d_out), h->stream);
+    if (e != hipSuccess) return fail(PSCL_EDEVICE, "tail scan launch: %s", hipGetErrorString(e));
     return PSCL_OK;
 }
 

@@ -697,8 +697,7 @@ hipError_t pscl_launch_dl_post(const pscl_post_params& Q, int64_t entries, hipSt
     // workgroups of PW wavefronts (2 PW entries in flight)
     const int PW = Q.narrow ? kPostWavesNarrow : kPostWavesWide;
     int64_t grid = (entries + PW * 8 - 1) / (PW * 8);
-    static const int64_t cap_env = getenv("PSCL_POST_GRID") ? atol(getenv("PSCL_POST_GRID")) : 0;  // tuning override
-    const int64_t gcap = cap_env >= 16 && cap_env <= 4096 ? cap_env : PSCL_POST_GRID;
+    const int64_t gcap = Q.grid_cap >= 16 && Q.grid_cap <= 4096 ? Q.grid_cap : PSCL_POST_GRID;  // (tuning knob)
     if (grid > gcap) grid = gcap;
     const int beta_lds = PSCL_POST_BETA_LDS && !Q.narrow && Q.beta && (size_t)Q.K * Q.K * 8 <= 32 * 1024;  // (LDS <= 64 KB)
     const size_t lds = beta_lds ? (size_t)Q.K * Q.K * 8 : 0;

@@ -452,8 +452,9 @@ __device__ __forceinline__ double pscl_ldexp_f64(double a, int e) { return __bui
 
 /* the screening tail of x = |v| without the clamp: valid while k = round(x log2 e) fits the
  * 32-bit exponent arithmetic, i.e. |v| < 2^30 (the result is then the clamped form's: both are
- * 0 above 745.2).  The decode kernel that uses it defers every frame with a channel LLR of
- * magnitude >= 2^22 (or NaN), which bounds every tree LLR by 128 * 2^22 = 2^29 */
+ * 0 above 745.2).  The decode kernel that uses it (PSCL_TAIL_ABS = 0 builds) defers every frame
+ * where one lane's share of the channel magnitudes sums to 2^25 or more (2^24 per half-share at
+ * L = 4), or to NaN: every tree LLR is then below 16 * 2^25 = 2^29 */
 PSCL_HD double pscl_softplus_tail_scr_nc(double v) {
     const double x = fabs(v);
     const double kd0 = pscl_fma(-x, PSCL_INVLN2, PSCL_EXP_SHIFT); /* low word = -k */
@@ -475,6 +476,61 @@ PSCL_HD double pscl_softplus_tail_scr_nc(double v) {
 }
 
 PSCL_HD double pscl_softplus_tail_scr(double v) { return pscl_softplus_tail_scr_nc(pscl_absmin(v, 4096.0)); }
+
+/*
+ * Screening tail with an ABSOLUTE error bound (round 4; the screening kernels' default,
+ * PSCL_TAIL_ABS): L = log1p(exp(-x)), x = |v|, in seven instructions, all fp32 after the
+ * conversion:
+ *
+ *   x32 = fl32(|v|)                     v_cvt_f32_f64 with |.| (inf for |v| > FLT_MAX)
+ *   t   = 2^(-x32 log2 e)               v_mul_f32, v_exp_f32 (0 once the exponent passes -150)
+ *   L   = log2(1 + t) ln 2              v_add_f32, v_log_f32, v_mul_f32, v_cvt_f64_f32
+ *
+ * Relative accuracy is lost (t's exponent carries fl32 roundings of x log2 e; 1 + t rounds to
+ * 2^-24), but the error is small in absolute terms everywhere, which is all the ordering
+ * certificates need: every comparison the screening pass makes involves a metric of at least
+ * ln 2 (a worse child pays |lam| + L >= ln 2; two distinct paths diverged where one took a
+ * worse child), and a metric is a sum of at most N = 128 increments, so its error is at most
+ * 128 * PSCL_TAIL_ABS_DELTA plus the fp64 summation error (relative, N * 2^-53).
+ *
+ * The bound is measured, not assumed: pscl_tail_abs_f32 is a function of the fp32 value x32
+ * alone, and tools/tests scan EVERY non-negative fp32 x32 (2^31 - 2^23 values, +inf included) on
+ * the device against the bit-exact glibc port (pscl_tail_abs_scan_device,
+ * tests/test_gpu_screening.py::test_tail_abs_exhaustive_device): max |L(x32) - glibc(x32)|
+ * = PSCL_TAIL_ABS_SCAN.  For fp64 x the conversion adds |x32 - x| * max|dL/dx| <=
+ * 2^-24 x e^-x / (1 + e^-x) <= 0.2785 * 2^-24, and glibc(x32) vs glibc(x) one ulp each
+ * (< 2^-52): PSCL_TAIL_ABS_DELTA bounds the sum.
+ */
+#ifndef PSCL_TAIL_ABS
+#define PSCL_TAIL_ABS 1
+#endif
+#define PSCL_LOG2E_F32 1.44269504088896341f
+#define PSCL_LN2_F32 0.693147180559945309f
+/* upper bound of the exhaustive device scan (see above; the measured value is in DESIGN.md §5.1a) */
+#ifndef PSCL_TAIL_ABS_SCAN
+#define PSCL_TAIL_ABS_SCAN (3.0 / 16777216.0)
+#endif
+#define PSCL_TAIL_ABS_DELTA (PSCL_TAIL_ABS_SCAN + 0.2785 / 16777216.0 + 2.0 * 2.220446049250313e-16)
+/* certificate margin: two metrics' errors (2 * 128 * delta), rounded up */
+#define PSCL_TAIL_ABS_MARGIN (2.0 * 128.0 * PSCL_TAIL_ABS_DELTA * 1.0001)
+
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ float pscl_log2_f32(float a) { return __builtin_amdgcn_logf(a); }
+__device__ __forceinline__ float pscl_cvt_abs_f32(double v) {
+    float r;
+    asm("v_cvt_f32_f64 %0, |%1|" : "=v"(r) : "v"(v));
+    return r;
+}
+#else
+#define pscl_log2_f32(a) log2f(a)
+#define pscl_cvt_abs_f32(v) ((float)fabs(v))
+#endif
+
+PSCL_HD float pscl_tail_abs_f32(float x32) {
+    const float t = pscl_exp2_f32(x32 * -PSCL_LOG2E_F32);
+    return pscl_log2_f32(1.0f + t) * PSCL_LN2_F32;
+}
+PSCL_HD double pscl_softplus_tail_abs(double v) { return (double)pscl_tail_abs_f32(pscl_cvt_abs_f32(v)); }
 
 /* L = log1p(exp(-|v|)), the part of logaddexp(0, +-v) shared by both bit hypotheses. */
 PSCL_HD double pscl_softplus_tail(double v, const uint64_t* T) {

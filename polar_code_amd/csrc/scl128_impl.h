@@ -335,6 +335,11 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
         // b - a <= margin, a < b not certain
         auto near_or_below = [](uint32_t a, uint32_t b) { return (int32_t)(b - a) <= (int32_t)PSCL_SCR_H; };
         auto hiw = [](double m) { return (uint32_t)(pscl_asu64(m) >> 32); };
+        // PSCL_TAIL_ABS: the tail's error is absolute (glibc_softplus.h), so an ordering a < b of
+        // two screening metrics is certain when b exceeds a by the absolute margin plus a relative
+        // 2^-40 for the fp64 summation: hi(b) > hi(up(a)), up(a) = a (1 + 2^-40) + margin (one fma;
+        // the high words of non-negative doubles order like the values)
+        auto hiw_up = [&](double m) { return hiw(__builtin_fma(m, 1.0 + 0x1p-40, PSCL_TAIL_ABS_MARGIN)); };
 
         // phase body, specialised on t = phi mod 16 (the subtree shape of the phase is fixed by
         // t); blk = phi / 16 is a compile-time constant too in the CODE != 0 kernels
@@ -528,7 +533,8 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
             } else {
                 Lt = (PSCL_ABLATE & 1) ? lam * 0.5
                      : (APX ? ((PSCL_APX_ABLATE & 1) ? fabs(lam) * 0x1p-20
-                                                       : (kTailNC ? pscl_softplus_tail_scr_nc(lam) : pscl_softplus_tail_scr(lam)))
+                                                       : (PSCL_TAIL_ABS ? pscl_softplus_tail_abs(lam)
+                                                          : (kTailNC ? pscl_softplus_tail_scr_nc(lam) : pscl_softplus_tail_scr(lam))))
                             : pscl_softplus_tail_bf(lam, T));
             }
             const bool frozen_even = !is_info && !(phi & 1);
@@ -586,13 +592,14 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     // full list: the better children survive when every worse child exceeds the
                     // largest better child by the margin (group max of the high words over
                     // duplicated keys)
-                    uint32_t mx = merge_from_lower<G, LMAX>(hiw(mg), hiw(mg), lane);
+                    const uint32_t kx = PSCL_TAIL_ABS ? hiw_up(mg) : hiw(mg);
+                    uint32_t mx = merge_from_lower<G, LMAX>(kx, kx, lane);
                     static_for<Ly::LOG_LM>([&](auto SC) {
                         constexpr int S = 1 << decltype(SC)::value;
                         const uint32_t o = grot32c<G, S>(mx, lane);
                         mx = o > mx ? o : mx;
                     });
-                    const uint64_t badm = wmask(near_or_below(mx, hiw(mb)));
+                    const uint64_t badm = wmask(PSCL_TAIL_ABS ? hiw(mb) <= mx : near_or_below(mx, hiw(mb)));
 #ifdef PSCL_STATS  // screening full-list info phases by the wave's worst frame: worse children
                    // within the margin of the largest better child (0, 1, 2, >= 3) -> slots 12..15
                     if (lane == 0 && P.counters) {
@@ -629,7 +636,8 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                     const uint64_t claim = group_prefix_mask<G>(L + 1);
                     const uint64_t bnd = claim & ~group_prefix_mask<G>(L);
                     const uint32_t nmh = (uint32_t)(nm >> 32);
-                    amb |= ((wmask(rr != (uint32_t)g) & claim) | (wmask(near_or_below(prev_lane32(nmh), nmh)) & bnd)) & vmask;
+                    const bool bnear = PSCL_TAIL_ABS ? nmh <= prev_lane32(hiw_up(pscl_asf64(nm))) : near_or_below(prev_lane32(nmh), nmh);
+                    amb |= ((wmask(rr != (uint32_t)g) & claim) | (wmask(bnear) & bnd)) & vmask;
 #ifdef PSCL_DEBUG_AMB
                     {
                         const uint64_t cm = wmask(rr != (uint32_t)g) & claim & vmask, bm = wmask(near_or_below(prev_lane32(nmh), nmh)) & bnd & vmask;
@@ -858,8 +866,16 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
             const int c = __builtin_amdgcn_ds_permute((gbase + (g & LMAX) + (int)(r & (LMAX - 1))) << 2, g) & (G - 1);
             const uint32_t rr = bperm32(r, gbase + c);
             const uint32_t nh = bperm32(kh, gbase + c);
+            bool fnear;
+            if constexpr (PSCL_TAIL_ABS) {
+                uint32_t ku = g < cnt ? hiw_up(metric) : 0x7ff00000u;
+                ku = merge_from_lower<G, LMAX>(ku, ku, lane);
+                fnear = nh <= prev_lane32(bperm32(ku, gbase + c));
+            } else {
+                fnear = near_or_below(prev_lane32(nh), nh);
+            }
             const uint64_t live = kFixedList ? group_prefix_mask<G>(cnt) : wmask(g < cnt);
-            amb |= ((wmask(rr != (uint32_t)g) & live) | (wmask(near_or_below(prev_lane32(nh), nh)) & live & KGE1)) & vmask;
+            amb |= ((wmask(rr != (uint32_t)g) & live) | (wmask(fnear) & live & KGE1)) & vmask;
 #ifdef PSCL_DEBUG_AMB
             if (f0 == 0 && lane < 16) printf("final lane %d r %u c %d rr %u kh %08x nh %08x prev %08x\n", lane, r, c, rr, kh, nh, prev_lane32(nh));
 #endif

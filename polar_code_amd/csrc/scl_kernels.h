@@ -57,6 +57,7 @@ struct pscl_decode_params {
     int32_t* amb_elist;          // or (bucket-list launches): [NSEG][bcap] entry ids by bucket, appended
                                  // instead (amb_count then [NSEG * CSTRIDE]); their flags PSCL_DL_DEFERRED
     int out_by_row;              // 1: outputs, reference words and counts at LLR row fidx[b]
+    int wpg_cap;                 // 0, or an upper bound on the wavefronts per workgroup (tuning knob)
     int64_t grid_cap;            // 0, or an upper bound on the workgroups of the launch (the
                                  // kernels stride over frames; a d_count launch of few frames)
     // code lengths above 128 (scl_long.hip): information set as N/64 words, and the global
@@ -135,6 +136,7 @@ struct pscl_post_params {
     const uint64_t* exp_table;   // glibc exp table (exact metric tails)
     int rounds;                  // min(retries, K)
     int narrow;                  // small workgroups, beta through L2 (pipelined calls, dl_post_kernel)
+    int64_t grid_cap;            // 0, or the workgroup cap of a launch (tuning knob; default PSCL_POST_GRID)
     int init;
     const int32_t* in_count;     // bucket counts of this round (init: unused, cap entries)
     const int32_t* in_list;      // bucket lists of this round ([NSEG][cap] entry ids)
@@ -220,6 +222,8 @@ hipError_t pscl_launch_dl_compact(const uint8_t* flags, int64_t B, int64_t base,
                                   int32_t* count, hipStream_t s);
 hipError_t pscl_launch_iota64(int64_t* out, int64_t n, hipStream_t s);
 hipError_t pscl_launch_replay(const pscl_replay_params& R, int64_t cap, hipStream_t s);
+hipError_t pscl_launch_tail_abs_scan(uint32_t lo, uint32_t hi, const uint64_t* exp_table, unsigned long long* out,
+                                     hipStream_t s);
 hipError_t pscl_launch_softplus_tails(const double* v, int64_t n, const uint64_t* exp_table, double* exact,
                                      double* apx, hipStream_t s);
 hipError_t pscl_launch_dl_post(const pscl_post_params& Q, int64_t entries, hipStream_t s);

@@ -431,9 +431,8 @@ int pscl_decode_wpg(const pscl_decode_params& P) {
     if (P.long_mode) return 1;  // one wavefront per workgroup, state in global scratch
     const int cu_lds = 160 * 1024, tbl = P.wg_fixed_bytes;
     int best = 0, best_res = 0;
-    // DL-SCL retry rounds (bucket-list launches): workgroup size cap (tuning override)
-    static const int retry_cap = getenv("PSCL_RETRY_WPG") ? atoi(getenv("PSCL_RETRY_WPG")) : 0;
-    const int wmax = P.elist && retry_cap >= 1 && retry_cap < PSCL_MAX_WAVES_PER_WG ? retry_cap : PSCL_MAX_WAVES_PER_WG;
+    // workgroup size cap (tuning knob PSCL_TUNE_RETRY_WPG, set on the DL-SCL retry launches)
+    const int wmax = P.wpg_cap >= 1 && P.wpg_cap < PSCL_MAX_WAVES_PER_WG ? P.wpg_cap : PSCL_MAX_WAVES_PER_WG;
     for (int w = 1; w <= wmax; ++w) {
         const int wg = tbl + w * P.wave_bytes;
         if (wg > cu_lds) break;
@@ -659,8 +658,47 @@ __global__ void __launch_bounds__(256) softplus_tails_kernel(const double* v, in
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const double x = v[i];
         exact[i] = pscl_softplus_tail_bf(x, T);
-        apx[i] = pscl_softplus_tail_scr(x);
+        apx[i] = PSCL_TAIL_ABS ? pscl_softplus_tail_abs(x) : pscl_softplus_tail_scr(x);
     }
+}
+
+// diagnostic: max |pscl_tail_abs_f32(x32) - glibc tail(x32)| over the fp32 bit patterns
+// [lo, hi] (the screening tail is a function of x32 = fl32(|v|) alone: glibc_softplus.h).
+// out[0] = the largest error's fp64 bits (non-negative doubles order like their bit patterns),
+// out[1] = (high word of that error << 32) | its x32 bit pattern, for the argmax.
+__global__ void __launch_bounds__(256) tail_abs_scan_kernel(uint32_t lo, uint32_t hi, const uint64_t* exp_table,
+                                                             unsigned long long* out) {
+    __shared__ uint64_t T[PSCL_EXP_TABLE_WORDS];
+    for (int i = threadIdx.x; i < PSCL_EXP_TABLE_WORDS; i += blockDim.x) T[i] = exp_table[i];
+    __syncthreads();
+    unsigned long long best = 0, key = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= hi; i += stride) {
+        const float x32 = __uint_as_float((uint32_t)i);
+        const double ex = pscl_softplus_tail_bf((double)x32, T);
+        const double ap = (double)pscl_tail_abs_f32(x32);
+        const unsigned long long eb = (unsigned long long)pscl_asu64(fabs(ap - ex));
+        if (eb > best) {
+            best = eb;
+            key = ((eb >> 32) << 32) | (uint32_t)i;
+        }
+    }
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        const unsigned long long ob = __shfl_xor(best, s), ok = __shfl_xor(key, s);
+        best = ob > best ? ob : best;
+        key = ok > key ? ok : key;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(out, best);
+        atomicMax(out + 1, key);
+    }
+}
+
+hipError_t pscl_launch_tail_abs_scan(uint32_t lo, uint32_t hi, const uint64_t* exp_table, unsigned long long* out,
+                                     hipStream_t s) {
+    hipLaunchKernelGGL(tail_abs_scan_kernel, dim3(8192), dim3(256), 0, s, lo, hi, exp_table, out);
+    return hipGetLastError();
 }
 
 hipError_t pscl_launch_softplus_tails(const double* v, int64_t n, const uint64_t* exp_table, double* exact,

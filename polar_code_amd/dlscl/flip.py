@@ -172,12 +172,14 @@ def words_to_bits(words: np.ndarray, K: int) -> np.ndarray:
 
 
 def decode_with_retries_device(llr: np.ndarray, info_set, M: int, retries: int, *, crc=None, beta=None,
-                               device: int = 0, msg: Optional[np.ndarray] = None) -> dict:
+                               device: int = 0, msg: Optional[np.ndarray] = None,
+                               tuning: Optional[dict] = None) -> dict:
     """decode_with_retries for a batch [B, N] with the retry loop on the GPU.
 
     Returns best_bits [B, K] (final attempt), success [B], attempts [B], tried [B, R]
     (R = max(retries, 0), -1 padded), base_bits / base_pass (the baseline SCL), and with
     `msg` [B, K] the in-kernel counters {"scl": [...], "dl": [...]} (PSCL_CNT_* order).
+    `tuning`: schedule knobs for this call (Decoder.set_tuning; reset to the defaults after).
     """
     llr = np.ascontiguousarray(llr, dtype=np.float64)
     B, N = llr.shape
@@ -187,6 +189,17 @@ def decode_with_retries_device(llr: np.ndarray, info_set, M: int, retries: int, 
     W = dec.W
     R = max(int(retries), 0)
     out = {}
+    if tuning:
+        dec.set_tuning(**tuning)
+    try:
+        _retries_device(dec, llr, B, W, R, K, retries, crc, beta, msg, out)
+    finally:
+        if tuning:
+            dec.set_tuning(**{k: 0 for k in tuning})
+    return out
+
+
+def _retries_device(dec, llr, B, W, R, K, retries, crc, beta, msg, out) -> None:
     with _native.DeviceArena(dec) as mem:
         d_llr = mem.alloc(llr.nbytes)
         mem.upload(d_llr, llr)
@@ -221,7 +234,6 @@ def decode_with_retries_device(llr: np.ndarray, info_set, M: int, retries: int, 
         if msg is not None:
             out["counters"] = {"scl": mem.download(d_cs, _native.PSCL_NCOUNT * 8, np.int64),
                                "dl": mem.download(d_cd, _native.PSCL_NCOUNT * 8, np.int64)}
-    return out
 
 
 __all__ = ["choose_flip_index", "retry_with_flip", "decode_with_retries", "decode_with_retries_batch",

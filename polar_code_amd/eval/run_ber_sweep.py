@@ -38,7 +38,7 @@ from ..nr.polar.interleaver import subblock_interleave
 from ..polar import polar as polar_core
 from ..polar.crc import attach_crc
 from ..polar.polar import construct_info_set
-from ..utils.seeding import seed_all
+from ..utils.seeding import philox_stream_id, seed_all
 
 
 @dataclass
@@ -223,7 +223,7 @@ class PhiloxFrames:
         self._ensure(n)
         W = dec.W
         k_tx = self.payload_len  # payload bits; the CRC (if any) follows them
-        dec.channel_device(seed, int(round(EbN0_dB * 10)), EbN0_dB, self.payload_len / a.E, k_tx, frame0, n,
+        dec.channel_device(seed, philox_stream_id(EbN0_dB), EbN0_dB, self.payload_len / a.E, k_tx, frame0, n,
                            self.d_llr, self.d_msg)
         work = np.zeros(n)
         if a.scheme == "dl_scl" and self.crc is not None:

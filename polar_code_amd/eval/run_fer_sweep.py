@@ -32,7 +32,7 @@ from ..dlscl.flip import decode_with_retries, decode_with_retries_batch, decode_
 from ..polar.crc import attach_crc
 from ..polar.polar import construct_info_set, encode
 from ..polar.scl import decode_scl
-from ..utils.seeding import seed_all
+from ..utils.seeding import philox_stream_id, seed_all
 
 # counter vector, summed across ranks
 C_FRAMES, C_SCL_ERR, C_DL_ERR, C_SCL_BIT, C_DL_BIT, C_UNC_ERR, C_UNC_BIT, C_BITS, C_BITS_UNC, C_DL_WORK = range(10)
@@ -193,7 +193,7 @@ def _philox_block(c, seed, snr_db, frame0, n, info_set, M, crc, retries, beta, d
     """n frames generated on the device; SCL, DL-SCL and the uncoded baseline counted there."""
     cfg = config.get_config()
     dec = _native.get_decoder(cfg.N, info_set, M, crc, device, slot=slot)
-    sid = int(round(snr_db * 10))
+    sid = philox_stream_id(snr_db)
     if engine == "device":  # TX, uncoded baseline, SCL + DL-SCL and counting: one library call
         dec.set_beta(beta)
         cs, cd, cu = dec.simulate(seed, sid, snr_db, cfg.K / cfg.N, payload_bits, frame0, n, retries, include_uncoded)

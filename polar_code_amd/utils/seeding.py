@@ -24,4 +24,15 @@ def seed_all(seed: int, deterministic_torch: bool = False) -> None:
             torch.use_deterministic_algorithms(True)
 
 
-__all__ = ["seed_all"]
+def philox_stream_id(snr_db: float) -> int:
+    """Philox key word of one SNR point of a device-generated (--rng philox) sweep.  Points on the
+    0.1 dB grid keep round(10 Eb/N0) (the streams of every earlier sweep); any other point gets
+    2^31 + round(10^6 Eb/N0) mod 2^31, so grids down to 10^-6 dB never share a stream (two points
+    0.05 dB apart used to round to the same word and reuse each other's frames)."""
+    t = round(float(snr_db) * 10.0)
+    if abs(float(snr_db) * 10.0 - t) < 1e-9:
+        return int(t) & 0x7FFFFFFF
+    return (1 << 31) | (int(round(float(snr_db) * 1e6)) & 0x7FFFFFFF)
+
+
+__all__ = ["seed_all", "philox_stream_id"]

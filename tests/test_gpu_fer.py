@@ -77,11 +77,10 @@ def test_device_retry_loop_golden(golden):
 def test_device_retry_loop_equals_host_ranking(monkeypatch, M, retries, ebno, screen):
     """Device retry loop == numpy-ranked retries, frame by frame (3000 frames, ~30% failing);
     screen = 1: the retry decodes on the forced-bit screening instance plus the exact decode of
-    the entries it defers (PSCL_DL_SCREEN=1)."""
+    the entries it defers (tuning knob dl_screen = 1)."""
     from polar_code_amd.polar.polar import construct_info_set, encode
     from polar_code_amd.polar.crc import attach_crc
 
-    monkeypatch.setenv("PSCL_DL_SCREEN", screen)
 
     rng = np.random.default_rng(M * 100 + retries)
     info = construct_info_set(128, 64)
@@ -90,7 +89,8 @@ def test_device_retry_loop_equals_host_ranking(monkeypatch, M, retries, ebno, sc
     llr = 2.0 * ((1.0 - 2.0 * encode(msg)) + rng.normal(0, math.sqrt(var), size=(3000, 128))) / var
     beta = np.load(GOLDEN / "beta_M4.npy")
     for b in (beta, None):
-        dev = decode_with_retries_device(llr, info, M, retries, crc="0x1864CFB", beta=b)
+        dev = decode_with_retries_device(llr, info, M, retries, crc="0x1864CFB", beta=b,
+                                         tuning={"dl_screen": int(screen)})
         host = decode_with_retries_batch(llr, info, M, retries, crc="0x1864CFB", beta=b)
         assert 0.05 < (~dev["base_pass"]).mean() < (0.97 if ebno < 2 else 0.9)
         np.testing.assert_array_equal(dev["tried"], host["tried"])
@@ -144,20 +144,19 @@ def test_config3_grid_sweep(tmp_path):
     assert (tmp_path / "fer_M8.csv").exists()
 
 
-def test_device_retry_loop_chunked_pipeline(monkeypatch):
+def test_device_retry_loop_chunked_pipeline():
     """The chunked retry pipeline (retry rounds of chunk c overlapped with the baseline of c+1)
     gives the same per-frame results as the host ranking."""
     from polar_code_amd.polar.polar import construct_info_set, encode
     from polar_code_amd.polar.crc import attach_crc
 
-    monkeypatch.setenv("PSCL_DL_CHUNKS", "3")
     rng = np.random.default_rng(77)
     info = construct_info_set(128, 64)
     msg = attach_crc(rng.integers(0, 2, size=(5000, 40), dtype=np.int8), "0x1864CFB")
     var = 1.0 / (2.0 * 0.5 * 10 ** (3.0 / 10))
     llr = 2.0 * ((1.0 - 2.0 * encode(msg)) + rng.normal(0, math.sqrt(var), size=(5000, 128))) / var
     beta = np.load(GOLDEN / "beta_M4.npy")
-    dev = decode_with_retries_device(llr, info, 4, 8, crc="0x1864CFB", beta=beta, msg=msg)
+    dev = decode_with_retries_device(llr, info, 4, 8, crc="0x1864CFB", beta=beta, msg=msg, tuning={"dl_chunks": 3})
     host = decode_with_retries_batch(llr, info, 4, 8, crc="0x1864CFB", beta=beta)
     np.testing.assert_array_equal(dev["tried"], host["tried"])
     np.testing.assert_array_equal(dev["attempts"], host["attempts"])
@@ -166,14 +165,12 @@ def test_device_retry_loop_chunked_pipeline(monkeypatch):
 
 
 @pytest.mark.parametrize("chunks,split", [("1", "2"), ("2", "2"), ("1", "1")])
-def test_device_retry_loop_split_chains(monkeypatch, chunks, split):
+def test_device_retry_loop_split_chains(chunks, split):
     """Two concurrent retry chains per chunk (each on its own stream, >= 4096 failing frames)
     give the same per-frame results as the host ranking."""
     from polar_code_amd.polar.polar import construct_info_set, encode
     from polar_code_amd.polar.crc import attach_crc
 
-    monkeypatch.setenv("PSCL_DL_CHUNKS", chunks)
-    monkeypatch.setenv("PSCL_DL_SPLIT", split)
     rng = np.random.default_rng(78)
     B = 24000
     info = construct_info_set(128, 64)
@@ -181,7 +178,8 @@ def test_device_retry_loop_split_chains(monkeypatch, chunks, split):
     var = 1.0 / (2.0 * 0.5 * 10 ** (1.0 / 10))
     llr = 2.0 * ((1.0 - 2.0 * encode(msg)) + rng.normal(0, math.sqrt(var), size=(B, 128))) / var
     beta = np.load(GOLDEN / "beta_M4.npy")
-    dev = decode_with_retries_device(llr, info, 4, 8, crc="0x1864CFB", beta=beta, msg=msg)
+    dev = decode_with_retries_device(llr, info, 4, 8, crc="0x1864CFB", beta=beta, msg=msg,
+                                     tuning={"dl_chunks": int(chunks), "dl_split": int(split)})
     host = decode_with_retries_batch(llr, info, 4, 8, crc="0x1864CFB", beta=beta)
     assert (dev["attempts"] > 1).sum() >= 4096 * int(chunks) + 1000  # every chunk splits
     np.testing.assert_array_equal(dev["tried"], host["tried"])
@@ -229,6 +227,46 @@ def test_pipelined_dlscl_calls_equal_stream_ordered(L):
     np.testing.assert_array_equal(res[True][1], res[False][1], err_msg="counters")
     c = res[True][1]
     assert c[0][0] == nb * B and c[1][1] <= c[0][1] and (res[True][0][0][2] > 1).sum() > 1000
+
+
+def test_device_free_orders_pipelined_chains():
+    """pscl_device_free on the buffers of a pipelined DL-SCL call whose retry chains are still
+    deferred (no join): the free first enqueues and completes those chains, so freeing the call's
+    input rows and reference words right after it leaves its outputs and counters equal to the
+    stream-ordered call's."""
+    import ctypes as C
+
+    from polar_code_amd.polar.polar import construct_info_set
+
+    info = construct_info_set(128, 64)
+    beta = np.load(GOLDEN / "beta_M4.npy")
+    B, nc = 30_000, _native.PSCL_NCOUNT
+    res = {}
+    for pipe in (True, False):
+        dec = _native.Decoder(128, info, 4, "0x1864CFB")
+        dec.set_pipelined(pipe)
+        with _native.DeviceArena(dec) as mem:
+            d_out = (mem.alloc(B * 8), mem.alloc(B), mem.alloc(B * 4))
+            d_cnt = mem.alloc(2 * nc * 8)
+            mem.memset(d_cnt, 0, 2 * nc * 8)
+            raw = []
+            for nbytes in (B * 128 * 8, B * 8):
+                p = C.c_void_p()
+                _native.check(_native.lib().pscl_device_alloc(dec.handle, C.byref(p), nbytes))
+                raw.append(p.value)
+            d_llr, d_msg = raw
+            dec.channel_device(9, 71, 2.5, 0.5, 40, 0, B, d_llr, d_msg)
+            dec.dlscl_device(d_llr, B, 8, beta=beta, d_best=d_out[0], d_flags=d_out[1], d_attempts=d_out[2],
+                             d_ref=d_msg, k_payload=40, d_counters_scl=d_cnt, d_counters_dl=d_cnt + nc * 8)
+            for p in raw:  # no join: the chains of a pipelined call are still deferred here
+                _native.check(_native.lib().pscl_device_free(dec.handle, p))
+            res[pipe] = ([mem.download(d_out[0], B * 8, np.uint64), mem.download(d_out[1], B, np.uint8),
+                          mem.download(d_out[2], B * 4, np.int32)], mem.download(d_cnt, 2 * nc * 8, np.int64))
+        dec.close()
+    for k in range(3):
+        np.testing.assert_array_equal(res[True][0][k], res[False][0][k])
+    np.testing.assert_array_equal(res[True][1], res[False][1])
+    assert (res[True][0][2] > 1).sum() > 500
 
 
 @pytest.mark.parametrize("N,K,E,L", [(128, 88, 256, 8), (256, 128, 0, 4)])

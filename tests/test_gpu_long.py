@@ -98,13 +98,12 @@ def test_long_decode_with_retries_matches_oracle():
 @pytest.mark.parametrize("N,K,M,retries,use_beta,snr,chunks", [(256, 128, 4, 6, False, 2.0, "1"),
                                                              (256, 128, 8, 4, True, 1.5, "2"),
                                                              (512, 256, 4, 3, False, 1.25, "1")])
-def test_long_device_retry_loop(monkeypatch, N, K, M, retries, use_beta, snr, chunks):
+def test_long_device_retry_loop(N, K, M, retries, use_beta, snr, chunks):
     """The device DL-SCL loop at N > 128 (HIST long-kernel retry decodes, dense per-round state)
     equals the host-ranked batch form frame by frame (bits, CRC, attempts, tried indices) and
     the oracle on a sample; in-kernel counters match the host's counts."""
     from polar_code_amd.dlscl.flip import decode_with_retries_batch, decode_with_retries_device
 
-    monkeypatch.setenv("PSCL_DL_CHUNKS", chunks)
     rng = np.random.default_rng(N + K + M)
     info = construct_info_set(N, K)
     B = 600
@@ -114,7 +113,8 @@ def test_long_device_retry_loop(monkeypatch, N, K, M, retries, use_beta, snr, ch
     nv = 1.0 / (2.0 * K / N * 10 ** (snr / 10))
     llr = 2.0 * ((1.0 - 2.0 * _polar_transform(u)) + rng.normal(0.0, np.sqrt(nv), size=(B, N))) / nv
     beta = rng.random((K, K)).astype(np.float32) if use_beta else None  # (the reference stores beta in fp32)
-    dev = decode_with_retries_device(llr, info, M, retries, crc=POLY, beta=beta, msg=msg)
+    dev = decode_with_retries_device(llr, info, M, retries, crc=POLY, beta=beta, msg=msg,
+                                     tuning={"dl_chunks": int(chunks)})
     host = decode_with_retries_batch(llr, info, M, retries, crc=POLY, beta=beta)
     assert np.count_nonzero(host["attempts"] > 1) >= 50  # the retry loop is exercised
     for k in ("best_bits", "success", "attempts", "tried"):

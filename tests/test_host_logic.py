@@ -68,3 +68,16 @@ def test_f_g_helpers():
     b = np.array([-3.0, -1.0, 5.0, 0.25])
     np.testing.assert_array_equal(ppolar._f(a, b), [-1.0, 1.0, 0.0, -0.25])
     np.testing.assert_array_equal(ppolar._g(a, b, np.array([0, 1, 1, 0], np.int8)), [-2.0, 1.0, 5.0, -0.25])
+
+
+def test_philox_stream_ids_distinct_on_fine_grids():
+    """--rng philox: every SNR point of a grid gets its own Philox stream (0.1 dB points keep
+    their historical word round(10 Eb/N0); finer grids no longer collide)."""
+    from polar_code_amd.utils.seeding import philox_stream_id
+
+    assert [philox_stream_id(x) for x in (4.0, 4.5, 5.0, 6.5)] == [40, 45, 50, 65]
+    for step in (0.05, 0.01, 0.25, 0.125):
+        grid = np.round(np.arange(3.0, 7.0 + 1e-9, step), 6)
+        ids = [philox_stream_id(x) for x in grid]
+        assert len(set(ids)) == len(ids), step
+        assert all(0 <= i < 2 ** 32 for i in ids)

@@ -8,7 +8,7 @@ for v in $vars; do
   out=gpurun_out/dlv_${tag}_$v
   mkdir -p "$out"
   if [ "$v" = prod ]; then lp=""; else lp=tools/_variant/lib_$v.so; fi
-  PSCL_DL_SPLIT=${PSCL_DL_SPLIT:-2} PSCL_LIB_PATH=$lp timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$out" -o trace -- \
+  PSCL_LIB_PATH=$lp timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$out" -o trace -- \
       python3 bench.py --list 4 --retries 8 --steps 3 --warmup 1 --no-cpu-baseline --extra none > "$out/bench.log" 2>&1 || { echo "$v failed"; tail -5 "$out/bench.log"; exit 1; }
   python3 - "$out" "$v" <<'PY'
 import csv, sys
