@@ -123,6 +123,40 @@ def compute_roofline(e: dict, frames: int, launch_ms: float):
                      f"SIMD cycles (MI355X_MICROARCH.md constants table); {SIMDS} SIMDs x {CLOCK_HZ / 1e9:g} GHz")}
 
 
+def algorithmic_ops(N: int, K: int, L: int, crc_deg: int = 24):
+    """SURVEY.md §8(d)'s algorithmic work per frame, in lane operations, as an upper bound (every
+    path live at every phase): per path n N/2 f + n N/2 g LLR ops (fp64) and n N/2 partial-sum
+    XORs; N metric updates per path (exp + log1p: two transcendentals, one fp64 add); at each of
+    the K information phases a bitonic sort of the 2L children (2L/2 * lg(lg+1)/2 compare-exchanges,
+    lg = log2 2L; 80 at L = 8), a compare-exchange being a min and a max of fp64 keys; the CRC as
+    one K-column XOR per path (crc_deg <= 32 bits: one int op per column)."""
+    n = int(round(math.log2(N)))
+    llr, xor = L * n * N, L * n * N // 2
+    trans, madd = 2 * L * N, L * N
+    m = 2 * L
+    lg = int(round(math.log2(m)))
+    ce = K * (m // 2) * lg * (lg + 1) // 2
+    crc = L * K
+    return {"fp64": llr + madd + 2 * ce, "trans": trans, "int": xor + crc,
+            "detail": {"llr_ops": llr, "psum_xor": xor, "metric_exp_log1p": trans, "metric_add": madd,
+                       "sort_compare_exchanges": ce, "crc_xor": crc}}
+
+
+def compute_algorithmic(N: int, K: int, L: int, frames: int, launch_ms: float):
+    """VALU roofline on the ALGORITHMIC op count: §8(d)'s lane operations per
+    frame as wave64 instructions at the guide's per-class rates, over the SIMD cycles of the live
+    launch time.  Unlike `compute` (the issued instruction mix), a kernel issuing more instructions
+    than the algorithm needs cannot raise this fraction."""
+    ops = algorithmic_ops(N, K, L)
+    cyc = (CYC_F64 * ops["fp64"] + CYC_TRANS * ops["trans"] + CYC_OTHER * ops["int"]) / 64.0
+    avail = SIMDS * CLOCK_HZ * launch_ms * 1e-3
+    return {"bound": "valu-algorithmic", "unit": "SIMD-cycles/launch", "achieved": cyc * frames, "peak": avail,
+            "frac": cyc * frames / avail, "simd_cycles_per_frame": cyc, "lane_ops_per_frame": ops,
+            "note": ("SURVEY.md §8(d) op count (upper bound: all L paths live at every phase; exp and log1p one "
+                     f"transcendental each), priced per wave64 instruction at fp64 {CYC_F64}, transcendental "
+                     f"{CYC_TRANS}, int {CYC_OTHER} SIMD cycles; {SIMDS} SIMDs x {CLOCK_HZ / 1e9:g} GHz")}
+
+
 def fer_z(errs: int, frames: int, ref_errs: int, ref_frames: int = 2000):
     """Two-proportion z of errs/frames against the reference's ref_errs/ref_frames."""
     p, p0 = errs / max(frames, 1), ref_errs / ref_frames
@@ -173,10 +207,29 @@ def cpu_baseline(orc: Oracle, llr_host: np.ndarray, info, L: int, budget_s: floa
         dt = time.perf_counter() - t0
     what = (f"decode_with_retries (SCL L={L} + up to {retries} flips, beta)" if retries > 0
             else f"decode_scl L={L} + CRC select")
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
     rec = {"value": done / dt, "unit": "frames/s", "cores": orc.o.num_threads(), "kind": "port",
+           "threads_used": orc.o.num_threads(), "host_cpu_count": os.cpu_count(),
+           "affinity_cpus": len(aff) if aff is not None else None,
+           "affinity_mask": _cpu_ranges(aff) if aff is not None else None,
            "sample": f"{done} frames ({n} distinct frames of the step-0 batch, same LLRs as the GPU) through "
                      f"oracle/scl_oracle.c (C restatement of {what}), OpenMP over frames, {dt:.1f} s"}
     return rec, first, n
+
+
+def _cpu_ranges(cpus):
+    """Compact '0-15,32-47' form of a CPU list."""
+    out, i = [], 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(str(cpus[i]) if i == j else f"{cpus[i]}-{cpus[j]}")
+        i = j + 1
+    return ",".join(out)
 
 
 def parity(gpu_best_words: np.ndarray, gpu_flags: np.ndarray, ref, K: int, check_idx: bool):
@@ -291,7 +344,7 @@ def run_workload(ctx: Ctx, *, L: int, E: int, retries: int, beta, B: int, steps:
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     ctx.barrier()
-    launches, kern_ms = dec.timing_read()
+    (launches, kern_ms), (side_launches, side_ms) = dec.timing_read_split()
     dec.timing_enable(False)
     elapsed = ctx.max_over_ranks(elapsed)
     c = ctx.sum_over_ranks(counters)
@@ -302,7 +355,8 @@ def run_workload(ctx: Ctx, *, L: int, E: int, retries: int, beta, B: int, steps:
     dec.sync()
     torch.cuda.synchronize(dev)
     res = {"N": N, "K": K, "W": W, "L": L, "E": E, "B": B, "n_in": n_in, "info": info, "retries": retries,
-           "elapsed": elapsed, "launches": launches, "kern_ms": kern_ms, "c": c, "cdl": cdl, "kp": kp,
+           "elapsed": elapsed, "launches": launches, "kern_ms": kern_ms, "side_launches": side_launches,
+           "side_ms": side_ms, "c": c, "cdl": cdl, "kp": kp,
            "rate": rate, "build_hash": _native.build_hash(), "pipelined": pipelined,
            "best0": best.cpu().numpy().view(np.uint64), "flags0": flags.cpu().numpy()}
     if keep_buffers:
@@ -332,13 +386,17 @@ def extra_configs(args, ctx: Ctx, orc: Oracle | None):
         rec = {"ms_per_step": r["elapsed"] * 1e3 / args.extra_steps,
                "value": args.frames * args.extra_steps * ctx.world / r["elapsed"], "unit": "frames/s",
                "steps": args.extra_steps, "frames_per_gpu_per_step": args.frames,
-               "decode_ms_per_step": r["kern_ms"] / args.extra_steps, "launches": r["launches"],
+               "main_stream_kernel_ms_per_step": r["kern_ms"] / args.extra_steps, "main_stream_launches": r["launches"],
+               "side_stream_kernel_ms_per_step": r["side_ms"] / args.extra_steps, "side_stream_launches": r["side_launches"],
                "kernel": ("scl128_kernel<4> screening + exact re-decode (pipelined)" if name.startswith("config2") else
                           "scl128_kernel<4> baseline + scl128_kernel<4,FS> warm-started retry decodes + dl_post_kernel"
                           " rounds" if name.startswith("config4") else
                           "scl128_kernel<8,CH,CODE=2> screening (de-rate-match in staging) + exact re-decode"
                           " (pipelined)"),
-               "decode_timed": "screening launches" if r["pipelined"] else "all decode launches",
+               "kernel_timing": ("HIP events around each decode launch: main stream = the screening (plain) or "
+                                 "baseline (DL-SCL) decode of each step; side streams = DL-SCL retry decodes, "
+                                 "which overlap the main stream (the sums are not additive in wall time)"),
+               "roofline": extra_roofline(r, args.extra_steps),
                "fer": {"frames": frames, "frame_errors": int(c[1]), "fer": c[1] / max(frames, 1),
                        "payload_fer": c[3] / max(frames, 1)}}
         if kw["retries"]:
@@ -361,6 +419,26 @@ def extra_configs(args, ctx: Ctx, orc: Oracle | None):
         del r
         ctx.torch.cuda.empty_cache()
     return out
+
+
+def extra_roofline(r: dict, steps: int) -> dict:
+    """Roofline of an extra config's dominant kernel (its main-stream decode: the screening pass of
+    a plain decode, the baseline decode of a DL-SCL step): algorithmic HBM bytes per frame x B over
+    that kernel's mean live duration, the PMC-priced issue bound where a PMC entry of this build
+    and workload exists, and the algorithmic VALU fraction."""
+    B, L, N, K = r["B"], r["L"], r["N"], r["K"]
+    dom_ms = r["kern_ms"] / max(r["launches"], 1)
+    fb = frame_bytes(r["n_in"], r["W"])
+    achieved = fb * B / (dom_ms * 1e-3) / 1e9
+    wkey = f"scl_L{L}_N{N}_K{K}_B{B}" + (f"_E{r['E']}" if r["E"] else "") + (f"_dl{r['retries']}" if r["retries"] else "")
+    e, why = pmc_entry(wkey, r["build_hash"])
+    return {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
+            "traffic": float(e["hbm_bytes_per_launch"]) if e and "hbm_bytes_per_launch" in e else None,
+            "kernel": "scl128_kernel screening pass" if not r["retries"] else "scl128_kernel baseline decode",
+            "avg_launch_ms": dom_ms, "bytes_per_frame": fb, "pmc": why or "matched build",
+            "compute": compute_roofline(e, B, dom_ms) if e and "valu_instr_per_frame" in e else None,
+            "compute_algorithmic": compute_algorithmic(N, K, L, B, dom_ms),
+            "step_hbm_gbs": fb * B * steps / r["elapsed"] / 1e9}
 
 
 def free_port() -> int:
@@ -530,8 +608,8 @@ def main():
         launches, kern_ms = r["launches"], r["kern_ms"]
         avg_ms = kern_ms / max(launches, 1)
         fb = frame_bytes(n_in, W)
-        # DL mode: the step's decode launches (baseline + retry rounds) priced as one pass
-        # over the batch; otherwise one launch = one batch
+        # main-stream launches: one per step (the screening pass of a plain decode, the baseline
+        # decode of a DL-SCL step; the retry decodes run on side streams)
         per_batch_ms = kern_ms / args.steps if args.retries > 0 else avg_ms
         achieved = fb * B / (per_batch_ms * 1e-3) / 1e9
         wkey = f"scl_L{L}_N{N}_K{K}_B{B}" + (f"_E{E}" if E else "") + (f"_dl{args.retries}" if args.retries > 0 else "")
@@ -581,9 +659,12 @@ def main():
                          "timed": ("screening launch (pipelined: each step's exact re-decode of its deferred "
                                    "frames overlaps the next step's screening)" if r["pipelined"] else
                                    "decode launches of a step"),
-                         "avg_launch_ms": avg_ms, "launches": launches, "decode_ms_per_step": kern_ms / args.steps,
+                         "avg_launch_ms": avg_ms, "launches": launches,
+                         "main_stream_kernel_ms_per_step": kern_ms / args.steps,
+                         "side_stream_kernel_ms_per_step": r["side_ms"] / args.steps,
                          "bytes_per_frame": fb, "build_hash": r["build_hash"], "pmc": why or "matched build",
-                         "compute": compute},
+                         "compute": compute,
+                         "compute_algorithmic": compute_algorithmic(N, K, L, B, per_batch_ms)},
             "cpu_baseline": cpu,
             "parity": par,
             "fer": {"frames": int(c[0]), "frame_errors": int(c[1]), "fer": fer, "ber": c[2] / max(c[0] * K, 1),

@@ -325,6 +325,12 @@ int pscl_tail_abs_scan_device(pscl_handle* h, uint32_t lo, uint32_t hi, uint64_t
  */
 int pscl_timing_enable(pscl_handle* h, int enable);
 int pscl_timing_read(pscl_handle* h, int64_t* launches, double* total_ms);
+/* The same, split by stream: launches on the handle's stream (a plain decode's screening pass,
+ * a DL-SCL call's baseline decode) and on its side streams (DL-SCL retry decodes).  Side-stream
+ * launches overlap main-stream ones, so the two sums are not additive in wall time.  Any output
+ * pointer may be NULL. */
+int pscl_timing_read_split(pscl_handle* h, int64_t* main_launches, double* main_ms, int64_t* side_launches,
+                           double* side_ms);
 
 /* Launch geometry used by the decode kernel (for roofline bookkeeping): waves per
  * workgroup, workgroups per launch for B frames, LDS bytes per workgroup. */

@@ -41,7 +41,7 @@ EXPORTS = (
     "pscl_timing_read", "pscl_launch_info", "pscl_set_rate_match", "pscl_set_beta", "pscl_dlscl_device",
     "pscl_path_llrs_device", "pscl_uncoded_device", "pscl_simulate", "pscl_set_screening", "pscl_build_hash",
     "pscl_screening_count", "pscl_softplus_tails_device", "pscl_set_pipelined", "pscl_join",
-    "pscl_tail_abs_scan_device", "pscl_set_tuning",
+    "pscl_tail_abs_scan_device", "pscl_set_tuning", "pscl_timing_read_split",
 )
 
 # pscl_set_tuning knobs (include/polar_scl.h)
@@ -104,6 +104,7 @@ def lib() -> C.CDLL:
         "pscl_softplus_tails_device": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
         "pscl_tail_abs_scan_device": (C.c_int, [_vp, C.c_uint32, C.c_uint32, _vp]),
         "pscl_set_tuning": (C.c_int, [_vp, C.c_int, _i64]),
+        "pscl_timing_read_split": (C.c_int, [_vp, P(_i64), P(_dbl), P(_i64), P(_dbl)]),
         "pscl_device_count": (C.c_int, []),
         "pscl_create": (C.c_int, [P(_vp), C.c_int, C.c_int, P(_i32), C.c_int, C.c_int, _u64]),
         "pscl_destroy": (C.c_int, [_vp]),
@@ -404,6 +405,12 @@ class Decoder:
         n, ms = _i64(), _dbl()
         check(lib().pscl_timing_read(self._h, C.byref(n), C.byref(ms)))
         return int(n.value), float(ms.value)
+
+    def timing_read_split(self):
+        """((launches, ms) on the handle's stream, (launches, ms) on its side streams)."""
+        n0, t0, n1, t1 = _i64(), _dbl(), _i64(), _dbl()
+        check(lib().pscl_timing_read_split(self._h, C.byref(n0), C.byref(t0), C.byref(n1), C.byref(t1)))
+        return (int(n0.value), float(t0.value)), (int(n1.value), float(t1.value))
 
     def launch_info(self, B: int):
         w, g, lds = C.c_int(), _i64(), C.c_int()

@@ -150,6 +150,7 @@ struct pscl_handle {
     pscl_dl_call dl_defer;            // the last pipelined call, its chains not yet enqueued
     bool dl_defer_valid = false;
     std::vector<hipEvent_t> ev_pool;
+    std::vector<uint8_t> ev_main;     // per timed launch: 1 if it ran on the handle's stream
     size_t ev_used = 0;
     int64_t tune[PSCL_TUNE_COUNT] = {};  // pscl_set_tuning knobs (0 = the default schedule)
 };
@@ -286,6 +287,8 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
         }
         e0 = h->ev_pool[h->ev_used];
         e1 = h->ev_pool[h->ev_used + 1];
+        if (h->ev_main.size() < h->ev_pool.size() / 2) h->ev_main.resize(h->ev_pool.size() / 2);
+        h->ev_main[h->ev_used / 2] = st == h->stream ? 1 : 0;
         h->ev_used += 2;
         HIP_TRY(hipEventRecord(e0, st));
     }
@@ -1527,19 +1530,37 @@ int pscl_timing_enable(pscl_handle* h, int enable) {
     return PSCL_OK;
 }
 
-int pscl_timing_read(pscl_handle* h, int64_t* launches, double* total_ms) {
-    if (!h || !launches || !total_ms) return fail(PSCL_EINVAL, "bad arguments");
+int pscl_timing_read_split(pscl_handle* h, int64_t* main_launches, double* main_ms, int64_t* side_launches,
+                           double* side_ms) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
     int rc = enter(h);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(h->stream));
-    double tot = 0.0;
+    quiesce(h);
+    double tot[2] = {0.0, 0.0};
+    int64_t cnt[2] = {0, 0};
     for (size_t i = 0; i + 1 < h->ev_used; i += 2) {
         float ms = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, h->ev_pool[i], h->ev_pool[i + 1]));
-        tot += ms;
+        const int m = h->ev_main[i / 2] ? 0 : 1;
+        tot[m] += ms;
+        ++cnt[m];
     }
-    *launches = (int64_t)(h->ev_used / 2);
-    *total_ms = tot;
+    if (main_launches) *main_launches = cnt[0];
+    if (main_ms) *main_ms = tot[0];
+    if (side_launches) *side_launches = cnt[1];
+    if (side_ms) *side_ms = tot[1];
+    return PSCL_OK;
+}
+
+int pscl_timing_read(pscl_handle* h, int64_t* launches, double* total_ms) {
+    if (!h || !launches || !total_ms) return fail(PSCL_EINVAL, "bad arguments");
+    int64_t n0 = 0, n1 = 0;
+    double t0 = 0.0, t1 = 0.0;
+    const int rc = pscl_timing_read_split(h, &n0, &t0, &n1, &t1);
+    if (rc) return rc;
+    *launches = n0 + n1;
+    *total_ms = t0 + t1;
     return PSCL_OK;
 }
 
