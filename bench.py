@@ -563,7 +563,9 @@ def main():
     torch.cuda.set_device(device_index)
     dev = torch.device("cuda", device_index)
     dist = None
-    if world > 1:
+    # a process group under any launcher, world 1 included (the RCCL collectives then run on one
+    # GPU exactly as on eight); none for a plain `python bench.py`
+    if world > 1 or ("MASTER_ADDR" in os.environ and "WORLD_SIZE" in os.environ):
         import torch.distributed as dist
 
         backend = os.environ.get("PSCL_DIST_BACKEND", "nccl")  # nccl == RCCL over xGMI
@@ -651,7 +653,8 @@ def main():
             "data": "synthetic: on-device Philox4x32 BPSK/AWGN frames (payload->CRC24->polar->LLR), resident in HBM",
             "config": {"workload": workload, "retries": args.retries, "E": E or None,
                        "N": N, "K": K, "list_size": L, "ebno_db": args.ebno, "frames_per_gpu_per_step": B,
-                       "global_batch": B * world, "parallelism": f"frame-sharded x{world}"},
+                       "global_batch": B * world, "parallelism": f"frame-sharded x{world}",
+                       "collective": dist.get_backend() if dist else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS,
                          "traffic": traffic,

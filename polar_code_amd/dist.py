@@ -20,6 +20,7 @@ class Context:
     world: int = 1
     local_rank: int = 0
     backend: str = ""
+    group: bool = False  # a torch.distributed process group is initialised (any world size)
 
     @property
     def is_root(self) -> bool:
@@ -39,16 +40,23 @@ class Context:
 _CTX: Context | None = None
 
 
+def launcher_env() -> bool:
+    """True under a rank launcher (torchrun / bench.py --gpus N): WORLD_SIZE and MASTER_ADDR set."""
+    return "WORLD_SIZE" in os.environ and "MASTER_ADDR" in os.environ
+
+
 def init(backend: str | None = None) -> Context:
-    """Initialise torch.distributed from torchrun's environment (WORLD_SIZE > 1), else a
-    single-process context.  backend: "nccl" (RCCL) when the ranks own GPUs, else "gloo"."""
+    """Initialise torch.distributed from a launcher's environment -- at any world size, so a
+    world-1 torchrun job runs the same RCCL collectives as an 8-GPU one -- else a single-process
+    context with no group.  backend: "nccl" (RCCL) when the ranks own GPUs, else "gloo"."""
     global _CTX
     if _CTX is not None:
         return _CTX
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    group = False
+    if world > 1 or launcher_env():
         import torch
         import torch.distributed as dist
 
@@ -60,8 +68,19 @@ def init(backend: str | None = None) -> Context:
                 dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
             else:
                 dist.init_process_group(backend=backend)
-    _CTX = Context(rank=rank, world=world, local_rank=local, backend=backend or "")
+        group = True
+        import sys
+
+        print(f"[dist] process group: backend={dist.get_backend()} world={world} rank={rank}", file=sys.stderr,
+              flush=True)
+    _CTX = Context(rank=rank, world=world, local_rank=local, backend=backend or "", group=group)
     return _CTX
+
+
+def _collective(ctx: Context) -> bool:
+    """Whether the helpers below run a collective: whenever a process group exists (world 1
+    included: the RCCL path then runs on one GPU), never without one."""
+    return ctx.group or ctx.world > 1
 
 
 def shard(total: int, rank: int, world: int) -> tuple[int, int]:
@@ -74,7 +93,7 @@ def shard(total: int, rank: int, world: int) -> tuple[int, int]:
 def allreduce_sum(vec: np.ndarray, ctx: Context | None = None) -> np.ndarray:
     """SUM of an int64/float64 vector over all ranks (identity when world == 1)."""
     ctx = ctx or _CTX or Context()
-    if ctx.world <= 1:
+    if not _collective(ctx):
         return np.asarray(vec)
     import torch
     import torch.distributed as dist
@@ -90,7 +109,7 @@ def allgather(vec: np.ndarray, ctx: Context | None = None) -> np.ndarray:
     """[world, len(vec)]: every rank's vector, in rank order (vec[None] when world == 1)."""
     ctx = ctx or _CTX or Context()
     v = np.ascontiguousarray(vec)
-    if ctx.world <= 1:
+    if not _collective(ctx):
         return v[None, :].copy()
     import torch
     import torch.distributed as dist
@@ -105,7 +124,7 @@ def allgather(vec: np.ndarray, ctx: Context | None = None) -> np.ndarray:
 
 def allreduce_min(x: float, ctx: Context | None = None) -> float:
     ctx = ctx or _CTX or Context()
-    if ctx.world <= 1:
+    if not _collective(ctx):
         return float(x)
     import torch
     import torch.distributed as dist
@@ -119,7 +138,7 @@ def allreduce_min(x: float, ctx: Context | None = None) -> float:
 
 def allreduce_max(x: float, ctx: Context | None = None) -> float:
     ctx = ctx or _CTX or Context()
-    if ctx.world <= 1:
+    if not _collective(ctx):
         return float(x)
     import torch
     import torch.distributed as dist
@@ -133,7 +152,7 @@ def allreduce_max(x: float, ctx: Context | None = None) -> float:
 
 def barrier(ctx: Context | None = None) -> None:
     ctx = ctx or _CTX or Context()
-    if ctx.world > 1:
+    if _collective(ctx):
         import torch.distributed as dist
 
         dist.barrier()
@@ -141,7 +160,7 @@ def barrier(ctx: Context | None = None) -> None:
 
 def finalize() -> None:
     global _CTX
-    if _CTX is not None and _CTX.world > 1:
+    if _CTX is not None and _collective(_CTX):
         import torch.distributed as dist
 
         if dist.is_initialized():

@@ -97,3 +97,47 @@ def test_bench_gpus2_launches_its_own_ranks():
     assert line[1]["fer"]["frames"] == 4 * B
     for k in ("frame_errors", "ber", "payload_fer", "payload_ber"):
         assert line[1]["fer"][k] == line[2]["fer"][k], k
+
+
+def _world1(argv, group: bool, timeout=240):
+    """One process of `python argv...`: with a world-1 launcher environment (a process group on
+    the default backend, nccl = RCCL on this GPU) or with none (no group).  Returns its output."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                            "MASTER_PORT", "PSCL_SHARE_GPU", "PSCL_DIST_BACKEND")}
+    env["PYTHONPATH"] = str(ROOT) + os.pathsep + os.environ.get("PYTHONPATH", "")
+    if group:
+        env.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    res = subprocess.run([sys.executable, *argv], cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert res.returncode == 0, (res.stdout + res.stderr)[-3000:]
+    return res.stdout, res.stderr
+
+
+def test_world1_rccl_group_equals_no_group(tmp_path):
+    """The RCCL (backend nccl) collective path of every sharded entry point, executed on one GPU
+    in a world-1 process group: run_fer_sweep --rng philox (counter all-reduce, max of the wall
+    time), run_ber_sweep --rng philox at config 5's shape (all-gather + MIN/SUM all-reduces of the
+    exact stop rule) and bench.py (timing MAX, counter SUM) give the same rows and counts as the
+    same runs without a process group."""
+    fer = ["-m", "polar_code_amd.eval.run_fer_sweep", "--M", "8", "--frames", "150000", "--snr_lo", "4.5",
+           "--snr_hi", "5", "--snr_step", "0.5", "--retries", "8", "--beta", str(GOLDEN / "beta_M8.npy"),
+           "--rng", "philox", "--batch", "60000", "--include_uncoded", "--no_plot"]
+    ber = ["-m", "polar_code_amd.eval.run_ber_sweep", "--scheme", "nr_polar_scl", "--K_payload", "64", "--K_crc",
+           "24", "--E", "256", "--N", "128", "--M", "8", "--EbN0_lo", "1.0", "--EbN0_hi", "2.0", "--EbN0_step",
+           "0.5", "--bits_cap", "3000000", "--err_cap", "2000", "--rng", "philox", "--batch", "20000"]
+    bench = ["bench.py", "--frames", "100000", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--extra", "none"]
+    out = {}
+    for group in (False, True):
+        d = tmp_path / f"g{int(group)}"
+        so, se = _world1(fer + ["--out_dir", str(d), "--plot_dir", str(d)], group)
+        assert ("backend=nccl world=1" in se) == group, se[-2000:]
+        fer_csv = (d / "fer_M8.csv").read_text()
+        so, se = _world1(ber + ["--out", str(d / "ber.csv")], group)
+        assert ("backend=nccl world=1" in se) == group, se[-2000:]
+        ber_csv = (d / "ber.csv").read_text()
+        so, _ = _world1(bench, group)
+        line = json.loads([x for x in so.splitlines() if x.startswith("{")][-1])
+        assert line["config"]["collective"] == ("nccl" if group else None)
+        out[group] = (fer_csv, ber_csv, line["fer"])
+    assert out[True][0] == out[False][0] and out[True][0].count("\n") == 3
+    assert out[True][1] == out[False][1]
+    assert out[True][2] == out[False][2] and out[True][2]["frames"] == 300_000
