@@ -332,6 +332,18 @@ int pscl_timing_read(pscl_handle* h, int64_t* launches, double* total_ms);
 int pscl_timing_read_split(pscl_handle* h, int64_t* main_launches, double* main_ms, int64_t* side_launches,
                            double* side_ms);
 
+/*
+ * The product's host (CPU) decoder: pscl_decode's contract and outputs (bit-identical) without a
+ * GPU or a handle -- decode_scl (dl_scl_polar/polar/scl.py:108-209) for the reference's
+ * CPU-only runs (BASELINE config 1: run_fer_sweep on CPU).  Any power-of-two N <= PSCL_MAX_N,
+ * 1 <= L <= 255, crc_poly as pscl_create (0 = none); forced as pscl_decode ({-1, 0, 1} per info
+ * bit, or NULL); bits, cands as int8 0/1.  Frames are split over `threads` host threads (0 = all
+ * hardware threads).  PSCL_EINVAL for invalid arguments.  No HIP call is made.
+ */
+int pscl_decode_cpu(int N, const int32_t* info_set, int K, int L, uint64_t crc_poly, const double* llr, int64_t B,
+                    const int8_t* forced, int32_t* n_paths, int8_t* best_bits, uint8_t* crc_pass, int32_t* best_idx,
+                    double* metrics, int8_t* cands, double* info_llrs, int threads);
+
 /* Launch geometry used by the decode kernel (for roofline bookkeeping): waves per
  * workgroup, workgroups per launch for B frames, LDS bytes per workgroup. */
 int pscl_launch_info(pscl_handle* h, int64_t B, int* waves_per_wg, int64_t* grid, int* lds_bytes);

@@ -41,7 +41,7 @@ EXPORTS = (
     "pscl_timing_read", "pscl_launch_info", "pscl_set_rate_match", "pscl_set_beta", "pscl_dlscl_device",
     "pscl_path_llrs_device", "pscl_uncoded_device", "pscl_simulate", "pscl_set_screening", "pscl_build_hash",
     "pscl_screening_count", "pscl_softplus_tails_device", "pscl_set_pipelined", "pscl_join",
-    "pscl_tail_abs_scan_device", "pscl_set_tuning", "pscl_timing_read_split",
+    "pscl_tail_abs_scan_device", "pscl_set_tuning", "pscl_timing_read_split", "pscl_decode_cpu",
 )
 
 # pscl_set_tuning knobs (include/polar_scl.h)
@@ -104,6 +104,8 @@ def lib() -> C.CDLL:
         "pscl_softplus_tails_device": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
         "pscl_tail_abs_scan_device": (C.c_int, [_vp, C.c_uint32, C.c_uint32, _vp]),
         "pscl_set_tuning": (C.c_int, [_vp, C.c_int, _i64]),
+        "pscl_decode_cpu": (C.c_int, [C.c_int, P(_i32), C.c_int, C.c_int, _u64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                      _vp, _vp, C.c_int]),
         "pscl_timing_read_split": (C.c_int, [_vp, P(_i64), P(_dbl), P(_i64), P(_dbl)]),
         "pscl_device_count": (C.c_int, []),
         "pscl_create": (C.c_int, [P(_vp), C.c_int, C.c_int, P(_i32), C.c_int, C.c_int, _u64]),
@@ -418,6 +420,60 @@ class Decoder:
         return int(w.value), int(g.value), int(lds.value)
 
 
+class CpuDecoder:
+    """The product's host decoder (pscl_decode_cpu): Decoder.decode's contract and outputs, bit for
+    bit, with no GPU -- the reference's CPU-only runs (BASELINE config 1).  device = "cpu"."""
+
+    def __init__(self, N: int, info_set, L: int, crc=None, threads: int = 0):
+        info = np.ascontiguousarray(np.asarray(info_set).astype(np.int32).ravel())
+        self.N, self.K, self.L = int(N), int(info.size), int(L)
+        self.info_set = info
+        self.crc_poly = poly_value(crc)
+        self.crc_deg = max(self.crc_poly.bit_length() - 1, 0)
+        self.W = (self.K + 63) // 64 if self.K else 1
+        self.E = 0
+        self.device = "cpu"
+        self.threads = int(threads or os.environ.get("PSCL_CPU_THREADS", "0") or 0)
+        if self.N < 2 or self.N & (self.N - 1) or self.N > PSCL_MAX_N:
+            raise ValueError("Channel LLR length must be a power of two")
+        if self.crc_poly and self.K <= self.crc_deg:
+            raise ValueError("Message too short for the provided CRC polynomial")
+
+    def decode(self, llr: np.ndarray, forced: np.ndarray | None = None, *, want_metrics=True,
+               want_cands=True, want_info_llrs=True):
+        llr = np.ascontiguousarray(llr, dtype=np.float64)
+        if llr.ndim == 1:
+            llr = llr[None, :]
+        B = llr.shape[0]
+        if llr.shape[1] != self.N:
+            raise ValueError("Channel LLR length must be a power of two")
+        if forced is not None:
+            forced = np.ascontiguousarray(forced, dtype=np.int8).reshape(B, self.K)
+            if np.any((forced < -1) | (forced > 1)):
+                raise ValueError("force_info_bits entries must be -1, 0, or 1")
+        out = {
+            "n_paths": np.zeros(B, np.int32),
+            "best_bits": np.zeros((B, self.K), np.int8),
+            "crc_pass": np.zeros(B, np.uint8),
+            "best_idx": np.zeros(B, np.int32),
+            "metrics": np.full((B, self.L), np.nan) if want_metrics else None,
+            "cands": np.zeros((B, self.L, self.K), np.int8) if want_cands else None,
+            "info_llrs": np.full((B, self.L, self.K), np.nan) if want_info_llrs else None,
+        }
+        check(lib().pscl_decode_cpu(self.N, self.info_set.ctypes.data_as(C.POINTER(_i32)), self.K, self.L,
+                                    self.crc_poly, _ptr(llr), B, _ptr(forced), _ptr(out["n_paths"]),
+                                    _ptr(out["best_bits"]), _ptr(out["crc_pass"]), _ptr(out["best_idx"]),
+                                    _ptr(out["metrics"]), _ptr(out["cands"]), _ptr(out["info_llrs"]), self.threads))
+        out["crc_pass"] = out["crc_pass"].astype(bool)
+        return out
+
+    def sync(self) -> None:
+        pass
+
+    def close(self) -> None:
+        pass
+
+
 _CACHE: dict = {}
 _CACHE_LOCK = threading.Lock()
 
@@ -426,12 +482,18 @@ def get_decoder(N: int, info_set, L: int, crc=None, device: int = 0, E: int = 0,
     """Cached Decoder per (N, info set, L, CRC, device, rate-matched length E, slot).  Distinct
     slots are distinct handles (own streams and scratch), for concurrent host threads."""
     info = np.asarray(info_set).astype(np.int64).ravel()
-    key = (int(N), info.tobytes(), int(L), poly_value(crc), int(device), int(E), int(slot))
+    cpu = isinstance(device, str) and device == "cpu"
+    key = (int(N), info.tobytes(), int(L), poly_value(crc), "cpu" if cpu else int(device), int(E), int(slot))
     with _CACHE_LOCK:
         dec = _CACHE.get(key)
         if dec is None:
             if len(_CACHE) > 64:
                 _CACHE.clear()
+            if cpu:
+                if E:
+                    raise NotImplementedError("the CPU decoder takes internal (de-rate-matched) LLRs")
+                dec = _CACHE[key] = CpuDecoder(N, info, L, crc)
+                return dec
             dec = Decoder(N, info, L, crc, device)
             if E:
                 dec.set_rate_match(E)

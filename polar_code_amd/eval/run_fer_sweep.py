@@ -238,6 +238,11 @@ def run_sweep(args: argparse.Namespace) -> List[Dict[str, float]]:
     seed_all(args.seed)
     ctx = dist.init()
     device = ctx.device
+    engine = args.dl_engine
+    if args.device == "cpu":  # the product's host decoder (pscl_decode_cpu), no GPU touched
+        if args.rng != "replay":
+            raise ValueError("--device cpu decodes the reference's NumPy stream (--rng replay); philox is on-device")
+        device, engine = "cpu", "host"
     info_set = construct_info_set(cfg.N, cfg.K)
     payload_bits = cfg.K - cfg.crc_bits
     snr_points = (np.arange(args.snr_lo, args.snr_hi + 1e-9, args.snr_step) if args.snr_step > 0
@@ -258,7 +263,7 @@ def run_sweep(args: argparse.Namespace) -> List[Dict[str, float]]:
             for b0, b1 in blocks:
                 payload, msg, llr, llr_unc = stream.take(b0, b1)
                 _count_block(c, msg, llr, payload, llr_unc, info_set, args.M, cfg.crc_poly, args.retries, beta, device,
-                             args.dl_engine)
+                             engine)
         else:
             # batches in flight on `--streams` handles (own HIP streams), one host thread each:
             # one batch's TX and DL-SCL retry chain overlap another's decode; counts add exactly
@@ -298,7 +303,8 @@ def run_sweep(args: argparse.Namespace) -> List[Dict[str, float]]:
     if ctx.is_root:
         write_outputs(results, args)
         if args.verbose:
-            print(f"decoded {args.frames * len(snr_points)} frames x2 (SCL + DL-SCL) on {ctx.world} GPU(s) in "
+            where = "the host CPU" if device == "cpu" else f"{ctx.world} GPU(s)"
+            print(f"decoded {args.frames * len(snr_points)} frames x2 (SCL + DL-SCL) on {where} in "
                   f"{elapsed:.2f} s ({args.rng} channel)")
     return results
 
@@ -373,6 +379,8 @@ def build_argparser() -> argparse.ArgumentParser:
                         help="philox: batches in flight per GPU (one handle/stream and host thread each)")
     parser.add_argument("--dl_engine", choices=["device", "host"], default="device",
                         help="device: DL-SCL retry loop on the GPU; host: numpy flip ranking (reference calls)")
+    parser.add_argument("--device", choices=["gpu", "cpu"], default="gpu",
+                        help="cpu: the product's host decoder (no GPU; --rng replay, host flip ranking)")
     parser.add_argument("--no_plot", action="store_true")
     parser.add_argument("--verbose", action="store_true")
     return parser
