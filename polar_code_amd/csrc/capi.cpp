@@ -3,8 +3,9 @@
 // Host side of the engine: validates arguments with the reference's error semantics
 // (scl.py:117-131, crc.py:40-49), precomputes the per-code constants (information mask,
 // CRC syndrome/remainder columns, glibc exp table), owns device scratch and the stream,
-// and launches the kernels in scl_kernels.hip.  There is no CPU decode path: every
-// decode runs on the GPU, and calls fail with PSCL_EDEVICE when no GPU is present.
+// and launches the kernels in scl_kernels.hip.  Every handle entry point runs on the GPU and
+// fails with PSCL_EDEVICE when no GPU is present; the product's host decoder for GPU-less runs
+// is the handle-free pscl_decode_cpu (scl_cpu.cpp).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdarg.h>
@@ -1336,6 +1337,11 @@ int pscl_uncoded_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, doubl
     return PSCL_OK;
 }
 
+namespace {
+int channel_launch(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
+                   int64_t frame0, int64_t B, double* d_llr, uint64_t* d_msg, int64_t* d_unc);
+}
+
 int pscl_simulate(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
                   int64_t frame0, int64_t B, int retries, int include_uncoded, int64_t* counters) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
@@ -1359,10 +1365,12 @@ int pscl_simulate(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno
     HIP_TRY(hipMemsetAsync(d_cnt, 0, sizeof(int64_t) * 3 * PSCL_NCOUNT, h->stream));
     for (int64_t f = 0; f < B; f += chunk) {
         const int64_t n = B - f < chunk ? B - f : chunk;
-        if ((rc = pscl_channel_device(h, seed, stream_id, ebno_db, rate, k_payload, frame0 + f, n, (double*)d_llr,
-                                      (uint64_t*)d_msg)))
+        // N <= 128: the uncoded baseline is counted by the TX launch itself (same payload draw)
+        const bool unc_fused = include_uncoded && N <= PSCL_FAST_N;
+        if ((rc = channel_launch(h, seed, stream_id, ebno_db, rate, k_payload, frame0 + f, n, (double*)d_llr,
+                                 (uint64_t*)d_msg, unc_fused ? cs + 2 * PSCL_NCOUNT : nullptr)))
             return rc;
-        if (include_uncoded &&
+        if (include_uncoded && !unc_fused &&
             (rc = pscl_uncoded_device(h, seed, stream_id, ebno_db, k_payload, frame0 + f, n, cs + 2 * PSCL_NCOUNT)))
             return rc;
         if ((rc = pscl_dlscl_device(h, (const double*)d_llr, n, retries, (uint64_t*)d_best, (uint8_t*)d_flags, nullptr,
@@ -1374,8 +1382,11 @@ int pscl_simulate(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno
     return PSCL_OK;
 }
 
-int pscl_channel_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
-                        int64_t frame0, int64_t B, double* d_llr, uint64_t* d_msg) {
+namespace {
+// the TX launch (pscl_channel_device); d_unc != null also counts the uncoded baseline of the
+// same frames (N <= 128: channel_kernel's phase A) at unc_ebno_db
+int channel_launch(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
+                   int64_t frame0, int64_t B, double* d_llr, uint64_t* d_msg, int64_t* d_unc) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
     if (B < 0 || frame0 < 0) return fail(PSCL_EINVAL, "B and frame0 must be >= 0");
     if (B == 0) return PSCL_OK;
@@ -1399,15 +1410,26 @@ int pscl_channel_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, doubl
     const double ebno = pow(10.0, ebno_db / 10.0);
     P.noise_var = 1.0 / (2.0 * rate * ebno);
     P.sigma = sqrt(P.noise_var);
+    P.llr_scale = 2.0 / P.noise_var;
     P.frame0 = frame0;
     P.B = B;
     P.llr = d_llr;
     P.msg = d_msg;
     P.rm_E = h->rm_E;
     P.rm_order = h->d_rm_order;
+    if (d_unc) {
+        P.unc_counters = d_unc;
+        P.unc_sigma = sqrt(1.0 / (2.0 * ebno));  // run_fer_sweep.py:66-67 (uncoded: R = 1)
+    }
     hipError_t e = pscl_launch_channel(P, h->stream);
     if (e != hipSuccess) return fail(PSCL_EDEVICE, "channel kernel launch: %s", hipGetErrorString(e));
     return PSCL_OK;
+}
+}  // namespace
+
+int pscl_channel_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
+                        int64_t frame0, int64_t B, double* d_llr, uint64_t* d_msg) {
+    return channel_launch(h, seed, stream_id, ebno_db, rate, k_payload, frame0, B, d_llr, d_msg, nullptr);
 }
 
 int pscl_set_rate_match(pscl_handle* h, int E) {

@@ -194,6 +194,9 @@ struct pscl_channel_params {
     const uint64_t* xtab;        // [ceil(K/8)][256][2]: codeword x of message byte k = v (linear)
     const uint32_t* crctab;      // [ceil(k_payload/8)][256]: CRC remainder of payload byte k = v
     double sigma, noise_var;
+    double llr_scale;            // 2 / noise_var: LLR = (symbol + sigma z) * llr_scale
+    double unc_sigma;            // uncoded baseline (run_fer_sweep.py:111-121): its noise sigma (R = 1)
+    int64_t* unc_counters;       // [PSCL_NCOUNT] or null: count the uncoded baseline in the same launch
     int64_t frame0, B;
     double* llr;                 // [B][N] (or [B][E] with rate matching)
     uint64_t* msg;               // [B][W] or null

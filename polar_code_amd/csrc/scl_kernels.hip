@@ -344,19 +344,39 @@ __device__ __forceinline__ u32x4 philox4x32(u32x4 c, uint32_t k0, uint32_t k1) {
     return c;
 }
 
+// Box-Muller pair from one Philox block (a, bb): u1 in (0, 1] from the top 53 bits of a, u2 in
+// [0, 1) from the top 24 bits of bb; radius and angle with the fp32 hardware transcendentals
+// (v_log_f32, v_sqrt_f32, v_sin/cos_f32 in revolutions), the pair widened to fp64.  u1 keeps
+// all 53 bits (its fp32 image is normal down to 2^-53), so the tail reaches 8.57 sigma like an
+// fp64 draw; the fp32 roundings perturb a normal by ~1e-6 sigma, far below Monte-Carlo error
+// (tests/test_gpu_channel.py states the tolerance).  One fp64 log and sincospi per pair took
+// most of the TX kernel's time.
+__device__ __forceinline__ void bm_pair(uint64_t a, uint64_t bb, double& z0, double& z1) {
+    const float u1 = (float)(((double)(a >> 11) + 1.0) * 0x1p-53);
+    const float u2 = (float)(uint32_t)(bb >> 40) * 0x1p-24f;
+    const float rad = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // -2 ln u1
+    z0 = (double)(rad * __builtin_amdgcn_cosf(u2));
+    z1 = (double)(rad * __builtin_amdgcn_sinf(u2));
+}
+
 // TX chain, two phases per wavefront of 64 frames:
 //   A  lane = frame: Philox payload, CRC remainder and codeword from byte tables (both maps
 //      are GF(2)-linear), message words stored;
 //   B  per frame: its codeword broadcast through SGPRs, lanes generate the Box-Muller pairs
 //      and store the LLR row with coalesced writes.
 // Stream: payload = Philox(frame, draw 0xffffffff); noise pair c = lane + 64 q of a frame =
-// Philox(frame, c) -> symbols c + 64 q and c + 64 q + 64 (c < 64).
+// Philox(frame, c) -> symbols c + 64 q and c + 64 q + 64 (c < 64).  With P.unc_counters the
+// uncoded baseline of the same frames is counted in phase A too (the payload already drawn;
+// noise pairs Philox(frame, 0x40000000 + c), as uncoded_kernel): one launch for the TX chain and
+// the uncoded BPSK baseline of run_fer_sweep.py:79-121.
 __global__ void __launch_bounds__(256) channel_kernel(const pscl_channel_params P) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t k0 = (uint32_t)P.seed, k1 = (uint32_t)(P.seed >> 32) ^ (P.stream_id * 0x85EBCA6Bu);
     const int E = P.rm_E ? P.rm_E : P.N;
     const int kp = P.k_payload;
     const int nb = (P.K + 7) >> 3, nbp = (kp + 7) >> 3;
+    if (P.unc_counters && blockIdx.x == 0 && threadIdx.x == 0)
+        atomicAdd(reinterpret_cast<unsigned long long*>(P.unc_counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
     for (int64_t base = ((int64_t)blockIdx.x * 4 + wave) * 64; base < P.B; base += (int64_t)gridDim.x * 256) {
         // ---- A: one frame per lane
         const int64_t idx = base + lane;
@@ -387,6 +407,32 @@ __global__ void __launch_bounds__(256) channel_kernel(const pscl_channel_params 
             P.msg[idx * P.W] = m0;
             if (P.W > 1) P.msg[idx * P.W + 1] = m1;
         }
+        if (P.unc_counters) {  // uncoded BPSK of the payload (kp <= 128 here: one payload block)
+            int berr = 0;
+            if (idx < P.B) {
+                const uint64_t p0 = ((uint64_t)rb.y << 32) | rb.x, p1 = ((uint64_t)rb.w << 32) | rb.z;
+                for (int c = 0; 2 * c < kp; ++c) {
+                    const u32x4 rn = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), 0x40000000u + (uint32_t)c, 0u}, k0, k1);
+                    double z[2];
+                    bm_pair(((uint64_t)rn.y << 32) | rn.x, ((uint64_t)rn.w << 32) | rn.z, z[0], z[1]);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int q = 2 * c + h;
+                        if (q < kp) {
+                            const int bit = (int)(((q < 64 ? p0 : p1) >> (q & 63)) & 1ULL);
+                            const double y = (bit ? -1.0 : 1.0) + P.unc_sigma * z[h];
+                            berr += (y < 0.0 ? 1 : 0) != bit;
+                        }
+                    }
+                }
+            }
+            const int fe = pscl::wave_sum(berr ? 1 : 0), be = pscl::wave_sum(berr);
+            if (lane == 0) {
+                unsigned long long* C = reinterpret_cast<unsigned long long*>(P.unc_counters);
+                if (fe) atomicAdd(C + PSCL_CNT_FRAME_ERR, (unsigned long long)fe);
+                if (be) atomicAdd(C + PSCL_CNT_BIT_ERR, (unsigned long long)be);
+            }
+        }
         // ---- B: AWGN per frame, 2 symbols per lane per Philox block (NR: symbol p = x[order[p % N]])
         const int nf = (P.B - base) < 64 ? (int)(P.B - base) : 64;
         for (int j = 0; j < nf; ++j) {
@@ -398,13 +444,8 @@ __global__ void __launch_bounds__(256) channel_kernel(const pscl_channel_params 
             double* row = P.llr + (base + j) * E;
             for (int q = 0; q * 128 < E; ++q) {
                 const u32x4 rn = philox4x32(u32x4{(uint32_t)fj, (uint32_t)(fj >> 32), (uint32_t)(lane + 64 * q), 0u}, k0, k1);
-                const uint64_t a = ((uint64_t)rn.y << 32) | rn.x, bb = ((uint64_t)rn.w << 32) | rn.z;
-                const double uu1 = ((double)(a >> 11) + 1.0) * 0x1p-53;  // (0, 1]
-                const double uu2 = (double)(bb >> 11) * 0x1p-53;         // [0, 1)
-                const double rad = sqrt(-2.0 * log(uu1));
-                double sn, cs;
-                sincospi(2.0 * uu2, &sn, &cs);
-                const double z[2] = {rad * cs, rad * sn};
+                double z[2];
+                bm_pair(((uint64_t)rn.y << 32) | rn.x, ((uint64_t)rn.w << 32) | rn.z, z[0], z[1]);
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const int p = lane + 64 * h + 128 * q;
@@ -412,8 +453,7 @@ __global__ void __launch_bounds__(256) channel_kernel(const pscl_channel_params 
                         const int pos = P.rm_E ? P.rm_order[p % P.N] : p;
                         const uint64_t xw = pos < 64 ? xa : xb;
                         const double sym = ((xw >> (pos & 63)) & 1) ? -1.0 : 1.0;
-                        const double received = sym + P.sigma * z[h];
-                        row[p] = 2.0 * received / P.noise_var;
+                        row[p] = (sym + P.sigma * z[h]) * P.llr_scale;
                     }
                 }
             }
@@ -569,13 +609,8 @@ __global__ void __launch_bounds__(256) channel_long_kernel(const pscl_channel_pa
         double* row = P.llr + idx * E;
         for (int q = 0; q * 128 < E; ++q) {
             const u32x4 rn = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), (uint32_t)(lane + 64 * q), 0u}, k0, k1);
-            const uint64_t a = ((uint64_t)rn.y << 32) | rn.x, bb = ((uint64_t)rn.w << 32) | rn.z;
-            const double uu1 = ((double)(a >> 11) + 1.0) * 0x1p-53;  // (0, 1]
-            const double uu2 = (double)(bb >> 11) * 0x1p-53;         // [0, 1)
-            const double rad = sqrt(-2.0 * log(uu1));
-            double sn, cs;
-            sincospi(2.0 * uu2, &sn, &cs);
-            const double z[2] = {rad * cs, rad * sn};
+            double z[2];
+            bm_pair(((uint64_t)rn.y << 32) | rn.x, ((uint64_t)rn.w << 32) | rn.z, z[0], z[1]);
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int p = lane + 64 * h + 128 * q;
@@ -583,8 +618,7 @@ __global__ void __launch_bounds__(256) channel_long_kernel(const pscl_channel_pa
                 const uint64_t xw = pscl::shfl_u64(x, pos >> 6);  // (every lane takes part)
                 if (p < E) {
                     const double sym = ((xw >> (pos & 63)) & 1) ? -1.0 : 1.0;
-                    const double received = sym + P.sigma * z[h];
-                    row[p] = 2.0 * received / P.noise_var;
+                    row[p] = (sym + P.sigma * z[h]) * P.llr_scale;
                 }
             }
         }
@@ -609,20 +643,15 @@ __global__ void __launch_bounds__(256) uncoded_kernel(const pscl_channel_params 
                 r1 = ((uint64_t)rb.w << 32) | rb.z;
             }
             const u32x4 rn = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), 0x40000000u + (uint32_t)c, 0u}, k0, k1);
-            const uint64_t a = ((uint64_t)rn.y << 32) | rn.x, bb = ((uint64_t)rn.w << 32) | rn.z;
-            const double uu1 = ((double)(a >> 11) + 1.0) * 0x1p-53;
-            const double uu2 = (double)(bb >> 11) * 0x1p-53;
-            const double rad = sqrt(-2.0 * log(uu1));
-            double sn, cs;
-            sincospi(2.0 * uu2, &sn, &cs);
-            const double z[2] = {rad * cs, rad * sn};
+            double z[2];
+            bm_pair(((uint64_t)rn.y << 32) | rn.x, ((uint64_t)rn.w << 32) | rn.z, z[0], z[1]);
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int q = 2 * c + h;
                 if (q < kp) {
                     const int bit = (int)((((q & 127) < 64 ? r0 : r1) >> (q & 63)) & 1ULL);
                     const double y = (bit ? -1.0 : 1.0) + P.sigma * z[h];
-                    berr += ((2.0 * y / P.noise_var) < 0.0 ? 1 : 0) != bit;
+                    berr += (y < 0.0 ? 1 : 0) != bit;  // (2 y / var < 0 <=> y < 0: var > 0)
                 }
             }
         }

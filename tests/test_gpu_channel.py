@@ -1,7 +1,10 @@
 """The on-device TX chain (pscl_channel_device) against a NumPy restatement of its stream.
 
-Payload bits, CRC, codeword and message words must match exactly; LLRs agree to ~1e-12
-(the host uses libm log/sin/cos, the device the ROCm device library).  Covers plain N=128,
+Payload bits, CRC, codeword and message words must match exactly.  The Box-Muller pairs are
+computed in fp32 with the hardware transcendentals (v_log_f32, v_sqrt_f32, v_sin/cos_f32, in
+csrc/scl_kernels.hip bm_pair) and widened to fp64; the host restates them with numpy float32
+libm calls, so the normals agree to ~1e-6 (tolerance stated in each test), with every
+systematic slip (range, scaling, pairing) far outside it.  Covers plain N=128,
 short codes, K > 64 (two message words), NR rate matching (repetition and puncturing) and the
 long codes (N = 256..1024: channel_long_kernel, payloads beyond one Philox block).
 """
@@ -44,6 +47,15 @@ def host_payload(k0, k1, lo, hi, kp):
     return pay
 
 
+def host_bm(a, bb):
+    """bm_pair (scl_kernels.hip) in numpy float32: the pair of normals of Philox outputs a, bb."""
+    u1 = (((a >> np.uint64(11)).astype(np.float64) + 1.0) * 2.0 ** -53).astype(np.float32)
+    u2 = (bb >> np.uint64(40)).astype(np.float32) * np.float32(2.0 ** -24)
+    rad = np.sqrt(np.float32(-1.3862943611198906) * np.log2(u1))
+    ang = np.float32(2 * np.pi) * u2
+    return (rad * np.cos(ang)).astype(np.float64), (rad * np.sin(ang)).astype(np.float64)
+
+
 def host_stream(seed, stream_id, frame0, B, N, info, K, kp, crc, ebno_db, rate, E=0, order=None):
     k0 = seed & 0xFFFFFFFF
     k1 = ((seed >> 32) ^ ((stream_id * 0x85EBCA6B) & 0xFFFFFFFF)) & 0xFFFFFFFF
@@ -61,16 +73,13 @@ def host_stream(seed, stream_id, frame0, B, N, info, K, kp, crc, ebno_db, rate, 
         c2 = np.arange(64, dtype=np.uint64) + np.uint64(64 * q)
         cx, cy, cz, cw2 = philox4x32((lo[:, None], hi[:, None], c2[None, :], np.zeros((1, 64), np.uint64)), k0, k1)
         a, bb = (cy << np.uint64(32)) | cx, (cw2 << np.uint64(32)) | cz
-        u1 = ((a >> np.uint64(11)).astype(np.float64) + 1.0) * 2.0 ** -53
-        u2 = (bb >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
-        rad = np.sqrt(-2.0 * np.log(u1))
-        zz = (rad * np.cos(2 * np.pi * u2), rad * np.sin(2 * np.pi * u2))
+        zz = host_bm(a, bb)
         for h in range(2):
             p = np.arange(64) + 64 * h + 128 * q
             ok = p < Etot
             pos = order[p[ok] % N] if E else p[ok]
             sym = 1.0 - 2.0 * cw[:, pos]
-            llr[:, p[ok]] = 2.0 * (sym + np.sqrt(nvar) * zz[h][:, ok]) / nvar
+            llr[:, p[ok]] = (sym + np.sqrt(nvar) * zz[h][:, ok]) * (2.0 / nvar)
     return msg, llr
 
 
@@ -112,7 +121,10 @@ def test_channel_stream(N, K, crc, E):
     msg, ref = host_stream(seed, sid, frame0, B, N, info, K, kp, crc, 3.0, rate, E, order)
     got = ((words[:, :, None] >> np.arange(64, dtype=np.uint64)) & np.uint64(1)).reshape(B, -1)[:, :K]
     np.testing.assert_array_equal(got.astype(np.int8), msg)
-    np.testing.assert_allclose(llr, ref, rtol=1e-11, atol=1e-11)
+    # normals within 2e-5 (fp32 hardware vs libm transcendentals), i.e. LLRs within 2e-5 * 2 / sigma
+    sig = np.sqrt(1.0 / (2.0 * rate * 10 ** 0.3))
+    err = np.abs(llr - ref) * sig / 2.0
+    assert err.max() < 2e-5 and np.median(err) < 1e-6, (err.max(), np.median(err))
 
 
 @pytest.mark.parametrize("kp", [40, 200])
@@ -135,19 +147,37 @@ def test_uncoded_stream(kp):
     pay = host_payload(k0, k1, lo, hi, kp)
     nvar = 1.0 / (2.0 * 10 ** (ebno / 10.0))
     err = np.zeros((B, kp), bool)
+    amb = np.zeros((B, kp), bool)
     for c in range((kp + 1) // 2):
         c2 = np.full(B, 0x40000000 + c, np.uint64)
         cx, cy, cz, cw2 = philox4x32((lo, hi, c2, np.zeros(B, np.uint64)), k0, k1)
         a, bb = (cy << np.uint64(32)) | cx, (cw2 << np.uint64(32)) | cz
-        u1 = ((a >> np.uint64(11)).astype(np.float64) + 1.0) * 2.0 ** -53
-        u2 = (bb >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
-        rad = np.sqrt(-2.0 * np.log(u1))
-        zz = (rad * np.cos(2 * np.pi * u2), rad * np.sin(2 * np.pi * u2))
+        zz = host_bm(a, bb)
         for h in range(2):
             q = 2 * c + h
             if q < kp:
                 y = (1.0 - 2.0 * pay[:, q]) + np.sqrt(nvar) * zz[h]
-                err[:, q] = (2.0 * y / nvar < 0.0) != (pay[:, q] == 1)
+                err[:, q] = (y < 0.0) != (pay[:, q] == 1)
+                amb[:, q] = np.abs(y) < 1e-4  # decisions the fp32 tolerance could flip
     assert cnt[_native.CNT_FRAMES] == B
-    assert cnt[_native.CNT_FRAME_ERR] == int(err.any(axis=1).sum())
-    assert cnt[_native.CNT_BIT_ERR] == int(err.sum())
+    n_amb = int(amb.sum())
+    assert n_amb < 10
+    assert abs(cnt[_native.CNT_FRAME_ERR] - int(err.any(axis=1).sum())) <= n_amb
+    assert abs(cnt[_native.CNT_BIT_ERR] - int(err.sum())) <= n_amb
+
+
+def test_simulate_uncoded_fused_equals_uncoded_kernel():
+    """pscl_simulate counts the uncoded baseline inside the TX launch (N <= 128): the same
+    frames' uncoded FER/BER counters as the stand-alone uncoded_device launch, exactly."""
+    info = construct_info_set(128, 64)
+    dec = _native.Decoder(128, info, 8, "0x1864CFB")
+    B, frame0, seed, sid, ebno = 200_000, 1000, 0xABC, 50, 4.0
+    nc = _native.PSCL_NCOUNT
+    sim = dec.simulate(seed, sid, ebno, 0.5, 40, frame0, B, 0, include_uncoded=True)
+    with _native.DeviceArena(dec) as mem:
+        d_cnt = mem.alloc(nc * 8)
+        mem.memset(d_cnt, 0, nc * 8)
+        dec.uncoded_device(seed, sid, ebno, 40, frame0, B, d_cnt)
+        unc = mem.download(d_cnt, nc * 8, np.int64)
+    np.testing.assert_array_equal(sim[2], unc)
+    assert unc[_native.CNT_FRAMES] == B and 0.1 < unc[_native.CNT_FRAME_ERR] / B < 0.5

@@ -1,6 +1,6 @@
 """Per-SNR wall time of the Philox FER sweep (TX + SCL + DL-SCL + counters on the GPU).
 
-    python tools/sweep_timing.py [M] [frames_per_snr] [batch] [threads]
+    python tools/sweep_timing.py [M] [frames_per_snr] [batch] [threads] [snr,snr,...]
 """
 import sys
 import time
@@ -15,8 +15,9 @@ M = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 frames = int(sys.argv[2]) if len(sys.argv) > 2 else 4_000_000
 batch = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 19
 streams = int(sys.argv[4]) if len(sys.argv) > 4 else 2
+snrs = [float(x) for x in sys.argv[5].split(",")] if len(sys.argv) > 5 else [4.0, 4.5, 5.0, 5.5, 6.0, 6.5]
 
-for rep, snr in enumerate((4.0, 4.0, 4.5, 5.0, 5.5, 6.0, 6.5)):  # the first pass warms up
+for rep, snr in enumerate([snrs[0]] + snrs):  # the first pass warms up
     c = np.zeros(rfs.NCOUNT, np.int64)
     args = rfs.build_argparser().parse_args(
         ["--M", str(M), "--frames", str(frames), "--snr_lo", str(snr), "--snr_hi", str(snr), "--snr_step", "0",
