@@ -74,6 +74,13 @@ int pscl_screening_fs_available(const pscl_decode_params& P) {
     return spec_code(P) == 1;
 }
 
+// the screening launch of this plain decode runs the lane-per-path kernel (scl128_lane.hip):
+// the (128,64) code, L = 8, plain channel rows
+int pscl_lane_available(const pscl_decode_params& P) {
+    if (!PSCL_LANE || !P.apx || P.force || P.sc_hard || P.rm_E || P.fidx || P.d_count || P.elist || P.L != 8) return 0;
+    return P.N == 128 && spec_code(P) == 1;
+}
+
 int pscl_screening_available(const pscl_decode_params& P) {
     if (!P.fast || P.force || P.sc_hard || P.L != pscl_decode_lmax(P.L)) return 0;
     const int code = spec_code(P);

@@ -1,0 +1,484 @@
+// scl128_lane.hip -- the lane-per-path screening decoder for N = 128, L = 8 (the headline decode,
+// BASELINE.json: P(128,64)+CRC-24 SCL L = 8) and its launch.
+//
+// Same contract as the screening pass of scl128_kernel (scl128_impl.h, APX = true; DESIGN.md
+// §5.1a): a plain decode of the compiled-in (128,64) code whose path metrics carry the
+// bounded-error tail (pscl_softplus_tail_abs); every ordering decision it makes must clear the
+// absolute margin, and a frame with an uncertain one is appended to P.amb_list for the exact
+// re-decode (the exact kernel, launched by capi.cpp).  Results are therefore bit-identical to
+// decode_scl (dl_scl_polar/polar/scl.py:108-209).
+//
+// Mapping (the difference from scl128_kernel): ONE lane per list path, G = L = 8 lanes per frame,
+// F = 8 frames per wavefront.  scl128_kernel gives each frame 2L = 16 lanes, the upper half
+// holding the bit-1 children; every per-path step (leaf, tail, metric, list bookkeeping) then runs
+// on half-used lanes.  Here a lane holds both children of its path during an information phase:
+//   * frozen phase: leaf, tail, metric advance (no ordering decision);
+//   * information phase, list growing (its first log2 L): every child survives, bit-1 children
+//     move to lanes cnt..2cnt-1;
+//   * information phase, full list: if every worse child clears the largest better child by the
+//     margin (one DPP max over the frame's 8 lanes) the better children stay in place (the
+//     common case); else the 2L children are ranked (each lane counts the keys below its two
+//     children: 7 lane permutations -- quad_perm xor 1..3 and the half-row mirror composed with
+//     them -- of DPP-fused subtract + add-with-carry), the survivor set is certified (exactly L
+//     survivors, the largest survivor's margin-raised key below the smallest non-survivor's key)
+//     and each freed lane pulls the j-th surviving worse child of its frame (j-th set bit of an
+//     8-bit mask, computed in VALU) with ds_bpermute;
+//   * depths 1-3 recomputed every 16 phases from the frame's 128 channel LLRs, which the 8 lanes
+//     hold in registers (16 each); depths 3-6 in LDS slots with lazy copies (slot tables), as
+//     scl128_kernel.
+// LDS per frame: depths 3..6 = 30 L doubles (1920 B at L = 8), the left-sibling partial sums of
+// the depth-1..3 recompute aliased onto depth 6 (dead at a recompute phase); 15 KB per wavefront,
+// 10 wavefronts per CU.  One wavefront per workgroup (no barriers); the epilogue's u-byte gather
+// and CRC syndrome tables are read from global memory (L1/L2-resident).
+#include "scl128_impl.h"
+
+namespace {
+
+template <int LMAX>
+struct LaneLayout {
+    static constexpr int G = LMAX;
+    static constexpr int F = 64 / G;
+    static constexpr int LOG_G = __builtin_ctz(G);
+    static constexpr int OFF3 = 0;              // [8][L][2]
+    static constexpr int OFF4 = OFF3 + 16 * LMAX;  // [4][L][2]
+    static constexpr int OFF5 = OFF4 + 8 * LMAX;   // [2][L][2]
+    static constexpr int OFF6 = OFF5 + 4 * LMAX;   // [1][L][2]; recompute phases: partial sums (16 B per path)
+    // 30 L doubles: at L = 8, 240 = 16 (mod 32), so frames start alternately on the two 128-byte
+    // halves of the 256-byte bank row and a ds_read_b128 lane group (lanes of 4 frames) touching one
+    // pair index of its paths' slots covers 4 distinct 64-byte quarters
+    static constexpr int FSTRIDE = OFF6 + 2 * LMAX;
+};
+
+// intra-frame lane permutations of an 8-lane group (DPP controls): quad_perm xor 1, 2, 3, and the
+// half-row mirror (lane i <-> 7 - i), which maps one quad onto the other
+constexpr int kQX1 = 0xB1, kQX2 = 0x4E, kQX3 = 0x1B, kQID = 0xE4, kHMIR = 0x141;
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+
+// rank counts of this lane's two children against the two children of lane pi(this lane):
+// rg += [og < kg] + [ob < kg], rb += [og < kb] + [ob < kb], the other lane's keys read through the
+// DPP permutation CTRL of og / ob (hand-scheduled: inline asm is not hazard-checked, so the first
+// instruction waits out a VALU write of the key registers)
+template <int CTRL>
+__device__ __forceinline__ void rank_pair(uint32_t og, uint32_t ob, uint32_t kg, uint32_t kb, uint32_t& rg, uint32_t& rb) {
+    uint32_t t;
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_sub_co_u32_dpp %0, vcc, %3, %5 quad_perm:[%7,%8,%9,%10] row_mask:0xf bank_mask:0xf\n\t"
+        "v_addc_co_u32 %1, vcc, 0, %1, vcc\n\t"
+        "v_sub_co_u32_dpp %0, vcc, %4, %5 quad_perm:[%7,%8,%9,%10] row_mask:0xf bank_mask:0xf\n\t"
+        "v_addc_co_u32 %1, vcc, 0, %1, vcc\n\t"
+        "v_sub_co_u32_dpp %0, vcc, %3, %6 quad_perm:[%7,%8,%9,%10] row_mask:0xf bank_mask:0xf\n\t"
+        "v_addc_co_u32 %2, vcc, 0, %2, vcc\n\t"
+        "v_sub_co_u32_dpp %0, vcc, %4, %6 quad_perm:[%7,%8,%9,%10] row_mask:0xf bank_mask:0xf\n\t"
+        "v_addc_co_u32 %2, vcc, 0, %2, vcc"
+        : "=&v"(t), "+v"(rg), "+v"(rb)
+        : "v"(og), "v"(ob), "v"(kg), "v"(kb), "i"(CTRL & 3), "i"((CTRL >> 2) & 3), "i"((CTRL >> 4) & 3),
+          "i"((CTRL >> 6) & 3)
+        : "vcc");
+}
+
+// max / min / sum of v over the 8 lanes of each frame (3 DPP steps)
+__device__ __forceinline__ uint32_t frame_max8(uint32_t v) {
+    uint32_t o = dpp32<kQX1>(v);
+    v = o > v ? o : v;
+    o = dpp32<kQX2>(v);
+    v = o > v ? o : v;
+    o = dpp32<kHMIR>(v);
+    return o > v ? o : v;
+}
+__device__ __forceinline__ uint32_t frame_min8(uint32_t v) {
+    uint32_t o = dpp32<kQX1>(v);
+    v = o < v ? o : v;
+    o = dpp32<kQX2>(v);
+    v = o < v ? o : v;
+    o = dpp32<kHMIR>(v);
+    return o < v ? o : v;
+}
+__device__ __forceinline__ uint32_t frame_sum8(uint32_t v) {
+    v += dpp32<kQX1>(v);
+    v += dpp32<kQX2>(v);
+    return v + dpp32<kHMIR>(v);
+}
+
+// position of the j-th set bit (j < popcount(m)) of an 8-bit mask, branch-free
+__device__ __forceinline__ uint32_t nth_set_bit8(uint32_t m, uint32_t j) {
+    const uint32_t c4 = __builtin_popcount(m & 15u);
+    const bool h4 = j >= c4;
+    j = h4 ? j - c4 : j;
+    m = h4 ? (m >> 4) : (m & 15u);
+    const uint32_t c2 = __builtin_popcount(m & 3u);
+    const bool h2 = j >= c2;
+    j = h2 ? j - c2 : j;
+    m = h2 ? (m >> 2) : m;
+    const bool h1 = j >= (m & 1u);
+    return (h4 ? 4u : 0u) + (h2 ? 2u : 0u) + (h1 ? 1u : 0u);
+}
+
+// the one-swap tier between the keep-the-better-children path and the full ranking
+#ifndef PSCL_LANE_SWAP
+#define PSCL_LANE_SWAP 1
+#endif
+
+#ifndef PSCL_LANE_WAVES_PER_EU
+#define PSCL_LANE_WAVES_PER_EU 2
+#endif
+
+template <int LMAX, int CODE>
+__global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(const pscl_decode_params P) {
+    static_assert(LMAX == 8, "the lane-per-path decoder is built for L = 8");
+    using Ly = LaneLayout<LMAX>;
+    constexpr int G = Ly::G, F = Ly::F, LOG_G = Ly::LOG_G;
+    constexpr int K = kSpecK[CODE], PW = (K + 63) / 64;
+    constexpr uint64_t info0 = kSpecInfo[CODE][0], info1 = kSpecInfo[CODE][1];
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double* const A = reinterpret_cast<double*>(smem);
+    const int lane = threadIdx.x & 63;
+    const int fl = lane >> LOG_G, p = lane & (G - 1), gbase = lane & ~(G - 1);
+    double* const Af = A + fl * Ly::FSTRIDE;
+    const uint8_t* const GT = reinterpret_cast<const uint8_t*>(P.epi_table);   // [16][256] u-byte -> info bits
+    const uint32_t* const ST = reinterpret_cast<const uint32_t*>(GT + 16 * 256);  // [K/4][16] nibble -> syndrome
+    auto hiw = [](double m) { return (uint32_t)(pscl_asu64(m) >> 32); };
+    auto hiw_up = [&](double m) { return hiw(__builtin_fma(m, 1.0 + 0x1p-40, PSCL_TAIL_ABS_MARGIN)); };
+
+    for (int64_t f0 = (int64_t)blockIdx.x * F; f0 < P.B; f0 += (int64_t)gridDim.x * F) {
+        const int64_t fi = f0 + fl;
+        const bool fvalid = fi < P.B;
+        const int64_t frow = fvalid ? fi : f0;  // (a tail wave's empty slots decode a copy of frame f0)
+        const double* chan = P.llr + frow * kN;
+        // the frame's channel LLRs in registers: elements e = p (c[m] = chan[p + 16 m]) and
+        // e = p + 8 (c[8 + m]) of the depth-3 node -- the same at all 8 depth-1..3 recomputes
+        double c[16];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            c[m] = chan[p + 16 * m];
+            c[8 + m] = chan[p + 8 + 16 * m];
+        }
+        // frames whose channel magnitudes could overflow the fp64 metric sums or carry a NaN go to
+        // the exact re-decode (the lane's 16 values summed; NaN propagates through the sum)
+        double cs = fabs(c[0]);
+#pragma unroll
+        for (int m = 1; m < 16; ++m) cs = cs + fabs(c[m]);
+        uint64_t amb = wmask(!(cs < 0x1p25));
+        const uint64_t vmask = wmask(fvalid);
+
+        double metric = 0.0;
+        uint64_t u0 = 0, u1 = 0;  // decided bits
+        uint32_t tab = 0;          // LDS slot of depths 3..6 (4 bits each)
+        uint32_t lastbit = 0;      // the bit decided at the previous phase
+
+        auto phase = [&](auto PC) {
+            constexpr int phi = decltype(PC)::value;
+            constexpr int t = phi & 15;
+            constexpr int start = t ? kn - __builtin_ctz((unsigned)t) : ((phi >> 4) ? 3 - __builtin_ctz((unsigned)(phi >> 4)) : 1);
+            constexpr bool is_info = ((phi < 64 ? info0 : info1) >> (phi & 63)) & 1;
+            constexpr int jb = phi < 64 ? __builtin_popcountll(info0 & ((1ULL << (phi & 63)) - 1))
+                                        : __builtin_popcountll(info0) + __builtin_popcountll(info1 & ((1ULL << (phi & 63)) - 1));
+            constexpr int cnt = jb >= 3 ? LMAX : (1 << jb);  // live paths (min(2^j, L))
+#ifdef PSCL_PHASE_MARKERS  // asm listing analysis only (tools/isa_phase_stats.py)
+            asm volatile("; PHASE %0" ::"n"(t));
+#endif
+
+            // ---- depths 1-3 recomputed from the channel (phi % 16 == 0)
+            if constexpr (start <= 3) {
+                constexpr bool r1 = phi >= 64, r2 = (phi >> 5) & 1, r3 = (phi >> 4) & 1;
+                uint4* const xs = reinterpret_cast<uint4*>(Af + Ly::OFF6);
+                if constexpr (r1 || r2 || r3) {
+                    uint64_t X1 = 0;
+                    uint32_t X2 = 0, X3 = 0;
+                    if (r1) X1 = polar_transform64(u0);
+                    if (r2) {
+                        constexpr int lo = phi - (phi & 31) - 32;
+                        X2 = polar_transform32((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)));
+                    }
+                    if (r3) {
+                        constexpr int lo = phi - 16;
+                        X3 = polar_transform16((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)) & 0xffffu);
+                    }
+                    xs[p] = make_uint4((uint32_t)X1, (uint32_t)(X1 >> 32), X2, X3);
+                    wave_lds_fence();
+                }
+                // the depth-1 f node is the same for every path before phase 64, and depth 2 too
+                // at phases 0 and 16
+                constexpr bool shared2 = !r1 && !r2;
+                double d1l[2][4], d2s[2][2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) d1l[h][m] = r1 ? 0.0 : f_minsum(c[8 * h + m], c[8 * h + m + 4]);
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) d2s[h][s2] = shared2 ? f_minsum(d1l[h][s2], d1l[h][s2 + 2]) : 0.0;
+                }
+                constexpr int npaths = cnt;
+#pragma unroll
+                for (int q0 = 0; q0 < npaths; ++q0) {
+                    // lane p takes path (q0 + p) mod L: the 8 lanes' stores hit 8 distinct bank groups
+                    const int q = npaths == LMAX ? ((q0 + p) & (LMAX - 1)) : q0;
+                    uint64_t x1 = 0;
+                    uint32_t x2 = 0, x3 = 0;
+                    if constexpr (r1 || r2 || r3) {
+                        const uint4 xv = xs[q];
+                        x1 = ((uint64_t)xv.y << 32) | xv.x;
+                        x2 = xv.z;
+                        x3 = xv.w;
+                    }
+                    double d3[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const uint32_t e = (uint32_t)(p + 8 * h);
+                        double d1[4];
+#pragma unroll
+                        for (int m = 0; m < 4; ++m)
+                            d1[m] = r1 ? g_node_wbit(c[8 * h + m], c[8 * h + m + 4], (uint32_t)(x1 >> (32 * (m >> 1))), e + 16 * (m & 1))
+                                       : d1l[h][m];
+                        double d2[2];
+#pragma unroll
+                        for (int s2 = 0; s2 < 2; ++s2)
+                            d2[s2] = shared2 ? d2s[h][s2] : (r2 ? g_node_wbit(d1[s2], d1[s2 + 2], x2, e + 16 * s2) : f_minsum(d1[s2], d1[s2 + 2]));
+                        d3[h] = r3 ? g_node_wbit(d2[0], d2[1], x3, e) : f_minsum(d2[0], d2[1]);
+                    }
+                    // elements p and p + 8 of slot q: one pair ([8][L][2] layout)
+                    *reinterpret_cast<double2*>(Af + Ly::OFF3 + (p * LMAX + q) * 2) = make_double2(d3[0], d3[1]);
+                }
+                wave_lds_fence();
+            }
+            // ---- depths 4..6: this lane's own path; the first rewritten depth reads the parent slot
+            if constexpr (start <= 6) {
+                uint32_t xsb = 0;  // partial sums of the first rewritten node's left sibling (g node)
+                if constexpr (phi && start >= 4) {
+                    constexpr int w = 1 << (kn - start), lo = phi - w;
+                    xsb = polar_transform8((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)) & ((1u << w) - 1u));
+                }
+                static_for<3>([&](auto DI) {
+                    constexpr int D = 4 + decltype(DI)::value;
+                    if constexpr (D >= start) {
+                        constexpr int W = 1 << (kn - D), HW = W / 2;
+                        constexpr int OFF_IN = D == 4 ? Ly::OFF3 : (D == 5 ? Ly::OFF4 : Ly::OFF5);
+                        constexpr int OFF_OUT = D == 4 ? Ly::OFF4 : (D == 5 ? Ly::OFF5 : Ly::OFF6);
+                        constexpr bool first = D == start || (D == 4 && start < 4);
+                        constexpr bool is_g = D == start && phi != 0;
+                        const int sin = first ? slot_at(tab, D - 1) : p;  // (depth 3 at a recompute: own slot p)
+                        const int sin_eff = (D == 4 && start <= 3) ? p : sin;
+                        const double* in = Af + OFF_IN + sin_eff * 2;
+                        double o[W];
+#pragma unroll
+                        for (int k = 0; k < W; ++k) {
+                            const double2 ab = *reinterpret_cast<const double2*>(in + k * LMAX * 2);
+                            o[k] = is_g ? g_node(ab.x, ab.y, (xsb >> k) & 1u) : f_minsum(ab.x, ab.y);
+                        }
+                        double* out = Af + OFF_OUT + p * 2;
+                        if constexpr (HW >= 1) {
+#pragma unroll
+                            for (int k = 0; k < (HW ? HW : 1); ++k)
+                                *reinterpret_cast<double2*>(out + k * LMAX * 2) = make_double2(o[k], o[k + HW]);
+                        }
+                        wave_lds_fence();
+                    }
+                });
+                // this path's own slot at every depth rewritten this phase
+                constexpr int s0 = start < 3 ? 3 : start;
+                constexpr uint32_t mask = (0xffffu << (4 * (s0 - 3))) & 0xffffu;
+                tab = (tab & ~mask) | ((uint32_t)p * 0x1111u & mask);
+            }
+            // ---- leaf LLR and metric tail (scl.py:80-82, 102-105)
+            const double2 lab = *reinterpret_cast<const double2*>(Af + Ly::OFF6 + (start <= 6 ? p : slot_at(tab, 6)) * 2);
+            const double lam = (phi & 1) ? g_node(lab.x, lab.y, lastbit) : f_minsum(lab.x, lab.y);
+            const double Lt = pscl_softplus_tail_abs(lam);
+            if constexpr (!is_info) {  // frozen: bit 0 (scl.py:149-153)
+                metric = metric + (relu_neg(lam) + Lt);
+                lastbit = 0;
+                return;
+            }
+            // information phase: better child (along the LLR sign) mg, worse child mb
+            const double mg = metric + Lt, mb = mg + fabs(lam);
+            const uint32_t gbit = sign_bit(lam);
+            if constexpr (cnt < LMAX) {
+                // growing list: every child survives; bit-1 children to lanes cnt..2cnt-1
+                const double m0 = gbit ? mb : mg, m1 = gbit ? mg : mb;
+                const int src = gbase + (p & (cnt - 1));
+                const uint32_t b = (p & cnt) ? 1u : 0u;
+                const uint64_t pm1 = shfl_u64(pscl_asu64(m1), src);
+                metric = b ? pscl_asf64(pm1) : m0;
+                u0 = shfl_u64(u0, src);
+                if (phi >= 64) u1 = shfl_u64(u1, src);
+                tab = bperm32(tab, src);
+                if (phi < 64) u0 |= (uint64_t)b << phi; else u1 |= (uint64_t)b << (phi - 64);
+                lastbit = b;
+                return;
+            }
+            // full list: keep the better children when every worse child clears the largest
+            // better child by the margin (the stable sort's outcome; ties never reach the sort)
+            const uint32_t kgu = hiw_up(mg), kb = hiw(mb);
+            const uint32_t mx = frame_max8(kgu);
+            const bool bad = kb <= mx;  // this worse child is not clear of every better child
+            const uint64_t badm = wmask(bad);
+            if ((badm & vmask) == 0) {
+                metric = mg;
+                lastbit = gbit;
+                if (phi < 64) u0 |= (uint64_t)gbit << phi; else u1 |= (uint64_t)gbit << (phi - 64);
+                return;
+            }
+            const uint32_t sh = (uint32_t)gbase & 31u;
+            const uint32_t bad8 = ((fl < 4 ? (uint32_t)badm : (uint32_t)(badm >> 32)) >> sh) & 0xffu;
+#if PSCL_LANE_SWAP
+            // one-swap path (every frame of the wave has at most one worse child w that is not
+            // clear): the survivors are the better children but the largest, gmax, plus w -- certain
+            // when w and the second-largest better child are both below gmax by the margin (every
+            // other worse child already clears every better child, hence w too); else the frame is
+            // deferred (its boundary is within the margin, which no ranking could certify either)
+            if ((wmask(__builtin_popcount(bad8) > 1) & vmask) == 0) {
+                const uint32_t kg = hiw(mg);
+                const uint32_t gmaxh = frame_max8(kg);
+                const bool ismax = kg == gmaxh;
+                const uint32_t nmax = frame_sum8(ismax ? 1u : 0u);
+                const uint32_t g2u = frame_max8(ismax ? 0u : kgu);
+                const uint32_t wu = frame_max8(bad ? hiw_up(mb) : 0u);
+                const bool swap = bad8 != 0;
+                amb |= wmask(swap && !(nmax == 1u && g2u < gmaxh && wu < gmaxh)) & vmask;
+                const int src = (gbase + (int)__builtin_ctz(bad8 | 0x100u)) & 63;  // (frames without a swap: unused)
+                const uint32_t tw = tab | ((gbit ^ 1u) << 31);
+                const uint64_t pmb = shfl_u64(pscl_asu64(mb), src);
+                const uint64_t pu0 = shfl_u64(u0, src);
+                const uint64_t pu1 = phi >= 64 ? shfl_u64(u1, src) : 0ULL;
+                const uint32_t ptw = bperm32(tw, src);
+                uint32_t b = gbit;
+                if (swap && ismax) {
+                    metric = pscl_asf64(pmb);
+                    u0 = pu0;
+                    u1 = pu1;
+                    tab = ptw & 0x7fffffffu;
+                    b = ptw >> 31;
+                } else {
+                    metric = mg;
+                }
+                if (phi < 64) u0 |= (uint64_t)b << phi; else u1 |= (uint64_t)b << (phi - 64);
+                lastbit = b;
+                return;
+            }
+#endif
+            // rank the 2L children of each frame: counts of keys (high words) strictly below each
+            const uint32_t kg = hiw(mg);
+            uint32_t rg = 0, rb = kg < kb ? 1u : 0u;
+            rank_pair<kQX1>(kg, kb, kg, kb, rg, rb);
+            rank_pair<kQX2>(kg, kb, kg, kb, rg, rb);
+            rank_pair<kQX3>(kg, kb, kg, kb, rg, rb);
+            const uint32_t mkg = dpp32<kHMIR>(kg), mkb = dpp32<kHMIR>(kb);
+            rank_pair<kQID>(mkg, mkb, kg, kb, rg, rb);
+            rank_pair<kQX1>(mkg, mkb, kg, kb, rg, rb);
+            rank_pair<kQX2>(mkg, mkb, kg, kb, rg, rb);
+            rank_pair<kQX3>(mkg, mkb, kg, kb, rg, rb);
+            const bool keep_g = rg < (uint32_t)LMAX, win_b = rb < (uint32_t)LMAX;
+            // certificate: exactly L survivors, and the largest survivor (raised by the margin)
+            // below the smallest non-survivor
+            const uint32_t kbu = hiw_up(mb);
+            const uint32_t su = keep_g ? (win_b ? kbu : kgu) : (win_b ? kbu : 0u);
+            const uint32_t nm = keep_g ? (win_b ? 0xffffffffu : kb) : kg;
+            const uint32_t nsurv = frame_sum8((keep_g ? 1u : 0u) + (win_b ? 1u : 0u));
+            const uint32_t smax = frame_max8(su), nmin = frame_min8(nm);
+            amb |= wmask(!(nsurv == (uint32_t)LMAX && nmin > smax)) & vmask;
+            // freed lanes take the surviving worse children: the j-th freed lane of a frame pulls
+            // the j-th winner (both counted in lane order)
+            const uint64_t fw = wmask(!keep_g), ww = wmask(win_b);
+            const uint32_t f8 = ((fl < 4 ? (uint32_t)fw : (uint32_t)(fw >> 32)) >> sh) & 0xffu;
+            const uint32_t w8 = ((fl < 4 ? (uint32_t)ww : (uint32_t)(ww >> 32)) >> sh) & 0xffu;
+            const uint32_t j = __builtin_popcount(f8 & ((1u << p) - 1u));
+            const int src = gbase + (int)nth_set_bit8(w8, j);
+            const uint32_t tw = tab | ((gbit ^ 1u) << 31);  // the worse child's bit rides on the table word
+            const uint64_t pmb = shfl_u64(pscl_asu64(mb), src);
+            const uint64_t pu0 = shfl_u64(u0, src);
+            const uint64_t pu1 = phi >= 64 ? shfl_u64(u1, src) : 0ULL;
+            const uint32_t ptw = bperm32(tw, src);
+            uint32_t b = gbit;
+            if (!keep_g) {
+                metric = pscl_asf64(pmb);
+                u0 = pu0;
+                u1 = pu1;
+                tab = ptw & 0x7fffffffu;
+                b = ptw >> 31;
+            } else {
+                metric = mg;
+            }
+            if (phi < 64) u0 |= (uint64_t)b << phi; else u1 |= (uint64_t)b << (phi - 64);
+            lastbit = b;
+        };
+        static_for<kN>([&](auto PC) { phase(PC); });
+
+        // ---- epilogue: candidates u[info_set], CRC syndrome, final list order certified,
+        // best = first CRC pass in list order (scl.py:176-209)
+        uint64_t ib0 = 0, ib1 = 0;
+        {
+            int off = 0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const uint32_t byte = (uint32_t)(((k < 8 ? u0 : u1) >> (8 * (k & 7))) & 255u);
+                const uint64_t cb = GT[k * 256 + byte];
+                if (off < 64) {
+                    ib0 |= cb << off;
+                    if (off > 56) ib1 |= cb >> (64 - off);
+                } else {
+                    ib1 |= cb << (off - 64);
+                }
+                off += __builtin_popcount((uint32_t)(((k < 8 ? info0 : info1) >> (8 * (k & 7))) & 255u));
+            }
+        }
+        uint32_t syn = 0;
+        if (P.has_crc) {
+            constexpr int k4 = (K + 3) >> 2;
+#pragma unroll
+            for (int m = 0; m < k4; ++m)
+                syn ^= ST[m * 16 + (uint32_t)(((m < 16 ? ib0 : ib1) >> (4 * (m & 15))) & 15u)];
+        }
+        // list position = rank of the metric among the frame's L (high words); certified when all
+        // pairs are apart by the margin (then the ranks are distinct and equal the exact order)
+        const uint32_t kh = hiw(metric), ku = hiw_up(metric);
+        uint32_t r = 0;
+        bool near = false;
+        auto cmp_perm = [&](uint32_t oh, uint32_t ou) {
+            r += oh < kh ? 1u : 0u;
+            near = near || !(ku < oh || ou < kh);
+        };
+        cmp_perm(dpp32<kQX1>(kh), dpp32<kQX1>(ku));
+        cmp_perm(dpp32<kQX2>(kh), dpp32<kQX2>(ku));
+        cmp_perm(dpp32<kQX3>(kh), dpp32<kQX3>(ku));
+        const uint32_t mh = dpp32<kHMIR>(kh), mu = dpp32<kHMIR>(ku);
+        cmp_perm(mh, mu);
+        cmp_perm(dpp32<kQX1>(mh), dpp32<kQX1>(mu));
+        cmp_perm(dpp32<kQX2>(mh), dpp32<kQX2>(mu));
+        cmp_perm(dpp32<kQX3>(mh), dpp32<kQX3>(mu));
+        amb |= wmask(near) & vmask;
+        const bool famb = ((amb >> gbase) & 0xffULL) != 0;
+        if (famb && p == 0 && fvalid) P.amb_list[atomicAdd(P.amb_count, 1)] = fi;
+        // best: the lowest list position whose candidate passes the CRC (position 0 if none)
+        const uint32_t pass = P.has_crc ? (syn == 0 ? 1u : 0u) : 1u;
+        const uint32_t keyb = pass ? r : 8u + r;
+        const uint32_t kbest = frame_min8(keyb);
+        if (fvalid && !famb && keyb == kbest) {
+            const int best = (int)(kbest & 7u);
+            const bool bpass = kbest < 8u;
+            if (P.best) {
+                P.best[fi * PW] = ib0;
+                if (PW > 1) P.best[fi * PW + 1] = ib1;
+            }
+            if (P.flags) P.flags[fi] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
+            if (P.n_paths) P.n_paths[fi] = LMAX;
+            if (P.ref) count_errors(P.counters, ib0, ib1, P.ref[fi * PW], PW > 1 ? P.ref[fi * PW + 1] : 0, P.k_payload, bpass);
+        }
+        wave_lds_fence();
+    }
+    if (P.ref && blockIdx.x == 0 && threadIdx.x == 0)
+        atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
+}
+
+}  // namespace
+
+// the lane-per-path screening launch of a plain (128,64) L = 8 decode; lds = LDS bytes per
+// workgroup (one wavefront)
+int pscl_lane_lds_bytes() { return LaneLayout<8>::F * LaneLayout<8>::FSTRIDE * 8; }
+
+hipError_t pscl_launch_lane(const pscl_decode_params& P, int64_t grid, hipStream_t s) {
+    hipLaunchKernelGGL((scl_lane_kernel<8, 1>), dim3((unsigned)grid), dim3(64), pscl_lane_lds_bytes(), s, P);
+    return hipGetLastError();
+}

@@ -213,6 +213,14 @@ hipError_t pscl_launch_long(const pscl_decode_params& P, int hist, hipStream_t s
 void pscl_decode_layout(pscl_decode_params& P, int hist);
 int pscl_fast128_fstride(int L, int ch);
 int pscl_screening_available(const pscl_decode_params& P);  // scl128.hip
+// lane-per-path screening decoder (scl128_lane.hip): (128,64), L = 8, plain decodes; PSCL_LANE = 0
+// builds time scl128_kernel's screening instance instead
+#ifndef PSCL_LANE
+#define PSCL_LANE 1
+#endif
+int pscl_lane_available(const pscl_decode_params& P);
+int pscl_lane_lds_bytes();
+hipError_t pscl_launch_lane(const pscl_decode_params& P, int64_t grid, hipStream_t s);
 int pscl_screening_fs_available(const pscl_decode_params& P);  // forced-bit screening (DL-SCL retries)
 hipError_t pscl_launch_decode128(const pscl_decode_params& P, int hist, int wpg, int64_t grid, int lds, hipStream_t s);
 int64_t pscl_decode_grid(const pscl_decode_params& P);

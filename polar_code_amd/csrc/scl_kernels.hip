@@ -548,6 +548,10 @@ void pscl_decode_layout(pscl_decode_params& P, int hist) {
 
 hipError_t pscl_launch_decode(const pscl_decode_params& P, int hist, hipStream_t s) {
     if (P.long_mode) return pscl_launch_long(P, hist, s);
+    if (!hist && pscl_lane_available(P)) {  // one wavefront of 8 frames per workgroup
+        const int64_t g = (P.B + 7) / 8;
+        return pscl_launch_lane(P, g < 1 ? 1 : (g > (1 << 20) ? (1 << 20) : g), s);
+    }
     if (pscl_decode_wpg(P) < 1) return hipErrorInvalidValue;
     const int64_t grid = pscl_decode_grid(P);
     if (P.fast) return pscl_launch_decode128(P, hist, pscl_decode_wpg(P), grid, decode_lds_bytes(P, hist), s);

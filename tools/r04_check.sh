@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round-4 GPU check: screening + channel tests, lane-kernel A/B, bench line, config-3 trace.
+set -o pipefail
+tag=${1:-r04}
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_gpu_screening.py tests/test_gpu_channel.py -x -q -s --timeout 250 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/${tag}_tests.log; grep -E "scan:|screening tail" gpurun_out/${tag}_tests.log
+[ $rc -eq 0 ] || { grep -E "Error|error|assert" gpurun_out/${tag}_tests.log | head -20; exit 1; }
+timeout -k 10 400 bash tools/ab_bench.sh "prod noswap nolane reltail" 2 || exit 1
+bash tools/quick_gpu.sh ${tag} || exit 1
+bash tools/profile_sim_trace.sh ${tag} 4.0,5.0
