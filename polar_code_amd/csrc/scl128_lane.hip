@@ -81,30 +81,41 @@ __device__ __forceinline__ void rank_pair(uint32_t og, uint32_t ob, uint32_t kg,
         : "vcc");
 }
 
-// max / min / sum of v over the 8 lanes of each frame (3 DPP steps)
-__device__ __forceinline__ uint32_t frame_max8(uint32_t v) {
+// max / min / sum of v over the G lanes of each frame (G = 4: two quad_perm steps; G = 8: and
+// the half-row mirror)
+template <int G>
+__device__ __forceinline__ uint32_t frame_max(uint32_t v) {
     uint32_t o = dpp32<kQX1>(v);
     v = o > v ? o : v;
     o = dpp32<kQX2>(v);
     v = o > v ? o : v;
-    o = dpp32<kHMIR>(v);
-    return o > v ? o : v;
+    if constexpr (G == 8) {
+        o = dpp32<kHMIR>(v);
+        v = o > v ? o : v;
+    }
+    return v;
 }
-__device__ __forceinline__ uint32_t frame_min8(uint32_t v) {
+template <int G>
+__device__ __forceinline__ uint32_t frame_min(uint32_t v) {
     uint32_t o = dpp32<kQX1>(v);
     v = o < v ? o : v;
     o = dpp32<kQX2>(v);
     v = o < v ? o : v;
-    o = dpp32<kHMIR>(v);
-    return o < v ? o : v;
+    if constexpr (G == 8) {
+        o = dpp32<kHMIR>(v);
+        v = o < v ? o : v;
+    }
+    return v;
 }
-__device__ __forceinline__ uint32_t frame_sum8(uint32_t v) {
+template <int G>
+__device__ __forceinline__ uint32_t frame_sum(uint32_t v) {
     v += dpp32<kQX1>(v);
     v += dpp32<kQX2>(v);
-    return v + dpp32<kHMIR>(v);
+    if constexpr (G == 8) v += dpp32<kHMIR>(v);
+    return v;
 }
 
-// position of the j-th set bit (j < popcount(m)) of an 8-bit mask, branch-free
+// position of the j-th set bit (j < popcount(m)) of a mask of at most 8 bits, branch-free
 __device__ __forceinline__ uint32_t nth_set_bit8(uint32_t m, uint32_t j) {
     const uint32_t c4 = __builtin_popcount(m & 15u);
     const bool h4 = j >= c4;
@@ -129,9 +140,11 @@ __device__ __forceinline__ uint32_t nth_set_bit8(uint32_t m, uint32_t j) {
 
 template <int LMAX, int CODE>
 __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(const pscl_decode_params P) {
-    static_assert(LMAX == 8, "the lane-per-path decoder is built for L = 8");
+    static_assert(LMAX == 4 || LMAX == 8, "the lane-per-path decoder is built for L = 4 and 8");
     using Ly = LaneLayout<LMAX>;
     constexpr int G = Ly::G, F = Ly::F, LOG_G = Ly::LOG_G;
+    constexpr int EPL = 16 / G;                 // depth-3 elements per lane at a recompute
+    constexpr uint32_t GM = (1u << G) - 1u;     // a frame's bits in a lane mask
     constexpr int K = kSpecK[CODE], PW = (K + 63) / 64;
     constexpr uint64_t info0 = kSpecInfo[CODE][0], info1 = kSpecInfo[CODE][1];
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -149,19 +162,18 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
         const bool fvalid = fi < P.B;
         const int64_t frow = fvalid ? fi : f0;  // (a tail wave's empty slots decode a copy of frame f0)
         const double* chan = P.llr + frow * kN;
-        // the frame's channel LLRs in registers: elements e = p (c[m] = chan[p + 16 m]) and
-        // e = p + 8 (c[8 + m]) of the depth-3 node -- the same at all 8 depth-1..3 recomputes
-        double c[16];
+        // the frame's channel LLRs in registers: the lane's depth-3 elements e_k = p + G k (k < EPL)
+        // need c[8 k + m] = chan[e_k + 16 m] -- the same at all 8 depth-1..3 recomputes
+        double c[8 * EPL];
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            c[m] = chan[p + 16 * m];
-            c[8 + m] = chan[p + 8 + 16 * m];
-        }
+        for (int k = 0; k < EPL; ++k)
+#pragma unroll
+            for (int m = 0; m < 8; ++m) c[8 * k + m] = chan[p + G * k + 16 * m];
         // frames whose channel magnitudes could overflow the fp64 metric sums or carry a NaN go to
-        // the exact re-decode (the lane's 16 values summed; NaN propagates through the sum)
+        // the exact re-decode (the lane's values summed; NaN propagates through the sum)
         double cs = fabs(c[0]);
 #pragma unroll
-        for (int m = 1; m < 16; ++m) cs = cs + fabs(c[m]);
+        for (int m = 1; m < 8 * EPL; ++m) cs = cs + fabs(c[m]);
         uint64_t amb = wmask(!(cs < 0x1p25));
         const uint64_t vmask = wmask(fvalid);
 
@@ -177,7 +189,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
             constexpr bool is_info = ((phi < 64 ? info0 : info1) >> (phi & 63)) & 1;
             constexpr int jb = phi < 64 ? __builtin_popcountll(info0 & ((1ULL << (phi & 63)) - 1))
                                         : __builtin_popcountll(info0) + __builtin_popcountll(info1 & ((1ULL << (phi & 63)) - 1));
-            constexpr int cnt = jb >= 3 ? LMAX : (1 << jb);  // live paths (min(2^j, L))
+            constexpr int cnt = jb >= LOG_G ? LMAX : (1 << jb);  // live paths (min(2^j, L))
 #ifdef PSCL_PHASE_MARKERS  // asm listing analysis only (tools/isa_phase_stats.py)
             asm volatile("; PHASE %0" ::"n"(t));
 #endif
@@ -204,9 +216,9 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
                 // the depth-1 f node is the same for every path before phase 64, and depth 2 too
                 // at phases 0 and 16
                 constexpr bool shared2 = !r1 && !r2;
-                double d1l[2][4], d2s[2][2];
+                double d1l[EPL][4], d2s[EPL][2];
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
+                for (int h = 0; h < EPL; ++h) {
 #pragma unroll
                     for (int m = 0; m < 4; ++m) d1l[h][m] = r1 ? 0.0 : f_minsum(c[8 * h + m], c[8 * h + m + 4]);
 #pragma unroll
@@ -225,10 +237,10 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
                         x2 = xv.z;
                         x3 = xv.w;
                     }
-                    double d3[2];
+                    double d3[EPL];
 #pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const uint32_t e = (uint32_t)(p + 8 * h);
+                    for (int h = 0; h < EPL; ++h) {
+                        const uint32_t e = (uint32_t)(p + G * h);
                         double d1[4];
 #pragma unroll
                         for (int m = 0; m < 4; ++m)
@@ -240,8 +252,10 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
                             d2[s2] = shared2 ? d2s[h][s2] : (r2 ? g_node_wbit(d1[s2], d1[s2 + 2], x2, e + 16 * s2) : f_minsum(d1[s2], d1[s2 + 2]));
                         d3[h] = r3 ? g_node_wbit(d2[0], d2[1], x3, e) : f_minsum(d2[0], d2[1]);
                     }
-                    // elements p and p + 8 of slot q: one pair ([8][L][2] layout)
-                    *reinterpret_cast<double2*>(Af + Ly::OFF3 + (p * LMAX + q) * 2) = make_double2(d3[0], d3[1]);
+                    // elements e_k and e_k + 8 = e_{k + EPL/2} of slot q: one pair ([8][L][2] layout)
+#pragma unroll
+                    for (int h = 0; h < EPL / 2; ++h)
+                        *reinterpret_cast<double2*>(Af + Ly::OFF3 + ((p + G * h) * LMAX + q) * 2) = make_double2(d3[h], d3[h + EPL / 2]);
                 }
                 wave_lds_fence();
             }
@@ -312,7 +326,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
             // full list: keep the better children when every worse child clears the largest
             // better child by the margin (the stable sort's outcome; ties never reach the sort)
             const uint32_t kgu = hiw_up(mg), kb = hiw(mb);
-            const uint32_t mx = frame_max8(kgu);
+            const uint32_t mx = frame_max<G>(kgu);
             const bool bad = kb <= mx;  // this worse child is not clear of every better child
             const uint64_t badm = wmask(bad);
             if ((badm & vmask) == 0) {
@@ -322,7 +336,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
                 return;
             }
             const uint32_t sh = (uint32_t)gbase & 31u;
-            const uint32_t bad8 = ((fl < 4 ? (uint32_t)badm : (uint32_t)(badm >> 32)) >> sh) & 0xffu;
+            const uint32_t bad8 = ((fl < F / 2 ? (uint32_t)badm : (uint32_t)(badm >> 32)) >> sh) & GM;
 #if PSCL_LANE_SWAP
             // one-swap path (every frame of the wave has at most one worse child w that is not
             // clear): the survivors are the better children but the largest, gmax, plus w -- certain
@@ -331,14 +345,14 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
             // deferred (its boundary is within the margin, which no ranking could certify either)
             if ((wmask(__builtin_popcount(bad8) > 1) & vmask) == 0) {
                 const uint32_t kg = hiw(mg);
-                const uint32_t gmaxh = frame_max8(kg);
+                const uint32_t gmaxh = frame_max<G>(kg);
                 const bool ismax = kg == gmaxh;
-                const uint32_t nmax = frame_sum8(ismax ? 1u : 0u);
-                const uint32_t g2u = frame_max8(ismax ? 0u : kgu);
-                const uint32_t wu = frame_max8(bad ? hiw_up(mb) : 0u);
+                const uint32_t nmax = frame_sum<G>(ismax ? 1u : 0u);
+                const uint32_t g2u = frame_max<G>(ismax ? 0u : kgu);
+                const uint32_t wu = frame_max<G>(bad ? hiw_up(mb) : 0u);
                 const bool swap = bad8 != 0;
                 amb |= wmask(swap && !(nmax == 1u && g2u < gmaxh && wu < gmaxh)) & vmask;
-                const int src = (gbase + (int)__builtin_ctz(bad8 | 0x100u)) & 63;  // (frames without a swap: unused)
+                const int src = (gbase + (int)__builtin_ctz(bad8 | (1u << G))) & 63;  // (frames without a swap: unused)
                 const uint32_t tw = tab | ((gbit ^ 1u) << 31);
                 const uint64_t pmb = shfl_u64(pscl_asu64(mb), src);
                 const uint64_t pu0 = shfl_u64(u0, src);
@@ -365,25 +379,27 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
             rank_pair<kQX1>(kg, kb, kg, kb, rg, rb);
             rank_pair<kQX2>(kg, kb, kg, kb, rg, rb);
             rank_pair<kQX3>(kg, kb, kg, kb, rg, rb);
-            const uint32_t mkg = dpp32<kHMIR>(kg), mkb = dpp32<kHMIR>(kb);
-            rank_pair<kQID>(mkg, mkb, kg, kb, rg, rb);
-            rank_pair<kQX1>(mkg, mkb, kg, kb, rg, rb);
-            rank_pair<kQX2>(mkg, mkb, kg, kb, rg, rb);
-            rank_pair<kQX3>(mkg, mkb, kg, kb, rg, rb);
+            if constexpr (G == 8) {  // the other quad of the frame, through the half-row mirror
+                const uint32_t mkg = dpp32<kHMIR>(kg), mkb = dpp32<kHMIR>(kb);
+                rank_pair<kQID>(mkg, mkb, kg, kb, rg, rb);
+                rank_pair<kQX1>(mkg, mkb, kg, kb, rg, rb);
+                rank_pair<kQX2>(mkg, mkb, kg, kb, rg, rb);
+                rank_pair<kQX3>(mkg, mkb, kg, kb, rg, rb);
+            }
             const bool keep_g = rg < (uint32_t)LMAX, win_b = rb < (uint32_t)LMAX;
             // certificate: exactly L survivors, and the largest survivor (raised by the margin)
             // below the smallest non-survivor
             const uint32_t kbu = hiw_up(mb);
             const uint32_t su = keep_g ? (win_b ? kbu : kgu) : (win_b ? kbu : 0u);
             const uint32_t nm = keep_g ? (win_b ? 0xffffffffu : kb) : kg;
-            const uint32_t nsurv = frame_sum8((keep_g ? 1u : 0u) + (win_b ? 1u : 0u));
-            const uint32_t smax = frame_max8(su), nmin = frame_min8(nm);
+            const uint32_t nsurv = frame_sum<G>((keep_g ? 1u : 0u) + (win_b ? 1u : 0u));
+            const uint32_t smax = frame_max<G>(su), nmin = frame_min<G>(nm);
             amb |= wmask(!(nsurv == (uint32_t)LMAX && nmin > smax)) & vmask;
             // freed lanes take the surviving worse children: the j-th freed lane of a frame pulls
             // the j-th winner (both counted in lane order)
             const uint64_t fw = wmask(!keep_g), ww = wmask(win_b);
-            const uint32_t f8 = ((fl < 4 ? (uint32_t)fw : (uint32_t)(fw >> 32)) >> sh) & 0xffu;
-            const uint32_t w8 = ((fl < 4 ? (uint32_t)ww : (uint32_t)(ww >> 32)) >> sh) & 0xffu;
+            const uint32_t f8 = ((fl < F / 2 ? (uint32_t)fw : (uint32_t)(fw >> 32)) >> sh) & GM;
+            const uint32_t w8 = ((fl < F / 2 ? (uint32_t)ww : (uint32_t)(ww >> 32)) >> sh) & GM;
             const uint32_t j = __builtin_popcount(f8 & ((1u << p) - 1u));
             const int src = gbase + (int)nth_set_bit8(w8, j);
             const uint32_t tw = tab | ((gbit ^ 1u) << 31);  // the worse child's bit rides on the table word
@@ -443,21 +459,23 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
         cmp_perm(dpp32<kQX1>(kh), dpp32<kQX1>(ku));
         cmp_perm(dpp32<kQX2>(kh), dpp32<kQX2>(ku));
         cmp_perm(dpp32<kQX3>(kh), dpp32<kQX3>(ku));
-        const uint32_t mh = dpp32<kHMIR>(kh), mu = dpp32<kHMIR>(ku);
-        cmp_perm(mh, mu);
-        cmp_perm(dpp32<kQX1>(mh), dpp32<kQX1>(mu));
-        cmp_perm(dpp32<kQX2>(mh), dpp32<kQX2>(mu));
-        cmp_perm(dpp32<kQX3>(mh), dpp32<kQX3>(mu));
+        if constexpr (G == 8) {
+            const uint32_t mh = dpp32<kHMIR>(kh), mu = dpp32<kHMIR>(ku);
+            cmp_perm(mh, mu);
+            cmp_perm(dpp32<kQX1>(mh), dpp32<kQX1>(mu));
+            cmp_perm(dpp32<kQX2>(mh), dpp32<kQX2>(mu));
+            cmp_perm(dpp32<kQX3>(mh), dpp32<kQX3>(mu));
+        }
         amb |= wmask(near) & vmask;
-        const bool famb = ((amb >> gbase) & 0xffULL) != 0;
+        const bool famb = ((amb >> gbase) & (uint64_t)GM) != 0;
         if (famb && p == 0 && fvalid) P.amb_list[atomicAdd(P.amb_count, 1)] = fi;
         // best: the lowest list position whose candidate passes the CRC (position 0 if none)
         const uint32_t pass = P.has_crc ? (syn == 0 ? 1u : 0u) : 1u;
-        const uint32_t keyb = pass ? r : 8u + r;
-        const uint32_t kbest = frame_min8(keyb);
+        const uint32_t keyb = pass ? r : (uint32_t)LMAX + r;
+        const uint32_t kbest = frame_min<G>(keyb);
         if (fvalid && !famb && keyb == kbest) {
-            const int best = (int)(kbest & 7u);
-            const bool bpass = kbest < 8u;
+            const int best = (int)(kbest & (uint32_t)(LMAX - 1));
+            const bool bpass = kbest < (uint32_t)LMAX;
             if (P.best) {
                 P.best[fi * PW] = ib0;
                 if (PW > 1) P.best[fi * PW + 1] = ib1;
@@ -474,11 +492,18 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
 
 }  // namespace
 
-// the lane-per-path screening launch of a plain (128,64) L = 8 decode; lds = LDS bytes per
-// workgroup (one wavefront)
-int pscl_lane_lds_bytes() { return LaneLayout<8>::F * LaneLayout<8>::FSTRIDE * 8; }
+// the lane-per-path screening launch of a plain (128,64) decode at L = 4 or 8: one wavefront of
+// 64 / L frames per workgroup, LDS = 30 L doubles per frame (15 KB per workgroup at both sizes)
+int pscl_lane_frames_per_wg(int L) { return 64 / L; }
 
 hipError_t pscl_launch_lane(const pscl_decode_params& P, int64_t grid, hipStream_t s) {
-    hipLaunchKernelGGL((scl_lane_kernel<8, 1>), dim3((unsigned)grid), dim3(64), pscl_lane_lds_bytes(), s, P);
+    if (P.L == 8)
+        hipLaunchKernelGGL((scl_lane_kernel<8, 1>), dim3((unsigned)grid), dim3(64),
+                           LaneLayout<8>::F * LaneLayout<8>::FSTRIDE * 8, s, P);
+    else if (P.L == 4)
+        hipLaunchKernelGGL((scl_lane_kernel<4, 1>), dim3((unsigned)grid), dim3(64),
+                           LaneLayout<4>::F * LaneLayout<4>::FSTRIDE * 8, s, P);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }

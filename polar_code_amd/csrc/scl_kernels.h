@@ -218,8 +218,11 @@ int pscl_screening_available(const pscl_decode_params& P);  // scl128.hip
 #ifndef PSCL_LANE
 #define PSCL_LANE 1
 #endif
+#ifndef PSCL_LANE4
+#define PSCL_LANE4 1
+#endif
 int pscl_lane_available(const pscl_decode_params& P);
-int pscl_lane_lds_bytes();
+int pscl_lane_frames_per_wg(int L);
 hipError_t pscl_launch_lane(const pscl_decode_params& P, int64_t grid, hipStream_t s);
 int pscl_screening_fs_available(const pscl_decode_params& P);  // forced-bit screening (DL-SCL retries)
 hipError_t pscl_launch_decode128(const pscl_decode_params& P, int hist, int wpg, int64_t grid, int lds, hipStream_t s);

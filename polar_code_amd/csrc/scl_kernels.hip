@@ -548,8 +548,9 @@ void pscl_decode_layout(pscl_decode_params& P, int hist) {
 
 hipError_t pscl_launch_decode(const pscl_decode_params& P, int hist, hipStream_t s) {
     if (P.long_mode) return pscl_launch_long(P, hist, s);
-    if (!hist && pscl_lane_available(P)) {  // one wavefront of 8 frames per workgroup
-        const int64_t g = (P.B + 7) / 8;
+    if (!hist && pscl_lane_available(P)) {  // one wavefront of 64 / L frames per workgroup
+        const int fw = pscl_lane_frames_per_wg(P.L);
+        const int64_t g = (P.B + fw - 1) / fw;
         return pscl_launch_lane(P, g < 1 ? 1 : (g > (1 << 20) ? (1 << 20) : g), s);
     }
     if (pscl_decode_wpg(P) < 1) return hipErrorInvalidValue;
