@@ -329,6 +329,13 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
             const uint32_t mx = frame_max<G>(kgu);
             const bool bad = kb <= mx;  // this worse child is not clear of every better child
             const uint64_t badm = wmask(bad);
+#ifdef PSCL_STATS  // diagnostic build (tools/fastpath_stats.py): full-list info phases per wave by
+                   // tier: counters[12] kept in place, [13] one swap, [14] full ranking
+            const bool one = (wmask(__builtin_popcount(((fl < F / 2 ? (uint32_t)badm : (uint32_t)(badm >> 32)) >> (gbase & 31)) & GM) > 1) & vmask) == 0;
+            if (lane == 0 && P.counters) {
+                atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + ((badm & vmask) == 0 ? 12 : (one ? 13 : 14)), 1ULL);
+            }
+#endif
             if ((badm & vmask) == 0) {
                 metric = mg;
                 lastbit = gbit;

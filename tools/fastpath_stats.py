@@ -33,5 +33,9 @@ c = cnt.cpu().tolist()
 print(f"L={L} {ebno} dB: frozen {c[8]} skipped {c[9]} ({c[9] / max(c[8], 1):.1%}); info full {c[10]} "
       f"kept {c[11]} ({c[11] / max(c[10] + c[11], 1):.1%}); FER {c[1] / B:.4f}")
 tot = max(sum(c[12:16]), 1)
-print("screening full-list info phases (waves) by worst frame's near-worse children: " +
-      ", ".join(f"{k}: {c[12 + i]} ({c[12 + i] / tot:.1%})" for i, k in enumerate(["0", "1", "2", ">=3"])))
+if os.environ.get("PSCL_LANE_STATS"):  # the lane-per-path kernel's tiers (scl128_lane.hip)
+    print("lane kernel full-list info phases (waves): " +
+          ", ".join(f"{k}: {c[12 + i]} ({c[12 + i] / tot:.1%})" for i, k in enumerate(["kept", "one swap", "ranked"])))
+else:
+    print("screening full-list info phases (waves) by worst frame's near-worse children: " +
+          ", ".join(f"{k}: {c[12 + i]} ({c[12 + i] / tot:.1%})" for i, k in enumerate(["0", "1", "2", ">=3"])))
