@@ -134,6 +134,12 @@ __device__ __forceinline__ uint32_t nth_set_bit8(uint32_t m, uint32_t j) {
 #define PSCL_LANE_SWAP 1
 #endif
 
+// L = 4: keep the lane's 32 channel LLRs in registers across the frame (1) or re-read them at each
+// depth-1..3 recompute (0)
+#ifndef PSCL_LANE_CREG4
+#define PSCL_LANE_CREG4 0
+#endif
+
 #ifndef PSCL_LANE_WAVES_PER_EU
 #define PSCL_LANE_WAVES_PER_EU 2
 #endif
@@ -164,11 +170,17 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
         const double* chan = P.llr + frow * kN;
         // the frame's channel LLRs in registers: the lane's depth-3 elements e_k = p + G k (k < EPL)
         // need c[8 k + m] = chan[e_k + 16 m] -- the same at all 8 depth-1..3 recomputes
+        // (CREG = false, L = 4 by default: the 32 values are re-read from the L2-resident row at each
+        // recompute instead, which keeps them out of the registers of the other phases)
+        constexpr bool CREG = G == 8 || PSCL_LANE_CREG4;
         double c[8 * EPL];
+        auto load_chan = [&]() {
 #pragma unroll
-        for (int k = 0; k < EPL; ++k)
+            for (int k = 0; k < EPL; ++k)
 #pragma unroll
-            for (int m = 0; m < 8; ++m) c[8 * k + m] = chan[p + G * k + 16 * m];
+                for (int m = 0; m < 8; ++m) c[8 * k + m] = chan[p + G * k + 16 * m];
+        };
+        load_chan();
         // frames whose channel magnitudes could overflow the fp64 metric sums or carry a NaN go to
         // the exact re-decode (the lane's values summed; NaN propagates through the sum)
         double cs = fabs(c[0]);
@@ -197,6 +209,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
             // ---- depths 1-3 recomputed from the channel (phi % 16 == 0)
             if constexpr (start <= 3) {
                 constexpr bool r1 = phi >= 64, r2 = (phi >> 5) & 1, r3 = (phi >> 4) & 1;
+                if constexpr (!CREG && phi > 0) load_chan();
                 uint4* const xs = reinterpret_cast<uint4*>(Af + Ly::OFF6);
                 if constexpr (r1 || r2 || r3) {
                     uint64_t X1 = 0;

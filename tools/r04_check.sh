@@ -7,7 +7,7 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_screening.py tests/test_gpu
 rc=$?; tail -3 gpurun_out/${tag}_tests.log; grep -E "scan:|screening tail" gpurun_out/${tag}_tests.log
 [ $rc -eq 0 ] || { grep -E "Error|error|assert" gpurun_out/${tag}_tests.log | head -20; exit 1; }
 timeout -k 10 400 bash tools/ab_bench.sh "prod noswap nolane reltail" 2 || exit 1
-echo "L=4:"; timeout -k 10 300 bash tools/ab_bench.sh "prod nolane" 2 --list 4 || exit 1
+echo "L=4:"; timeout -k 10 300 bash tools/ab_bench.sh "prod creg4 nolane" 2 --list 4 || exit 1
 bash tools/quick_gpu.sh ${tag} || exit 1
 bash tools/profile_sim_trace.sh ${tag} 4.0,5.0
 for L in 8 4; do PSCL_LANE_STATS=1 PSCL_LIB_PATH=tools/_variant/lib_lanestats.so timeout -k 10 120 python3 tools/fastpath_stats.py $L 5.0; done
