@@ -237,6 +237,16 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
 int pscl_simulate(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
                   int64_t frame0, int64_t B, int retries, int include_uncoded, int64_t* counters);
 
+/*
+ * pscl_simulate without the host round trip: the point is enqueued on the handle's stream and its
+ * counters ADDED into d_counters (device int64 [3][PSCL_NCOUNT]: SCL, DL-SCL, uncoded; the caller
+ * zeroes them).  On a pipelined handle (pscl_set_pipelined) the point's DL-SCL retry chains
+ * overlap the next call's TX and baseline decode (run_fer_sweep's next SNR point); the counters
+ * are complete after pscl_join / pscl_sync / any other entry point.  Results equal pscl_simulate's.
+ */
+int pscl_simulate_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
+                         int64_t frame0, int64_t B, int retries, int include_uncoded, int64_t* d_counters);
+
 int pscl_device_alloc(pscl_handle* h, void** d_ptr, int64_t bytes);
 /* (pscl_device_free first orders and completes the handle's pending pipelined work, which may
  * still use the buffer) */

@@ -42,6 +42,7 @@ EXPORTS = (
     "pscl_path_llrs_device", "pscl_uncoded_device", "pscl_simulate", "pscl_set_screening", "pscl_build_hash",
     "pscl_screening_count", "pscl_softplus_tails_device", "pscl_set_pipelined", "pscl_join",
     "pscl_tail_abs_scan_device", "pscl_set_tuning", "pscl_timing_read_split", "pscl_decode_cpu",
+    "pscl_simulate_device",
 )
 
 # pscl_set_tuning knobs (include/polar_scl.h)
@@ -104,6 +105,8 @@ def lib() -> C.CDLL:
         "pscl_softplus_tails_device": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
         "pscl_tail_abs_scan_device": (C.c_int, [_vp, C.c_uint32, C.c_uint32, _vp]),
         "pscl_set_tuning": (C.c_int, [_vp, C.c_int, _i64]),
+        "pscl_simulate_device": (C.c_int, [_vp, _u64, C.c_uint32, _dbl, _dbl, C.c_int, _i64, _i64, C.c_int, C.c_int,
+                                           _vp]),
         "pscl_decode_cpu": (C.c_int, [C.c_int, P(_i32), C.c_int, C.c_int, _u64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
                                       _vp, _vp, C.c_int]),
         "pscl_timing_read_split": (C.c_int, [_vp, P(_i64), P(_dbl), P(_i64), P(_dbl)]),
@@ -349,6 +352,15 @@ class Decoder:
                                       float(rate), int(k_payload), int(frame0), int(B), int(retries),
                                       int(bool(include_uncoded)), out.ctypes.data))
         return out
+
+    def simulate_device(self, seed: int, stream_id: int, ebno_db: float, rate: float, k_payload: int, frame0: int,
+                        B: int, retries: int, include_uncoded: bool, d_counters: int) -> None:
+        """pscl_simulate enqueued, counters ADDED into device int64 [3, PSCL_NCOUNT] at d_counters
+        (complete after join()/sync(); on a pipelined handle the retry chains overlap the next call)."""
+        with self._lock:
+            check(lib().pscl_simulate_device(self._h, int(seed) & (2**64 - 1), int(stream_id) & 0xFFFFFFFF,
+                                             float(ebno_db), float(rate), int(k_payload), int(frame0), int(B),
+                                             int(retries), int(bool(include_uncoded)), d_counters))
 
     def screening_count(self) -> int:
         """Frames the last screening decode handed to the exact re-decode (synchronizes)."""

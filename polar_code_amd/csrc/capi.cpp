@@ -1313,14 +1313,25 @@ int pscl_sc_decode(pscl_handle* h, const double* llr, int64_t B, int8_t* bits) {
     return decode_host(h, llr, B, nullptr, np.data(), bits, nullptr, nullptr, nullptr, nullptr, nullptr, 1);
 }
 
+namespace {
+int uncoded_launch(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, int k_payload, int64_t frame0,
+                   int64_t B, int64_t* d_counters, bool no_enter);
+}
+
 int pscl_uncoded_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, int k_payload,
                         int64_t frame0, int64_t B, int64_t* d_counters) {
+    return uncoded_launch(h, seed, stream_id, ebno_db, k_payload, frame0, B, d_counters, false);
+}
+
+namespace {
+int uncoded_launch(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, int k_payload, int64_t frame0,
+                   int64_t B, int64_t* d_counters, bool no_enter) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
     if (B < 0 || frame0 < 0) return fail(PSCL_EINVAL, "B and frame0 must be >= 0");
     if (B == 0) return PSCL_OK;
     if (!d_counters) return fail(PSCL_EINVAL, "d_counters is NULL");
     if (k_payload < 0 || k_payload > PSCL_MAX_N) return fail(PSCL_EINVAL, "k_payload out of range");
-    int rc = enter(h);
+    int rc = no_enter ? set_device(h) : enter(h);
     if (rc) return rc;
     pscl_channel_params P;
     memset(&P, 0, sizeof(P));
@@ -1336,10 +1347,62 @@ int pscl_uncoded_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, doubl
     if (e != hipSuccess) return fail(PSCL_EDEVICE, "uncoded kernel launch: %s", hipGetErrorString(e));
     return PSCL_OK;
 }
+}  // namespace
 
 namespace {
 int channel_launch(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
-                   int64_t frame0, int64_t B, double* d_llr, uint64_t* d_msg, int64_t* d_unc);
+                   int64_t frame0, int64_t B, double* d_llr, uint64_t* d_msg, int64_t* d_unc, bool no_enter = false);
+
+// One SNR point of run_sweep enqueued (pscl_simulate / pscl_simulate_device): chunks of at most
+// 2^20 frames through handle scratch (N * 8 bytes of LLRs per frame: about 1 GiB per chunk at
+// N = 128), each = TX (+ the uncoded baseline) + pscl_dlscl_device.  On a pipelined handle every
+// chunk is one pipelined DL-SCL call: its retry chains overlap the next chunk's (or the next
+// point's) TX and baseline, so the two scratch sets alternate with the DL-SCL call parity, and a
+// set is rewritten only after the chains of the call two back that used it have ended.
+int simulate_enqueue(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
+                     int64_t frame0, int64_t B, int retries, int include_uncoded, int64_t* cs) {
+    const int64_t chunk = B < (1 << 20) ? B : (1 << 20);
+    const int W = h->W, N = h->N;
+    int rc;
+    for (int64_t f = 0; f < B; f += chunk) {
+        const int64_t n = B - f < chunk ? B - f : chunk;
+        const int par = h->pipelined ? h->dl_par : 0;
+        if (h->pipelined && h->dl_pending[par]) {  // (the chains that last read this scratch set)
+            HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_dl[par], 0));
+            h->dl_pending[par] = false;
+        }
+        const int base = par ? 66 : 30;
+        void *d_llr, *d_msg, *d_best, *d_flags;
+        if ((rc = ensure(h, base, (size_t)chunk * N * 8, &d_llr))) return rc;
+        if ((rc = ensure(h, base + 1, (size_t)chunk * W * 8, &d_msg))) return rc;
+        if ((rc = ensure(h, base + 2, (size_t)chunk * W * 8, &d_best))) return rc;
+        if ((rc = ensure(h, base + 3, (size_t)chunk, &d_flags))) return rc;
+        // N <= 128: the uncoded baseline is counted by the TX launch itself (same payload draw)
+        const bool unc_fused = include_uncoded && N <= PSCL_FAST_N;
+        if ((rc = channel_launch(h, seed, stream_id, ebno_db, rate, k_payload, frame0 + f, n, (double*)d_llr,
+                                 (uint64_t*)d_msg, unc_fused ? cs + 2 * PSCL_NCOUNT : nullptr, true)))
+            return rc;
+        if (include_uncoded && !unc_fused &&
+            (rc = uncoded_launch(h, seed, stream_id, ebno_db, k_payload, frame0 + f, n, cs + 2 * PSCL_NCOUNT, true)))
+            return rc;
+        if ((rc = pscl_dlscl_device(h, (const double*)d_llr, n, retries, (uint64_t*)d_best, (uint8_t*)d_flags, nullptr,
+                                    nullptr, 0, (const uint64_t*)d_msg, k_payload, cs, cs + PSCL_NCOUNT)))
+            return rc;
+    }
+    return PSCL_OK;
+}
+}  // namespace
+
+int pscl_simulate_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
+                         int64_t frame0, int64_t B, int retries, int include_uncoded, int64_t* d_counters) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    if (!d_counters) return fail(PSCL_EINVAL, "d_counters is NULL");
+    if (B < 0 || frame0 < 0) return fail(PSCL_EINVAL, "B and frame0 must be >= 0");
+    if (B == 0) return PSCL_OK;
+    int rc = set_device(h);
+    if (rc) return rc;
+    if ((rc = join_pipe(h, 1))) return rc;  // (plain decodes' pending re-decodes; DL chains keep overlapping)
+    return simulate_enqueue(h, seed, stream_id, ebno_db, rate, k_payload, frame0, B, retries, include_uncoded, d_counters);
 }
 
 int pscl_simulate(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
@@ -1351,32 +1414,13 @@ int pscl_simulate(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno
     if (B == 0) return PSCL_OK;
     int rc = enter(h);
     if (rc) return rc;
-    // chunks of at most 2^20 frames through handle scratch: N * 8 bytes of LLRs per frame
-    // (1 KiB at N = 128: about 1 GiB per 2^20-frame chunk)
-    const int64_t chunk = B < (1 << 20) ? B : (1 << 20);
-    const int W = h->W, N = h->N;
-    void *d_llr, *d_msg, *d_best, *d_flags, *d_cnt;
-    if ((rc = ensure(h, 30, (size_t)chunk * N * 8, &d_llr))) return rc;
-    if ((rc = ensure(h, 31, (size_t)chunk * W * 8, &d_msg))) return rc;
-    if ((rc = ensure(h, 32, (size_t)chunk * W * 8, &d_best))) return rc;
-    if ((rc = ensure(h, 33, (size_t)chunk, &d_flags))) return rc;
+    void* d_cnt;
     if ((rc = ensure(h, 34, sizeof(int64_t) * 3 * PSCL_NCOUNT, &d_cnt))) return rc;
-    int64_t* cs = (int64_t*)d_cnt;
     HIP_TRY(hipMemsetAsync(d_cnt, 0, sizeof(int64_t) * 3 * PSCL_NCOUNT, h->stream));
-    for (int64_t f = 0; f < B; f += chunk) {
-        const int64_t n = B - f < chunk ? B - f : chunk;
-        // N <= 128: the uncoded baseline is counted by the TX launch itself (same payload draw)
-        const bool unc_fused = include_uncoded && N <= PSCL_FAST_N;
-        if ((rc = channel_launch(h, seed, stream_id, ebno_db, rate, k_payload, frame0 + f, n, (double*)d_llr,
-                                 (uint64_t*)d_msg, unc_fused ? cs + 2 * PSCL_NCOUNT : nullptr)))
-            return rc;
-        if (include_uncoded && !unc_fused &&
-            (rc = pscl_uncoded_device(h, seed, stream_id, ebno_db, k_payload, frame0 + f, n, cs + 2 * PSCL_NCOUNT)))
-            return rc;
-        if ((rc = pscl_dlscl_device(h, (const double*)d_llr, n, retries, (uint64_t*)d_best, (uint8_t*)d_flags, nullptr,
-                                    nullptr, 0, (const uint64_t*)d_msg, k_payload, cs, cs + PSCL_NCOUNT)))
-            return rc;
-    }
+    if ((rc = simulate_enqueue(h, seed, stream_id, ebno_db, rate, k_payload, frame0, B, retries, include_uncoded,
+                               (int64_t*)d_cnt)))
+        return rc;
+    if ((rc = join_pipe(h))) return rc;  // (a pipelined handle: this call's chains, then the counters)
     HIP_TRY(hipMemcpyAsync(counters, d_cnt, sizeof(int64_t) * 3 * PSCL_NCOUNT, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     return PSCL_OK;
@@ -1384,9 +1428,10 @@ int pscl_simulate(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno
 
 namespace {
 // the TX launch (pscl_channel_device); d_unc != null also counts the uncoded baseline of the
-// same frames (N <= 128: channel_kernel's phase A) at unc_ebno_db
+// same frames (N <= 128: channel_kernel's phase A); no_enter: pending pipelined DL-SCL chains stay
+// where they are (pscl_simulate_device: they overlap this TX)
 int channel_launch(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
-                   int64_t frame0, int64_t B, double* d_llr, uint64_t* d_msg, int64_t* d_unc) {
+                   int64_t frame0, int64_t B, double* d_llr, uint64_t* d_msg, int64_t* d_unc, bool no_enter) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
     if (B < 0 || frame0 < 0) return fail(PSCL_EINVAL, "B and frame0 must be >= 0");
     if (B == 0) return PSCL_OK;
@@ -1394,7 +1439,7 @@ int channel_launch(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebn
     if (!(rate > 0)) return fail(PSCL_EINVAL, "rate must be positive");
     if (k_payload + h->crc_deg != h->K || k_payload < 0)
         return fail(PSCL_EINVAL, "k_payload (%d) + crc degree (%d) must equal K (%d)", k_payload, h->crc_deg, h->K);
-    int rc = enter(h);
+    int rc = no_enter ? set_device(h) : enter(h);
     if (rc) return rc;
     pscl_channel_params P;
     memset(&P, 0, sizeof(P));

@@ -188,6 +188,35 @@ def _add_common(c, cs, cu, n, K, payload_bits, include_uncoded):
         c[C_BITS_UNC] += n * payload_bits
 
 
+def _philox_sweep_device(args, snr_points, ranges, info_set, beta, device, payload_bits):
+    """Every SNR point of this rank on the device in ONE pipelined pass: per block one
+    pscl_simulate_device call (TX, uncoded baseline, SCL + DL-SCL, counters added on the device),
+    the handle pipelined so each block's DL-SCL retry chains overlap the next block's -- and the
+    next SNR point's -- TX and baseline decode; one join at the end.  Returns int64 counters
+    [points, 3, PSCL_NCOUNT] (rows SCL, DL-SCL, uncoded), equal to per-point pscl_simulate calls."""
+    cfg = config.get_config()
+    dec = _native.get_decoder(cfg.N, info_set, args.M, cfg.crc_poly, device)
+    dec.set_beta(beta)
+    nc = _native.PSCL_NCOUNT
+    batch = args.batch or (1 << 20)
+    dec.set_pipelined(True)
+    try:
+        with _native.DeviceArena(dec) as mem:
+            d_cnt = mem.alloc(len(snr_points) * 3 * nc * 8)
+            mem.memset(d_cnt, 0, len(snr_points) * 3 * nc * 8)
+            for i, snr_db in enumerate(snr_points):
+                start, stop = ranges[i]
+                for b0 in range(start, stop, batch):
+                    dec.simulate_device(args.seed, philox_stream_id(float(snr_db)), float(snr_db), cfg.K / cfg.N,
+                                        payload_bits, b0, min(stop, b0 + batch) - b0, args.retries,
+                                        args.include_uncoded, d_cnt + i * 3 * nc * 8)
+            dec.join()
+            dec.sync()
+            return mem.download(d_cnt, len(snr_points) * 3 * nc * 8, np.int64).reshape(len(snr_points), 3, nc)
+    finally:
+        dec.set_pipelined(False)
+
+
 def _philox_block(c, seed, snr_db, frame0, n, info_set, M, crc, retries, beta, device, include_uncoded,
                   payload_bits, engine="device", slot=0):
     """n frames generated on the device; SCL, DL-SCL and the uncoded baseline counted there."""
@@ -250,7 +279,13 @@ def run_sweep(args: argparse.Namespace) -> List[Dict[str, float]]:
     beta = np.load(args.beta) if args.beta else None
     results: List[Dict[str, float]] = []
     t0 = time.perf_counter()
-    for snr_db in snr_points:
+    # philox + device engine: the whole sweep enqueued at once (retry chains overlap the next
+    # point's TX and baseline), the counters read at the end
+    sweep_cnt = None
+    if args.rng == "philox" and engine == "device":
+        rng_ = [dist.shard(args.frames, ctx.rank, ctx.world)] * len(snr_points)
+        sweep_cnt = _philox_sweep_device(args, snr_points, rng_, info_set, beta, device, payload_bits)
+    for ip, snr_db in enumerate(snr_points):
         c = np.zeros(NCOUNT, np.int64)
         start, stop = dist.shard(args.frames, ctx.rank, ctx.world)
         # philox: one pscl_simulate call per 2^20 frames by default -- a call's DL-SCL retry rounds
@@ -258,7 +293,13 @@ def run_sweep(args: argparse.Namespace) -> List[Dict[str, float]]:
         # (5 dB, 10^6 frames: 155 M frames/s at 2^19 on two streams, 185 M at 2^20)
         batch = args.batch or (1 << 20 if args.rng == "philox" else 1 << 19)
         blocks = [(b0, min(stop, b0 + batch)) for b0 in range(start, stop, batch)]
-        if args.rng == "replay":
+        if sweep_cnt is not None:
+            cs, cd, cu = sweep_cnt[ip]
+            c[C_DL_ERR] += int(cd[_native.CNT_FRAME_ERR])
+            c[C_DL_BIT] += int(cd[_native.CNT_BIT_ERR])
+            c[C_DL_WORK] += int(cd[_native.CNT_RETRIES])
+            _add_common(c, cs, cu, stop - start, cfg.K, payload_bits, args.include_uncoded)
+        elif args.rng == "replay":
             stream = ReplayStream(args.seed, float(snr_db), payload_bits, cfg.crc_poly, args.include_uncoded)
             for b0, b1 in blocks:
                 payload, msg, llr, llr_unc = stream.take(b0, b1)
@@ -271,7 +312,7 @@ def run_sweep(args: argparse.Namespace) -> List[Dict[str, float]]:
                 cs = np.zeros(NCOUNT, np.int64)
                 for b0, b1 in blocks[slot::nstreams]:
                     _philox_block(cs, args.seed, float(snr_db), b0, b1 - b0, info_set, args.M, cfg.crc_poly,
-                                  args.retries, beta, device, args.include_uncoded, payload_bits, args.dl_engine, slot)
+                                  args.retries, beta, device, args.include_uncoded, payload_bits, engine, slot)
                 return cs
             nstreams = max(1, min(args.streams, len(blocks)))
             if nstreams == 1:

@@ -338,3 +338,29 @@ def test_simulate_one_call_equals_separate_calls():
         sep = mem.download(d_cnt, 3 * nc * 8, np.int64).reshape(3, nc)
     np.testing.assert_array_equal(one, sep)
     assert one[0][0] == B and one[1][1] <= one[0][1] and one[2][0] == B
+
+
+def test_pipelined_sweep_equals_per_point_simulate():
+    """run_fer_sweep --rng philox enqueues the whole sweep on a pipelined handle
+    (pscl_simulate_device: each block's DL-SCL chains overlap the next block's and the next SNR
+    point's TX and baseline): every point's SCL, DL-SCL and uncoded counters equal the
+    stream-ordered per-block pscl_simulate calls'."""
+    from polar_code_amd.eval import run_fer_sweep as rfs
+    from polar_code_amd.polar.polar import construct_info_set
+    from polar_code_amd.utils.seeding import philox_stream_id
+
+    info = construct_info_set(128, 64)
+    beta = np.load(GOLDEN / "beta_M8.npy")
+    args = rfs.build_argparser().parse_args(["--M", "8", "--retries", "8", "--rng", "philox", "--include_uncoded",
+                                             "--batch", "70000", "--seed", "3"])
+    pts = [3.5, 4.0, 5.0]
+    ranges = [(0, 150_000), (20_000, 160_000), (0, 90_001)]
+    got = rfs._philox_sweep_device(args, pts, ranges, info, beta, 0, 40)
+    dec = _native.Decoder(128, info, 8, "0x1864CFB")
+    dec.set_beta(beta)
+    for i, (snr, (a, b)) in enumerate(zip(pts, ranges)):
+        want = np.zeros((3, _native.PSCL_NCOUNT), np.int64)
+        for b0 in range(a, b, 70000):
+            want += dec.simulate(3, philox_stream_id(snr), snr, 0.5, 40, b0, min(b, b0 + 70000) - b0, 8, True)
+        np.testing.assert_array_equal(got[i], want, err_msg=f"{snr} dB")
+        assert want[1][_native.CNT_FRAME_ERR] <= want[0][_native.CNT_FRAME_ERR]
