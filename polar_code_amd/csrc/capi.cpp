@@ -125,6 +125,7 @@ struct pscl_handle {
     hipEvent_t ev_base[2] = {nullptr, nullptr}, ev_retry[2] = {nullptr, nullptr}, ev_join = nullptr;
     int32_t* h_count = nullptr;          // pinned: failing-frame counts of the two chunk parities
     double* d_beta = nullptr;         // [K][K] DL-SCL flip metric (null = |L0|)
+    double beta_absmax = 0.0;         // max |beta| (dl_post_kernel's certificate)
     uint64_t* d_epi = nullptr;        // scl128 epilogue tables (gather + syndrome)
     uint64_t* d_xtab = nullptr;       // TX: codeword of each message byte value
     uint32_t* d_crctab = nullptr;     // TX: CRC remainder of each payload byte value
@@ -730,6 +731,9 @@ int pscl_set_beta(pscl_handle* h, const double* beta) {
     if (!h->d_beta) HIP_TRY(hipMalloc(&h->d_beta, bytes));
     HIP_TRY(hipStreamSynchronize(h->stream));  // a previous round may still read the old matrix
     HIP_TRY(hipMemcpy(h->d_beta, beta, bytes, hipMemcpyHostToDevice));
+    double mx = 0.0;
+    for (size_t i = 0; i < (size_t)h->K * h->K; ++i) mx = fabs(beta[i]) > mx ? fabs(beta[i]) : mx;
+    h->beta_absmax = mx != mx ? INFINITY : mx;  // (NaN: every certificate fails, exact sums)
     return PSCL_OK;
 }
 
@@ -776,6 +780,7 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     Q.tried = S.tried;
     Q.ntried = S.nt;
     Q.beta = h->d_beta;
+    Q.beta_absmax = h->beta_absmax;
     Q.force = S.force;
     Q.warm_metric = S.warm_metric;
     Q.warm_u = S.warm_u;

@@ -218,6 +218,11 @@ __global__ void __launch_bounds__(256) replay_kernel(const pscl_replay_params R,
 #ifndef PSCL_POST_BETA_LDS
 #define PSCL_POST_BETA_LDS 1
 #endif
+// the flip metric's sums with fused multiply-adds, certified against the exact sums' bound (1), or
+// the exact index-order sums throughout (0)
+#ifndef PSCL_POST_FMA
+#define PSCL_POST_FMA 1
+#endif
 constexpr int kPostWavesWide = 8, kPostWavesNarrow = 4;
 constexpr int kPostIters = 32;  // entry pairs per wavefront between flushes
 
@@ -422,9 +427,36 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(4)
                 // all, and the dependent adds of the chains interleave)
                 constexpr int MC = KC ? (KC + 31) / 32 : 4;
                 double qv[MC];
+                auto argmin = [&]() {  // (key, index) over the untried candidates of this half
+                    bk = ~0ULL;
+                    bj = 0x7fffffff;
 #pragma unroll
-                for (int m = 0; m < MC; ++m) qv[m] = 0.0;
-                if (Q.beta && !(PSCL_POST_ABLATE & 4)) {
+                    for (int m = 0; m < MC; ++m) {
+                        const int j = hl + 32 * m;
+                        if (j < K) {
+                            const bool seen = ((j < 64 ? t0 : t1) >> (j & 63)) & 1ULL;
+                            const uint64_t key = seen ? ~0ULL : order_key(qv[m]);
+                            if (key < bk) {  // lower m first: ties keep the lower index
+                                bk = key;
+                                bj = j;
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int sft = 1; sft < 32; sft <<= 1) {
+                        const uint64_t ok = pscl::shfl_u64(bk, lane ^ sft);
+                        const int oj = __shfl(bj, lane ^ sft);
+                        if (ok < bk || (ok == bk && oj < bj)) {
+                            bk = ok;
+                            bj = oj;
+                        }
+                    }
+                };
+                // exact sums: index order, each product and sum rounded (the oracle's restatement
+                // of numpy's abs_l0 @ beta)
+                auto sums_exact = [&]() {
+#pragma unroll
+                    for (int m = 0; m < MC; ++m) qv[m] = 0.0;
                     const double* bc = beta + hl;
 #pragma unroll 4
                     for (int k = 0; k < K; ++k) {
@@ -433,30 +465,56 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(4)
                         for (int m = 0; m < MC; ++m)
                             if (hl + 32 * m < K) qv[m] = qv[m] + ak * bc[k * K + 32 * m];
                     }
+                };
+                if (Q.beta && !(PSCL_POST_ABLATE & 4)) {
+#if PSCL_POST_FMA
+                    // screening sums with fused multiply-adds (half the VALU), then a certificate:
+                    // |q_fma - q_exact| <= (gamma_64 + gamma_65) S, S = sum_k |L0_k| |beta_kj| <=
+                    // ||L0||_1 max|beta|, so a best candidate whose screening sum is below every
+                    // other untried candidate's by twice that bound is the exact (q, index) argmin;
+                    // else the exact sums are recomputed (both halves: the certified one gets the
+                    // same index back)
+#pragma unroll
+                    for (int m = 0; m < MC; ++m) qv[m] = 0.0;
+                    const double* bc = beta + hl;
+#pragma unroll 4
+                    for (int k = 0; k < K; ++k) {
+                        const double ak = nxt[k];
+#pragma unroll
+                        for (int m = 0; m < MC; ++m)
+                            if (hl + 32 * m < K) qv[m] = __builtin_fma(ak, bc[k * K + 32 * m], qv[m]);
+                    }
+                    argmin();
+                    double as = 0.0;
+#pragma unroll
+                    for (int m = 0; m < MC; ++m) as = as + (hl + 32 * m < K ? nxt[hl + 32 * m] : 0.0);
+#pragma unroll
+                    for (int sft = 1; sft < 32; sft <<= 1) as = as + pscl_asf64(pscl::shfl_u64(pscl_asu64(as), lane ^ sft));
+                    const double e2 = as * Q.beta_absmax * (264.0 * 0x1p-53);  // 2 E, with 1.5 % slack
+                    double qmine = qv[0];
+#pragma unroll
+                    for (int m = 1; m < MC; ++m) qmine = (bj >> 5) == m ? qv[m] : qmine;
+                    const double qb = pscl_asf64(pscl::shfl_u64(pscl_asu64(qmine), hb + (bj & 31)));
+                    const double thr = qb + e2 * (1.0 + 0x1p-40);
+                    bool near = false;
+#pragma unroll
+                    for (int m = 0; m < MC; ++m) {
+                        const int j = hl + 32 * m;
+                        const bool seen = ((j < 64 ? t0 : t1) >> (j & 63)) & 1ULL;
+                        near = near || (j < K && j != bj && !seen && !(qv[m] > thr));
+                    }
+                    if (__ballot(near && more)) {
+                        sums_exact();
+                        argmin();
+                    }
+#else
+                    sums_exact();
+                    argmin();
+#endif
                 } else {
 #pragma unroll
                     for (int m = 0; m < MC; ++m) qv[m] = hl + 32 * m < K ? nxt[hl + 32 * m] : 0.0;
-                }
-#pragma unroll
-                for (int m = 0; m < MC; ++m) {
-                    const int j = hl + 32 * m;
-                    if (j < K) {
-                        const bool seen = ((j < 64 ? t0 : t1) >> (j & 63)) & 1ULL;
-                        const uint64_t key = seen ? ~0ULL : order_key(qv[m]);
-                        if (key < bk) {  // lower m first: ties keep the lower index
-                            bk = key;
-                            bj = j;
-                        }
-                    }
-                }
-#pragma unroll
-                for (int sft = 1; sft < 32; sft <<= 1) {  // argmin of (key, index) within the half
-                    const uint64_t ok = pscl::shfl_u64(bk, lane ^ sft);
-                    const int oj = __shfl(bj, lane ^ sft);
-                    if (ok < bk || (ok == bk && oj < bj)) {
-                        bk = ok;
-                        bj = oj;
-                    }
+                    argmin();
                 }
                 const int idx = bj;  // (half-uniform) an untried index exists: rounds <= min(retries, K)
                 const int phis = Q.info_set[idx < K ? idx : 0];

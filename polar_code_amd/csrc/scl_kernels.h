@@ -147,6 +147,7 @@ struct pscl_post_params {
     uint64_t* tried;             // [cap][2] tried-index bit sets
     int32_t* ntried;             // [cap]
     const double* beta;          // [K][K] or null
+    double beta_absmax;          // max |beta| (the flip metric certificate's bound)
     uint64_t* force;             // [cap][2][W]
     double* warm_metric;         // [cap][NSEG]
     uint64_t* warm_u;            // [cap][2]
