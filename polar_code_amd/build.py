@@ -23,7 +23,7 @@ LIB = PKG / "libpolar_mi355x.so"
 ARCH = os.environ.get("PSCL_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-HIP_SOURCES = ["scl_kernels.hip", "scl128.hip", "scl128_spec.hip", "scl128_lane.hip", "scl_long.hip", "dlscl.hip", "capi.cpp",
+HIP_SOURCES = ["scl_kernels.hip", "scl128.hip", "scl128_spec.hip", "scl128_lane.hip", "scl_lane_long.hip", "scl_long.hip", "dlscl.hip", "capi.cpp",
                "scl_cpu.cpp"]
 HIP_DEPS = HIP_SOURCES + ["scl_kernels.h", "scl_device.h", "scl128_impl.h", "glibc_softplus.h", "exp_table.inc"]
 # scl128_spec.hip is compiled once per (information-set code, list size): 8 objects

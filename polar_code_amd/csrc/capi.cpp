@@ -297,8 +297,11 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
     // Plain decodes of the compiled-in N = 128 codes (no metrics, candidates, decision LLRs,
     // forced bits or row indirection requested) run as a screening decode plus an exact
     // re-decode of the frames it could not certify; the two launches count as one decode.
-    const bool screen = h->screen && P.fast && !hist && !P.metrics && !P.cands && !P.force && !P.sc_hard && !P.fidx &&
-                        !P.d_count && pscl_screening_available(P);
+    // (long codes: the lane-per-path screening kernel, scl_lane_long.hip, N = 256..1024, L = 4, 8)
+    pscl_decode_params T = P;
+    T.apx = 1;
+    const bool screen = h->screen && !hist && !P.metrics && !P.cands && !P.force && !P.sc_hard && !P.fidx &&
+                        !P.d_count && (P.fast ? pscl_screening_available(P) != 0 : pscl_lane_long_available(T) != 0);
     hipError_t err;
     if (!(screen && pipe)) {
         const int rc = join_pipe(h, 1);
@@ -477,21 +480,22 @@ int pscl_create(pscl_handle** out, int device, int N, const int32_t* info_set, i
     {
         // scl128 epilogue: gather[k][v] = the information bits of u-byte k (value v), compacted
         // in index order; syn[m][v] = XOR of the CRC check columns of info bits 4m..4m+3 set in v
-        const int k4 = (K + 3) / 4;
-        std::vector<uint8_t> epi((size_t)16 * 256 + (size_t)k4 * 16 * 4, 0);
-        for (int k = 0; k < 16; ++k)
+        // (N > 128: N / 8 gather tables, scl_lane_long.hip)
+        const int k4 = (K + 3) / 4, nby = N > 128 ? N / 8 : 16;
+        std::vector<uint8_t> epi((size_t)nby * 256 + (size_t)k4 * 16 * 4, 0);
+        for (int k = 0; k < nby; ++k)
             for (int v = 0; v < 256; ++v) {
                 int c = 0, cntb = 0;
                 for (int t = 0; t < 8; ++t) {
                     const int p = 8 * k + t;
-                    if (p < 128 && ((h->info_mask[p >> 6] >> (p & 63)) & 1ULL)) {
+                    if (p < N && ((h->info_words[p >> 6] >> (p & 63)) & 1ULL)) {
                         if ((v >> t) & 1) c |= 1 << cntb;
                         cntb++;
                     }
                 }
                 epi[(size_t)k * 256 + v] = (uint8_t)c;
             }
-        uint32_t* syn = reinterpret_cast<uint32_t*>(epi.data() + 16 * 256);
+        uint32_t* syn = reinterpret_cast<uint32_t*>(epi.data() + (size_t)nby * 256);
         for (int m = 0; m < k4; ++m)
             for (int v = 0; v < 16; ++v) {
                 uint32_t acc = 0;

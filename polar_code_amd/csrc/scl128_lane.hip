@@ -30,7 +30,7 @@
 // the depth-1..3 recompute aliased onto depth 6 (dead at a recompute phase); 15 KB per wavefront,
 // 10 wavefronts per CU.  One wavefront per workgroup (no barriers); the epilogue's u-byte gather
 // and CRC syndrome tables are read from global memory (L1/L2-resident).
-#include "scl128_impl.h"
+#include "scl_lane.h"
 
 namespace {
 
@@ -48,91 +48,6 @@ struct LaneLayout {
     // pair index of its paths' slots covers 4 distinct 64-byte quarters
     static constexpr int FSTRIDE = OFF6 + 2 * LMAX;
 };
-
-// intra-frame lane permutations of an 8-lane group (DPP controls): quad_perm xor 1, 2, 3, and the
-// half-row mirror (lane i <-> 7 - i), which maps one quad onto the other
-constexpr int kQX1 = 0xB1, kQX2 = 0x4E, kQX3 = 0x1B, kQID = 0xE4, kHMIR = 0x141;
-
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
-}
-
-// rank counts of this lane's two children against the two children of lane pi(this lane):
-// rg += [og < kg] + [ob < kg], rb += [og < kb] + [ob < kb], the other lane's keys read through the
-// DPP permutation CTRL of og / ob (hand-scheduled: inline asm is not hazard-checked, so the first
-// instruction waits out a VALU write of the key registers)
-template <int CTRL>
-__device__ __forceinline__ void rank_pair(uint32_t og, uint32_t ob, uint32_t kg, uint32_t kb, uint32_t& rg, uint32_t& rb) {
-    uint32_t t;
-    asm volatile(
-        "s_nop 1\n\t"
-        "v_sub_co_u32_dpp %0, vcc, %3, %5 quad_perm:[%7,%8,%9,%10] row_mask:0xf bank_mask:0xf\n\t"
-        "v_addc_co_u32 %1, vcc, 0, %1, vcc\n\t"
-        "v_sub_co_u32_dpp %0, vcc, %4, %5 quad_perm:[%7,%8,%9,%10] row_mask:0xf bank_mask:0xf\n\t"
-        "v_addc_co_u32 %1, vcc, 0, %1, vcc\n\t"
-        "v_sub_co_u32_dpp %0, vcc, %3, %6 quad_perm:[%7,%8,%9,%10] row_mask:0xf bank_mask:0xf\n\t"
-        "v_addc_co_u32 %2, vcc, 0, %2, vcc\n\t"
-        "v_sub_co_u32_dpp %0, vcc, %4, %6 quad_perm:[%7,%8,%9,%10] row_mask:0xf bank_mask:0xf\n\t"
-        "v_addc_co_u32 %2, vcc, 0, %2, vcc"
-        : "=&v"(t), "+v"(rg), "+v"(rb)
-        : "v"(og), "v"(ob), "v"(kg), "v"(kb), "i"(CTRL & 3), "i"((CTRL >> 2) & 3), "i"((CTRL >> 4) & 3),
-          "i"((CTRL >> 6) & 3)
-        : "vcc");
-}
-
-// max / min / sum of v over the G lanes of each frame (G = 4: two quad_perm steps; G = 8: and
-// the half-row mirror)
-template <int G>
-__device__ __forceinline__ uint32_t frame_max(uint32_t v) {
-    uint32_t o = dpp32<kQX1>(v);
-    v = o > v ? o : v;
-    o = dpp32<kQX2>(v);
-    v = o > v ? o : v;
-    if constexpr (G == 8) {
-        o = dpp32<kHMIR>(v);
-        v = o > v ? o : v;
-    }
-    return v;
-}
-template <int G>
-__device__ __forceinline__ uint32_t frame_min(uint32_t v) {
-    uint32_t o = dpp32<kQX1>(v);
-    v = o < v ? o : v;
-    o = dpp32<kQX2>(v);
-    v = o < v ? o : v;
-    if constexpr (G == 8) {
-        o = dpp32<kHMIR>(v);
-        v = o < v ? o : v;
-    }
-    return v;
-}
-template <int G>
-__device__ __forceinline__ uint32_t frame_sum(uint32_t v) {
-    v += dpp32<kQX1>(v);
-    v += dpp32<kQX2>(v);
-    if constexpr (G == 8) v += dpp32<kHMIR>(v);
-    return v;
-}
-
-// position of the j-th set bit (j < popcount(m)) of a mask of at most 8 bits, branch-free
-__device__ __forceinline__ uint32_t nth_set_bit8(uint32_t m, uint32_t j) {
-    const uint32_t c4 = __builtin_popcount(m & 15u);
-    const bool h4 = j >= c4;
-    j = h4 ? j - c4 : j;
-    m = h4 ? (m >> 4) : (m & 15u);
-    const uint32_t c2 = __builtin_popcount(m & 3u);
-    const bool h2 = j >= c2;
-    j = h2 ? j - c2 : j;
-    m = h2 ? (m >> 2) : m;
-    const bool h1 = j >= (m & 1u);
-    return (h4 ? 4u : 0u) + (h2 ? 2u : 0u) + (h1 ? 1u : 0u);
-}
-
-// the one-swap tier between the keep-the-better-children path and the full ranking
-#ifndef PSCL_LANE_SWAP
-#define PSCL_LANE_SWAP 1
-#endif
 
 // L = 4: keep the lane's 32 channel LLRs in registers across the frame (1) or re-read them at each
 // depth-1..3 recompute (0)

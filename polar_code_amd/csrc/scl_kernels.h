@@ -225,6 +225,9 @@ int pscl_screening_available(const pscl_decode_params& P);  // scl128.hip
 int pscl_lane_available(const pscl_decode_params& P);
 int pscl_lane_frames_per_wg(int L);
 hipError_t pscl_launch_lane(const pscl_decode_params& P, int64_t grid, hipStream_t s);
+// scl_lane_long.hip: the lane-per-path screening decoder of the long codes (N = 256..1024, L = 4, 8)
+int pscl_lane_long_available(const pscl_decode_params& P);
+hipError_t pscl_launch_lane_long(const pscl_decode_params& P, hipStream_t s);
 int pscl_screening_fs_available(const pscl_decode_params& P);  // forced-bit screening (DL-SCL retries)
 hipError_t pscl_launch_decode128(const pscl_decode_params& P, int hist, int wpg, int64_t grid, int lds, hipStream_t s);
 int64_t pscl_decode_grid(const pscl_decode_params& P);

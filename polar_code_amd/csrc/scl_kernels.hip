@@ -547,7 +547,10 @@ void pscl_decode_layout(pscl_decode_params& P, int hist) {
 }
 
 hipError_t pscl_launch_decode(const pscl_decode_params& P, int hist, hipStream_t s) {
-    if (P.long_mode) return pscl_launch_long(P, hist, s);
+    if (P.long_mode) {
+        if (!hist && P.apx) return pscl_launch_lane_long(P, s);  // (screening: lane-per-path only)
+        return pscl_launch_long(P, hist, s);
+    }
     if (!hist && pscl_lane_available(P)) {  // one wavefront of 64 / L frames per workgroup
         const int fw = pscl_lane_frames_per_wg(P.L);
         const int64_t g = (P.B + fw - 1) / fw;

@@ -1,0 +1,512 @@
+// scl_lane_long.hip -- the lane-per-path screening decoder for the longer codes (N = 256, 512,
+// 1024; L = 4, 8; any information set) and its launch.
+//
+// The long-code form of scl128_lane.hip: a plain decode whose path
+// metrics carry the bounded-error tail (pscl_softplus_tail_abs), every ordering decision
+// certified by the absolute margin of an N-phase metric (2 N DELTA), a frame with an uncertain
+// decision appended to P.amb_list and re-decoded exactly by scl_long_kernel (capi.cpp).  Results
+// are therefore bit-identical to decode_scl (dl_scl_polar/polar/scl.py:108-209; any power-of-two
+// N, scl.py:25-30).
+//
+// Mapping: one lane per list path, G = L lanes per frame, 64 / L frames per wavefront, the
+// state of a frame in registers and LDS -- no global scratch (scl_long_kernel keeps one frame per
+// wavefront and its trees in global memory, latency-bound at ~6 us per phase).
+//   * phases run in blocks of 16 (a runtime loop over N / 16 blocks; the 16 positions of a block
+//     unrolled): the information set is a runtime bitmask (one 16-bit slice per block, scalar);
+//   * depths R = n-4 .. n-1 (node widths 16, 8, 4, 2) in LDS slots with lazy copies, as N = 128;
+//   * depths 1..R recomputed from the channel row at every block start: element e < 16 of the
+//     depth-R node of path q reduces the 2^R channel LLRs chan[e + 16 m] through R f/g levels,
+//     level l a g node when bit (R - l) of the block index is set, with the left sibling's
+//     partial sums (published per path in LDS by the path's lane).  The depth-1 f node is
+//     path-independent and computed once per element.  N = 256 at L = 8 keeps the lane's 32
+//     channel LLRs in registers; otherwise they are re-read (L2) at each block start;
+//   * decided bits: the current block's 16 in a register (compile-time shifts within the block),
+//     merged into N / 64 words at the block end; a clone pulls the words in use;
+//   * list steps (frozen / growing / keep-better / one swap / ranked), the final order and the
+//     epilogue as scl128_lane.hip, with the information-bit gather from N / 8 byte tables.
+#include "scl_lane.h"
+
+namespace {
+
+template <int NL, int LMAX>
+struct LongLaneLayout {
+    static constexpr int N = 1 << NL;
+    static constexpr int R = NL - 4;           // the widest stored depth (node width 16)
+    static constexpr int G = LMAX;
+    static constexpr int F = 64 / G;
+    static constexpr int LOG_G = __builtin_ctz(G);
+    static constexpr int OFF0 = 0;              // depth R:   [8][L][2] doubles
+    static constexpr int OFF1 = 16 * LMAX;      // depth R+1: [4][L][2]
+    static constexpr int OFF2 = 24 * LMAX;      // depth R+2: [2][L][2]
+    static constexpr int OFF3 = 28 * LMAX;      // depth R+3: [1][L][2]
+    // partial sums of the depth-1..R left siblings, per path: level l (node width N >> l) at
+    // 32-bit word xoff(l), max(1, (N >> l) / 32) words
+    static constexpr int xsz(int l) { return (N >> l) / 32 > 1 ? (N >> l) / 32 : 1; }
+    static constexpr int xoff(int l) { return l <= 1 ? 0 : xoff(l - 1) + xsz(l - 1); }
+    static constexpr int XWORDS = xoff(R + 1);  // N / 32
+    static constexpr int OFFX = 30 * LMAX;      // [L][XWORDS] uint32
+    static constexpr int RAW = OFFX + LMAX * XWORDS / 2;
+    // frames start alternately on the two 128-byte halves of the 256-byte bank row (as N = 128)
+    static constexpr int FSTRIDE = RAW + (((16 - RAW) % 32) + 32) % 32;
+};
+
+#ifndef PSCL_LANE_LONG_WAVES_PER_EU
+#define PSCL_LANE_LONG_WAVES_PER_EU 2
+#endif
+
+// word k of the register array u, k wave-uniform
+template <int NW>
+__device__ __forceinline__ uint64_t uword(const uint64_t (&u)[NW], int k) {
+    uint64_t r = u[0];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) r = k == i ? u[i] : r;
+    return r;
+}
+
+template <int NL, int LMAX>
+__global__ void __launch_bounds__(64, PSCL_LANE_LONG_WAVES_PER_EU) scl_lane_long_kernel(const pscl_decode_params P) {
+    static_assert(LMAX == 4 || LMAX == 8, "the lane-per-path decoder is built for L = 4 and 8");
+    static_assert(NL >= 8 && NL <= 10, "N = 256 .. 1024");
+    using Ly = LongLaneLayout<NL, LMAX>;
+    constexpr int N = Ly::N, R = Ly::R, G = Ly::G, F = Ly::F, LOG_G = Ly::LOG_G;
+    constexpr int CE = 1 << R;          // channel LLRs per depth-R element
+    constexpr int NW = N / 64;          // decided-bit words per path
+    constexpr int EPL = 16 / G;         // depth-R elements per lane at a block start
+    constexpr uint32_t GM = (1u << G) - 1u;
+    constexpr bool CREG = EPL * CE <= 32;  // N = 256, L = 8: the lane's channel LLRs stay in registers
+    // every metric carries N tail terms: two metrics differ from their exact values by < 2 N DELTA
+    constexpr double MARGIN = 2.0 * N * PSCL_TAIL_ABS_DELTA * 1.0001;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double* const A = reinterpret_cast<double*>(smem);
+    const int lane = threadIdx.x & 63;
+    const int fl = lane >> LOG_G, p = lane & (G - 1), gbase = lane & ~(G - 1);
+    double* const Af = A + fl * Ly::FSTRIDE;
+    uint32_t* const XS = reinterpret_cast<uint32_t*>(Af + Ly::OFFX);
+    const uint8_t* const GT = reinterpret_cast<const uint8_t*>(P.epi_table);        // [N/8][256] u-byte -> info bits
+    const uint32_t* const ST = reinterpret_cast<const uint32_t*>(GT + (N / 8) * 256);  // [K/4][16] nibble -> syndrome
+    const int K = P.K, W = P.W;
+    auto hiw = [](double m) { return (uint32_t)(pscl_asu64(m) >> 32); };
+    auto hiw_up = [&](double m) { return hiw(__builtin_fma(m, 1.0 + 0x1p-40, MARGIN)); };
+    auto slot_rel = [](uint32_t tab, int dr) { return (int)((tab >> (4 * dr)) & 15u); };
+
+    for (int64_t f0 = (int64_t)blockIdx.x * F; f0 < P.B; f0 += (int64_t)gridDim.x * F) {
+        const int64_t fi = f0 + fl;
+        const bool fvalid = fi < P.B;
+        const int64_t frow = fvalid ? fi : f0;  // (a tail wave's empty slots decode a copy of frame f0)
+        const double* chan = P.llr + frow * N;
+        // the lane's depth-R elements e_h = p + G h (h < EPL) reduce ch[m] = chan[e_h + 16 m]
+        double c[CREG ? EPL * CE : 1];
+        uint64_t amb;
+        {
+            double cs = 0.0;  // NaN / overflow guard over the lane's channel LLRs (the 8 lanes: all N)
+#pragma unroll
+            for (int h = 0; h < EPL; ++h)
+#pragma unroll
+                for (int m = 0; m < CE; ++m) {
+                    const double v = chan[p + G * h + 16 * m];
+                    if constexpr (CREG) c[CE * h + m] = v;
+                    cs = cs + fabs(v);
+                }
+            amb = wmask(!(cs < 0x1p25));
+        }
+        const uint64_t vmask = wmask(fvalid);
+
+        double metric = 0.0;
+        uint64_t u[NW];
+#pragma unroll
+        for (int k = 0; k < NW; ++k) u[k] = 0;
+        uint32_t ub = 0;       // bits of the current block's phases
+        uint32_t tab = 0;      // LDS slot of depths R..R+3 (4 bits each)
+        uint32_t lastbit = 0;  // the bit decided at the previous phase
+        int cnt = 1;           // live paths (wave-uniform)
+
+        // pull the state of lane src (words of phases below block b only)
+        auto pull_u = [&](int src, int b) {
+#pragma unroll
+            for (int k = 0; k < NW; ++k)
+                if (64 * k < 16 * b) u[k] = shfl_u64(u[k], src);
+        };
+
+        for (int b = 0; b < N / 16; ++b) {
+            const uint32_t info16 = (uint32_t)(P.info_words[b >> 2] >> (16 * (b & 3))) & 0xffffu;
+
+            // ---- depths 1..R from the channel (block start)
+            {
+                // left-sibling partial sums of every g level, published by each path's lane
+                if (b) {
+                    static_for<R>([&](auto LI) {
+                        constexpr int l = 1 + decltype(LI)::value;
+                        constexpr int w = N >> l;  // node width at depth l
+                        const int k = b >> (R - l);
+                        if (k & 1) {
+                            const int lo = (k - 1) * w;  // left sibling u[lo, lo + w)
+                            uint32_t* xo = XS + p * Ly::XWORDS + Ly::xoff(l);
+                            if constexpr (w >= 64) {
+                                constexpr int nw = w / 64;
+                                uint64_t x[nw];
+#pragma unroll
+                                for (int i = 0; i < nw; ++i) x[i] = polar_transform64(uword<NW>(u, (lo >> 6) + i));
+#pragma unroll
+                                for (int s = 1; s < nw; s <<= 1)
+#pragma unroll
+                                    for (int i = 0; i < nw; ++i)
+                                        if (!(i & s)) x[i] ^= x[i + s];
+#pragma unroll
+                                for (int i = 0; i < nw; ++i) {
+                                    xo[2 * i] = (uint32_t)x[i];
+                                    xo[2 * i + 1] = (uint32_t)(x[i] >> 32);
+                                }
+                            } else {
+                                const uint32_t seg = (uint32_t)(uword<NW>(u, lo >> 6) >> (lo & 63));
+                                xo[0] = w == 32 ? polar_transform32(seg) : polar_transform16(seg & 0xffffu);
+                            }
+                        }
+                    });
+                    wave_lds_fence();
+                }
+                const bool r1 = (b >> (R - 1)) & 1;
+#pragma unroll
+                for (int h = 0; h < EPL; ++h) {
+                    const uint32_t e = (uint32_t)(p + G * h);
+                    double ch[CE];
+                    if constexpr (CREG) {
+#pragma unroll
+                        for (int m = 0; m < CE; ++m) ch[m] = c[CE * h + m];
+                    } else {
+#pragma unroll
+                        for (int m = 0; m < CE; ++m) ch[m] = chan[e + 16 * m];
+                    }
+                    // depth 1 before phase N/2: the same f node for every path
+                    double v1s[CE / 2];
+                    if (!r1) {
+#pragma unroll
+                        for (int m = 0; m < CE / 2; ++m) v1s[m] = f_minsum(ch[m], ch[m + CE / 2]);
+                    }
+#pragma unroll
+                    for (int q0 = 0; q0 < LMAX; ++q0) {
+                        if (q0 >= cnt) break;
+                        // lane p takes path (q0 + p) mod L: the lanes' stores hit distinct bank groups
+                        const int q = cnt == LMAX ? ((q0 + p) & (LMAX - 1)) : q0;
+                        const uint32_t* xq = XS + q * Ly::XWORDS;
+                        // depths 1 and 2 together: v[m] (m < CE/4) = depth-2 value at e + 16 m
+                        double v[CE / 4];
+                        const bool r2 = (b >> (R - 2)) & 1;
+                        if (!r1) {
+                            if (r2) {
+#pragma unroll
+                                for (int m = 0; m < CE / 4; ++m)
+                                    v[m] = g_node_wbit(v1s[m], v1s[m + CE / 4], xq[Ly::xoff(2) + (m >> 1)], e + 16 * (m & 1));
+                            } else {
+#pragma unroll
+                                for (int m = 0; m < CE / 4; ++m) v[m] = f_minsum(v1s[m], v1s[m + CE / 4]);
+                            }
+                        } else {
+#pragma unroll
+                            for (int m = 0; m < CE / 4; ++m) {
+                                const int m2 = m + CE / 4;  // the depth-1 pair (m, m2)
+                                const double a = g_node_wbit(ch[m], ch[m + CE / 2], xq[Ly::xoff(1) + (m >> 1)], e + 16 * (m & 1));
+                                const double bb = g_node_wbit(ch[m2], ch[m2 + CE / 2], xq[Ly::xoff(1) + (m2 >> 1)], e + 16 * (m2 & 1));
+                                v[m] = r2 ? g_node_wbit(a, bb, xq[Ly::xoff(2) + (m >> 1)], e + 16 * (m & 1)) : f_minsum(a, bb);
+                            }
+                        }
+                        // depths 3..R
+                        static_for<R - 2>([&](auto LI) {
+                            constexpr int l = 3 + decltype(LI)::value;
+                            constexpr int nl = CE >> l;  // values per element at depth l
+                            if ((b >> (R - l)) & 1) {
+#pragma unroll
+                                for (int m = 0; m < nl; ++m)
+                                    v[m] = g_node_wbit(v[m], v[m + nl], xq[Ly::xoff(l) + (m >> 1)], e + 16 * (m & 1));
+                            } else {
+#pragma unroll
+                                for (int m = 0; m < nl; ++m) v[m] = f_minsum(v[m], v[m + nl]);
+                            }
+                        });
+                        // element e of slot q: pair index e & 7, half e >> 3 ([8][L][2] layout)
+                        Af[Ly::OFF0 + ((e & 7) * LMAX + q) * 2 + (e >> 3)] = v[0];
+                    }
+                }
+                wave_lds_fence();
+            }
+
+            auto phase = [&](auto TC) {
+                constexpr int t = decltype(TC)::value;
+                constexpr int start = t ? NL - __builtin_ctz((unsigned)t) : R;  // (t = 0: depth R just written)
+                const bool is_info = (info16 >> t) & 1u;
+                // ---- depths R+1 .. n-1: this lane's own path; the first rewritten depth reads the parent slot
+                if constexpr (start <= NL - 1) {
+                    uint32_t xsb = 0;  // partial sums of the first rewritten node's left sibling (g node)
+                    if constexpr (t) {
+                        constexpr int w = 1 << (NL - start);
+                        xsb = polar_transform8((ub >> (t - w)) & ((1u << w) - 1u));
+                    }
+                    static_for<3>([&](auto DI) {
+                        constexpr int dr = 1 + decltype(DI)::value;  // depth R + dr
+                        constexpr int D = R + dr;
+                        if constexpr (D >= start) {
+                            constexpr int Wd = 1 << (NL - D), HW = Wd / 2;
+                            constexpr int OFF_IN = dr == 1 ? Ly::OFF0 : (dr == 2 ? Ly::OFF1 : Ly::OFF2);
+                            constexpr int OFF_OUT = dr == 1 ? Ly::OFF1 : (dr == 2 ? Ly::OFF2 : Ly::OFF3);
+                            constexpr bool first = D == start || (dr == 1 && t == 0);
+                            constexpr bool is_g = D == start && t != 0;
+                            const int sin = (t == 0 && dr == 1) ? p : (first ? slot_rel(tab, dr - 1) : p);
+                            const double* in = Af + OFF_IN + sin * 2;
+                            double o[Wd];
+#pragma unroll
+                            for (int k = 0; k < Wd; ++k) {
+                                const double2 ab = *reinterpret_cast<const double2*>(in + k * LMAX * 2);
+                                o[k] = is_g ? g_node(ab.x, ab.y, (xsb >> k) & 1u) : f_minsum(ab.x, ab.y);
+                            }
+                            double* out = Af + OFF_OUT + p * 2;
+#pragma unroll
+                            for (int k = 0; k < HW; ++k)
+                                *reinterpret_cast<double2*>(out + k * LMAX * 2) = make_double2(o[k], o[k + HW]);
+                            wave_lds_fence();
+                        }
+                    });
+                    // this path's own slot at every depth rewritten this phase
+                    constexpr int s0 = start - R;
+                    constexpr uint32_t mask = (0xffffu << (4 * s0)) & 0xffffu;
+                    tab = (tab & ~mask) | ((uint32_t)p * 0x1111u & mask);
+                }
+                // ---- leaf LLR and metric tail (scl.py:80-82, 102-105)
+                const double2 lab = *reinterpret_cast<const double2*>(Af + Ly::OFF3 + (start <= NL - 1 ? p : slot_rel(tab, 3)) * 2);
+                const double lam = (t & 1) ? g_node(lab.x, lab.y, lastbit) : f_minsum(lab.x, lab.y);
+                const double Lt = pscl_softplus_tail_abs(lam);
+                if (!is_info) {  // frozen: bit 0 (scl.py:149-153)
+                    metric = metric + (relu_neg(lam) + Lt);
+                    lastbit = 0;
+                    return;
+                }
+                // information phase: better child (along the LLR sign) mg, worse child mb
+                const double mg = metric + Lt, mb = mg + fabs(lam);
+                const uint32_t gbit = sign_bit(lam);
+                if (cnt < LMAX) {
+                    // growing list: every child survives; bit-1 children to lanes cnt..2cnt-1
+                    const double m0 = gbit ? mb : mg, m1 = gbit ? mg : mb;
+                    const int src = gbase + (p & (cnt - 1));
+                    const uint32_t bt = (p & cnt) ? 1u : 0u;
+                    const uint64_t pm1 = shfl_u64(pscl_asu64(m1), src);
+                    metric = bt ? pscl_asf64(pm1) : m0;  // (lanes below cnt: src is the lane itself)
+                    pull_u(src, b);
+                    ub = bperm32(ub, src) | (bt << t);
+                    tab = bperm32(tab, src);
+                    lastbit = bt;
+                    cnt *= 2;
+                    return;
+                }
+                // full list: keep the better children when every worse child clears the largest
+                // better child by the margin (the stable sort's outcome; ties never reach the sort)
+                const uint32_t kgu = hiw_up(mg), kb = hiw(mb);
+                const uint32_t mx = frame_max<G>(kgu);
+                const bool bad = kb <= mx;
+                const uint64_t badm = wmask(bad);
+                if ((badm & vmask) == 0) {
+                    metric = mg;
+                    lastbit = gbit;
+                    ub |= gbit << t;
+                    return;
+                }
+                const uint32_t sh = (uint32_t)gbase & 31u;
+                const uint32_t bad8 = ((fl < F / 2 ? (uint32_t)badm : (uint32_t)(badm >> 32)) >> sh) & GM;
+                int src;
+                bool take;  // this lane's path becomes a pulled worse child
+#if PSCL_LANE_SWAP
+                if ((wmask(__builtin_popcount(bad8) > 1) & vmask) == 0) {
+                    // one swap per frame at most (scl128_lane.hip): the largest better child gives
+                    // way to the one unclear worse child, certified by the margin or deferred
+                    const uint32_t kg = hiw(mg);
+                    const uint32_t gmaxh = frame_max<G>(kg);
+                    const bool ismax = kg == gmaxh;
+                    const uint32_t nmax = frame_sum<G>(ismax ? 1u : 0u);
+                    const uint32_t g2u = frame_max<G>(ismax ? 0u : kgu);
+                    const uint32_t wu = frame_max<G>(bad ? hiw_up(mb) : 0u);
+                    const bool swap = bad8 != 0;
+                    amb |= wmask(swap && !(nmax == 1u && g2u < gmaxh && wu < gmaxh)) & vmask;
+                    src = (gbase + (int)__builtin_ctz(bad8 | (1u << G))) & 63;
+                    take = swap && ismax;
+                } else
+#endif
+                {
+                    // rank the 2L children of each frame: counts of keys (high words) strictly below each
+                    const uint32_t kg = hiw(mg);
+                    uint32_t rg = 0, rb = kg < kb ? 1u : 0u;
+                    rank_pair<kQX1>(kg, kb, kg, kb, rg, rb);
+                    rank_pair<kQX2>(kg, kb, kg, kb, rg, rb);
+                    rank_pair<kQX3>(kg, kb, kg, kb, rg, rb);
+                    if constexpr (G == 8) {
+                        const uint32_t mkg = dpp32<kHMIR>(kg), mkb = dpp32<kHMIR>(kb);
+                        rank_pair<kQID>(mkg, mkb, kg, kb, rg, rb);
+                        rank_pair<kQX1>(mkg, mkb, kg, kb, rg, rb);
+                        rank_pair<kQX2>(mkg, mkb, kg, kb, rg, rb);
+                        rank_pair<kQX3>(mkg, mkb, kg, kb, rg, rb);
+                    }
+                    const bool keep_g = rg < (uint32_t)LMAX, win_b = rb < (uint32_t)LMAX;
+                    const uint32_t kbu = hiw_up(mb);
+                    const uint32_t su = keep_g ? (win_b ? kbu : kgu) : (win_b ? kbu : 0u);
+                    const uint32_t nm = keep_g ? (win_b ? 0xffffffffu : kb) : kg;
+                    const uint32_t nsurv = frame_sum<G>((keep_g ? 1u : 0u) + (win_b ? 1u : 0u));
+                    const uint32_t smax = frame_max<G>(su), nmin = frame_min<G>(nm);
+                    amb |= wmask(!(nsurv == (uint32_t)LMAX && nmin > smax)) & vmask;
+                    const uint64_t fw = wmask(!keep_g), ww = wmask(win_b);
+                    const uint32_t f8 = ((fl < F / 2 ? (uint32_t)fw : (uint32_t)(fw >> 32)) >> sh) & GM;
+                    const uint32_t w8 = ((fl < F / 2 ? (uint32_t)ww : (uint32_t)(ww >> 32)) >> sh) & GM;
+                    const uint32_t j = __builtin_popcount(f8 & ((1u << p) - 1u));
+                    src = gbase + (int)nth_set_bit8(w8, j);
+                    take = !keep_g;
+                }
+                // the worse child's bit rides on the table word
+                const uint32_t tw = tab | ((gbit ^ 1u) << 31);
+                const uint64_t pmb = shfl_u64(pscl_asu64(mb), src);
+                const uint32_t ptw = bperm32(tw, src);
+                const uint32_t pub = bperm32(ub, src);
+                uint64_t pu[NW];
+#pragma unroll
+                for (int k = 0; k < NW; ++k) pu[k] = 64 * k < 16 * b ? shfl_u64(u[k], src) : 0ULL;
+                uint32_t bt = gbit;
+                if (take) {
+                    metric = pscl_asf64(pmb);
+#pragma unroll
+                    for (int k = 0; k < NW; ++k) u[k] = pu[k];
+                    ub = pub;
+                    tab = ptw & 0x7fffffffu;
+                    bt = ptw >> 31;
+                } else {
+                    metric = mg;
+                }
+                ub |= bt << t;
+                lastbit = bt;
+            };
+            static_for<16>([&](auto TC) { phase(TC); });
+            // the block's bits into their word
+#pragma unroll
+            for (int k = 0; k < NW; ++k)
+                if (k == (b >> 2)) u[k] |= (uint64_t)ub << (16 * (b & 3));
+            ub = 0;
+        }
+
+        // ---- epilogue: candidates u[info_set], CRC syndrome, final list order certified,
+        // best = first CRC pass in list order (scl.py:176-209)
+        uint64_t ib[NW];
+#pragma unroll
+        for (int k = 0; k < NW; ++k) ib[k] = 0;
+        {
+            int off = 0;  // information bits before byte k (wave-uniform)
+#pragma unroll
+            for (int k = 0; k < N / 8; ++k) {
+                const uint32_t byte = (uint32_t)((u[k >> 3] >> (8 * (k & 7))) & 255u);
+                const uint64_t cb = GT[k * 256 + byte];
+                const int wi = off >> 6, sb = off & 63;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) {
+                    if (w == wi) ib[w] |= cb << sb;
+                    if (w == wi + 1 && sb > 56) ib[w] |= cb >> (64 - sb);
+                }
+                off += __builtin_popcount((uint32_t)((P.info_words[k >> 3] >> (8 * (k & 7))) & 255u));
+            }
+        }
+        uint32_t syn = 0;
+        if (P.has_crc) {
+            const int k4 = (K + 3) >> 2;
+#pragma unroll
+            for (int w = 0; w < NW; ++w)
+#pragma unroll
+                for (int jn = 0; jn < 16; ++jn) {
+                    const int m = 16 * w + jn;
+                    if (m < k4) syn ^= ST[m * 16 + (uint32_t)((ib[w] >> (4 * jn)) & 15u)];
+                }
+        }
+        // list position = rank of the metric among the frame's L (high words); certified when all
+        // pairs are apart by the margin (then the ranks are distinct and equal the exact order)
+        const uint32_t kh = hiw(metric), ku = hiw_up(metric);
+        uint32_t r = 0;
+        bool near = false;
+        auto cmp_perm = [&](uint32_t oh, uint32_t ou) {
+            r += oh < kh ? 1u : 0u;
+            near = near || !(ku < oh || ou < kh);
+        };
+        cmp_perm(dpp32<kQX1>(kh), dpp32<kQX1>(ku));
+        cmp_perm(dpp32<kQX2>(kh), dpp32<kQX2>(ku));
+        cmp_perm(dpp32<kQX3>(kh), dpp32<kQX3>(ku));
+        if constexpr (G == 8) {
+            const uint32_t mh = dpp32<kHMIR>(kh), mu = dpp32<kHMIR>(ku);
+            cmp_perm(mh, mu);
+            cmp_perm(dpp32<kQX1>(mh), dpp32<kQX1>(mu));
+            cmp_perm(dpp32<kQX2>(mh), dpp32<kQX2>(mu));
+            cmp_perm(dpp32<kQX3>(mh), dpp32<kQX3>(mu));
+        }
+        amb |= wmask(near) & vmask;
+        const bool famb = ((amb >> gbase) & (uint64_t)GM) != 0;
+        if (famb && p == 0 && fvalid) P.amb_list[atomicAdd(P.amb_count, 1)] = fi;
+        const uint32_t pass = P.has_crc ? (syn == 0 ? 1u : 0u) : 1u;
+        const uint32_t keyb = pass ? r : (uint32_t)LMAX + r;
+        const uint32_t kbest = frame_min<G>(keyb);
+        if (fvalid && !famb && keyb == kbest) {
+            const int best = (int)(kbest & (uint32_t)(LMAX - 1));
+            const bool bpass = kbest < (uint32_t)LMAX;
+            if (P.best)
+#pragma unroll
+                for (int w = 0; w < NW; ++w)
+                    if (w < W) P.best[fi * W + w] = ib[w];
+            if (P.flags) P.flags[fi] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
+            if (P.n_paths) P.n_paths[fi] = LMAX;
+            if (P.ref) {  // run_fer_sweep.py:91-109, run_ber_sweep.py:77-82,156
+                int bit_err = 0, pay_err = 0;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) {
+                    if (w < W) {
+                        const uint64_t dff = ib[w] ^ P.ref[fi * W + w];
+                        const int kp = P.k_payload - 64 * w;
+                        const uint64_t pm = kp >= 64 ? ~0ULL : (kp > 0 ? ((1ULL << kp) - 1) : 0ULL);
+                        bit_err += __popcll(dff);
+                        pay_err += __popcll(dff & pm);
+                    }
+                }
+                unsigned long long* C = reinterpret_cast<unsigned long long*>(P.counters);
+                if (!bpass) atomicAdd(C + PSCL_CNT_FRAME_ERR, 1ULL);
+                if (bit_err) atomicAdd(C + PSCL_CNT_BIT_ERR, (unsigned long long)bit_err);
+                if (pay_err) {
+                    atomicAdd(C + PSCL_CNT_PAYLOAD_ERR, 1ULL);
+                    atomicAdd(C + PSCL_CNT_PAYLOAD_BIT, (unsigned long long)pay_err);
+                }
+            }
+        }
+        wave_lds_fence();
+    }
+    if (P.ref && blockIdx.x == 0 && threadIdx.x == 0)
+        atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
+}
+
+template <int NL, int LMAX>
+hipError_t launch_lane_long(const pscl_decode_params& P, hipStream_t s) {
+    using Ly = LongLaneLayout<NL, LMAX>;
+    const int64_t g0 = (P.B + Ly::F - 1) / Ly::F;
+    const int64_t grid = g0 < 1 ? 1 : (g0 > (1 << 20) ? (1 << 20) : g0);
+    hipLaunchKernelGGL((scl_lane_long_kernel<NL, LMAX>), dim3((unsigned)grid), dim3(64), Ly::F * Ly::FSTRIDE * 8, s, P);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+#ifndef PSCL_LANE_LONG
+#define PSCL_LANE_LONG 1
+#endif
+
+// the screening launch of this plain long-code decode runs the lane-per-path kernel: N = 256,
+// 512 or 1024, L = 4 or 8, plain channel rows, at least log2 L information bits (a full list)
+int pscl_lane_long_available(const pscl_decode_params& P) {
+    if (!PSCL_LANE_LONG || !P.apx || P.force || P.sc_hard || P.rm_E || P.fidx || P.d_count || P.elist) return 0;
+    if (!P.info_words || !P.epi_table || P.out_by_row) return 0;
+    if (P.L != 8 && P.L != 4) return 0;
+    if (P.N != 256 && P.N != 512 && P.N != 1024) return 0;
+    return P.K >= (P.L == 8 ? 3 : 2);
+}
+
+hipError_t pscl_launch_lane_long(const pscl_decode_params& P, hipStream_t s) {
+    if (!pscl_lane_long_available(P)) return hipErrorInvalidValue;
+    switch (P.N) {
+        case 256: return P.L == 8 ? launch_lane_long<8, 8>(P, s) : launch_lane_long<8, 4>(P, s);
+        case 512: return P.L == 8 ? launch_lane_long<9, 8>(P, s) : launch_lane_long<9, 4>(P, s);
+        default: return P.L == 8 ? launch_lane_long<10, 8>(P, s) : launch_lane_long<10, 4>(P, s);
+    }
+}

@@ -89,6 +89,7 @@ __global__ void PSCL_LONG_BOUNDS scl_long_kernel(const pscl_decode_params P) {
     const int64_t Bn = P.d_count ? (*P.d_count < P.B ? (int64_t)*P.d_count : P.B) : P.B;
     for (int64_t f = blockIdx.x; f < Bn; f += gridDim.x) {
         const int64_t frow = P.fidx ? P.fidx[f] : f;
+        const int64_t fo = P.out_by_row ? frow : f;  // output row (the re-decode of screened frames: their own rows)
         // depth 0: the channel row (NR: de-rate-match + de-interleave while staging)
         if (P.rm_E == 0) {
             const double* src = P.llr + frow * N;
@@ -274,7 +275,7 @@ __global__ void PSCL_LONG_BOUNDS scl_long_kernel(const pscl_decode_params P) {
             return word;
         };
         if (active) {
-            const int64_t row = f * L + lane;
+            const int64_t row = fo * L + lane;
             if (P.metrics) P.metrics[row] = metric;
             if (P.cands)
                 for (int wi = 0; wi < W; ++wi) P.cands[row * W + wi] = cand_word(lane, wi);
@@ -294,7 +295,7 @@ __global__ void PSCL_LONG_BOUNDS scl_long_kernel(const pscl_decode_params P) {
                     int cur_q = lane, jj = K - 1;
                     for (int ph = N - 1; ph >= 0; --ph) {
                         if (info_bit(ph)) {
-                            P.best_info_llrs[f * K + jj] = hist_llr[(size_t)jj * L + cur_q];
+                            P.best_info_llrs[fo * K + jj] = hist_llr[(size_t)jj * L + cur_q];
                             --jj;
                         }
                         cur_q = hist_par[(size_t)ph * L + cur_q];
@@ -303,17 +304,17 @@ __global__ void PSCL_LONG_BOUNDS scl_long_kernel(const pscl_decode_params P) {
                 int bit_err = 0, pay_err = 0;
                 for (int wi = 0; wi < W; ++wi) {
                     const uint64_t word = cand_word(lane, wi);
-                    if (P.best) P.best[f * W + wi] = word;
+                    if (P.best) P.best[fo * W + wi] = word;
                     if (P.ref) {
-                        const uint64_t dff = word ^ P.ref[f * W + wi];
+                        const uint64_t dff = word ^ P.ref[fo * W + wi];
                         const int kp = P.k_payload - 64 * wi;
                         const uint64_t pm = kp >= 64 ? ~0ULL : (kp > 0 ? ((1ULL << kp) - 1) : 0ULL);
                         bit_err += __popcll(dff);
                         pay_err += __popcll(dff & pm);
                     }
                 }
-                if (P.flags) P.flags[f] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
-                if (P.n_paths) P.n_paths[f] = cnt;
+                if (P.flags) P.flags[fo] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
+                if (P.n_paths) P.n_paths[fo] = cnt;
                 if (P.ref) {  // run_fer_sweep.py:91-109, run_ber_sweep.py:77-82,156
                     unsigned long long* C = reinterpret_cast<unsigned long long*>(P.counters);
                     if (!bpass) atomicAdd(C + PSCL_CNT_FRAME_ERR, 1ULL);
@@ -327,7 +328,7 @@ __global__ void PSCL_LONG_BOUNDS scl_long_kernel(const pscl_decode_params P) {
         }
         wave_mem_fence();  // the next frame reuses this workgroup's scratch
     }
-    if (P.ref && blockIdx.x == 0 && threadIdx.x == 0)
+    if (P.ref && !P.out_by_row && blockIdx.x == 0 && threadIdx.x == 0)
         atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
 }
 

@@ -1,0 +1,122 @@
+"""GPU: the long-code screening decoder (csrc/scl_lane_long.hip, N = 256..1024, L = 4 and 8)
+against the exact long-code kernel (scl_long.hip, screening off) and the oracle.
+
+A plain decode (best bits and CRC flags only) of a long code runs the lane-per-path screening
+kernel plus the exact re-decode of the frames it defers; its outputs must equal the exact
+kernel's bit for bit (and, on a sample, the reference algorithm's: oracle.decode_scl, restating
+dl_scl_polar/polar/scl.py:108-209).  Codes: construct_info_set(N, K) + CRC-24 at Eb/N0 points in
+each code's waterfall (tools/long_bench.py), a K that is no multiple of 64, no CRC, integer LLRs
+(exact metric ties: must be deferred), and huge / NaN-free extreme LLRs."""
+import numpy as np
+import pytest
+
+import oracle
+from polar_code_amd import _native
+from polar_code_amd.polar.crc import attach_crc
+from polar_code_amd.polar.polar import _polar_transform, construct_info_set
+
+pytestmark = pytest.mark.gpu
+POLY = "0x1864CFB"
+
+
+def _frames(N, K, B, ebno, seed, crc=POLY):
+    rng = np.random.default_rng(seed)
+    info = construct_info_set(N, K)
+    kp = K - 24 if crc else K
+    msg = rng.integers(0, 2, size=(B, kp), dtype=np.int8)
+    if crc:
+        msg = attach_crc(msg, crc)
+    u = np.zeros((B, N), np.int8)
+    u[:, info] = msg
+    nv = 1.0 / (2.0 * K / N * 10 ** (ebno / 10))
+    llr = 2.0 * ((1.0 - 2.0 * _polar_transform(u)) + rng.normal(0.0, np.sqrt(nv), size=(B, N))) / nv
+    return info, llr
+
+
+def _screened_vs_exact(N, info, L, crc, llr):
+    scr = _native.Decoder(N, info, L, crc)
+    ex = _native.Decoder(N, info, L, crc)
+    ex.set_screening(False)
+    a = scr.decode(llr, want_metrics=False, want_cands=False, want_info_llrs=False)
+    n_def = scr.screening_count()
+    b = ex.decode(llr, want_metrics=False, want_cands=False, want_info_llrs=False)
+    np.testing.assert_array_equal(a["best_bits"], b["best_bits"])
+    np.testing.assert_array_equal(a["crc_pass"], b["crc_pass"])
+    np.testing.assert_array_equal(a["best_idx"], b["best_idx"])
+    np.testing.assert_array_equal(a["n_paths"], b["n_paths"])
+    return a, n_def
+
+
+@pytest.mark.parametrize("N,K,L,ebno,B", [(256, 128, 8, 4.0, 6000), (256, 128, 4, 4.0, 6000),
+                                          (512, 256, 8, 5.0, 3000), (512, 256, 4, 5.0, 3000),
+                                          (1024, 512, 8, 6.0, 1500), (1024, 512, 4, 6.0, 1500),
+                                          (256, 100, 8, 2.5, 3000), (512, 300, 8, 3.0, 1500)])
+def test_lane_long_equals_exact(N, K, L, ebno, B):
+    info, llr = _frames(N, K, B, ebno, seed=N * 7 + K + L)
+    a, n_def = _screened_vs_exact(N, info, L, POLY, llr)
+    print(f"N={N} K={K} L={L} {ebno} dB: {n_def} of {B} frames deferred ({100.0 * n_def / B:.3f} %), "
+          f"FER {1.0 - a['crc_pass'].mean():.4f}")
+    assert n_def < B // 4  # the screening pass decides most frames itself
+    for f in range(0, B, B // 6):  # the reference algorithm on a sample
+        n, c, m, il, bi = oracle.decode_scl(llr[f], info, L, crc=POLY)
+        np.testing.assert_array_equal(a["best_bits"][f], c[bi], err_msg=f"frame {f}")
+        assert bool(a["crc_pass"][f]) == oracle.check_crc(c[bi], POLY), f
+
+
+@pytest.mark.parametrize("N,L", [(256, 8), (1024, 4)])
+def test_lane_long_no_crc(N, L):
+    info, llr = _frames(N, N // 4, 1000, 2.0, seed=N + L, crc=None)
+    a, _ = _screened_vs_exact(N, info, L, None, llr)
+    assert a["crc_pass"].all()
+    for f in range(0, 1000, 250):
+        n, c, m, il, bi = oracle.decode_scl(llr[f], info, L, crc=None)
+        np.testing.assert_array_equal(a["best_bits"][f], c[bi], err_msg=f"frame {f}")
+
+
+@pytest.mark.parametrize("N,L", [(256, 8), (512, 4)])
+def test_lane_long_ties_and_extremes_defer(N, L):
+    """Integer LLRs (exact metric ties through the stable sort), noiseless +-1 rows and rows with
+    LLRs beyond 2^25 must reach the exact kernel; the outputs equal it everywhere."""
+    info, llr = _frames(N, N // 2, 600, 1.5, seed=3 * N + L)
+    llr[:200] = np.round(llr[:200])
+    llr[200:300] = np.sign(llr[200:300])
+    llr[300:320, 5] = 3.0e8
+    a, n_def = _screened_vs_exact(N, info, L, POLY, llr)
+    assert n_def >= 100  # the noiseless rows tie at every information phase
+    for f in [0, 1, 200, 201, 300, 301]:
+        n, c, m, il, bi = oracle.decode_scl(llr[f], info, L, crc=POLY)
+        np.testing.assert_array_equal(a["best_bits"][f], c[bi], err_msg=f"frame {f}")
+
+
+def test_lane_long_device_counters_equal_exact():
+    """In-kernel FER/BER counting through the screening pass (certified frames counted by the
+    lane kernel, deferred ones by the exact re-decode at their own rows) equals the exact run."""
+    N, K, L, B = 256, 128, 8, 4000
+    info, llr = _frames(N, K, B, 3.5, seed=11)
+    rng = np.random.default_rng(11)
+    msg = attach_crc(rng.integers(0, 2, size=(B, K - 24), dtype=np.int8), POLY)  # (same stream as _frames)
+    counts = []
+    for on in (True, False):
+        dec = _native.Decoder(N, info, L, POLY)
+        dec.set_screening(on)
+        W = dec.W
+        words = np.zeros((B, W), np.uint64)
+        for jj in range(K):
+            words[:, jj >> 6] |= msg[:, jj].astype(np.uint64) << np.uint64(jj & 63)
+        with _native.DeviceArena(dec) as mem:
+            d_llr, d_ref = mem.alloc(llr.nbytes), mem.alloc(words.nbytes)
+            d_best, d_flags, d_cnt = mem.alloc(B * W * 8), mem.alloc(B), mem.alloc(64)
+            mem.upload(d_llr, llr)
+            mem.upload(d_ref, words)
+            mem.memset(d_cnt, 0, 64)
+            dec.decode_device(d_llr, B, d_best=d_best, d_flags=d_flags, d_ref=d_ref, k_payload=K - 24,
+                              d_counters=d_cnt)
+            dec.sync()
+            counts.append((mem.download(d_cnt, 64, np.int64)[:5].copy(), mem.download(d_best, B * W * 8, np.uint64),
+                           mem.download(d_flags, B, np.uint8)))
+        dec.close()
+    (c1, b1, f1), (c0, b0, f0) = counts
+    np.testing.assert_array_equal(c1, c0)
+    np.testing.assert_array_equal(b1, b0)
+    np.testing.assert_array_equal(f1, f0)
+    assert c1[0] == B and c1[1] > 0
