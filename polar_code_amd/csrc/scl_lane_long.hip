@@ -40,10 +40,10 @@ struct LongLaneLayout {
     static constexpr int OFF2 = 24 * LMAX;      // depth R+2: [2][L][2]
     static constexpr int OFF3 = 28 * LMAX;      // depth R+3: [1][L][2]
     // partial sums of the depth-1..R left siblings, per path: level l (node width N >> l) at
-    // 32-bit word xoff(l), max(1, (N >> l) / 32) words
-    static constexpr int xsz(int l) { return (N >> l) / 32 > 1 ? (N >> l) / 32 : 1; }
-    static constexpr int xoff(int l) { return l <= 1 ? 0 : xoff(l - 1) + xsz(l - 1); }
-    static constexpr int XWORDS = xoff(R + 1);  // N / 32
+    // 32-bit word xoff(l) = sum of (N >> l') / 32 over l' < l, max(1, (N >> l) / 32) words
+    template <int l>
+    static constexpr int xoff = (N >> 5) - (N >> (4 + l));
+    static constexpr int XWORDS = N / 32;
     static constexpr int OFFX = 30 * LMAX;      // [L][XWORDS] uint32
     static constexpr int RAW = OFFX + LMAX * XWORDS / 2;
     // frames start alternately on the two 128-byte halves of the 256-byte bank row (as N = 128)
@@ -140,7 +140,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_LONG_WAVES_PER_EU) scl_lane_long
                         const int k = b >> (R - l);
                         if (k & 1) {
                             const int lo = (k - 1) * w;  // left sibling u[lo, lo + w)
-                            uint32_t* xo = XS + p * Ly::XWORDS + Ly::xoff(l);
+                            uint32_t* xo = XS + p * Ly::XWORDS + Ly::template xoff<l>;
                             if constexpr (w >= 64) {
                                 constexpr int nw = w / 64;
                                 uint64_t x[nw];
@@ -195,7 +195,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_LONG_WAVES_PER_EU) scl_lane_long
                             if (r2) {
 #pragma unroll
                                 for (int m = 0; m < CE / 4; ++m)
-                                    v[m] = g_node_wbit(v1s[m], v1s[m + CE / 4], xq[Ly::xoff(2) + (m >> 1)], e + 16 * (m & 1));
+                                    v[m] = g_node_wbit(v1s[m], v1s[m + CE / 4], xq[Ly::template xoff<2> + (m >> 1)], e + 16 * (m & 1));
                             } else {
 #pragma unroll
                                 for (int m = 0; m < CE / 4; ++m) v[m] = f_minsum(v1s[m], v1s[m + CE / 4]);
@@ -204,9 +204,9 @@ __global__ void __launch_bounds__(64, PSCL_LANE_LONG_WAVES_PER_EU) scl_lane_long
 #pragma unroll
                             for (int m = 0; m < CE / 4; ++m) {
                                 const int m2 = m + CE / 4;  // the depth-1 pair (m, m2)
-                                const double a = g_node_wbit(ch[m], ch[m + CE / 2], xq[Ly::xoff(1) + (m >> 1)], e + 16 * (m & 1));
-                                const double bb = g_node_wbit(ch[m2], ch[m2 + CE / 2], xq[Ly::xoff(1) + (m2 >> 1)], e + 16 * (m2 & 1));
-                                v[m] = r2 ? g_node_wbit(a, bb, xq[Ly::xoff(2) + (m >> 1)], e + 16 * (m & 1)) : f_minsum(a, bb);
+                                const double a = g_node_wbit(ch[m], ch[m + CE / 2], xq[Ly::template xoff<1> + (m >> 1)], e + 16 * (m & 1));
+                                const double bb = g_node_wbit(ch[m2], ch[m2 + CE / 2], xq[Ly::template xoff<1> + (m2 >> 1)], e + 16 * (m2 & 1));
+                                v[m] = r2 ? g_node_wbit(a, bb, xq[Ly::template xoff<2> + (m >> 1)], e + 16 * (m & 1)) : f_minsum(a, bb);
                             }
                         }
                         // depths 3..R
@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_LONG_WAVES_PER_EU) scl_lane_long
                             if ((b >> (R - l)) & 1) {
 #pragma unroll
                                 for (int m = 0; m < nl; ++m)
-                                    v[m] = g_node_wbit(v[m], v[m + nl], xq[Ly::xoff(l) + (m >> 1)], e + 16 * (m & 1));
+                                    v[m] = g_node_wbit(v[m], v[m + nl], xq[Ly::template xoff<l> + (m >> 1)], e + 16 * (m & 1));
                             } else {
 #pragma unroll
                                 for (int m = 0; m < nl; ++m) v[m] = f_minsum(v[m], v[m + nl]);
