@@ -165,9 +165,42 @@ __global__ void __launch_bounds__(64, PSCL_LANE_LONG_WAVES_PER_EU) scl_lane_long
                     wave_lds_fence();
                 }
                 const bool r1 = (b >> (R - 1)) & 1;
-#pragma unroll
-                for (int h = 0; h < EPL; ++h) {
+                const bool r2 = (b >> (R - 2)) & 1;
+                auto elem = [&](auto HC) {
+                    const int h = HC;
                     const uint32_t e = (uint32_t)(p + G * h);
+                    // every path of the element: depths 1-2 by first(q, xq, v), then depths 3..R
+                    auto paths = [&](auto&& first) {
+                        auto path = [&](int q0) {
+                            // lane p takes path (q0 + p) mod L: the lanes' stores hit distinct bank groups
+                            const int q = cnt == LMAX ? ((q0 + p) & (LMAX - 1)) : q0;
+                            const uint32_t* xq = XS + q * Ly::XWORDS;
+                            double v[CE / 4];  // depth-2 values at e + 16 m
+                            first(xq, v);
+                            static_for<R - 2>([&](auto LI) {
+                                constexpr int l = 3 + decltype(LI)::value;
+                                constexpr int nl = CE >> l;  // values per element at depth l
+                                if ((b >> (R - l)) & 1) {
+#pragma unroll
+                                    for (int m = 0; m < nl; ++m)
+                                        v[m] = g_node_wbit(v[m], v[m + nl], xq[Ly::template xoff<l> + (m >> 1)], e + 16 * (m & 1));
+                                } else {
+#pragma unroll
+                                    for (int m = 0; m < nl; ++m) v[m] = f_minsum(v[m], v[m + nl]);
+                                }
+                            });
+                            // element e of slot q: pair index e & 7, half e >> 3 ([8][L][2] layout)
+                            Af[Ly::OFF0 + ((e & 7) * LMAX + q) * 2 + (e >> 3)] = v[0];
+                        };
+                        if constexpr (CREG) {
+#pragma unroll
+                            for (int q0 = 0; q0 < LMAX; ++q0)
+                                if (q0 < cnt) path(q0);
+                        } else {
+#pragma nounroll
+                            for (int q0 = 0; q0 < cnt; ++q0) path(q0);
+                        }
+                    };
                     double ch[CE];
                     if constexpr (CREG) {
 #pragma unroll
@@ -176,55 +209,47 @@ __global__ void __launch_bounds__(64, PSCL_LANE_LONG_WAVES_PER_EU) scl_lane_long
 #pragma unroll
                         for (int m = 0; m < CE; ++m) ch[m] = chan[e + 16 * m];
                     }
-                    // depth 1 before phase N/2: the same f node for every path
-                    double v1s[CE / 2];
                     if (!r1) {
+                        // depth 1 before phase N/2: the same f node for every path (the channel
+                        // values die here: only the shared half-size set stays live)
+                        double v1s[CE / 2];
 #pragma unroll
                         for (int m = 0; m < CE / 2; ++m) v1s[m] = f_minsum(ch[m], ch[m + CE / 2]);
-                    }
-#pragma unroll
-                    for (int q0 = 0; q0 < LMAX; ++q0) {
-                        if (q0 >= cnt) break;
-                        // lane p takes path (q0 + p) mod L: the lanes' stores hit distinct bank groups
-                        const int q = cnt == LMAX ? ((q0 + p) & (LMAX - 1)) : q0;
-                        const uint32_t* xq = XS + q * Ly::XWORDS;
-                        // depths 1 and 2 together: v[m] (m < CE/4) = depth-2 value at e + 16 m
-                        double v[CE / 4];
-                        const bool r2 = (b >> (R - 2)) & 1;
-                        if (!r1) {
-                            if (r2) {
+                        if (r2)
+                            paths([&](const uint32_t* xq, double* v) {
 #pragma unroll
                                 for (int m = 0; m < CE / 4; ++m)
                                     v[m] = g_node_wbit(v1s[m], v1s[m + CE / 4], xq[Ly::template xoff<2> + (m >> 1)], e + 16 * (m & 1));
-                            } else {
+                            });
+                        else
+                            paths([&](const uint32_t* xq, double* v) {
 #pragma unroll
                                 for (int m = 0; m < CE / 4; ++m) v[m] = f_minsum(v1s[m], v1s[m + CE / 4]);
-                            }
-                        } else {
+                            });
+                    } else {
+                        // depths 1 and 2 together from the channel (depth-1 pair (m, m + CE/4))
+                        auto d1 = [&](const uint32_t* xq, int m) {
+                            return g_node_wbit(ch[m], ch[m + CE / 2], xq[Ly::template xoff<1> + (m >> 1)], e + 16 * (m & 1));
+                        };
+                        if (r2)
+                            paths([&](const uint32_t* xq, double* v) {
 #pragma unroll
-                            for (int m = 0; m < CE / 4; ++m) {
-                                const int m2 = m + CE / 4;  // the depth-1 pair (m, m2)
-                                const double a = g_node_wbit(ch[m], ch[m + CE / 2], xq[Ly::template xoff<1> + (m >> 1)], e + 16 * (m & 1));
-                                const double bb = g_node_wbit(ch[m2], ch[m2 + CE / 2], xq[Ly::template xoff<1> + (m2 >> 1)], e + 16 * (m2 & 1));
-                                v[m] = r2 ? g_node_wbit(a, bb, xq[Ly::template xoff<2> + (m >> 1)], e + 16 * (m & 1)) : f_minsum(a, bb);
-                            }
-                        }
-                        // depths 3..R
-                        static_for<R - 2>([&](auto LI) {
-                            constexpr int l = 3 + decltype(LI)::value;
-                            constexpr int nl = CE >> l;  // values per element at depth l
-                            if ((b >> (R - l)) & 1) {
+                                for (int m = 0; m < CE / 4; ++m)
+                                    v[m] = g_node_wbit(d1(xq, m), d1(xq, m + CE / 4), xq[Ly::template xoff<2> + (m >> 1)], e + 16 * (m & 1));
+                            });
+                        else
+                            paths([&](const uint32_t* xq, double* v) {
 #pragma unroll
-                                for (int m = 0; m < nl; ++m)
-                                    v[m] = g_node_wbit(v[m], v[m + nl], xq[Ly::template xoff<l> + (m >> 1)], e + 16 * (m & 1));
-                            } else {
-#pragma unroll
-                                for (int m = 0; m < nl; ++m) v[m] = f_minsum(v[m], v[m + nl]);
-                            }
-                        });
-                        // element e of slot q: pair index e & 7, half e >> 3 ([8][L][2] layout)
-                        Af[Ly::OFF0 + ((e & 7) * LMAX + q) * 2 + (e >> 3)] = v[0];
+                                for (int m = 0; m < CE / 4; ++m) v[m] = f_minsum(d1(xq, m), d1(xq, m + CE / 4));
+                            });
                     }
+                };
+                if constexpr (CREG) {
+                    static_for<EPL>([&](auto HC) { elem(HC); });
+                } else {
+                    // one element at a time: its 2^R channel LLRs are the recompute's largest live set
+#pragma nounroll
+                    for (int h = 0; h < EPL; ++h) elem(h);
                 }
                 wave_lds_fence();
             }
@@ -360,14 +385,16 @@ __global__ void __launch_bounds__(64, PSCL_LANE_LONG_WAVES_PER_EU) scl_lane_long
                 const uint64_t pmb = shfl_u64(pscl_asu64(mb), src);
                 const uint32_t ptw = bperm32(tw, src);
                 const uint32_t pub = bperm32(ub, src);
-                uint64_t pu[NW];
+                // (word by word: one pulled word live at a time)
 #pragma unroll
-                for (int k = 0; k < NW; ++k) pu[k] = 64 * k < 16 * b ? shfl_u64(u[k], src) : 0ULL;
+                for (int k = 0; k < NW; ++k)
+                    if (64 * k < 16 * b) {
+                        const uint64_t x = shfl_u64(u[k], src);
+                        u[k] = take ? x : u[k];
+                    }
                 uint32_t bt = gbit;
                 if (take) {
                     metric = pscl_asf64(pmb);
-#pragma unroll
-                    for (int k = 0; k < NW; ++k) u[k] = pu[k];
                     ub = pub;
                     tab = ptw & 0x7fffffffu;
                     bt = ptw >> 31;
