@@ -161,7 +161,8 @@ def test_uncoded_stream(kp):
                 amb[:, q] = np.abs(y) < 1e-4  # decisions the fp32 tolerance could flip
     assert cnt[_native.CNT_FRAMES] == B
     n_amb = int(amb.sum())
-    assert n_amb < 10
+    # (|y| < 1e-4 holds for ~3.6e-5 of the decisions at 1 dB: ~22 expected of 6e5 at kp = 200)
+    assert n_amb < 60
     assert abs(cnt[_native.CNT_FRAME_ERR] - int(err.any(axis=1).sum())) <= n_amb
     assert abs(cnt[_native.CNT_BIT_ERR] - int(err.sum())) <= n_amb
 
