@@ -671,7 +671,7 @@ int pscl_set_pipelined(pscl_handle* h, int enable) {
 
 int pscl_set_tuning(pscl_handle* h, int knob, int64_t value) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
-    static const int64_t lim[PSCL_TUNE_COUNT][2] = {{0, 0}, {0, 1}, {0, 64}, {0, 2}, {0, 1}, {0, 4096}, {0, PSCL_MAX_WAVES_PER_WG}};
+    static const int64_t lim[PSCL_TUNE_COUNT][2] = {{0, 0}, {0, 1}, {0, 64}, {0, 2}, {0, 1}, {0, 4096}, {0, PSCL_MAX_WAVES_PER_WG}, {0, 2}};
     if (knob < 1 || knob >= PSCL_TUNE_COUNT) return fail(PSCL_EINVAL, "unknown tuning knob %d", knob);
     if (value < lim[knob][0] || value > lim[knob][1] || (knob == PSCL_TUNE_POST_GRID && value && value < 16))
         return fail(PSCL_EINVAL, "tuning knob %d: value %lld out of range", knob, (long long)value);
@@ -1192,6 +1192,9 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
         P.ref = d_ref ? d_ref + c0 * W : nullptr;
         P.k_payload = k_payload;
         P.counters = d_counters_scl;
+        // (N = 128: the lane-per-path screening kernel only where PSCL_TUNE_DL_LANE asks for it --
+        // beside a DL-SCL retry chain the two-lanes-per-path form measured faster)
+        if (rounds > 0) P.no_lane = (h->tune[PSCL_TUNE_DL_LANE] ? h->tune[PSCL_TUNE_DL_LANE] : PSCL_DL_LANE_DEFAULT) != 1;
         if (pscl_decode_wpg(P) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
         if ((rc = launch_decode(h, P, 0))) return rc;
         if (rounds > 0) {

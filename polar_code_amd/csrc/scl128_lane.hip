@@ -50,9 +50,10 @@ struct LaneLayout {
 };
 
 // L = 4: keep the lane's 32 channel LLRs in registers across the frame (1) or re-read them at each
-// depth-1..3 recompute (0)
+// depth-1..3 recompute (0).  Measured (tools/ab_bench.sh, config 2, two rounds): 1.649 / 1.655 ms
+// against 1.672 / 1.668
 #ifndef PSCL_LANE_CREG4
-#define PSCL_LANE_CREG4 0
+#define PSCL_LANE_CREG4 1
 #endif
 
 #ifndef PSCL_LANE_WAVES_PER_EU
@@ -85,8 +86,8 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
         const double* chan = P.llr + frow * kN;
         // the frame's channel LLRs in registers: the lane's depth-3 elements e_k = p + G k (k < EPL)
         // need c[8 k + m] = chan[e_k + 16 m] -- the same at all 8 depth-1..3 recomputes
-        // (CREG = false, L = 4 by default: the 32 values are re-read from the L2-resident row at each
-        // recompute instead, which keeps them out of the registers of the other phases)
+        // (CREG = false, an L = 4 build option: the 32 values are re-read from the L2-resident row at
+        // each recompute instead, which keeps them out of the registers of the other phases)
         constexpr bool CREG = G == 8 || PSCL_LANE_CREG4;
         double c[8 * EPL];
         auto load_chan = [&]() {

@@ -58,6 +58,8 @@ struct pscl_decode_params {
                                  // instead (amb_count then [NSEG * CSTRIDE]); their flags PSCL_DL_DEFERRED
     int out_by_row;              // 1: outputs, reference words and counts at LLR row fidx[b]
     int wpg_cap;                 // 0, or an upper bound on the wavefronts per workgroup (tuning knob)
+    int no_lane;                 // 1: a screening launch takes the two-lanes-per-path kernel even where
+                                 // the lane-per-path one exists (PSCL_TUNE_DL_LANE)
     int64_t grid_cap;            // 0, or an upper bound on the workgroups of the launch (the
                                  // kernels stride over frames; a d_count launch of few frames)
     // code lengths above 128 (scl_long.hip): information set as N/64 words, and the global
@@ -225,6 +227,11 @@ int pscl_screening_available(const pscl_decode_params& P);  // scl128.hip
 int pscl_lane_available(const pscl_decode_params& P);
 int pscl_lane_frames_per_wg(int L);
 hipError_t pscl_launch_lane(const pscl_decode_params& P, int64_t grid, hipStream_t s);
+// the DL-SCL baseline decode's screening kernel at N = 128 (PSCL_TUNE_DL_LANE default): 1 the
+// lane-per-path kernel, 2 the two-lanes-per-path one
+#ifndef PSCL_DL_LANE_DEFAULT
+#define PSCL_DL_LANE_DEFAULT 2
+#endif
 // scl_lane_long.hip: the lane-per-path screening decoder of the long codes (N = 256..1024, L = 4, 8)
 int pscl_lane_long_available(const pscl_decode_params& P);
 hipError_t pscl_launch_lane_long(const pscl_decode_params& P, hipStream_t s);

@@ -1,4 +1,5 @@
-"""Throughput of the long-code decoder (csrc/scl_long.hip), N = 256..1024, on one GPU.
+"""Throughput of the long-code decoders (csrc/scl_lane_long.hip screening + scl_long.hip exact
+re-decode; L = 32: scl_long.hip alone), N = 256..1024, on one GPU.
 
     python tools/long_bench.py            (GPU box)
 Frames: random BPSK/AWGN codewords of construct_info_set(N, K) + CRC-24 at an Eb/N0 in each
@@ -93,8 +94,11 @@ for N, K, L, B, snr in [(256, 128, 8, 200_000, 4.0), (512, 256, 8, 100_000, 5.0)
     d_llr = torch.from_numpy(llr).cuda()
     best = torch.empty((B, dec.W), dtype=torch.int64, device="cuda")
     flags = torch.empty(B, dtype=torch.uint8, device="cuda")
+    best2 = torch.empty_like(best)
+    flags2 = torch.empty_like(flags)
     dec.decode_device(d_llr.data_ptr(), B, d_best=best.data_ptr(), d_flags=flags.data_ptr())
     torch.cuda.synchronize()
+    n_def = dec.screening_count()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     steps = 3
     e0.record(stream)
@@ -104,6 +108,26 @@ for N, K, L, B, snr in [(256, 128, 8, 200_000, 4.0), (512, 256, 8, 100_000, 5.0)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / steps
     fer = float(((flags.cpu().numpy() & 0x80) == 0).mean())
+    # pipelined handle (as bench.py): each call's exact re-decode of its deferred frames overlaps
+    # the next call's screening pass; alternating output buffers, the last re-decode inside the
+    # timed region (join)
+    dec.set_pipelined(True)
+    outs = [(best, flags), (best2, flags2)]
+    for i in range(2):
+        dec.decode_device(d_llr.data_ptr(), B, d_best=outs[i][0].data_ptr(), d_flags=outs[i][1].data_ptr())
+    dec.join()
+    torch.cuda.synchronize()
+    psteps = 6
+    e0.record(stream)
+    for i in range(psteps):
+        dec.decode_device(d_llr.data_ptr(), B, d_best=outs[i & 1][0].data_ptr(), d_flags=outs[i & 1][1].data_ptr())
+    dec.join()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    pms = e0.elapsed_time(e1) / psteps
+    same = bool(torch.equal(best, best2) and torch.equal(flags, flags2))
     print(f"N={N} K={K} L={L} {snr:g} dB: {B / ms * 1e3 / 1e6:.2f} M frames/s ({ms:.2f} ms per {B} frames), "
-          f"input {B * N * 8 / ms / 1e6:.1f} GB/s, FER {fer:.4f}", flush=True)
+          f"pipelined {B / pms * 1e3 / 1e6:.2f} M frames/s ({pms:.2f} ms), input {B * N * 8 / pms / 1e6:.1f} GB/s, "
+          f"FER {fer:.4f}, deferred to the exact kernel {n_def} ({100.0 * n_def / B:.2f} %), outputs equal {same}",
+          flush=True)
     dec.close()

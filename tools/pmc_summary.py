@@ -20,7 +20,8 @@ def load(d):
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in sorted(Path(d).glob("p*/pmc_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if "scl_decode_kernel" in r["Kernel_Name"] or "scl128_kernel" in r["Kernel_Name"]:
+            if any(k in r["Kernel_Name"] for k in ("scl_decode_kernel", "scl128_kernel", "scl_lane_kernel",
+                                                    "scl_lane_long_kernel")):
                 agg[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     if not agg:
         return {}
@@ -66,6 +67,10 @@ def main():
         out["valu_mix_per_frame"] = mix
     if "SQ_LDS_BANK_CONFLICT" in c:
         out["lds_bank_conflict_cycles"] = c["SQ_LDS_BANK_CONFLICT"]
+        if "SQ_LDS_IDX_ACTIVE" in c and c["SQ_LDS_IDX_ACTIVE"] > 0:
+            out["lds_bank_conflict_frac"] = round(c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"], 4)
+            out["lds_bank_conflict_frac_def"] = "SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (cycles)"
+            print(f"LDS bank conflict cycles / LDS active cycles = {out['lds_bank_conflict_frac']}")
     for k in ("SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES"):
         if k in c:
             out[k.lower()] = c[k]
