@@ -304,7 +304,8 @@ int pscl_join(pscl_handle* h);
  *   PSCL_TUNE_POST_GRID     16..4096: workgroup cap of the DL-SCL post pass (default 512)
  *   PSCL_TUNE_RETRY_WPG     1..4: wavefronts per workgroup of the retry decodes (default: by LDS)
  *   PSCL_TUNE_DL_LANE       1: a DL-SCL baseline decode (N = 128) on the lane-per-path screening
- *                           kernel; 2: on the two-lanes-per-path one (default: 2)
+ *                           kernel; 2: on the two-lanes-per-path one (default: 1 at L = 8, 2 at
+ *                           L = 4)
  */
 #define PSCL_TUNE_DL_SCREEN 1
 #define PSCL_TUNE_DL_CHUNKS 2

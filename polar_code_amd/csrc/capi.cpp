@@ -1192,9 +1192,14 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
         P.ref = d_ref ? d_ref + c0 * W : nullptr;
         P.k_payload = k_payload;
         P.counters = d_counters_scl;
-        // (N = 128: the lane-per-path screening kernel only where PSCL_TUNE_DL_LANE asks for it --
-        // beside a DL-SCL retry chain the two-lanes-per-path form measured faster)
-        if (rounds > 0) P.no_lane = (h->tune[PSCL_TUNE_DL_LANE] ? h->tune[PSCL_TUNE_DL_LANE] : PSCL_DL_LANE_DEFAULT) != 1;
+        // (N = 128: the DL-SCL baseline's screening kernel, PSCL_TUNE_DL_LANE; by default the
+        // lane-per-path one at L = 8 and the two-lanes-per-path one at L = 4, which measured faster
+        // beside the retry chains)
+        if (rounds > 0) {
+            const int64_t dl_lane = h->tune[PSCL_TUNE_DL_LANE] ? h->tune[PSCL_TUNE_DL_LANE]
+                                                               : (PSCL_DL_LANE_DEFAULT ? PSCL_DL_LANE_DEFAULT : (h->L == 8 ? 1 : 2));
+            P.no_lane = dl_lane != 1;
+        }
         if (pscl_decode_wpg(P) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
         if ((rc = launch_decode(h, P, 0))) return rc;
         if (rounds > 0) {

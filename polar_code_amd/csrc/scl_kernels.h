@@ -228,9 +228,9 @@ int pscl_lane_available(const pscl_decode_params& P);
 int pscl_lane_frames_per_wg(int L);
 hipError_t pscl_launch_lane(const pscl_decode_params& P, int64_t grid, hipStream_t s);
 // the DL-SCL baseline decode's screening kernel at N = 128 (PSCL_TUNE_DL_LANE default): 1 the
-// lane-per-path kernel, 2 the two-lanes-per-path one
+// lane-per-path kernel, 2 the two-lanes-per-path one, 0 by list size (lane-per-path at L = 8)
 #ifndef PSCL_DL_LANE_DEFAULT
-#define PSCL_DL_LANE_DEFAULT 2
+#define PSCL_DL_LANE_DEFAULT 0
 #endif
 // scl_lane_long.hip: the lane-per-path screening decoder of the long codes (N = 256..1024, L = 4, 8)
 int pscl_lane_long_available(const pscl_decode_params& P);
