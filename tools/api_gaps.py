@@ -1,0 +1,34 @@
+"""Host-side view of a rocprofv3 --kernel-trace --hip-trace run: HIP API calls longer than a
+threshold (allocation, synchronisation, copies) in time order, beside the main-stream kernels.
+
+    python tools/api_gaps.py <trace dir> [min_us]
+"""
+import csv
+import glob
+import sys
+
+d = sys.argv[1]
+min_us = float(sys.argv[2]) if len(sys.argv) > 2 else 100.0
+ev = []
+for f in glob.glob(d + "/**/*hip_api_trace.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if (e - s) / 1e3 >= min_us:
+            ev.append((s, e, "API " + r["Function"]))
+for f in glob.glob(d + "/**/*kernel_trace.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if (e - s) / 1e3 >= min_us:
+            ev.append((s, e, "K%s %s" % (r.get("Queue_Id", ""), r["Kernel_Name"][:60])))
+ev.sort()
+if not ev:
+    sys.exit("no events")
+t0 = ev[0][0]
+tot = {}
+for s, e, n in ev:
+    print(f"{(s - t0) / 1e3:10.1f} {(e - s) / 1e3:9.1f}  {n}")
+    if n.startswith("API"):
+        tot[n] = tot.get(n, 0.0) + (e - s) / 1e3
+print("API totals (us, calls >= threshold):")
+for n, v in sorted(tot.items(), key=lambda x: -x[1]):
+    print(f"  {v:10.1f}  {n}")
