@@ -15,6 +15,7 @@
 #include <string.h>
 
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "polar_scl.h"
@@ -99,6 +100,13 @@ struct pscl_dl_call {
     bool pipe = false;
 };
 
+// depth of the DL-SCL pipeline (pscl_set_pipelined): a pipelined call's compaction output and, for
+// pscl_simulate_device, its TX buffers are one of kDlPar sets, rewritten only after the retry chains
+// of the call kDlPar back have ended -- the handle's stream runs up to kDlPar - 1 calls ahead of
+// the chains (2 measured 175 M frames/s on the config-3 sweep, the stream waiting on chains of the
+// low-SNR points)
+constexpr int kDlPar = 4;
+
 struct pscl_handle {
     int device = 0;
     int N = 0, n = 0, K = 0, L = 0, W = 1, crc_deg = 0;
@@ -118,12 +126,15 @@ struct pscl_handle {
     int rm_E = 0;                     // NR rate matching (0 = off)
     int32_t* d_rm_src = nullptr;      // [N] de-interleave gather index
     int32_t* d_rm_order = nullptr;    // [N] interleaver order
-    DevBuf scratch[80];
+    DevBuf scratch[96];
     hipStream_t retry_stream[2] = {nullptr, nullptr};  // DL-SCL retry chains of the two chunk parities
     hipStream_t side_stream[2] = {nullptr, nullptr};   // their deferred-entry work (PSCL_TUNE_DL_SCREEN)
+    // the side streams of the other pipelining mode (their priority differs, create_priority_stream),
+    // kept across pscl_set_pipelined switches: a stream creation costs ~0.5 ms of host time
+    hipStream_t stash_pipe = nullptr, stash_retry[2] = {nullptr, nullptr}, stash_side[2] = {nullptr, nullptr};
     hipEvent_t ev_scr[2] = {nullptr, nullptr}, ev_def[2] = {nullptr, nullptr};
-    hipEvent_t ev_base[2] = {nullptr, nullptr}, ev_retry[2] = {nullptr, nullptr}, ev_join = nullptr;
-    int32_t* h_count = nullptr;          // pinned: failing-frame counts of the two chunk parities
+    hipEvent_t ev_base[kDlPar] = {}, ev_retry[kDlPar] = {}, ev_join = nullptr;
+    int32_t* h_count = nullptr;          // pinned: failing-frame counts of the chunk parities
     double* d_beta = nullptr;         // [K][K] DL-SCL flip metric (null = |L0|)
     double beta_absmax = 0.0;         // max |beta| (dl_post_kernel's certificate)
     uint64_t* d_epi = nullptr;        // scl128 epilogue tables (gather + syndrome)
@@ -146,9 +157,13 @@ struct pscl_handle {
     // pipelined pscl_dlscl_device: a call's retry chains (and its DL counters) stay on the retry
     // streams and overlap the next call's baseline decode; the calls alternate the compaction
     // parity (act/cnt), ev_dl[p] marks the end of parity p's chains
-    hipEvent_t ev_dl[2] = {nullptr, nullptr};
-    bool dl_pending[2] = {false, false};
+    hipEvent_t ev_dl[kDlPar] = {};
+    bool dl_pending[kDlPar] = {};
     int dl_par = 0;
+    // how many calls back a pipelined call's own buffers may still be in use: 2 for the caller's
+    // buffers (the pscl_set_pipelined contract: free again at the second following call),
+    // kDlPar for pscl_simulate_device's own scratch sets
+    int dl_back = 2;
     pscl_dl_call dl_defer;            // the last pipelined call, its chains not yet enqueued
     bool dl_defer_valid = false;
     std::vector<hipEvent_t> ev_pool;
@@ -193,8 +208,8 @@ int join_pipe(pscl_handle* h, int what = 3) {
         const int rc = dl_enqueue_deferred(h);
         if (rc) return rc;
     }
-    for (int p = 0; p < 2; ++p) {
-        if ((what & 1) && h->px_pending[p]) {
+    for (int p = 0; p < kDlPar; ++p) {
+        if ((what & 1) && p < 2 && h->px_pending[p]) {
             HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_px[p], 0));
             h->px_pending[p] = false;
         }
@@ -220,6 +235,13 @@ void quiesce(pscl_handle* h) {
 // the handle's current mode asks for (create_priority_stream)
 void drop_side_streams(pscl_handle* h) {
     quiesce(h);
+    if (h->stash_pipe) hipStreamDestroy(h->stash_pipe);
+    h->stash_pipe = nullptr;
+    for (int i = 0; i < 2; ++i) {
+        if (h->stash_retry[i]) hipStreamDestroy(h->stash_retry[i]);
+        if (h->stash_side[i]) hipStreamDestroy(h->stash_side[i]);
+        h->stash_retry[i] = h->stash_side[i] = nullptr;
+    }
     if (h->pipe_stream) hipStreamDestroy(h->pipe_stream);
     h->pipe_stream = nullptr;
     for (int i = 0; i < 2; ++i) {
@@ -579,9 +601,10 @@ int pscl_destroy(pscl_handle* h) {
     if (h->d_crctab) hipFree(h->d_crctab);
     for (int i = 0; i < 2; ++i)
         if (h->retry_stream[i]) hipStreamSynchronize(h->retry_stream[i]);
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kDlPar; ++i) {
         if (h->ev_base[i]) hipEventDestroy(h->ev_base[i]);
         if (h->ev_retry[i]) hipEventDestroy(h->ev_retry[i]);
+        if (h->ev_dl[i]) hipEventDestroy(h->ev_dl[i]);
     }
     if (h->ev_join) hipEventDestroy(h->ev_join);
     if (h->h_count) hipHostFree(h->h_count);
@@ -593,11 +616,15 @@ int pscl_destroy(pscl_handle* h) {
         if (h->ev_def[i]) hipEventDestroy(h->ev_def[i]);
     }
     for (int i = 0; i < 2; ++i) {
-        if (h->ev_dl[i]) hipEventDestroy(h->ev_dl[i]);
         if (h->ev_pscr[i]) hipEventDestroy(h->ev_pscr[i]);
         if (h->ev_px[i]) hipEventDestroy(h->ev_px[i]);
     }
     if (h->pipe_stream) hipStreamDestroy(h->pipe_stream);
+    if (h->stash_pipe) hipStreamDestroy(h->stash_pipe);
+    for (int i = 0; i < 2; ++i) {
+        if (h->stash_retry[i]) hipStreamDestroy(h->stash_retry[i]);
+        if (h->stash_side[i]) hipStreamDestroy(h->stash_side[i]);
+    }
     if (h->own_stream) hipStreamDestroy(h->own_stream);
     delete h;
     return PSCL_OK;
@@ -664,7 +691,15 @@ int pscl_set_pipelined(pscl_handle* h, int enable) {
     int rc = set_device(h);
     if (rc) return rc;
     if ((rc = join_pipe(h))) return rc;
-    if (h->pipelined != (enable != 0)) drop_side_streams(h);
+    if (h->pipelined != (enable != 0)) {
+        // the other mode's streams in, this mode's to the stash (drained first)
+        quiesce(h);
+        std::swap(h->pipe_stream, h->stash_pipe);
+        for (int i = 0; i < 2; ++i) {
+            std::swap(h->retry_stream[i], h->stash_retry[i]);
+            std::swap(h->side_stream[i], h->stash_side[i]);
+        }
+    }
     h->pipelined = enable != 0;
     return PSCL_OK;
 }
@@ -968,9 +1003,14 @@ constexpr int kMinSplit = 2048;
 struct DlBufs {
     DlState S[2];         // chain state (S[k] on retry stream k)
     DlLongState LS = {};  // (long codes)
-    int32_t* cnt[2] = {};  // failing-frame count of the two compaction parities
-    int64_t* act[2] = {};  // their frame indices
+    int32_t* cnt[kDlPar] = {};  // failing-frame count of the compaction parities
+    int64_t* act[kDlPar] = {};  // their frame indices
 };
+
+// compaction parity of chunk c: a pipelined call (one chunk) takes the handle's rotating parity,
+// the chunks of an unpipelined call alternate two
+inline int dl_parity(const pscl_dl_call& a, int64_t c) { return a.pipe ? a.pbase : (int)(c & 1); }
+constexpr int kCntSlot[kDlPar] = {22, 27, 80, 82}, kActSlot[kDlPar] = {23, 28, 81, 83};
 
 // streams, events and scratch of a DL-SCL call (everything sized before any work is queued:
 // an allocation synchronizes the device)
@@ -980,20 +1020,22 @@ int dl_setup(pscl_handle* h, const pscl_dl_call& a, DlBufs& b) {
     const int64_t cap = a.cap;
     for (int i = 0; i < 2; ++i)
         if (!h->retry_stream[i]) HIP_TRY(create_priority_stream(h, &h->retry_stream[i]));
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kDlPar; ++i) {
         if (!h->ev_base[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_base[i], hipEventDisableTiming));
         if (!h->ev_retry[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_retry[i], hipEventDisableTiming));
         if (!h->ev_dl[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_dl[i], hipEventDisableTiming));
+    }
+    for (int i = 0; i < 2; ++i) {
         if (!h->side_stream[i]) HIP_TRY(create_priority_stream(h, &h->side_stream[i]));
         if (!h->ev_scr[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_scr[i], hipEventDisableTiming));
         if (!h->ev_def[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_def[i], hipEventDisableTiming));
     }
     if (!h->ev_join) HIP_TRY(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
-    if (!h->h_count) HIP_TRY(hipHostMalloc((void**)&h->h_count, 16, hipHostMallocDefault));
+    if (!h->h_count) HIP_TRY(hipHostMalloc((void**)&h->h_count, 4 * kDlPar, hipHostMallocDefault));
     const size_t NS = PSCL_DL_NSEG;
-    for (int i = 0; i < (a.nch >= 2 || a.pipe ? 2 : 1); ++i) {
+    for (int i = 0; i < (a.pipe ? kDlPar : (a.nch >= 2 ? 2 : 1)); ++i) {
         void *pc, *pa;
-        if ((rc = ensure(h, 22 + 5 * i, 4, &pc)) || (rc = ensure(h, 23 + 5 * i, (size_t)cap * 8, &pa))) return rc;
+        if ((rc = ensure(h, kCntSlot[i], 4, &pc)) || (rc = ensure(h, kActSlot[i], (size_t)cap * 8, &pa))) return rc;
         b.cnt[i] = (int32_t*)pc;
         b.act[i] = (int64_t*)pa;
     }
@@ -1055,7 +1097,7 @@ int dl_setup(pscl_handle* h, const pscl_dl_call& a, DlBufs& b) {
 // (waiting for its baseline) and enqueues the rounds on the retry streams; ev_retry[p] marks
 // their end on retry stream 0
 int dl_chain(pscl_handle* h, const pscl_dl_call& a, const DlBufs& b, int64_t c) {
-    const int p = (int)((c + a.pbase) & 1);
+    const int p = dl_parity(a, c);
     const int64_t cap = a.cap;
     HIP_TRY(hipEventSynchronize(h->ev_base[p]));
     const int A = h->h_count[p];
@@ -1164,12 +1206,20 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
     }
     if ((rc = join_pipe(h, a.pipe ? 1 : 3))) return rc;
     a.pbase = a.pipe ? h->dl_par : 0;  // compaction parity of chunk 0
-    if (a.pipe && h->dl_pending[a.pbase]) {
-        // the chains of the call two back (same parity) may still read their compaction output and
-        // write their call's outputs: they end before this call starts (the contract of
-        // pscl_set_pipelined: a call's buffers are free again at the second following call)
-        HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_dl[a.pbase], 0));
-        h->dl_pending[a.pbase] = false;
+    if (a.pipe) {
+        // the chains of the call dl_back calls back may still write their call's outputs (and, kDlPar
+        // back, read this parity's compaction output): they end before this call starts (the
+        // contract of pscl_set_pipelined: a call's buffers are free again at the second following
+        // call; the chains run in call order, so the later call's end covers the earlier one's)
+        const int q = (a.pbase + kDlPar - h->dl_back) % kDlPar;
+        if (h->dl_pending[q]) {
+            HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_dl[q], 0));
+            h->dl_pending[q] = false;
+        }
+        if (h->dl_pending[a.pbase]) {
+            HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_dl[a.pbase], 0));
+            h->dl_pending[a.pbase] = false;
+        }
     }
     const int W = h->W;
     const int64_t row = h->rm_E ? h->rm_E : h->N;
@@ -1203,7 +1253,7 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
         if (pscl_decode_wpg(P) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
         if ((rc = launch_decode(h, P, 0))) return rc;
         if (rounds > 0) {
-            const int p = (int)((c + a.pbase) & 1);
+            const int p = dl_parity(a, c);
             if (c >= 2) HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[p], 0));  // the parity's indices free again
             HIP_TRY(hipMemsetAsync(bufs.cnt[p], 0, 4, s));
             if ((e = pscl_launch_dl_compact(d_flags + c0, nc, c0, bufs.act[p], nullptr, bufs.cnt[p], s)) != hipSuccess)
@@ -1219,12 +1269,12 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
         if ((rc = dl_enqueue_deferred(h))) return rc;
         h->dl_defer = a;
         h->dl_defer_valid = true;
-        h->dl_par ^= 1;
+        h->dl_par = (h->dl_par + 1) % kDlPar;
         return PSCL_OK;
     }
     if (rounds > 0) {
         if ((rc = dl_chain(h, a, bufs, nch - 1))) return rc;
-        HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[(nch - 1 + a.pbase) & 1], 0));  // chains run in order on stream 0
+        HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[dl_parity(a, nch - 1)], 0));  // chains run in order on stream 0
     }
     if (d_ref) {
         e = pscl_launch_dl_count(d_best, d_flags, d_ref, B, W, k_payload, d_counters_dl, s);
@@ -1374,8 +1424,8 @@ int channel_launch(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebn
 // 2^20 frames through handle scratch (N * 8 bytes of LLRs per frame: about 1 GiB per chunk at
 // N = 128), each = TX (+ the uncoded baseline) + pscl_dlscl_device.  On a pipelined handle every
 // chunk is one pipelined DL-SCL call: its retry chains overlap the next chunk's (or the next
-// point's) TX and baseline, so the two scratch sets alternate with the DL-SCL call parity, and a
-// set is rewritten only after the chains of the call two back that used it have ended.
+// point's) TX and baseline, so kDlPar scratch sets rotate with the DL-SCL call parity, and a set
+// is rewritten only after the chains of the call kDlPar back that used it have ended.
 int simulate_enqueue(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
                      int64_t frame0, int64_t B, int retries, int include_uncoded, int64_t* cs) {
     const int64_t chunk = B < (1 << 20) ? B : (1 << 20);
@@ -1388,7 +1438,8 @@ int simulate_enqueue(pscl_handle* h, uint64_t seed, uint32_t stream_id, double e
             HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_dl[par], 0));
             h->dl_pending[par] = false;
         }
-        const int base = par ? 66 : 30;
+        static const int kSimSlot[kDlPar] = {30, 66, 84, 88};
+        const int base = kSimSlot[par];
         void *d_llr, *d_msg, *d_best, *d_flags;
         if ((rc = ensure(h, base, (size_t)chunk * N * 8, &d_llr))) return rc;
         if ((rc = ensure(h, base + 1, (size_t)chunk * W * 8, &d_msg))) return rc;
@@ -1402,9 +1453,11 @@ int simulate_enqueue(pscl_handle* h, uint64_t seed, uint32_t stream_id, double e
         if (include_uncoded && !unc_fused &&
             (rc = uncoded_launch(h, seed, stream_id, ebno_db, k_payload, frame0 + f, n, cs + 2 * PSCL_NCOUNT, true)))
             return rc;
-        if ((rc = pscl_dlscl_device(h, (const double*)d_llr, n, retries, (uint64_t*)d_best, (uint8_t*)d_flags, nullptr,
-                                    nullptr, 0, (const uint64_t*)d_msg, k_payload, cs, cs + PSCL_NCOUNT)))
-            return rc;
+        h->dl_back = kDlPar;  // (its own scratch set: kDlPar sets rotate with the call parity)
+        rc = pscl_dlscl_device(h, (const double*)d_llr, n, retries, (uint64_t*)d_best, (uint8_t*)d_flags, nullptr, nullptr,
+                               0, (const uint64_t*)d_msg, k_payload, cs, cs + PSCL_NCOUNT);
+        h->dl_back = 2;
+        if (rc) return rc;
     }
     return PSCL_OK;
 }

@@ -62,11 +62,7 @@ __device__ __forceinline__ void wave_mem_fence() {
 #define PSCL_LONG_BOUNDS __launch_bounds__(64)
 #endif
 
-// LDSRES: the workgroup's frame state in LDS instead of global scratch (one frame per workgroup,
-// up to ~150 KB): the launches of few frames -- the exact re-decode of a screening pass's deferred
-// frames, the DL-SCL retry decodes -- are bound by one frame's phase latency, which LDS round trips
-// cut several-fold; the many-frame launches keep global scratch and 8 waves per SIMD
-template <int LMAX, bool HIST, bool LDSRES = false>
+template <int LMAX, bool HIST>
 __global__ void PSCL_LONG_BOUNDS scl_long_kernel(const pscl_decode_params P) {
     constexpr int G = 2 * LMAX;  // candidate lanes: path p in lane p, its bit-1 child in lane p + LMAX
     __shared__ uint64_t T[PSCL_EXP_TABLE_WORDS];
@@ -83,8 +79,7 @@ __global__ void PSCL_LONG_BOUNDS scl_long_kernel(const pscl_decode_params P) {
     const int N = P.N, n = P.n, K = P.K, L = P.L, W = P.W, NW = N >> 6;
     const bool path_lane = lane < LMAX;
     const int cpath = lane & (LMAX - 1);
-    extern __shared__ __attribute__((aligned(16))) unsigned char long_lds[];
-    unsigned char* base = LDSRES ? long_lds : reinterpret_cast<unsigned char*>(P.long_scratch) + (size_t)blockIdx.x * P.long_block_bytes;
+    unsigned char* base = reinterpret_cast<unsigned char*>(P.long_scratch) + (size_t)blockIdx.x * P.long_block_bytes;
     double* tree = reinterpret_cast<double*>(base);
     uint64_t* ubuf = reinterpret_cast<uint64_t*>(base + long_tree_doubles(N, LMAX) * 8);  // [2][LMAX][NW]
     double* hist_llr = reinterpret_cast<double*>(ubuf + 2 * LMAX * NW);                  // [K][L]
@@ -337,43 +332,8 @@ __global__ void PSCL_LONG_BOUNDS scl_long_kernel(const pscl_decode_params P) {
         atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
 }
 
-// static LDS of the kernel (exp table, partial-sum words, exchange arrays) beside the dynamic state
-constexpr int kLongStaticLds = 8 * PSCL_EXP_TABLE_WORDS + 8 * 32 * kMaxXsWords + 64 + 32 * 16 + 64 * 8 + 64 * 4 + 32 * 8;
-constexpr int64_t kLdsMax = 160 * 1024;
-
-template <int LMAX, bool LDSRES>
-const void* long_fn(bool hist) {
-    return hist ? reinterpret_cast<const void*>(scl_long_kernel<LMAX, true, LDSRES>)
-                : reinterpret_cast<const void*>(scl_long_kernel<LMAX, false, LDSRES>);
-}
-
 template <int LMAX>
 hipError_t launch_long_l(const pscl_decode_params& P, int hist, int64_t grid, hipStream_t s) {
-    // a launch of few frames (a device-side count: deferred frames, retry entries) whose state fits
-    // in LDS takes the LDS-resident form, one workgroup per CU slot the LDS allows
-    const int64_t lds = P.long_block_bytes;
-    if (P.d_count && lds + kLongStaticLds <= kLdsMax) {
-        static bool attr[2] = {false, false};
-        if (!attr[hist ? 1 : 0]) {
-            hipError_t e = hipFuncSetAttribute(long_fn<LMAX, true>(hist != 0), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               (int)(kLdsMax - kLongStaticLds));
-            if (e != hipSuccess) return e;
-            attr[hist ? 1 : 0] = true;
-        }
-        static int cus = 0;
-        if (!cus) {
-            int dev = 0, n = 0;
-            cus = (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0) ? n : 256;
-        }
-        const int64_t per_cu = kLdsMax / (lds + kLongStaticLds);
-        const int64_t cap = (int64_t)cus * (per_cu < 1 ? 1 : per_cu);
-        const int64_t g = P.B < cap ? (P.B < 1 ? 1 : P.B) : cap;
-        if (hist)
-            hipLaunchKernelGGL((scl_long_kernel<LMAX, true, true>), dim3((unsigned)g), dim3(64), (size_t)lds, s, P);
-        else
-            hipLaunchKernelGGL((scl_long_kernel<LMAX, false, true>), dim3((unsigned)g), dim3(64), (size_t)lds, s, P);
-        return hipGetLastError();
-    }
     if (hist)
         hipLaunchKernelGGL((scl_long_kernel<LMAX, true>), dim3((unsigned)grid), dim3(64), 0, s, P);
     else
@@ -428,8 +388,7 @@ int64_t pscl_long_grid(int64_t B, int L) {
 }
 
 hipError_t pscl_launch_long(const pscl_decode_params& P, int hist, hipStream_t s) {
-    if (P.N > kMaxLongN || P.N < 256 || !P.info_words) return hipErrorInvalidValue;
-    if (!P.long_scratch && !(P.d_count && P.long_block_bytes + kLongStaticLds <= kLdsMax)) return hipErrorInvalidValue;
+    if (P.N > kMaxLongN || P.N < 256 || !P.long_scratch || !P.info_words) return hipErrorInvalidValue;
     const int64_t grid = pscl_decode_grid(P);
     switch (pscl_decode_lmax(P.L)) {
         case 1: return launch_long_l<1>(P, hist, grid, s);
