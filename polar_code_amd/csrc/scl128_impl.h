@@ -74,13 +74,14 @@ struct Layout128 {
     // the paths' left-sibling partial sums {X1 lo, X1 hi, X2, X3} at a depth-1..3 recompute,
     // 16 B per path: every lane reads them for all paths with ds_read_b128
     static constexpr int OFFX = OFF6 + 2 * LMAX;
-    // doubles per frame: padded to 256 B, plus (frames narrower than 16 lanes) one access
-    // footprint of the frame's lanes (2 G doubles) -- consecutive frames then start on different
-    // bank groups and a ds_read_b128 lane group, which mixes lanes of neighbouring frames, covers
-    // distinct banks (256-B strides put every frame of an 8-lane layout on the same 32 banks:
-    // 55 % of the L = 4 kernel's LDS cycles were bank conflicts, PSCL_L128_PAD = 0)
+    // doubles per frame, padded to 256 B: the frames of a wave then start on bank 0.  (With 8-lane
+    // frames, L = 4, every frame then uses the same 32 banks: 55 % of that kernel's LDS cycles are
+    // bank conflicts.  PSCL_L128_PAD = 1 offsets frames narrower than 16 lanes by one access
+    // footprint, 2 G doubles: conflicts 55 -> 37 %, but config 4 measured 3.64-3.68 ms per step
+    // against 3.46-3.48 -- the larger LDS per wavefront costs more beside the retry chains than
+    // the conflicts do -- profiles/r04j_l128_pad_ab.txt)
 #ifndef PSCL_L128_PAD
-#define PSCL_L128_PAD 1
+#define PSCL_L128_PAD 0
 #endif
     static constexpr int FSTRIDE = ((OFFX + 2 * LMAX + 31) & ~31) + (PSCL_L128_PAD && G < 16 ? 2 * G : 0);
     // position of element e of slot s in a node of width w
