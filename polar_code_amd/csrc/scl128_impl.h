@@ -249,6 +249,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
         const int64_t tot = pscl_bucket_prefix(P.bcount, P.bcap, bpre);
         Bn = tot < P.B ? tot : P.B;
     }
+    int cfe = 0, cbe = 0, cpe = 0, cpb = 0;  // this lane's error counts (flushed at the end)
     for (int64_t f0 = ((int64_t)blockIdx.x * wpg + wave) * F; f0 < Bn; f0 += wstride) {
         const int64_t fi = f0 + fl;
         const bool fvalid = fi < Bn;
@@ -934,13 +935,15 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 }
                 if (P.flags) P.flags[fo] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
                 if (P.n_paths) P.n_paths[fo] = cnt;
-                if (P.ref && !(APX && PSCL_APX_ABLATE))  // (ablation timings: wrong frames, no atomics)
-                    count_errors(P.counters, ib0, ib1, P.ref[fo * PW], PW > 1 ? P.ref[fo * PW + 1] : 0, P.k_payload,
-                                 bpass);
+                if (P.ref && !(APX && PSCL_APX_ABLATE)) {  // (ablation timings: wrong frames, no counts)
+                    const uint64_t ibw[2] = {ib0, ib1};
+                    tally_errors(ibw, P.ref + fo * PW, PW, P.k_payload, bpass, cfe, cbe, cpe, cpb);
+                }
             }
         }
         wave_lds_fence();
     }
+    if (P.ref) flush_counts(P.counters, cfe, cbe, cpe, cpb);
     if (P.ref && !P.out_by_row && blockIdx.x == 0 && threadIdx.x == 0)
         atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
 }

@@ -79,6 +79,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
     auto hiw = [](double m) { return (uint32_t)(pscl_asu64(m) >> 32); };
     auto hiw_up = [&](double m) { return hiw(__builtin_fma(m, 1.0 + 0x1p-40, PSCL_TAIL_ABS_MARGIN)); };
 
+    int cfe = 0, cbe = 0, cpe = 0, cpb = 0;  // this lane's error counts (flushed at the end)
     for (int64_t f0 = (int64_t)blockIdx.x * F; f0 < P.B; f0 += (int64_t)gridDim.x * F) {
         const int64_t fi = f0 + fl;
         const bool fvalid = fi < P.B;
@@ -418,12 +419,18 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
             }
             if (P.flags) P.flags[fi] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
             if (P.n_paths) P.n_paths[fi] = LMAX;
-            if (P.ref) count_errors(P.counters, ib0, ib1, P.ref[fi * PW], PW > 1 ? P.ref[fi * PW + 1] : 0, P.k_payload, bpass);
+            if (P.ref) {
+                const uint64_t ibw[2] = {ib0, ib1};
+                tally_errors(ibw, P.ref + fi * PW, PW, P.k_payload, bpass, cfe, cbe, cpe, cpb);
+            }
         }
         wave_lds_fence();
     }
-    if (P.ref && blockIdx.x == 0 && threadIdx.x == 0)
-        atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
+    if (P.ref) {
+        flush_counts(P.counters, cfe, cbe, cpe, cpb);
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
+    }
 }
 
 }  // namespace

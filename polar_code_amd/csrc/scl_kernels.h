@@ -227,6 +227,15 @@ int pscl_screening_available(const pscl_decode_params& P);  // scl128.hip
 int pscl_lane_available(const pscl_decode_params& P);
 int pscl_lane_frames_per_wg(int L);
 hipError_t pscl_launch_lane(const pscl_decode_params& P, int64_t grid, hipStream_t s);
+// workgroups of a lane-per-path decode that counts errors (P.ref): each wavefront strides over
+// frames and adds its counts once at the end
+#ifndef PSCL_LANE_COUNT_GRID
+#define PSCL_LANE_COUNT_GRID 32768
+#endif
+// the same for the two-lanes-per-path kernels (workgroups of up to PSCL_MAX_WAVES_PER_WG wavefronts)
+#ifndef PSCL_COUNT_GRID
+#define PSCL_COUNT_GRID 8192
+#endif
 // the DL-SCL baseline decode's screening kernel at N = 128 (PSCL_TUNE_DL_LANE default): 1 the
 // lane-per-path kernel, 2 the two-lanes-per-path one, 0 by list size (lane-per-path at L = 8)
 #ifndef PSCL_DL_LANE_DEFAULT

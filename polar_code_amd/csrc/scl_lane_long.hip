@@ -89,6 +89,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_LONG_WAVES_PER_EU) scl_lane_long
     auto hiw_up = [&](double m) { return hiw(__builtin_fma(m, 1.0 + 0x1p-40, MARGIN)); };
     auto slot_rel = [](uint32_t tab, int dr) { return (int)((tab >> (4 * dr)) & 15u); };
 
+    int cfe = 0, cbe = 0, cpe = 0, cpb = 0;  // this lane's error counts (flushed at the end)
     for (int64_t f0 = (int64_t)blockIdx.x * F; f0 < P.B; f0 += (int64_t)gridDim.x * F) {
         const int64_t fi = f0 + fl;
         const bool fvalid = fi < P.B;
@@ -478,37 +479,27 @@ __global__ void __launch_bounds__(64, PSCL_LANE_LONG_WAVES_PER_EU) scl_lane_long
             if (P.flags) P.flags[fi] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
             if (P.n_paths) P.n_paths[fi] = LMAX;
             if (P.ref) {  // run_fer_sweep.py:91-109, run_ber_sweep.py:77-82,156
-                int bit_err = 0, pay_err = 0;
+                uint64_t rw[NW];
 #pragma unroll
-                for (int w = 0; w < NW; ++w) {
-                    if (w < W) {
-                        const uint64_t dff = ib[w] ^ P.ref[fi * W + w];
-                        const int kp = P.k_payload - 64 * w;
-                        const uint64_t pm = kp >= 64 ? ~0ULL : (kp > 0 ? ((1ULL << kp) - 1) : 0ULL);
-                        bit_err += __popcll(dff);
-                        pay_err += __popcll(dff & pm);
-                    }
-                }
-                unsigned long long* C = reinterpret_cast<unsigned long long*>(P.counters);
-                if (!bpass) atomicAdd(C + PSCL_CNT_FRAME_ERR, 1ULL);
-                if (bit_err) atomicAdd(C + PSCL_CNT_BIT_ERR, (unsigned long long)bit_err);
-                if (pay_err) {
-                    atomicAdd(C + PSCL_CNT_PAYLOAD_ERR, 1ULL);
-                    atomicAdd(C + PSCL_CNT_PAYLOAD_BIT, (unsigned long long)pay_err);
-                }
+                for (int w = 0; w < NW; ++w) rw[w] = w < W ? P.ref[fi * W + w] : ib[w];
+                tally_errors(ib, rw, NW, P.k_payload, bpass, cfe, cbe, cpe, cpb);
             }
         }
         wave_lds_fence();
     }
-    if (P.ref && blockIdx.x == 0 && threadIdx.x == 0)
-        atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
+    if (P.ref) {
+        flush_counts(P.counters, cfe, cbe, cpe, cpb);
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
+    }
 }
 
 template <int NL, int LMAX>
 hipError_t launch_lane_long(const pscl_decode_params& P, hipStream_t s) {
     using Ly = LongLaneLayout<NL, LMAX>;
     const int64_t g0 = (P.B + Ly::F - 1) / Ly::F;
-    const int64_t grid = g0 < 1 ? 1 : (g0 > (1 << 20) ? (1 << 20) : g0);
+    const int64_t cap = P.ref ? PSCL_LANE_COUNT_GRID : (1 << 20);
+    const int64_t grid = g0 < 1 ? 1 : (g0 > cap ? cap : g0);
     hipLaunchKernelGGL((scl_lane_long_kernel<NL, LMAX>), dim3((unsigned)grid), dim3(64), Ly::F * Ly::FSTRIDE * 8, s, P);
     return hipGetLastError();
 }
