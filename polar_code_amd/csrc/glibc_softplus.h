@@ -491,7 +491,8 @@ PSCL_HD double pscl_softplus_tail_scr(double v) { return pscl_softplus_tail_scr_
  * certificates need: every comparison the screening pass makes involves a metric of at least
  * ln 2 (a worse child pays |lam| + L >= ln 2; two distinct paths diverged where one took a
  * worse child), and a metric is a sum of at most N = 128 increments, so its error is at most
- * 128 * PSCL_TAIL_ABS_DELTA plus the fp64 summation error (relative, N * 2^-53).
+ * 128 * PSCL_TAIL_ABS_DELTA plus the fp64 summation error (relative, N * 2^-53).  (The long-code
+ * kernel, scl_lane_long.hip, scales the margin to its N: 2 N PSCL_TAIL_ABS_DELTA.)
  *
  * The bound is measured, not assumed: pscl_tail_abs_f32 is a function of the fp32 value x32
  * alone, and tools/tests scan EVERY non-negative fp32 x32 (2^31 - 2^23 values, +inf included) on
@@ -506,7 +507,8 @@ PSCL_HD double pscl_softplus_tail_scr(double v) { return pscl_softplus_tail_scr_
 #endif
 #define PSCL_LOG2E_F32 1.44269504088896341f
 #define PSCL_LN2_F32 0.693147180559945309f
-/* upper bound of the exhaustive device scan (see above; the measured value is in DESIGN.md §5.1a) */
+/* upper bound of the exhaustive device scan: measured on MI355X 1.2338e-7 = 2.07 * 2^-24, at
+ * x32 = 0.28314 (tests/test_gpu_screening.py, profiles/r04c_screening_tests.txt) */
 #ifndef PSCL_TAIL_ABS_SCAN
 #define PSCL_TAIL_ABS_SCAN (3.0 / 16777216.0)
 #endif
