@@ -936,14 +936,23 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 if (P.flags) P.flags[fo] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
                 if (P.n_paths) P.n_paths[fo] = cnt;
                 if (P.ref && !(APX && PSCL_APX_ABLATE)) {  // (ablation timings: wrong frames, no counts)
-                    const uint64_t ibw[2] = {ib0, ib1};
-                    tally_errors(ibw, P.ref + fo * PW, PW, P.k_payload, bpass, cfe, cbe, cpe, cpb);
+                    if constexpr (HIST) {
+                        // (the history instances keep per-frame atomics: their register budget is
+                        // spent -- four more live counters spill further, and the rate-matched L = 8
+                        // history instance then measured wrong decision LLRs)
+                        count_errors(P.counters, ib0, ib1, P.ref[fo * PW], PW > 1 ? P.ref[fo * PW + 1] : 0, P.k_payload,
+                                     bpass);
+                    } else {
+                        const uint64_t ibw[2] = {ib0, ib1};
+                        tally_errors(ibw, P.ref + fo * PW, PW, P.k_payload, bpass, cfe, cbe, cpe, cpb);
+                    }
                 }
             }
         }
         wave_lds_fence();
     }
-    if (P.ref) flush_counts(P.counters, cfe, cbe, cpe, cpb);
+    if constexpr (!HIST)
+        if (P.ref) flush_counts(P.counters, cfe, cbe, cpe, cpb);
     if (P.ref && !P.out_by_row && blockIdx.x == 0 && threadIdx.x == 0)
         atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
 }
