@@ -289,6 +289,20 @@ void fill_decode_params(const pscl_handle* h, pscl_decode_params& P, int hist) {
     pscl_decode_layout(P, hist);
 }
 
+// a counting decode (P.ref) whose kernel stores per-wavefront counts: their buffer (scratch slot 92,
+// reused by every such launch of the handle: each is followed on its stream by its count-reduce
+// launch; the DL-SCL and pipelined paths launch decodes of one handle on one stream in order)
+int with_count_slots(pscl_handle* h, pscl_decode_params& P, int hist) {
+    P.cpart = nullptr;
+    const int64_t slots = pscl_decode_count_slots(P, hist);
+    if (slots <= 0) return PSCL_OK;
+    void* d;
+    const int rc = ensure(h, 92, (size_t)slots * 16, &d);
+    if (rc) return rc;
+    P.cpart = (int32_t*)d;
+    return PSCL_OK;
+}
+
 // scr_slot: the scratch buffer of a long-code decode (decodes that may run concurrently on
 // different streams need different slots)
 // pipe: the caller is a plain pscl_decode_device on a pipelined handle (see pscl_handle)
@@ -358,7 +372,9 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
         pscl_decode_layout(S, hist);  // (no exp table in LDS)
         S.amb_list = (int64_t*)d_list;
         S.amb_count = (int32_t*)d_cnt;
+        if ((rc = with_count_slots(h, S, hist))) return rc;
         err = pscl_launch_decode(S, hist, st);
+        if (err == hipSuccess && S.cpart) err = pscl_launch_count_reduce(S.cpart, pscl_decode_count_slots(S, hist), S.counters, st);
         h->screened = true;
         h->screened_slot = s_cnt;
 #ifdef PSCL_APX_ABLATE
@@ -391,7 +407,10 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
             err = pscl_launch_decode(X, hist, st);
         }
     } else {
+        const int rc = with_count_slots(h, P, hist);
+        if (rc) return rc;
         err = pscl_launch_decode(P, hist, st);
+        if (err == hipSuccess && P.cpart) err = pscl_launch_count_reduce(P.cpart, pscl_decode_count_slots(P, hist), P.counters, st);
     }
     if (err != hipSuccess) return fail(PSCL_EDEVICE, "decode kernel launch: %s", hipGetErrorString(err));
     if (h->timing) HIP_TRY(hipEventRecord(e1, st));

@@ -39,6 +39,20 @@ namespace {
 
 using namespace pscl;
 
+// a wavefront's error counts at the end of a counting launch: stored at its slot of P.cpart, or
+// added to P.counters with one atomic per counter (flush_counts)
+__device__ __forceinline__ void flush_counts_p(const pscl_decode_params& P, int64_t wslot, int fe, int be, int pe, int pb) {
+    if (P.cpart) {
+        fe = wave_sum(fe);
+        be = wave_sum(be);
+        pe = wave_sum(pe);
+        pb = wave_sum(pb);
+        if ((threadIdx.x & 63) == 0) reinterpret_cast<int4*>(P.cpart)[wslot] = make_int4(fe, be, pe, pb);
+    } else {
+        flush_counts(P.counters, fe, be, pe, pb);
+    }
+}
+
 constexpr int kN = 128;
 constexpr int kn = 7;
 
@@ -952,7 +966,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
         wave_lds_fence();
     }
     if constexpr (!HIST)
-        if (P.ref) flush_counts(P.counters, cfe, cbe, cpe, cpb);
+        if (P.ref) flush_counts_p(P, (int64_t)blockIdx.x * wpg + wave, cfe, cbe, cpe, cpb);
     if (P.ref && !P.out_by_row && blockIdx.x == 0 && threadIdx.x == 0)
         atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
 }

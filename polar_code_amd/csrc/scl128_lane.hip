@@ -427,7 +427,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
         wave_lds_fence();
     }
     if (P.ref) {
-        flush_counts(P.counters, cfe, cbe, cpe, cpb);
+        flush_counts_p(P, blockIdx.x, cfe, cbe, cpe, cpb);
         if (blockIdx.x == 0 && threadIdx.x == 0)
             atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
     }

@@ -58,6 +58,9 @@ struct pscl_decode_params {
                                  // instead (amb_count then [NSEG * CSTRIDE]); their flags PSCL_DL_DEFERRED
     int out_by_row;              // 1: outputs, reference words and counts at LLR row fidx[b]
     int wpg_cap;                 // 0, or an upper bound on the wavefronts per workgroup (tuning knob)
+    int32_t* cpart;              // or (counting launches, P.ref): per-wavefront error counts [slots][4]
+                                 // (frame, bit, payload-frame, payload-bit errors), stored instead of
+                                 // added, summed by pscl_launch_count_reduce (no same-address atomics)
     int no_lane;                 // 1: a screening launch takes the two-lanes-per-path kernel even where
                                  // the lane-per-path one exists (PSCL_TUNE_DL_LANE)
     int64_t grid_cap;            // 0, or an upper bound on the workgroups of the launch (the
@@ -227,15 +230,20 @@ int pscl_screening_available(const pscl_decode_params& P);  // scl128.hip
 int pscl_lane_available(const pscl_decode_params& P);
 int pscl_lane_frames_per_wg(int L);
 hipError_t pscl_launch_lane(const pscl_decode_params& P, int64_t grid, hipStream_t s);
-// workgroups of a lane-per-path decode that counts errors (P.ref): each wavefront strides over
-// frames and adds its counts once at the end
+// workgroups of a decode that adds its error counts with atomics (P.ref without P.cpart): each
+// wavefront strides over frames and adds its counts once at the end (lane-per-path kernels; the
+// two-lanes-per-path kernels' workgroups hold up to PSCL_MAX_WAVES_PER_WG wavefronts)
 #ifndef PSCL_LANE_COUNT_GRID
 #define PSCL_LANE_COUNT_GRID 32768
 #endif
-// the same for the two-lanes-per-path kernels (workgroups of up to PSCL_MAX_WAVES_PER_WG wavefronts)
 #ifndef PSCL_COUNT_GRID
 #define PSCL_COUNT_GRID 8192
 #endif
+// wavefront slots of the launch pscl_launch_decode makes for P (grid x wavefronts per workgroup)
+// when its kernel can store per-wavefront counts (P.cpart), else 0
+int64_t pscl_decode_count_slots(const pscl_decode_params& P, int hist);
+// counters[FRAME_ERR, BIT_ERR, PAYLOAD_ERR, PAYLOAD_BIT] += the sums of cpart[slots][4]
+hipError_t pscl_launch_count_reduce(const int32_t* cpart, int64_t slots, int64_t* counters, hipStream_t s);
 // the DL-SCL baseline decode's screening kernel at N = 128 (PSCL_TUNE_DL_LANE default): 1 the
 // lane-per-path kernel, 2 the two-lanes-per-path one, 0 by list size (lane-per-path at L = 8)
 #ifndef PSCL_DL_LANE_DEFAULT
@@ -244,6 +252,7 @@ hipError_t pscl_launch_lane(const pscl_decode_params& P, int64_t grid, hipStream
 // scl_lane_long.hip: the lane-per-path screening decoder of the long codes (N = 256..1024, L = 4, 8)
 int pscl_lane_long_available(const pscl_decode_params& P);
 hipError_t pscl_launch_lane_long(const pscl_decode_params& P, hipStream_t s);
+int64_t pscl_lane_long_grid(const pscl_decode_params& P);
 int pscl_screening_fs_available(const pscl_decode_params& P);  // forced-bit screening (DL-SCL retries)
 hipError_t pscl_launch_decode128(const pscl_decode_params& P, int hist, int wpg, int64_t grid, int lds, hipStream_t s);
 int64_t pscl_decode_grid(const pscl_decode_params& P);

@@ -533,7 +533,7 @@ int64_t pscl_decode_grid(const pscl_decode_params& P) {
     int64_t g = (P.B + per_wg - 1) / per_wg;
     // (counting launches, P.ref: at most PSCL_COUNT_GRID workgroups, whose wavefronts stride over
     // frames and add their counts once at the end)
-    const int64_t cmax = P.ref ? PSCL_COUNT_GRID : (1 << 20);
+    const int64_t cmax = P.ref && !P.cpart ? PSCL_COUNT_GRID : (1 << 20);
     const int64_t cap = P.grid_cap > 0 && P.grid_cap < cmax ? P.grid_cap : cmax;
     return g < 1 ? 1 : (g > cap ? cap : g);
 }
@@ -572,9 +572,9 @@ hipError_t pscl_launch_decode(const pscl_decode_params& P, int hist, hipStream_t
     if (!hist && pscl_lane_available(P)) {  // one wavefront of 64 / L frames per workgroup
         const int fw = pscl_lane_frames_per_wg(P.L);
         const int64_t g = (P.B + fw - 1) / fw;
-        // (counting launches: at most PSCL_LANE_COUNT_GRID wavefronts, each adding its frames'
-        // counts with one atomic per counter when it ends)
-        const int64_t cap = P.ref ? PSCL_LANE_COUNT_GRID : (1 << 20);
+        // (counting launches with atomics: at most PSCL_LANE_COUNT_GRID wavefronts, each adding its
+        // frames' counts with one atomic per counter when it ends)
+        const int64_t cap = P.ref && !P.cpart ? PSCL_LANE_COUNT_GRID : (1 << 20);
         return pscl_launch_lane(P, g < 1 ? 1 : (g > cap ? cap : g), s);
     }
     if (pscl_decode_wpg(P) < 1) return hipErrorInvalidValue;
@@ -591,6 +591,63 @@ hipError_t pscl_launch_decode(const pscl_decode_params& P, int hist, hipStream_t
 }
 
 int pscl_decode_lds(const pscl_decode_params& P, int hist) { return decode_lds_bytes(P, hist); }
+
+int64_t pscl_decode_count_slots(const pscl_decode_params& P0, int hist) {
+    if (!P0.ref || P0.out_by_row || hist) return 0;
+    pscl_decode_params P = P0;
+    P.cpart = reinterpret_cast<int32_t*>(16);  // (the grids of a launch that stores its counts)
+    if (P.long_mode) return P.apx && pscl_lane_long_available(P) ? pscl_lane_long_grid(P) : 0;
+    if (pscl_lane_available(P)) {
+        const int fw = pscl_lane_frames_per_wg(P.L);
+        const int64_t g = (P.B + fw - 1) / fw;
+        return g < 1 ? 1 : (g > (1 << 20) ? (1 << 20) : g);
+    }
+    if (!P.fast || pscl_decode_wpg(P) < 1) return 0;  // (the generic kernel adds per frame)
+    return pscl_decode_grid(P) * pscl_decode_wpg(P);
+}
+
+namespace {
+__global__ void __launch_bounds__(256) count_reduce_kernel(const int4* __restrict__ part, int64_t n, int64_t* counters) {
+    __shared__ long long acc[4][4];
+    long long a = 0, b = 0, c = 0, d = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int4 v = part[i];
+        a += v.x;
+        b += v.y;
+        c += v.z;
+        d += v.w;
+    }
+#pragma unroll
+    for (int sft = 32; sft >= 1; sft >>= 1) {
+        a += __shfl_xor(a, sft);
+        b += __shfl_xor(b, sft);
+        c += __shfl_xor(c, sft);
+        d += __shfl_xor(d, sft);
+    }
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        acc[wave][0] = a;
+        acc[wave][1] = b;
+        acc[wave][2] = c;
+        acc[wave][3] = d;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        const long long t = acc[0][threadIdx.x] + acc[1][threadIdx.x] + acc[2][threadIdx.x] + acc[3][threadIdx.x];
+        static constexpr int idx[4] = {PSCL_CNT_FRAME_ERR, PSCL_CNT_BIT_ERR, PSCL_CNT_PAYLOAD_ERR, PSCL_CNT_PAYLOAD_BIT};
+        if (t) atomicAdd(reinterpret_cast<unsigned long long*>(counters) + idx[threadIdx.x], (unsigned long long)t);
+    }
+}
+}  // namespace
+
+hipError_t pscl_launch_count_reduce(const int32_t* cpart, int64_t slots, int64_t* counters, hipStream_t s) {
+    if (slots <= 0) return hipSuccess;
+    int64_t g = (slots + 2047) / 2048;  // ~8 slots per thread
+    if (g > 256) g = 256;
+    hipLaunchKernelGGL(count_reduce_kernel, dim3((unsigned)g), dim3(256), 0, s, reinterpret_cast<const int4*>(cpart), slots,
+                       counters);
+    return hipGetLastError();
+}
 
 // uncoded BPSK baseline: one frame per lane, kp payload symbols, errors reduced per block
 // TX chain of the long codes (N > PSCL_FAST_N): one wavefront per frame, lane w holds word w

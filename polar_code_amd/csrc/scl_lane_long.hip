@@ -488,18 +488,23 @@ __global__ void __launch_bounds__(64, PSCL_LANE_LONG_WAVES_PER_EU) scl_lane_long
         wave_lds_fence();
     }
     if (P.ref) {
-        flush_counts(P.counters, cfe, cbe, cpe, cpb);
+        flush_counts_p(P, blockIdx.x, cfe, cbe, cpe, cpb);
         if (blockIdx.x == 0 && threadIdx.x == 0)
             atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
     }
 }
 
+int64_t lane_long_grid(const pscl_decode_params& P) {
+    const int F = 64 / P.L;
+    const int64_t g0 = (P.B + F - 1) / F;
+    const int64_t cap = P.ref && !P.cpart ? PSCL_LANE_COUNT_GRID : (1 << 20);
+    return g0 < 1 ? 1 : (g0 > cap ? cap : g0);
+}
+
 template <int NL, int LMAX>
 hipError_t launch_lane_long(const pscl_decode_params& P, hipStream_t s) {
     using Ly = LongLaneLayout<NL, LMAX>;
-    const int64_t g0 = (P.B + Ly::F - 1) / Ly::F;
-    const int64_t cap = P.ref ? PSCL_LANE_COUNT_GRID : (1 << 20);
-    const int64_t grid = g0 < 1 ? 1 : (g0 > cap ? cap : g0);
+    const int64_t grid = lane_long_grid(P);
     hipLaunchKernelGGL((scl_lane_long_kernel<NL, LMAX>), dim3((unsigned)grid), dim3(64), Ly::F * Ly::FSTRIDE * 8, s, P);
     return hipGetLastError();
 }
@@ -519,6 +524,8 @@ int pscl_lane_long_available(const pscl_decode_params& P) {
     if (P.N != 256 && P.N != 512 && P.N != 1024) return 0;
     return P.K >= (P.L == 8 ? 3 : 2);
 }
+
+int64_t pscl_lane_long_grid(const pscl_decode_params& P) { return lane_long_grid(P); }
 
 hipError_t pscl_launch_lane_long(const pscl_decode_params& P, hipStream_t s) {
     if (!pscl_lane_long_available(P)) return hipErrorInvalidValue;
