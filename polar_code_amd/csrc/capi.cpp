@@ -297,8 +297,10 @@ int with_count_slots(pscl_handle* h, pscl_decode_params& P, int hist) {
     const int64_t slots = pscl_decode_count_slots(P, hist);
     if (slots <= 0) return PSCL_OK;
     void* d;
+    const size_t had = h->scratch[92].n;
     const int rc = ensure(h, 92, (size_t)slots * 16, &d);
     if (rc) return rc;
+    if (h->scratch[92].n != had) HIP_TRY(hipMemset(d, 0, h->scratch[92].n));  // (then kept zero by the reduces)
     P.cpart = (int32_t*)d;
     return PSCL_OK;
 }

@@ -41,8 +41,11 @@ using namespace pscl;
 
 // a wavefront's error counts at the end of a counting launch: stored at its slot of P.cpart, or
 // added to P.counters with one atomic per counter (flush_counts)
+// (P.cpart is all zero between launches -- zeroed when allocated and by the reduce that reads it --
+// so a wavefront without errors, most of them at the SNRs of interest, stores nothing)
 __device__ __forceinline__ void flush_counts_p(const pscl_decode_params& P, int64_t wslot, int fe, int be, int pe, int pb) {
     if (P.cpart) {
+        if (!__builtin_amdgcn_ballot_w64((fe | be | pe | pb) != 0)) return;
         fe = wave_sum(fe);
         be = wave_sum(be);
         pe = wave_sum(pe);

@@ -242,8 +242,9 @@ hipError_t pscl_launch_lane(const pscl_decode_params& P, int64_t grid, hipStream
 // wavefront slots of the launch pscl_launch_decode makes for P (grid x wavefronts per workgroup)
 // when its kernel can store per-wavefront counts (P.cpart), else 0
 int64_t pscl_decode_count_slots(const pscl_decode_params& P, int hist);
-// counters[FRAME_ERR, BIT_ERR, PAYLOAD_ERR, PAYLOAD_BIT] += the sums of cpart[slots][4]
-hipError_t pscl_launch_count_reduce(const int32_t* cpart, int64_t slots, int64_t* counters, hipStream_t s);
+// counters[FRAME_ERR, BIT_ERR, PAYLOAD_ERR, PAYLOAD_BIT] += the sums of cpart[slots][4], which it
+// leaves zero (the kernels store only the slots of wavefronts with errors)
+hipError_t pscl_launch_count_reduce(int32_t* cpart, int64_t slots, int64_t* counters, hipStream_t s);
 // the DL-SCL baseline decode's screening kernel at N = 128 (PSCL_TUNE_DL_LANE default): 1 the
 // lane-per-path kernel, 2 the two-lanes-per-path one, 0 by list size (lane-per-path at L = 8)
 #ifndef PSCL_DL_LANE_DEFAULT

@@ -607,7 +607,7 @@ int64_t pscl_decode_count_slots(const pscl_decode_params& P0, int hist) {
 }
 
 namespace {
-__global__ void __launch_bounds__(256) count_reduce_kernel(const int4* __restrict__ part, int64_t n, int64_t* counters) {
+__global__ void __launch_bounds__(256) count_reduce_kernel(int4* __restrict__ part, int64_t n, int64_t* counters) {
     __shared__ long long acc[4][4];
     long long a = 0, b = 0, c = 0, d = 0;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
@@ -616,6 +616,7 @@ __global__ void __launch_bounds__(256) count_reduce_kernel(const int4* __restric
         b += v.y;
         c += v.z;
         d += v.w;
+        if (v.x | v.y | v.z | v.w) part[i] = make_int4(0, 0, 0, 0);  // (zero for the next launch)
     }
 #pragma unroll
     for (int sft = 32; sft >= 1; sft >>= 1) {
@@ -640,11 +641,11 @@ __global__ void __launch_bounds__(256) count_reduce_kernel(const int4* __restric
 }
 }  // namespace
 
-hipError_t pscl_launch_count_reduce(const int32_t* cpart, int64_t slots, int64_t* counters, hipStream_t s) {
+hipError_t pscl_launch_count_reduce(int32_t* cpart, int64_t slots, int64_t* counters, hipStream_t s) {
     if (slots <= 0) return hipSuccess;
     int64_t g = (slots + 2047) / 2048;  // ~8 slots per thread
     if (g > 256) g = 256;
-    hipLaunchKernelGGL(count_reduce_kernel, dim3((unsigned)g), dim3(256), 0, s, reinterpret_cast<const int4*>(cpart), slots,
+    hipLaunchKernelGGL(count_reduce_kernel, dim3((unsigned)g), dim3(256), 0, s, reinterpret_cast<int4*>(cpart), slots,
                        counters);
     return hipGetLastError();
 }
