@@ -388,7 +388,8 @@ def extra_configs(args, ctx: Ctx, orc: Oracle | None):
                "steps": args.extra_steps, "frames_per_gpu_per_step": args.frames,
                "main_stream_kernel_ms_per_step": r["kern_ms"] / args.extra_steps, "main_stream_launches": r["launches"],
                "side_stream_kernel_ms_per_step": r["side_ms"] / args.extra_steps, "side_stream_launches": r["side_launches"],
-               "kernel": ("scl128_kernel<4> screening + exact re-decode (pipelined)" if name.startswith("config2") else
+               "kernel": ("scl_lane_kernel<4> screening + scl128_kernel<4> exact re-decode (pipelined)"
+                          if name.startswith("config2") else
                           "scl128_kernel<4> baseline + scl128_kernel<4,FS> warm-started retry decodes + dl_post_kernel"
                           " rounds" if name.startswith("config4") else
                           "scl128_kernel<8,CH,CODE=2> screening (de-rate-match in staging) + exact re-decode"
@@ -434,7 +435,7 @@ def extra_roofline(r: dict, steps: int) -> dict:
     e, why = pmc_entry(wkey, r["build_hash"])
     return {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
             "traffic": float(e["hbm_bytes_per_launch"]) if e and "hbm_bytes_per_launch" in e else None,
-            "kernel": "scl128_kernel screening pass" if not r["retries"] else "scl128_kernel baseline decode",
+            "kernel": (dominant_kernel(N, K, L, r["E"], r["retries"])),
             "avg_launch_ms": dom_ms, "bytes_per_frame": fb, "pmc": why or "matched build",
             "compute": compute_roofline(e, B, dom_ms) if e and "valu_instr_per_frame" in e else None,
             "compute_algorithmic": compute_algorithmic(N, K, L, B, dom_ms),
@@ -492,6 +493,18 @@ def launch_ranks(n: int) -> int:
         sys.stderr.write(f"bench.py: rank(s) failed: {failed}\n")
         return 1
     return 0
+
+
+def dominant_kernel(N, K, L, E, retries):
+    """The kernel the step's dominant launch runs (pscl_launch_decode's choice for a plain or
+    DL-SCL baseline decode of this configuration)."""
+    if N == 128 and K == 64 and not E and (L == 8 or (L == 4 and not retries)):
+        return f"scl_lane_kernel<{L}> screening pass" + (" (DL-SCL baseline)" if retries else "")
+    if N == 128 and L <= 8:
+        return f"scl128_kernel<{L}> " + ("baseline decode" if retries else "screening pass")
+    if N > 128 and L in (4, 8) and not E and not retries:
+        return f"scl_lane_long_kernel<N={N},{L}> screening pass"
+    return "scl_long_kernel" if N > 128 else "scl_decode_kernel"
 
 
 def config3_sweep(args, ctx: Ctx):
@@ -659,7 +672,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS,
                          "traffic": traffic,
-                         "kernel": "scl128_kernel" if N == 128 and L <= 8 else "scl_decode_kernel",
+                         "kernel": dominant_kernel(N, K, L, E, args.retries),
                          "timed": ("screening launch (pipelined: each step's exact re-decode of its deferred "
                                    "frames overlaps the next step's screening)" if r["pipelined"] else
                                    "decode launches of a step"),

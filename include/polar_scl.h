@@ -256,13 +256,14 @@ int pscl_memcpy_dtoh(pscl_handle* h, void* dst, const void* d_src, int64_t bytes
 int pscl_memset_device(pscl_handle* h, void* d_dst, int value, int64_t bytes);
 
 /*
- * Screening decode (default on).  Plain decodes of the compiled-in N = 128 codes (no metrics,
- * candidates, decision LLRs, path counts, forced bits) run a screening pass whose path metrics
- * carry a proven relative error below 2^-41 (log1p by a truncated atanh series instead of
- * glibc's log1p); every list ordering it decides must clear a margin of 2^16 ulps, and frames
- * where one does not are re-decoded by the exact kernel.  Decoded bits, CRC flags and best
- * indices are identical to the exact decode (decode_scl, dl_scl_polar/polar/scl.py:108-209).
- * enable = 0 runs the exact kernel only.
+ * Screening decode (default on).  Plain decodes (no metrics, candidates, decision LLRs, path
+ * counts, forced bits) of the compiled-in N = 128 codes and of the long codes (N = 256..1024 at
+ * L = 4, 8) run a screening pass whose path metrics carry a tail log1p(exp(-|v|)) with a
+ * measured absolute error bound (fp32 exp2/log2; the bound checked exhaustively over every fp32
+ * input on the device); every list ordering it decides must clear a margin of twice the N-term
+ * metric error bound, and frames where one does not are re-decoded by the exact kernel.  Decoded
+ * bits, CRC flags and best indices are identical to the exact decode (decode_scl,
+ * dl_scl_polar/polar/scl.py:108-209).  enable = 0 runs the exact kernel only.
  */
 int pscl_set_screening(pscl_handle* h, int enable);
 
