@@ -72,6 +72,9 @@ def parse():
                     help="NR config 5: (128,88) = 64 payload + CRC-24 bits, rate matched to E transmitted "
                          "bits (run_ber_sweep.py nr_polar_scl); the TX kernel interleaves/repeats, the "
                          "decoder de-rate-matches in its channel staging")
+    ap.add_argument("--tune", type=str, default="",
+                    help="schedule knobs of the bench's decode handle, k=v[,k=v] (pscl_set_tuning: dl_screen, "
+                         "dl_chunks, dl_split, side_priority, post_grid, retry_wpg, dl_lane); A/B tools only")
     ap.add_argument("--extra", choices=["auto", "none"], default="auto",
                     help="auto: also time BASELINE configs 2, 4, 5 (extra_configs) after the headline")
     ap.add_argument("--extra-steps", type=int, default=10)
@@ -273,6 +276,9 @@ class Ctx:
             self.dist.barrier()
 
 
+TUNE: dict = {}  # --tune
+
+
 def run_workload(ctx: Ctx, *, L: int, E: int, retries: int, beta, B: int, steps: int, warmup: int, ebno: float,
                  seed: int, keep_buffers: bool = False):
     """Generate the batches on the device, run W untimed + K timed steps (barrier and
@@ -287,6 +293,8 @@ def run_workload(ctx: Ctx, *, L: int, E: int, retries: int, beta, B: int, steps:
     dec = _native.Decoder(N, info, L, POLY, device=ctx.device_index)
     if E:
         dec.set_rate_match(E)
+    if TUNE:
+        dec.set_tuning(**TUNE)
     n_in = E or N
     stream = torch.cuda.current_stream(dev)
     dec.set_stream(stream.cuda_stream)
@@ -560,6 +568,8 @@ def config3_sweep(args, ctx: Ctx):
 
 def main():
     args = parse()
+    if args.tune:
+        TUNE.update({k: int(v) for k, v in (kv.split("=") for kv in args.tune.split(","))})
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -665,7 +675,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: on-device Philox4x32 BPSK/AWGN frames (payload->CRC24->polar->LLR), resident in HBM",
-            "config": {"workload": workload, "retries": args.retries, "E": E or None,
+            "config": {"workload": workload, "retries": args.retries, "E": E or None, **({"tuning": TUNE} if TUNE else {}),
                        "N": N, "K": K, "list_size": L, "ebno_db": args.ebno, "frames_per_gpu_per_step": B,
                        "global_batch": B * world, "parallelism": f"frame-sharded x{world}",
                        "collective": dist.get_backend() if dist else None},
