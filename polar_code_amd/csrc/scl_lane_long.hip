@@ -53,6 +53,11 @@ struct LongLaneLayout {
 #ifndef PSCL_LANE_LONG_WAVES_PER_EU
 #define PSCL_LANE_LONG_WAVES_PER_EU 2
 #endif
+// N = 1024: the element recompute holds 64 channel LLRs (128 VGPRs); at 2 waves/SIMD (256 VGPRs)
+// it spills ~120 dwords, at 1 (512) none -- LDS allows 6 wavefronts per CU either way
+#ifndef PSCL_LANE_LONG1024_WAVES_PER_EU
+#define PSCL_LANE_LONG1024_WAVES_PER_EU 2
+#endif
 
 // word k of the register array u, k wave-uniform
 template <int NW>
@@ -64,7 +69,8 @@ __device__ __forceinline__ uint64_t uword(const uint64_t (&u)[NW], int k) {
 }
 
 template <int NL, int LMAX>
-__global__ void __launch_bounds__(64, PSCL_LANE_LONG_WAVES_PER_EU) scl_lane_long_kernel(const pscl_decode_params P) {
+__global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU : PSCL_LANE_LONG_WAVES_PER_EU)
+    scl_lane_long_kernel(const pscl_decode_params P) {
     static_assert(LMAX == 4 || LMAX == 8, "the lane-per-path decoder is built for L = 4 and 8");
     static_assert(NL >= 8 && NL <= 10, "N = 256 .. 1024");
     using Ly = LongLaneLayout<NL, LMAX>;
