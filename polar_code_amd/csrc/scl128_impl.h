@@ -199,6 +199,10 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 #define PSCL_TAIL_NC 1
 #endif
 
+// diagnostic builds only: the history instances with the aggregated counters
+#ifndef PSCL_HIST_AGG
+#define PSCL_HIST_AGG 0
+#endif
 #ifndef PSCL_WAVES_PER_EU
 #define PSCL_WAVES_PER_EU 4
 #endif
@@ -953,7 +957,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
                 if (P.flags) P.flags[fo] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
                 if (P.n_paths) P.n_paths[fo] = cnt;
                 if (P.ref && !(APX && PSCL_APX_ABLATE)) {  // (ablation timings: wrong frames, no counts)
-                    if constexpr (HIST) {
+                    if constexpr (HIST && !PSCL_HIST_AGG) {
                         // (the history instances keep per-frame atomics: their register budget is
                         // spent -- four more live counters spill further, and the rate-matched L = 8
                         // history instance then measured wrong decision LLRs)
@@ -968,7 +972,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU)
         }
         wave_lds_fence();
     }
-    if constexpr (!HIST)
+    if constexpr (!HIST || PSCL_HIST_AGG)
         if (P.ref) flush_counts_p(P, (int64_t)blockIdx.x * wpg + wave, cfe, cbe, cpe, cpb);
     if (P.ref && !P.out_by_row && blockIdx.x == 0 && threadIdx.x == 0)
         atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
