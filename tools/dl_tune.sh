@@ -11,6 +11,6 @@ for r in $(seq 1 $rounds); do
     i=$((i + 1))
     tn=""; [ "$cfg" != "-" ] && tn="--tune $cfg"
     timeout -k 10 200 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --extra none --list 4 --retries 8 $DLT_ARGS $tn > gpurun_out/dltune/$i.$r.log 2>&1 || { echo "[$cfg] failed"; tail -5 gpurun_out/dltune/$i.$r.log; exit 1; }
-    echo "[$cfg] $(grep '^{' gpurun_out/dltune/$i.$r.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms_per_step"],3), d["dl_scl"]["frame_errors"] if d.get("dl_scl") else None, d["parity"]["mismatches"])')"
+    echo "[$cfg] $(grep '^{' gpurun_out/dltune/$i.$r.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms_per_step"],3), d["dl_scl"]["frame_errors"] if d.get("dl_scl") else None, (d.get("parity") or {}).get("mismatches"))')"
   done
 done
