@@ -75,11 +75,14 @@ int pscl_screening_fs_available(const pscl_decode_params& P) {
 }
 
 // the screening launch of this plain decode runs the lane-per-path kernel (scl128_lane.hip):
-// the (128,64) code, L = 8 (and L = 4 unless PSCL_LANE4 = 0), plain channel rows
+// the (128,64) code on plain channel rows or the NR (128,88) code on rate-matched rows
+// (PSCL_LANE_NR), L = 8 (and L = 4 unless PSCL_LANE4 = 0)
 int pscl_lane_available(const pscl_decode_params& P) {
-    if (!PSCL_LANE || !P.apx || P.no_lane || P.force || P.sc_hard || P.rm_E || P.fidx || P.d_count || P.elist) return 0;
+    if (!PSCL_LANE || !P.apx || P.no_lane || P.force || P.sc_hard || P.fidx || P.d_count || P.elist) return 0;
     if (P.L != 8 && (P.L != 4 || !PSCL_LANE4)) return 0;
-    return P.N == 128 && spec_code(P) == 1;
+    if (P.N != 128) return 0;
+    const int code = spec_code(P);
+    return (code == 1 && !P.rm_E) || (code == 2 && P.rm_E && PSCL_LANE_NR);
 }
 
 int pscl_screening_available(const pscl_decode_params& P) {

@@ -84,7 +84,11 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
         const int64_t fi = f0 + fl;
         const bool fvalid = fi < P.B;
         const int64_t frow = fvalid ? fi : f0;  // (a tail wave's empty slots decode a copy of frame f0)
-        const double* chan = P.llr + frow * kN;
+        // CODE = 2 (the NR (128,88) code, config 5): the input rows are rate matched -- E received
+        // LLRs, de-rate-matched and de-interleaved per position as the values are loaded
+        constexpr bool RM = CODE == 2;
+        const double* chan = P.llr + frow * (RM ? (int64_t)P.rm_E : (int64_t)kN);
+        auto chan_at = [&](int i) -> double { return RM ? nr_stage(chan, P.rm_src[i], P.rm_E, kN) : chan[i]; };
         // the frame's channel LLRs in registers: the lane's depth-3 elements e_k = p + G k (k < EPL)
         // need c[8 k + m] = chan[e_k + 16 m] -- the same at all 8 depth-1..3 recomputes
         // (CREG = false, an L = 4 build option: the 32 values are re-read from the L2-resident row at
@@ -95,7 +99,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
 #pragma unroll
             for (int k = 0; k < EPL; ++k)
 #pragma unroll
-                for (int m = 0; m < 8; ++m) c[8 * k + m] = chan[p + G * k + 16 * m];
+                for (int m = 0; m < 8; ++m) c[8 * k + m] = chan_at(p + G * k + 16 * m);
         };
         load_chan();
         // frames whose channel magnitudes could overflow the fp64 metric sums or carry a NaN go to
@@ -440,12 +444,16 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
 int pscl_lane_frames_per_wg(int L) { return 64 / L; }
 
 hipError_t pscl_launch_lane(const pscl_decode_params& P, int64_t grid, hipStream_t s) {
-    if (P.L == 8)
-        hipLaunchKernelGGL((scl_lane_kernel<8, 1>), dim3((unsigned)grid), dim3(64),
-                           LaneLayout<8>::F * LaneLayout<8>::FSTRIDE * 8, s, P);
+    // (pscl_lane_available: the (128,64) code on plain rows, or the rate-matched NR (128,88) code)
+    const int lds8 = LaneLayout<8>::F * LaneLayout<8>::FSTRIDE * 8, lds4 = LaneLayout<4>::F * LaneLayout<4>::FSTRIDE * 8;
+    if (P.L == 8 && !P.rm_E)
+        hipLaunchKernelGGL((scl_lane_kernel<8, 1>), dim3((unsigned)grid), dim3(64), lds8, s, P);
+    else if (P.L == 8)
+        hipLaunchKernelGGL((scl_lane_kernel<8, 2>), dim3((unsigned)grid), dim3(64), lds8, s, P);
+    else if (P.L == 4 && !P.rm_E)
+        hipLaunchKernelGGL((scl_lane_kernel<4, 1>), dim3((unsigned)grid), dim3(64), lds4, s, P);
     else if (P.L == 4)
-        hipLaunchKernelGGL((scl_lane_kernel<4, 1>), dim3((unsigned)grid), dim3(64),
-                           LaneLayout<4>::F * LaneLayout<4>::FSTRIDE * 8, s, P);
+        hipLaunchKernelGGL((scl_lane_kernel<4, 2>), dim3((unsigned)grid), dim3(64), lds4, s, P);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();

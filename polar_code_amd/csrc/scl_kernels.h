@@ -224,6 +224,9 @@ int pscl_screening_available(const pscl_decode_params& P);  // scl128.hip
 #ifndef PSCL_LANE
 #define PSCL_LANE 1
 #endif
+#ifndef PSCL_LANE_NR
+#define PSCL_LANE_NR 1
+#endif
 #ifndef PSCL_LANE4
 #define PSCL_LANE4 1
 #endif
