@@ -290,17 +290,18 @@ void fill_decode_params(const pscl_handle* h, pscl_decode_params& P, int hist) {
 }
 
 // a counting decode (P.ref) whose kernel stores per-wavefront counts: their buffer (scratch slot 92,
-// reused by every such launch of the handle: each is followed on its stream by its count-reduce
-// launch; the DL-SCL and pipelined paths launch decodes of one handle on one stream in order)
-int with_count_slots(pscl_handle* h, pscl_decode_params& P, int hist) {
+// or 92 + parity for a pipelined plain decode, whose reduce runs on the side stream after its
+// re-decode and is ordered before the buffer's next use by ev_px; every other launch is followed
+// on its own stream by its count-reduce launch)
+int with_count_slots(pscl_handle* h, pscl_decode_params& P, int hist, int slot) {
     P.cpart = nullptr;
     const int64_t slots = pscl_decode_count_slots(P, hist);
     if (slots <= 0) return PSCL_OK;
     void* d;
-    const size_t had = h->scratch[92].n;
-    const int rc = ensure(h, 92, (size_t)slots * 16, &d);
+    const size_t had = h->scratch[slot].n;
+    const int rc = ensure(h, slot, (size_t)slots * 16, &d);
     if (rc) return rc;
-    if (h->scratch[92].n != had) HIP_TRY(hipMemset(d, 0, h->scratch[92].n));  // (then kept zero by the reduces)
+    if (h->scratch[slot].n != had) HIP_TRY(hipMemset(d, 0, h->scratch[slot].n));  // (then kept zero by the reduces)
     P.cpart = (int32_t*)d;
     return PSCL_OK;
 }
@@ -374,9 +375,10 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
         pscl_decode_layout(S, hist);  // (no exp table in LDS)
         S.amb_list = (int64_t*)d_list;
         S.amb_count = (int32_t*)d_cnt;
-        if ((rc = with_count_slots(h, S, hist))) return rc;
+        // (pipelined: the count buffers alternate with the call parity, and the reduce runs on the
+        // side stream after the re-decode, off the handle's stream)
+        if ((rc = with_count_slots(h, S, hist, pipe ? 92 + p : 92))) return rc;
         err = pscl_launch_decode(S, hist, st);
-        if (err == hipSuccess && S.cpart) err = pscl_launch_count_reduce(S.cpart, pscl_decode_count_slots(S, hist), S.counters, st);
         h->screened = true;
         h->screened_slot = s_cnt;
 #ifdef PSCL_APX_ABLATE
@@ -386,6 +388,8 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
 #else
         constexpr bool screen_only = false;  // the shipped library always re-decodes deferred frames
 #endif
+        if (err == hipSuccess && S.cpart && (!pipe || screen_only))
+            err = pscl_launch_count_reduce(S.cpart, pscl_decode_count_slots(S, hist), S.counters, st);
         if (err == hipSuccess && !screen_only) {
             pscl_decode_params X = P;  // exact decode of the listed frames, outputs at their rows
             X.fidx = (const int64_t*)d_list;
@@ -401,6 +405,8 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
                 HIP_TRY(hipEventRecord(h->ev_pscr[p], st));
                 HIP_TRY(hipStreamWaitEvent(h->pipe_stream, h->ev_pscr[p], 0));
                 err = pscl_launch_decode(X, hist, h->pipe_stream);
+                if (err == hipSuccess && S.cpart)
+                    err = pscl_launch_count_reduce(S.cpart, pscl_decode_count_slots(S, hist), S.counters, h->pipe_stream);
                 if (err != hipSuccess) return fail(PSCL_EDEVICE, "decode kernel launch: %s", hipGetErrorString(err));
                 HIP_TRY(hipEventRecord(h->ev_px[p], h->pipe_stream));
                 h->px_pending[p] = true;
@@ -409,7 +415,7 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
             err = pscl_launch_decode(X, hist, st);
         }
     } else {
-        const int rc = with_count_slots(h, P, hist);
+        const int rc = with_count_slots(h, P, hist, 92);
         if (rc) return rc;
         err = pscl_launch_decode(P, hist, st);
         if (err == hipSuccess && P.cpart) err = pscl_launch_count_reduce(P.cpart, pscl_decode_count_slots(P, hist), P.counters, st);
