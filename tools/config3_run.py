@@ -2,7 +2,7 @@
 4.0-6.5 dB, 10^6 frames per point, after an untimed 4.0-4.5 dB warm-up at another seed; prints the
 wall time of the timed pass (for rocprofv3 traces of the product path).
 
-    python tools/config3_run.py [frames] [lo] [hi]
+    python tools/config3_run.py [frames] [lo] [hi] [k=v,k=v]   (handle tuning knobs, A/B only)
 """
 import contextlib
 import io
@@ -20,6 +20,11 @@ from polar_code_amd.eval import run_fer_sweep as rfs  # noqa: E402
 frames = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 lo = float(sys.argv[2]) if len(sys.argv) > 2 else 4.0
 hi = float(sys.argv[3]) if len(sys.argv) > 3 else 6.5
+tune = dict((k, int(v)) for k, v in (kv.split("=") for kv in sys.argv[4].split(","))) if len(sys.argv) > 4 else {}
+if tune:  # the sweep's cached handle (run_fer_sweep: get_decoder(N, info, M, crc, device))
+    from polar_code_amd import _native
+    from polar_code_amd.polar.polar import construct_info_set
+    _native.get_decoder(128, construct_info_set(128, 64), 8, "0x1864CFB", 0).set_tuning(**tune)
 
 
 def run(a_lo, a_hi, seed, td):
@@ -38,5 +43,5 @@ def run(a_lo, a_hi, seed, td):
 with tempfile.TemporaryDirectory() as td:
     run(4.0, 4.5, 1, td)
     rows, t = run(lo, hi, 0, td)
-print(f"config 3 sweep {lo:g}-{hi:g} dB: {len(rows)} points x {frames} frames in {t * 1e3:.2f} ms = "
+print(f"config 3 sweep {lo:g}-{hi:g} dB{' ' + str(tune) if tune else ''}: {len(rows)} points x {frames} frames in {t * 1e3:.2f} ms = "
       f"{len(rows) * frames / t / 1e6:.1f} M frames/s", flush=True)
