@@ -733,7 +733,8 @@ int pscl_set_pipelined(pscl_handle* h, int enable) {
 
 int pscl_set_tuning(pscl_handle* h, int knob, int64_t value) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
-    static const int64_t lim[PSCL_TUNE_COUNT][2] = {{0, 0}, {0, 1}, {0, 64}, {0, 2}, {0, 1}, {0, 4096}, {0, PSCL_MAX_WAVES_PER_WG}, {0, 2}};
+    static const int64_t lim[PSCL_TUNE_COUNT][2] = {{0, 0}, {0, 2}, {0, 64}, {0, 2}, {0, 1}, {0, 4096}, {0, PSCL_MAX_WAVES_PER_WG}, {0, 2},
+                                                    {0, (int64_t)1 << 30}};
     if (knob < 1 || knob >= PSCL_TUNE_COUNT) return fail(PSCL_EINVAL, "unknown tuning knob %d", knob);
     if (value < lim[knob][0] || value > lim[knob][1] || (knob == PSCL_TUNE_POST_GRID && value && value < 16))
         return fail(PSCL_EINVAL, "tuning knob %d: value %lld out of range", knob, (long long)value);
@@ -886,7 +887,13 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     // bucket lists of their own (flags PSCL_DL_DEFERRED, which the post pass skips); on the side
     // stream the exact kernel decodes those (warm-started, as every retry decode) and a second
     // post pass handles them, overlapping the main post pass
-    const bool dl_screen = h->tune[PSCL_TUNE_DL_SCREEN] == 1;
+    // screening retry decodes: always (1), never (2), or for chains of many entries (0): at low SNR
+    // the rounds are throughput-bound and the screening decode's ~4x cheaper frames win (config 3,
+    // 4.0 dB point: 10.5 -> 9.0 ms); with few entries the exact decode of the deferred ones is one
+    // more latency per round (5.0 dB: 5.6 -> 6.1 ms), DESIGN.md §5.1b
+    const int64_t ds = h->tune[PSCL_TUNE_DL_SCREEN];
+    const int64_t ds_min = h->tune[PSCL_TUNE_DL_SCREEN_MIN] ? h->tune[PSCL_TUNE_DL_SCREEN_MIN] : PSCL_DL_SCREEN_MIN;
+    const bool dl_screen = ds == 1 || (ds == 0 && A >= ds_min);
     const bool scr = dl_screen && h->screen && S.dcnt && S.ob2 && side && pscl_screening_fs_available(H);
     pscl_decode_params HA, HX;
     pscl_post_params QD;
