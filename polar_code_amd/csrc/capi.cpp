@@ -734,7 +734,7 @@ int pscl_set_pipelined(pscl_handle* h, int enable) {
 int pscl_set_tuning(pscl_handle* h, int knob, int64_t value) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
     static const int64_t lim[PSCL_TUNE_COUNT][2] = {{0, 0}, {0, 2}, {0, 64}, {0, 2}, {0, 1}, {0, 4096}, {0, PSCL_MAX_WAVES_PER_WG}, {0, 2},
-                                                    {0, (int64_t)1 << 30}};
+                                                    {0, (int64_t)1 << 30}, {0, 2}};
     if (knob < 1 || knob >= PSCL_TUNE_COUNT) return fail(PSCL_EINVAL, "unknown tuning knob %d", knob);
     if (value < lim[knob][0] || value > lim[knob][1] || (knob == PSCL_TUNE_POST_GRID && value && value < 16))
         return fail(PSCL_EINVAL, "tuning knob %d: value %lld out of range", knob, (long long)value);
@@ -892,7 +892,8 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     // 4.0 dB point: 10.5 -> 9.0 ms); with few entries the exact decode of the deferred ones is one
     // more latency per round (5.0 dB: 5.6 -> 6.1 ms), DESIGN.md §5.1b
     const int64_t ds = h->tune[PSCL_TUNE_DL_SCREEN];
-    const int64_t ds_min = h->tune[PSCL_TUNE_DL_SCREEN_MIN] ? h->tune[PSCL_TUNE_DL_SCREEN_MIN] : PSCL_DL_SCREEN_MIN;
+    const int64_t ds_min = h->tune[PSCL_TUNE_DL_SCREEN_MIN] ? h->tune[PSCL_TUNE_DL_SCREEN_MIN]
+                                                            : (h->L >= 8 ? PSCL_DL_SCREEN_MIN8 : PSCL_DL_SCREEN_MIN);
     const bool dl_screen = ds == 1 || (ds == 0 && A >= ds_min);
     const bool scr = dl_screen && h->screen && S.dcnt && S.ob2 && side && pscl_screening_fs_available(H);
     pscl_decode_params HA, HX;
@@ -903,6 +904,7 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
         pscl_decode_layout(HA, 0);  // (no exp table in LDS)
         HA.amb_elist = S.dlist;
         HA.amb_count = S.dcnt;
+        HA.no_lane = h->tune[PSCL_TUNE_DL_RETRY_LANE] == 2 ? 1 : 0;  // (lane-per-path FS kernel by default)
         HX = H;
         HX.elist = S.dlist;
         HX.bcount = S.dcnt;

@@ -85,6 +85,15 @@ int pscl_lane_available(const pscl_decode_params& P) {
     return (code == 1 && !P.rm_E) || (code == 2 && P.rm_E && PSCL_LANE_NR);
 }
 
+// a screened DL-SCL retry round (bucket lists, forced bits, warm start, deferred entries to
+// bucket lists of their own) of the (128,64) code at L = 4, 8 runs the lane-per-path FS kernel
+int pscl_lane_fs_available(const pscl_decode_params& P) {
+    if (!PSCL_LANE_FS || !P.apx || P.no_lane || !P.force || P.sc_hard || !P.elist || !P.amb_elist || !P.fidx) return 0;
+    if (!P.warm_metric || !P.warm_u || P.d_count || P.ref || P.rm_E || P.N != 128 || P.out_by_row) return 0;
+    if (P.L != 8 && P.L != 4) return 0;
+    return spec_code(P) == 1;
+}
+
 int pscl_screening_available(const pscl_decode_params& P) {
     if (!P.fast || P.force || P.sc_hard || P.L != pscl_decode_lmax(P.L)) return 0;
     const int code = spec_code(P);

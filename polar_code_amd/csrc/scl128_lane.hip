@@ -60,7 +60,17 @@ struct LaneLayout {
 #define PSCL_LANE_WAVES_PER_EU 2
 #endif
 
-template <int LMAX, int CODE>
+// FS: the DL-SCL retry decodes (dlscl.hip, capi.cpp dl_retry_chunk) -- a round's entries read
+// bucket by bucket (P.elist), LLR rows by indirection (P.fidx), forced information bits (P.force:
+// the reference bits below the flip index, the flipped bit at it, scl.py:146-161) and the warm
+// start at the first 16-phase segment of the wavefront's bucket (P.warm_metric / P.warm_u, the
+// forced prefix's exact metric and bits written by the post pass).  The list of a frame then
+// grows from one path at its own phases: each frame carries its live-path count (lcnt = log2),
+// and an information phase is, per frame, forced (the single path takes the forced child, no
+// ordering decision), growing (every child survives) or full (the keep / one-swap / ranked
+// tiers, their certificates restricted to the full frames).  Frames it cannot certify go to
+// the deferred bucket lists (P.amb_elist, flags PSCL_DL_DEFERRED) for the exact FS kernel.
+template <int LMAX, int CODE, bool FS = false>
 __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(const pscl_decode_params P) {
     static_assert(LMAX == 4 || LMAX == 8, "the lane-per-path decoder is built for L = 4 and 8");
     using Ly = LaneLayout<LMAX>;
@@ -80,10 +90,27 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
     auto hiw_up = [&](double m) { return hiw(__builtin_fma(m, 1.0 + 0x1p-40, PSCL_TAIL_ABS_MARGIN)); };
 
     int cfe = 0, cbe = 0, cpe = 0, cpb = 0;  // this lane's error counts (flushed at the end)
-    for (int64_t f0 = (int64_t)blockIdx.x * F; f0 < P.B; f0 += (int64_t)gridDim.x * F) {
+    // frames of the launch: P.B, or (FS) the total of the round's bucket lists
+    int bpre[PSCL_DL_NSEG + 1];
+    int64_t Bn = P.B;
+    if constexpr (FS) {
+        const int64_t tot = pscl_bucket_prefix(P.bcount, P.bcap, bpre);
+        Bn = tot < P.B ? tot : P.B;
+    }
+    for (int64_t f0 = (int64_t)blockIdx.x * F; f0 < Bn; f0 += (int64_t)gridDim.x * F) {
         const int64_t fi = f0 + fl;
-        const bool fvalid = fi < P.B;
-        const int64_t frow = fvalid ? fi : f0;  // (a tail wave's empty slots decode a copy of frame f0)
+        const bool fvalid = fi < Bn;
+        const int64_t fsafe = fvalid ? fi : f0;  // (a tail wave's empty slots decode a copy of frame f0)
+        // FS: f = the entry id (force words, warm state, outputs), frow = its LLR row; seg0 = the
+        // warm-start segment (wave-uniform: the bucket of the wavefront's first entry -- later
+        // entries sit in the same or a later bucket, so every frame is still forced there)
+        int64_t f = fi, frow = fsafe;
+        int seg0 = 0;
+        if constexpr (FS) {
+            f = pscl_elist_entry(P, fsafe, bpre);
+            seg0 = pscl_bucket_of(f0, bpre);
+            frow = P.fidx[f];
+        }
         // CODE = 2 (the NR (128,88) code, config 5): the input rows are rate matched -- E received
         // LLRs, de-rate-matched and de-interleaved per position as the values are loaded
         constexpr bool RM = CODE == 2;
@@ -114,6 +141,30 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
         uint64_t u0 = 0, u1 = 0;  // decided bits
         uint32_t tab = 0;          // LDS slot of depths 3..6 (4 bits each)
         uint32_t lastbit = 0;      // the bit decided at the previous phase
+        uint64_t fm0 = 0, fm1 = 0, fv0 = 0, fv1 = 0;  // FS: force mask and values (information bits)
+        int lcnt = 0;                                 // FS: log2 of the frame's live paths
+        if constexpr (FS) {
+            const uint64_t* fr = P.force + f * 2 * PW;
+            fm0 = fr[0];
+            fv0 = fr[PW];
+            if (PW > 1) {
+                fm1 = fr[1];
+                fv1 = fr[PW + 1];
+            }
+            // warm start at phase 16 seg0: one path, its exact metric and bits below that phase
+            if (seg0 > 0) {
+                metric = P.warm_metric[f * PSCL_DL_NSEG + seg0];
+                const int lo = 16 * seg0;
+                u0 = P.warm_u[2 * f];
+                u1 = P.warm_u[2 * f + 1];
+                if (lo < 64) {
+                    u0 &= (1ULL << lo) - 1ULL;
+                    u1 = 0;
+                } else {
+                    u1 = lo == 64 ? 0ULL : (u1 & ((1ULL << (lo - 64)) - 1ULL));
+                }
+            }
+        }
 
         auto phase = [&](auto PC) {
             constexpr int phi = decltype(PC)::value;
@@ -158,7 +209,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
 #pragma unroll
                     for (int s2 = 0; s2 < 2; ++s2) d2s[h][s2] = shared2 ? f_minsum(d1l[h][s2], d1l[h][s2 + 2]) : 0.0;
                 }
-                constexpr int npaths = cnt;
+                constexpr int npaths = FS ? LMAX : cnt;  // (FS: the frames' list sizes differ)
 #pragma unroll
                 for (int q0 = 0; q0 < npaths; ++q0) {
                     // lane p takes path (q0 + p) mod L: the 8 lanes' stores hit 8 distinct bank groups
@@ -243,6 +294,97 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
             // information phase: better child (along the LLR sign) mg, worse child mb
             const double mg = metric + Lt, mb = mg + fabs(lam);
             const uint32_t gbit = sign_bit(lam);
+            if constexpr (FS) {
+                // per frame: forced, growing or full (frame-uniform); the own child first, then the
+                // lanes that take another path's child pull it in one exchange
+                const uint64_t fmw = jb < 64 ? fm0 : fm1, fvw = jb < 64 ? fv0 : fv1;
+                const bool forced = ((fmw >> (jb & 63)) & 1ULL) != 0;
+                const uint32_t fbit = (uint32_t)((fvw >> (jb & 63)) & 1ULL);
+                const bool full = !forced && lcnt == LOG_G, grow = !forced && lcnt < LOG_G;
+                const int cntf = 1 << lcnt;
+                const double m1 = gbit ? mg : mb;  // the bit-1 child
+                double nm = forced ? (fbit == gbit ? mg : mb) : (grow ? (gbit ? mb : mg) : mg);
+                uint32_t b = forced ? fbit : (grow ? 0u : gbit);
+                // growing: bit-1 children to lanes cnt..2cnt-1
+                bool pull = grow && (p & cntf) != 0;
+                int src = grow ? gbase + (p & (cntf - 1)) : lane;
+                const uint64_t fullm = wmask(full) & vmask;
+                const uint32_t kgu = hiw_up(mg), kb = hiw(mb);
+                const uint32_t mx = frame_max<G>(kgu);
+                const bool bad = kb <= mx;
+                const uint64_t badm = wmask(bad);
+                if ((badm & fullm) != 0) {  // some full frame has a worse child within the margin
+                    const uint32_t sh = (uint32_t)gbase & 31u;
+                    const uint32_t bad8 = ((fl < F / 2 ? (uint32_t)badm : (uint32_t)(badm >> 32)) >> sh) & GM;
+                    if ((wmask(__builtin_popcount(bad8) > 1) & fullm) == 0) {
+                        // one swap per full frame at most (see the plain form below)
+                        const uint32_t kg = hiw(mg);
+                        const uint32_t gmaxh = frame_max<G>(kg);
+                        const bool ismax = kg == gmaxh;
+                        const uint32_t nmax = frame_sum<G>(ismax ? 1u : 0u);
+                        const uint32_t g2u = frame_max<G>(ismax ? 0u : kgu);
+                        const uint32_t wu = frame_max<G>(bad ? hiw_up(mb) : 0u);
+                        const bool swap = bad8 != 0;
+                        amb |= wmask(full && swap && !(nmax == 1u && g2u < gmaxh && wu < gmaxh)) & vmask;
+                        if (full && swap && ismax) {
+                            pull = true;
+                            src = (gbase + (int)__builtin_ctz(bad8 | (1u << G))) & 63;
+                        }
+                    } else {
+                        // rank the 2L children of each frame (see the plain form below)
+                        const uint32_t kg = hiw(mg);
+                        uint32_t rg = 0, rb = kg < kb ? 1u : 0u;
+                        rank_pair<kQX1>(kg, kb, kg, kb, rg, rb);
+                        rank_pair<kQX2>(kg, kb, kg, kb, rg, rb);
+                        rank_pair<kQX3>(kg, kb, kg, kb, rg, rb);
+                        if constexpr (G == 8) {
+                            const uint32_t mkg = dpp32<kHMIR>(kg), mkb = dpp32<kHMIR>(kb);
+                            rank_pair<kQID>(mkg, mkb, kg, kb, rg, rb);
+                            rank_pair<kQX1>(mkg, mkb, kg, kb, rg, rb);
+                            rank_pair<kQX2>(mkg, mkb, kg, kb, rg, rb);
+                            rank_pair<kQX3>(mkg, mkb, kg, kb, rg, rb);
+                        }
+                        const bool keep_g = rg < (uint32_t)LMAX, win_b = rb < (uint32_t)LMAX;
+                        const uint32_t kbu = hiw_up(mb);
+                        const uint32_t su = keep_g ? (win_b ? kbu : kgu) : (win_b ? kbu : 0u);
+                        const uint32_t nmk = keep_g ? (win_b ? 0xffffffffu : kb) : kg;
+                        const uint32_t nsurv = frame_sum<G>((keep_g ? 1u : 0u) + (win_b ? 1u : 0u));
+                        const uint32_t smax = frame_max<G>(su), nmin = frame_min<G>(nmk);
+                        amb |= wmask(full && !(nsurv == (uint32_t)LMAX && nmin > smax)) & vmask;
+                        const uint64_t fw = wmask(!keep_g), ww = wmask(win_b);
+                        const uint32_t f8 = ((fl < F / 2 ? (uint32_t)fw : (uint32_t)(fw >> 32)) >> sh) & GM;
+                        const uint32_t w8 = ((fl < F / 2 ? (uint32_t)ww : (uint32_t)(ww >> 32)) >> sh) & GM;
+                        const uint32_t jj = __builtin_popcount(f8 & ((1u << p) - 1u));
+                        const int rsrc = gbase + (int)nth_set_bit8(w8, jj);
+                        if (full && !keep_g) {
+                            pull = true;
+                            src = rsrc;
+                        }
+                    }
+                }
+                if (wmask(pull) != 0) {
+                    // the child a puller takes: a full frame's worse child, a growing frame's bit-1
+                    // child; its bit rides on the table word
+                    const uint64_t pubm = pscl_asu64(full ? mb : m1);
+                    const uint32_t tw = tab | ((full ? (gbit ^ 1u) : 1u) << 31);
+                    const uint64_t pm = shfl_u64(pubm, src);
+                    const uint64_t pu0 = shfl_u64(u0, src);
+                    const uint64_t pu1 = phi >= 64 ? shfl_u64(u1, src) : 0ULL;
+                    const uint32_t ptw = bperm32(tw, src);
+                    if (pull) {
+                        nm = pscl_asf64(pm);
+                        u0 = pu0;
+                        u1 = pu1;
+                        tab = ptw & 0x7fffffffu;
+                        b = ptw >> 31;
+                    }
+                }
+                metric = nm;
+                if (phi < 64) u0 |= (uint64_t)b << phi; else u1 |= (uint64_t)b << (phi - 64);
+                lastbit = b;
+                lcnt += grow ? 1 : 0;
+                return;
+            }
             if constexpr (cnt < LMAX) {
                 // growing list: every child survives; bit-1 children to lanes cnt..2cnt-1
                 const double m0 = gbit ? mb : mg, m1 = gbit ? mg : mb;
@@ -361,7 +503,25 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
             if (phi < 64) u0 |= (uint64_t)b << phi; else u1 |= (uint64_t)b << (phi - 64);
             lastbit = b;
         };
-        static_for<kN>([&](auto PC) { phase(PC); });
+        if constexpr (FS) {
+            // entered at the warm-start segment: a fall-through switch over the 16-phase segments
+            auto seg = [&](auto SB) {
+                static_for<16>([&](auto TC) { phase(std::integral_constant<int, decltype(SB)::value * 16 + decltype(TC)::value>{}); });
+            };
+            using std::integral_constant;
+            switch (seg0) {
+                case 0: seg(integral_constant<int, 0>{}); [[fallthrough]];
+                case 1: seg(integral_constant<int, 1>{}); [[fallthrough]];
+                case 2: seg(integral_constant<int, 2>{}); [[fallthrough]];
+                case 3: seg(integral_constant<int, 3>{}); [[fallthrough]];
+                case 4: seg(integral_constant<int, 4>{}); [[fallthrough]];
+                case 5: seg(integral_constant<int, 5>{}); [[fallthrough]];
+                case 6: seg(integral_constant<int, 6>{}); [[fallthrough]];
+                default: seg(integral_constant<int, 7>{});
+            }
+        } else {
+            static_for<kN>([&](auto PC) { phase(PC); });
+        }
 
         // ---- epilogue: candidates u[info_set], CRC syndrome, final list order certified,
         // best = first CRC pass in list order (scl.py:176-209)
@@ -389,8 +549,10 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
                 syn ^= ST[m * 16 + (uint32_t)(((m < 16 ? ib0 : ib1) >> (4 * (m & 15))) & 15u)];
         }
         // list position = rank of the metric among the frame's L (high words); certified when all
-        // pairs are apart by the margin (then the ranks are distinct and equal the exact order)
-        const uint32_t kh = hiw(metric), ku = hiw_up(metric);
+        // pairs are apart by the margin (then the ranks are distinct and equal the exact order).
+        // FS: among the frame's live paths (lanes p < 2^lcnt; the others' keys above every metric)
+        const bool live = !FS || p < (1 << lcnt);
+        const uint32_t kh = live ? hiw(metric) : 0xffffffffu, ku = live ? hiw_up(metric) : 0xffffffffu;
         uint32_t r = 0;
         bool near = false;
         auto cmp_perm = [&](uint32_t oh, uint32_t ou) {
@@ -407,30 +569,39 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
             cmp_perm(dpp32<kQX2>(mh), dpp32<kQX2>(mu));
             cmp_perm(dpp32<kQX3>(mh), dpp32<kQX3>(mu));
         }
-        amb |= wmask(near) & vmask;
+        amb |= wmask(near && live) & vmask;
         const bool famb = ((amb >> gbase) & (uint64_t)GM) != 0;
-        if (famb && p == 0 && fvalid) P.amb_list[atomicAdd(P.amb_count, 1)] = fi;
+        if (famb && p == 0 && fvalid) {
+            if constexpr (FS) {  // DL-SCL retry round: into the entry's deferred bucket
+                const int fseg = pscl_bucket_of(fsafe, bpre);
+                const int slot = atomicAdd(P.amb_count + fseg * PSCL_DL_CSTRIDE, 1);
+                P.amb_elist[(int64_t)fseg * P.bcap + slot] = (int32_t)f;
+                P.flags[f] = PSCL_DL_DEFERRED;
+            } else {
+                P.amb_list[atomicAdd(P.amb_count, 1)] = fi;
+            }
+        }
         // best: the lowest list position whose candidate passes the CRC (position 0 if none)
         const uint32_t pass = P.has_crc ? (syn == 0 ? 1u : 0u) : 1u;
-        const uint32_t keyb = pass ? r : (uint32_t)LMAX + r;
+        const uint32_t keyb = live ? (pass ? r : (uint32_t)LMAX + r) : 0xffffu;
         const uint32_t kbest = frame_min<G>(keyb);
         if (fvalid && !famb && keyb == kbest) {
             const int best = (int)(kbest & (uint32_t)(LMAX - 1));
             const bool bpass = kbest < (uint32_t)LMAX;
             if (P.best) {
-                P.best[fi * PW] = ib0;
-                if (PW > 1) P.best[fi * PW + 1] = ib1;
+                P.best[f * PW] = ib0;
+                if (PW > 1) P.best[f * PW + 1] = ib1;
             }
-            if (P.flags) P.flags[fi] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
-            if (P.n_paths) P.n_paths[fi] = LMAX;
-            if (P.ref) {
+            if (P.flags) P.flags[f] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
+            if (P.n_paths) P.n_paths[f] = FS ? (1 << lcnt) : LMAX;
+            if (!FS && P.ref) {
                 const uint64_t ibw[2] = {ib0, ib1};
                 tally_errors(ibw, P.ref + fi * PW, PW, P.k_payload, bpass, cfe, cbe, cpe, cpb);
             }
         }
         wave_lds_fence();
     }
-    if (P.ref) {
+    if (!FS && P.ref) {
         flush_counts_p(P, blockIdx.x, cfe, cbe, cpe, cpb);
         if (blockIdx.x == 0 && threadIdx.x == 0)
             atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
@@ -454,6 +625,18 @@ hipError_t pscl_launch_lane(const pscl_decode_params& P, int64_t grid, hipStream
         hipLaunchKernelGGL((scl_lane_kernel<4, 1>), dim3((unsigned)grid), dim3(64), lds4, s, P);
     else if (P.L == 4)
         hipLaunchKernelGGL((scl_lane_kernel<4, 2>), dim3((unsigned)grid), dim3(64), lds4, s, P);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+// the lane-per-path forced-bit screening launch of a DL-SCL retry round (pscl_lane_fs_available)
+hipError_t pscl_launch_lane_fs(const pscl_decode_params& P, int64_t grid, hipStream_t s) {
+    const int lds8 = LaneLayout<8>::F * LaneLayout<8>::FSTRIDE * 8, lds4 = LaneLayout<4>::F * LaneLayout<4>::FSTRIDE * 8;
+    if (P.L == 8)
+        hipLaunchKernelGGL((scl_lane_kernel<8, 1, true>), dim3((unsigned)grid), dim3(64), lds8, s, P);
+    else if (P.L == 4)
+        hipLaunchKernelGGL((scl_lane_kernel<4, 1, true>), dim3((unsigned)grid), dim3(64), lds4, s, P);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();

@@ -227,6 +227,11 @@ int pscl_screening_available(const pscl_decode_params& P);  // scl128.hip
 #ifndef PSCL_LANE_NR
 #define PSCL_LANE_NR 1
 #endif
+// screened DL-SCL retry decodes of the (128,64) code on the lane-per-path kernel (1) or the
+// two-lanes-per-path forced-bit screening instance (0)
+#ifndef PSCL_LANE_FS
+#define PSCL_LANE_FS 1
+#endif
 #ifndef PSCL_LANE4
 #define PSCL_LANE4 1
 #endif
@@ -248,9 +253,15 @@ int64_t pscl_decode_count_slots(const pscl_decode_params& P, int hist);
 // counters[FRAME_ERR, BIT_ERR, PAYLOAD_ERR, PAYLOAD_BIT] += the sums of cpart[slots][4], which it
 // leaves zero (the kernels store only the slots of wavefronts with errors)
 hipError_t pscl_launch_count_reduce(int32_t* cpart, int64_t slots, int64_t* counters, hipStream_t s);
-// retry-chain entries from which the DL-SCL retry decodes screen (PSCL_TUNE_DL_SCREEN_MIN default)
+// retry-chain entries from which the DL-SCL retry decodes screen (PSCL_TUNE_DL_SCREEN_MIN default):
+// at L = 8 every chain (the lane-per-path FS kernel, config 3 sweep 199-201 -> 220-221 M frames/s),
+// at L = 4 the large ones (config 4, chains of ~19k entries: 3.43-3.47 against 3.79-3.85 ms
+// screened), profiles/r04q_lane_fs_ab.txt
 #ifndef PSCL_DL_SCREEN_MIN
 #define PSCL_DL_SCREEN_MIN 24576
+#endif
+#ifndef PSCL_DL_SCREEN_MIN8
+#define PSCL_DL_SCREEN_MIN8 1
 #endif
 // the DL-SCL baseline decode's screening kernel at N = 128 (PSCL_TUNE_DL_LANE default): 1 the
 // lane-per-path kernel, 2 the two-lanes-per-path one, 0 by list size (lane-per-path at L = 8)
@@ -262,6 +273,9 @@ int pscl_lane_long_available(const pscl_decode_params& P);
 hipError_t pscl_launch_lane_long(const pscl_decode_params& P, hipStream_t s);
 int64_t pscl_lane_long_grid(const pscl_decode_params& P);
 int pscl_screening_fs_available(const pscl_decode_params& P);  // forced-bit screening (DL-SCL retries)
+// the lane-per-path form of a screened DL-SCL retry decode (scl128_lane.hip, FS)
+int pscl_lane_fs_available(const pscl_decode_params& P);
+hipError_t pscl_launch_lane_fs(const pscl_decode_params& P, int64_t grid, hipStream_t s);
 hipError_t pscl_launch_decode128(const pscl_decode_params& P, int hist, int wpg, int64_t grid, int lds, hipStream_t s);
 int64_t pscl_decode_grid(const pscl_decode_params& P);
 int pscl_decode_wpg(const pscl_decode_params& P);

@@ -577,6 +577,11 @@ hipError_t pscl_launch_decode(const pscl_decode_params& P, int hist, hipStream_t
         const int64_t cap = P.ref && !P.cpart ? PSCL_LANE_COUNT_GRID : (1 << 20);
         return pscl_launch_lane(P, g < 1 ? 1 : (g > cap ? cap : g), s);
     }
+    if (!hist && pscl_lane_fs_available(P)) {  // (P.B: the round's entry capacity)
+        const int fw = pscl_lane_frames_per_wg(P.L);
+        const int64_t g = (P.B + fw - 1) / fw;
+        return pscl_launch_lane_fs(P, g < 1 ? 1 : (g > (1 << 20) ? (1 << 20) : g), s);
+    }
     if (pscl_decode_wpg(P) < 1) return hipErrorInvalidValue;
     const int64_t grid = pscl_decode_grid(P);
     if (P.fast) return pscl_launch_decode128(P, hist, pscl_decode_wpg(P), grid, decode_lds_bytes(P, hist), s);

@@ -12,7 +12,9 @@ FER/BER counters against counts recomputed on the host from the decoded bits.
   config 4  DL-SCL L=4, 8 flip retries, beta_M4, 10^6 frames     (flip.py:65-141)
   config 5  NR (128,88) rate matched to E=256, SCL L=8, 10^6      (scl_nr.py:40-57 front end)
 Configs 1 and 3 are covered by test_gpu_fer.py (config 1's CSV byte-identical to the
-reference's results/fer_M1.csv, config 3's 4.0-6.5 dB grid).
+reference's results/fer_M1.csv, config 3's 4.0-6.5 dB grid); config 3's DL-SCL decode (L = 8,
+beta_M8) is checked here against the oracle at 4.0 and 4.5 dB, and config 4 with every retry
+decode screened.
 """
 import numpy as np
 import pytest
@@ -117,38 +119,63 @@ def test_config5_nr_E256_L8_1e6_frames_vs_oracle():
     print(f"config 5: payload FER {cnt[PAY_ERR] / B:.6f}, BER {cnt[PAY_BIT] / (B * 64):.3e}, 0/{B} oracle mismatches")
 
 
-def test_config4_dlscl_L4_r8_beta4_1e6_frames_vs_oracle():
-    L, K, kp, R = 4, 64, 40, 8
+def _dl_config(L, beta_name, ebno, nb, seed, tuning=None):
+    """One DL-SCL batch of nb frames (8 flips, beta_<beta_name>) against the oracle's
+    decode_with_retries, frame by frame; returns (SCL counters, DL counters, oracle attempts)."""
+    K, kp, R = 64, 40, 8
     info = construct_info_set(128, K)
-    beta = np.load(GOLDEN / "beta_M4.npy")
+    beta = np.load(GOLDEN / f"beta_{beta_name}.npy")
     dec = _native.Decoder(128, info, L, POLY)
+    if tuning:
+        dec.set_tuning(**tuning)
     with _native.DeviceArena(dec) as mem:
-        d_llr, d_msg = _batch(dec, mem, L, K, kp, 0, seed=40)
-        d_best, d_flags, d_att = mem.alloc(B * 8), mem.alloc(B), mem.alloc(B * 4)
+        d_llr, d_msg = mem.alloc(nb * 128 * 8), mem.alloc(nb * 8)
+        dec.channel_device(seed, int(ebno * 10), ebno, K / 128, kp, 0, nb, d_llr, d_msg)
+        d_best, d_flags, d_att = mem.alloc(nb * 8), mem.alloc(nb), mem.alloc(nb * 4)
         d_cs, d_cd = mem.alloc(64), mem.alloc(64)
         mem.memset(d_cs, 0, 64)
         mem.memset(d_cd, 0, 64)
-        dec.dlscl_device(d_llr, B, R, beta=beta, d_best=d_best, d_flags=d_flags, d_attempts=d_att, d_ref=d_msg,
+        dec.dlscl_device(d_llr, nb, R, beta=beta, d_best=d_best, d_flags=d_flags, d_attempts=d_att, d_ref=d_msg,
                          k_payload=kp, d_counters_scl=d_cs, d_counters_dl=d_cd)
         dec.sync()
-        best = mem.download(d_best, B * 8, np.uint64).reshape(B, 1)
-        flags = mem.download(d_flags, B, np.uint8)
-        att = mem.download(d_att, B * 4, np.int32)
+        best = mem.download(d_best, nb * 8, np.uint64).reshape(nb, 1)
+        flags = mem.download(d_flags, nb, np.uint8)
+        att = mem.download(d_att, nb * 4, np.int32)
         cs, cd = mem.download(d_cs, 64, np.int64), mem.download(d_cd, 64, np.int64)
-        msg = mem.download(d_msg, B * 8, np.uint64).reshape(B, 1)
-        llr = mem.download(d_llr, B * 128 * 8, np.float64).reshape(B, 128)
+        msg = mem.download(d_msg, nb * 8, np.uint64).reshape(nb, 1)
+        llr = mem.download(d_llr, nb * 128 * 8, np.float64).reshape(nb, 128)
     dec.close()
     bits_o, ok_o, att_o = oracle.dl_batch(llr, info, L, R, POLY, beta)
     bits = words_to_bits(best, K)
     ok = (flags & 0x80) != 0
     bad = np.flatnonzero(np.any(bits != bits_o, axis=1) | (ok != ok_o) | (att != att_o))
-    assert bad.size == 0, f"DL-SCL differs from the oracle in {bad.size} frames, first {bad[:5]}"
+    assert bad.size == 0, f"DL-SCL L={L} differs from the oracle in {bad.size} frames, first {bad[:5]}"
     _check_counters(cd, _host_counts(bits, words_to_bits(msg, K), ok, kp), "DL-SCL")
     assert int(cd[RETRIES]) == int((att_o - 1).sum())  # one re-decode per flip tried
     base_fail = int(cs[FRAME_ERR])
-    assert cs[FRAMES] == B and base_fail == int(np.count_nonzero(att_o > 1))  # retried iff the baseline failed
+    assert cs[FRAMES] == nb and base_fail == int(np.count_nonzero(att_o > 1))  # retried iff the baseline failed
+    return cs, cd, att_o
+
+
+def test_config4_dlscl_L4_r8_beta4_1e6_frames_vs_oracle():
+    cs, cd, _ = _dl_config(4, "M4", EBNO, B, seed=40)
+    base_fail = int(cs[FRAME_ERR])
     # reference results/fer_M4.csv:2: SCL 91/2000, DL-SCL 71/2000 at 5 dB
     for got, ref in ((base_fail / B, 91 / 2000), (cd[FRAME_ERR] / B, 71 / 2000)):
         assert abs(got - ref) < 4 * np.sqrt(ref * (1 - ref) / 2000), (got, ref)
     print(f"config 4: SCL FER {base_fail / B:.5f}, DL-SCL FER {cd[FRAME_ERR] / B:.5f}, "
           f"{cd[RETRIES] / B:.3f} re-decodes/frame, 0/{B} oracle mismatches")
+
+
+@pytest.mark.parametrize("L,beta,ebno,nb,tuning", [
+    (8, "M8", 4.5, 200_000, None),               # config 3's DL-SCL point (L = 8: lane-per-path FS retry decodes)
+    (8, "M8", 4.0, 100_000, {"dl_retry_lane": 2}),  # the two-lanes-per-path screening instance
+    (4, "M4", 5.0, 1_000_000, {"dl_screen": 1}),  # config 4 with every retry decode screened (L = 4 lane FS)
+])
+def test_dlscl_screened_retry_decodes_vs_oracle(L, beta, ebno, nb, tuning):
+    """Screened DL-SCL retry rounds (forced-bit screening decodes + exact decodes of the entries
+    they defer) against the oracle on every frame: bits, CRC flags, attempt counts, counters."""
+    cs, cd, att_o = _dl_config(L, beta, ebno, nb, seed=60 + L, tuning=tuning)
+    assert int(np.count_nonzero(att_o > 2)) > nb // 200  # many multi-round entries (warm starts, growth)
+    print(f"L={L} {ebno} dB {tuning}: SCL FER {cs[FRAME_ERR] / nb:.5f}, DL-SCL FER {cd[FRAME_ERR] / nb:.5f}, "
+          f"0/{nb} oracle mismatches")

@@ -74,12 +74,15 @@ def test_device_retry_loop_golden(golden):
 # (1.5 dB: most frames fail, more than half of the chunk goes to one retry chain)
 @pytest.mark.parametrize("M,retries,ebno,screen", [(4, 8, 3.0, "0"), (8, 8, 3.5, "0"), (2, 3, 3.0, "0"), (1, 70, 4.0, "0"),
                                                    (4, 8, 1.5, "0"), (4, 8, 2.0, "1"), (8, 8, 2.5, "1"),
-                                                   (8, 8, 2.5, "2"), (4, 8, 2.0, "adaptive")])
+                                                   (8, 8, 2.5, "2"), (4, 8, 2.0, "adaptive"), (8, 8, 3.5, "1"),
+                                                   (4, 8, 3.0, "1"), (8, 8, 2.5, "1/2lane"), (4, 8, 2.0, "1/2lane")])
 def test_device_retry_loop_equals_host_ranking(monkeypatch, M, retries, ebno, screen):
     """Device retry loop == numpy-ranked retries, frame by frame (3000 frames, ~30% failing);
-    screen = 1: the retry decodes on the forced-bit screening instance plus the exact decode of
-    the entries it defers (tuning knob dl_screen = 1); 2: never; "adaptive": the default rule with
-    a threshold every chain here exceeds (dl_screen_min = 1)."""
+    screen = 1: the retry decodes on the forced-bit screening instance (lane per path: per-frame
+    forced / growing / full list) plus the exact decode of the entries it defers (tuning knob
+    dl_screen = 1); "1/2lane": the same on the two-lanes-per-path instance (dl_retry_lane = 2);
+    2: never; "adaptive": the default rule with a threshold every chain here exceeds
+    (dl_screen_min = 1)."""
     from polar_code_amd.polar.polar import construct_info_set, encode
     from polar_code_amd.polar.crc import attach_crc
 
@@ -93,6 +96,7 @@ def test_device_retry_loop_equals_host_ranking(monkeypatch, M, retries, ebno, sc
     for b in (beta, None):
         dev = decode_with_retries_device(llr, info, M, retries, crc="0x1864CFB", beta=b,
                                          tuning=({"dl_screen": int(screen)} if screen.isdigit() else
+                                                 {"dl_screen": 1, "dl_retry_lane": 2} if screen == "1/2lane" else
                                                  {"dl_screen": 0, "dl_screen_min": 1}))
         host = decode_with_retries_batch(llr, info, M, retries, crc="0x1864CFB", beta=b)
         assert 0.05 < (~dev["base_pass"]).mean() < (0.97 if ebno < 2 else 0.9)
