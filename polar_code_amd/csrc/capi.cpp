@@ -201,7 +201,7 @@ int set_device(pscl_handle* h) {
 
 // the handle's stream waits for the pending pipelined work (no host wait): what = 1 the plain
 // decodes' re-decodes, 2 the DL-SCL retry chains, 3 both
-int dl_enqueue_deferred(pscl_handle* h);
+int dl_enqueue_deferred(pscl_handle* h, bool beside = false);
 
 int join_pipe(pscl_handle* h, int what = 3) {
     if (what & 2) {  // a pipelined DL-SCL call's chains, enqueued first
@@ -821,7 +821,7 @@ struct DlState {
 
 int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const double* d_llr, uint64_t* d_best,
                    uint8_t* d_flags, int32_t* d_attempts, int32_t* d_tried, int tried_stride, int64_t* d_cnt_dl,
-                   hipStream_t st, hipStream_t side, hipEvent_t ev_s, hipEvent_t ev_d, bool narrow) {
+                   hipStream_t st, hipStream_t side, hipEvent_t ev_s, hipEvent_t ev_d, bool narrow, bool beside) {
     const int K = h->K, W = h->W;
     hipError_t e;
     const size_t bstride = (size_t)PSCL_DL_NSEG * PSCL_DL_CSTRIDE;
@@ -891,10 +891,14 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     // the rounds are throughput-bound and the screening decode's ~4x cheaper frames win (config 3,
     // 4.0 dB point: 10.5 -> 9.0 ms); with few entries the exact decode of the deferred ones is one
     // more latency per round (5.0 dB: 5.6 -> 6.1 ms), DESIGN.md §5.1b
+    // At L = 8 (the lane-per-path FS kernel) also every chain that runs beside a later baseline
+    // decode (the next pipelined call's, or the next chunk's): there the screened decodes' smaller
+    // GPU share wins even when the chain is short (config 3 sweep 199-201 -> 218-222 M frames/s),
+    // while a chain running alone (a single call, a join) keeps the latency-bound rule
     const int64_t ds = h->tune[PSCL_TUNE_DL_SCREEN];
-    const int64_t ds_min = h->tune[PSCL_TUNE_DL_SCREEN_MIN] ? h->tune[PSCL_TUNE_DL_SCREEN_MIN]
-                                                            : (h->L >= 8 ? PSCL_DL_SCREEN_MIN8 : PSCL_DL_SCREEN_MIN);
-    const bool dl_screen = ds == 1 || (ds == 0 && A >= ds_min);
+    const int64_t ds_min = h->tune[PSCL_TUNE_DL_SCREEN_MIN] ? h->tune[PSCL_TUNE_DL_SCREEN_MIN] : PSCL_DL_SCREEN_MIN;
+    const bool dl_screen =
+        ds == 1 || (ds == 0 && (A >= ds_min || (beside && h->L >= 8 && !h->tune[PSCL_TUNE_DL_SCREEN_MIN])));
     const bool scr = dl_screen && h->screen && S.dcnt && S.ob2 && side && pscl_screening_fs_available(H);
     pscl_decode_params HA, HX;
     pscl_post_params QD;
@@ -1132,7 +1136,7 @@ int dl_setup(pscl_handle* h, const pscl_dl_call& a, DlBufs& b) {
 // the retry chains of chunk c (compaction parity p): the host reads the chunk's failing count
 // (waiting for its baseline) and enqueues the rounds on the retry streams; ev_retry[p] marks
 // their end on retry stream 0
-int dl_chain(pscl_handle* h, const pscl_dl_call& a, const DlBufs& b, int64_t c) {
+int dl_chain(pscl_handle* h, const pscl_dl_call& a, const DlBufs& b, int64_t c, bool beside) {
     const int p = dl_parity(a, c);
     const int64_t cap = a.cap;
     HIP_TRY(hipEventSynchronize(h->ev_base[p]));
@@ -1160,7 +1164,7 @@ int dl_chain(pscl_handle* h, const pscl_dl_call& a, const DlBufs& b, int64_t c) 
         T.act = b.act[p] + (k ? A0 : 0);
         int r2 = dl_retry_chunk(h, T, k ? A - A0 : A0, a.rounds, a.d_llr, a.d_best, a.d_flags, a.d_attempts,
                                 a.d_tried, a.tried_stride, d_cdl, h->retry_stream[k], h->side_stream[k], h->ev_scr[k],
-                                h->ev_def[k], a.pipe);
+                                h->ev_def[k], a.pipe, beside);
         if (r2) return r2;
     }
     if (parts == 2) {  // both chains done before the parity's indices are reused
@@ -1172,15 +1176,16 @@ int dl_chain(pscl_handle* h, const pscl_dl_call& a, const DlBufs& b, int64_t c) 
 }
 
 // a pipelined call's retry chains and DL counters, enqueued on the retry streams (ev_dl marks
-// their end; join_pipe orders it into the handle's stream)
-int dl_enqueue_deferred(pscl_handle* h) {
+// their end; join_pipe orders it into the handle's stream); beside: the next call's baseline is on
+// the handle's stream, concurrent with them
+int dl_enqueue_deferred(pscl_handle* h, bool beside) {
     if (!h->dl_defer_valid) return PSCL_OK;
     h->dl_defer_valid = false;
     const pscl_dl_call a = h->dl_defer;
     DlBufs b;
     int rc = dl_setup(h, a, b);  // (the sizes of the call's own setup: no allocation)
     if (rc) return rc;
-    if ((rc = dl_chain(h, a, b, 0))) return rc;
+    if ((rc = dl_chain(h, a, b, 0, beside))) return rc;
     if (a.d_ref) {
         hipError_t e = pscl_launch_dl_count(a.d_best, a.d_flags, a.d_ref, a.B, h->W, a.k_payload, a.d_counters_dl,
                                             h->retry_stream[0]);
@@ -1296,20 +1301,20 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
                 return fail(PSCL_EDEVICE, "dl_compact launch: %s", hipGetErrorString(e));
             HIP_TRY(hipMemcpyAsync(h->h_count + p, bufs.cnt[p], 4, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipEventRecord(h->ev_base[p], s));
-            if (c >= 1 && (rc = dl_chain(h, a, bufs, c - 1))) return rc;
+            if (c >= 1 && (rc = dl_chain(h, a, bufs, c - 1, true))) return rc;
         }
     }
     if (a.pipe) {
         // the previous call's chains now (its baseline precedes this call's on the stream), this
         // call's at the next call or join
-        if ((rc = dl_enqueue_deferred(h))) return rc;
+        if ((rc = dl_enqueue_deferred(h, true))) return rc;
         h->dl_defer = a;
         h->dl_defer_valid = true;
         h->dl_par = (h->dl_par + 1) % kDlPar;
         return PSCL_OK;
     }
     if (rounds > 0) {
-        if ((rc = dl_chain(h, a, bufs, nch - 1))) return rc;
+        if ((rc = dl_chain(h, a, bufs, nch - 1, false))) return rc;
         HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[dl_parity(a, nch - 1)], 0));  // chains run in order on stream 0
     }
     if (d_ref) {

@@ -168,8 +168,8 @@ def test_config4_dlscl_L4_r8_beta4_1e6_frames_vs_oracle():
 
 
 @pytest.mark.parametrize("L,beta,ebno,nb,tuning", [
-    (8, "M8", 4.5, 200_000, None),               # config 3's DL-SCL point (L = 8: lane-per-path FS retry decodes)
-    (8, "M8", 4.0, 100_000, {"dl_retry_lane": 2}),  # the two-lanes-per-path screening instance
+    (8, "M8", 4.5, 200_000, {"dl_screen": 1}),   # config 3's DL-SCL point (L = 8: lane-per-path FS retry decodes)
+    (8, "M8", 4.0, 100_000, {"dl_screen": 1, "dl_retry_lane": 2}),  # the two-lanes-per-path screening instance
     (4, "M4", 5.0, 1_000_000, {"dl_screen": 1}),  # config 4 with every retry decode screened (L = 4 lane FS)
 ])
 def test_dlscl_screened_retry_decodes_vs_oracle(L, beta, ebno, nb, tuning):
