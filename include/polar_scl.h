@@ -317,6 +317,8 @@ int pscl_join(pscl_handle* h);
  *                           L = 4)
  *   PSCL_TUNE_DL_RETRY_LANE 2: screened retry decodes (N = 128) on the two-lanes-per-path forced-
  *                           bit instance instead of the lane-per-path one (default)
+ *   PSCL_TUNE_POST_PAIRS    1..32: entry pairs per wavefront the DL-SCL post pass grid is sized for
+ *                           (default 4; capped by PSCL_TUNE_POST_GRID)
  */
 #define PSCL_TUNE_DL_SCREEN 1
 #define PSCL_TUNE_DL_CHUNKS 2
@@ -327,7 +329,8 @@ int pscl_join(pscl_handle* h);
 #define PSCL_TUNE_DL_LANE 7
 #define PSCL_TUNE_DL_SCREEN_MIN 8
 #define PSCL_TUNE_DL_RETRY_LANE 9
-#define PSCL_TUNE_COUNT 10
+#define PSCL_TUNE_POST_PAIRS 10
+#define PSCL_TUNE_COUNT 11
 int pscl_set_tuning(pscl_handle* h, int knob, int64_t value);
 
 /*

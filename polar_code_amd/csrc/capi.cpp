@@ -734,7 +734,7 @@ int pscl_set_pipelined(pscl_handle* h, int enable) {
 int pscl_set_tuning(pscl_handle* h, int knob, int64_t value) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
     static const int64_t lim[PSCL_TUNE_COUNT][2] = {{0, 0}, {0, 2}, {0, 64}, {0, 2}, {0, 1}, {0, 4096}, {0, PSCL_MAX_WAVES_PER_WG}, {0, 2},
-                                                    {0, (int64_t)1 << 30}, {0, 2}};
+                                                    {0, (int64_t)1 << 30}, {0, 2}, {0, 32}};
     if (knob < 1 || knob >= PSCL_TUNE_COUNT) return fail(PSCL_EINVAL, "unknown tuning knob %d", knob);
     if (value < lim[knob][0] || value > lim[knob][1] || (knob == PSCL_TUNE_POST_GRID && value && value < 16))
         return fail(PSCL_EINVAL, "tuning knob %d: value %lld out of range", knob, (long long)value);
@@ -842,6 +842,7 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     Q.rounds = rounds;
     Q.narrow = narrow ? 1 : 0;  // (pipelined calls: beside the next call's baseline)
     Q.grid_cap = h->tune[PSCL_TUNE_POST_GRID];
+    Q.pairs = h->tune[PSCL_TUNE_POST_PAIRS];
     Q.cap = A;
     Q.act = S.act;
     Q.tried = S.tried;

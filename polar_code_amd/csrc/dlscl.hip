@@ -215,6 +215,18 @@ __global__ void __launch_bounds__(256) replay_kernel(const pscl_replay_params R,
 #ifndef PSCL_POST_GRID
 #define PSCL_POST_GRID 512
 #endif
+#ifndef PSCL_POST_PAIRS
+#define PSCL_POST_PAIRS 2
+#endif
+// unroll of the flip metric's sums over k: beta rows in flight per lane (read through L2 in the
+// narrow form)
+// occupancy hint of the post pass (waves per SIMD; 4 caps it at 128 VGPRs)
+#ifndef PSCL_POST_WPE
+#define PSCL_POST_WPE 4
+#endif
+#ifndef PSCL_POST_UNROLL
+#define PSCL_POST_UNROLL 4
+#endif
 #ifndef PSCL_POST_BETA_LDS
 #define PSCL_POST_BETA_LDS 1
 #endif
@@ -255,7 +267,7 @@ __device__ __forceinline__ uint64_t bcast64(uint64_t v, int l) {
 
 // NC, KC: N and K compiled in (128 and 64 / 88: the BASELINE codes) or 0 (from Q)
 template <int NC, int KC, int PW>
-__global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(4))) dl_post_kernel(const pscl_post_params Q, int beta_lds) {
+__global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PSCL_POST_WPE))) dl_post_kernel(const pscl_post_params Q, int beta_lds) {
     constexpr int kPostWaves = PW, kPostChunk = PostShared<PW>::kChunk;
     __shared__ PostShared<PW> S;
     extern __shared__ double sbeta[];  // [K][K] when beta_lds
@@ -458,7 +470,7 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(4)
 #pragma unroll
                     for (int m = 0; m < MC; ++m) qv[m] = 0.0;
                     const double* bc = beta + hl;
-#pragma unroll 4
+#pragma unroll PSCL_POST_UNROLL
                     for (int k = 0; k < K; ++k) {
                         const double ak = nxt[k];
 #pragma unroll
@@ -477,7 +489,7 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(4)
 #pragma unroll
                     for (int m = 0; m < MC; ++m) qv[m] = 0.0;
                     const double* bc = beta + hl;
-#pragma unroll 4
+#pragma unroll PSCL_POST_UNROLL
                     for (int k = 0; k < K; ++k) {
                         const double ak = nxt[k];
 #pragma unroll
@@ -752,9 +764,10 @@ hipError_t pscl_launch_replay(const pscl_replay_params& R, int64_t cap, hipStrea
 
 hipError_t pscl_launch_dl_post(const pscl_post_params& Q, int64_t entries, hipStream_t s) {
     if (entries <= 0) return hipSuccess;
-    // workgroups of PW wavefronts (2 PW entries in flight)
+    // workgroups of PW wavefronts (2 PW entries in flight), sized for `pairs` entry pairs per wavefront
     const int PW = Q.narrow ? kPostWavesNarrow : kPostWavesWide;
-    int64_t grid = (entries + PW * 8 - 1) / (PW * 8);
+    const int64_t pairs = Q.pairs >= 1 && Q.pairs <= 32 ? Q.pairs : PSCL_POST_PAIRS;
+    int64_t grid = (entries + PW * 2 * pairs - 1) / (PW * 2 * pairs);
     const int64_t gcap = Q.grid_cap >= 16 && Q.grid_cap <= 4096 ? Q.grid_cap : PSCL_POST_GRID;  // (tuning knob)
     if (grid > gcap) grid = gcap;
     const int beta_lds = PSCL_POST_BETA_LDS && !Q.narrow && Q.beta && (size_t)Q.K * Q.K * 8 <= 32 * 1024;  // (LDS <= 64 KB)

@@ -142,6 +142,7 @@ struct pscl_post_params {
     int rounds;                  // min(retries, K)
     int narrow;                  // small workgroups, beta through L2 (pipelined calls, dl_post_kernel)
     int64_t grid_cap;            // 0, or the workgroup cap of a launch (tuning knob; default PSCL_POST_GRID)
+    int64_t pairs;               // 0, or the entry pairs per wavefront the grid is sized for (tuning knob)
     int init;
     const int32_t* in_count;     // bucket counts of this round (init: unused, cap entries)
     const int32_t* in_list;      // bucket lists of this round ([NSEG][cap] entry ids)
