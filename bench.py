@@ -561,6 +561,10 @@ def config3_sweep(args, ctx: Ctx):
                         "4.0-6.5 dB step 0.5 (one pipelined pass: pscl_simulate_device per block)",
             "frames_per_point": frames, "wall_s": total_t, "value": frames * len(pts) / total_t,
             "unit": "frames/s (SCL + DL-SCL + uncoded per frame, whole sweep)", "points": pts,
+            "kernels": ("channel_kernel TX (+ uncoded count) + scl_lane_kernel<8> baseline + retry rounds: "
+                        "scl_lane_kernel<8,FS> screened retry decodes (chains beside the next point's baseline, "
+                        "or of >= 24576 entries) or scl128_kernel<8,FS> exact ones, exact re-decodes of the "
+                        "deferred entries, dl_post_kernel"),
             "point_5db": {"wall_s": t5, "frames_per_s": frames / t5, "fer_scl": rows5[0]["fer_scl"],
                           "fer_dl": rows5[0]["fer_dl"]},
             "reference": "results/fer_M8.csv:2 (5 dB): fer_scl 26/2000, fer_dl 20/2000"}
