@@ -293,7 +293,10 @@ void fill_decode_params(const pscl_handle* h, pscl_decode_params& P, int hist) {
 // or 92 + parity for a pipelined plain decode, whose reduce runs on the side stream after its
 // re-decode and is ordered before the buffer's next use by ev_px; every other launch is followed
 // on its own stream by its count-reduce launch)
-int with_count_slots(pscl_handle* h, pscl_decode_params& P, int hist, int slot) {
+// A (re)allocated buffer is zeroed on the decode's own stream st: a plain hipMemset runs on the null
+// stream, which the handle's non-blocking streams do not wait for -- the decode could store (and its
+// reduce read) partials before the zeroing lands (an intermittent counter mismatch)
+int with_count_slots(pscl_handle* h, pscl_decode_params& P, int hist, int slot, hipStream_t st) {
     P.cpart = nullptr;
     const int64_t slots = pscl_decode_count_slots(P, hist);
     if (slots <= 0) return PSCL_OK;
@@ -301,7 +304,7 @@ int with_count_slots(pscl_handle* h, pscl_decode_params& P, int hist, int slot) 
     const size_t had = h->scratch[slot].n;
     const int rc = ensure(h, slot, (size_t)slots * 16, &d);
     if (rc) return rc;
-    if (h->scratch[slot].n != had) HIP_TRY(hipMemset(d, 0, h->scratch[slot].n));  // (then kept zero by the reduces)
+    if (h->scratch[slot].n != had) HIP_TRY(hipMemsetAsync(d, 0, h->scratch[slot].n, st));  // (then kept zero by the reduces)
     P.cpart = (int32_t*)d;
     return PSCL_OK;
 }
@@ -377,7 +380,7 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
         S.amb_count = (int32_t*)d_cnt;
         // (pipelined: the count buffers alternate with the call parity, and the reduce runs on the
         // side stream after the re-decode, off the handle's stream)
-        if ((rc = with_count_slots(h, S, hist, pipe ? 92 + p : 92))) return rc;
+        if ((rc = with_count_slots(h, S, hist, pipe ? 92 + p : 92, st))) return rc;
         err = pscl_launch_decode(S, hist, st);
         h->screened = true;
         h->screened_slot = s_cnt;
@@ -415,7 +418,7 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
             err = pscl_launch_decode(X, hist, st);
         }
     } else {
-        const int rc = with_count_slots(h, P, hist, 92);
+        const int rc = with_count_slots(h, P, hist, 92, st);
         if (rc) return rc;
         err = pscl_launch_decode(P, hist, st);
         if (err == hipSuccess && P.cpart) err = pscl_launch_count_reduce(P.cpart, pscl_decode_count_slots(P, hist), P.counters, st);
