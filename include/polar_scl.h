@@ -309,9 +309,9 @@ int pscl_join(pscl_handle* h);
  *   PSCL_TUNE_DL_SCREEN_MIN 1..2^30: entries of a retry chain from which PSCL_TUNE_DL_SCREEN = 0
  *                           screens its retry decodes (default 24576: the throughput regime of
  *                           low-SNR points -- fewer entries take the exact decode, whose deferred-
- *                           entry latency would otherwise sit on every round; at L = 8 the default
- *                           also screens every chain that runs beside a later baseline decode,
- *                           a pipelined call's or a chunk's)
+ *                           entry latency would otherwise sit on every round; the default also
+ *                           screens every chain that runs beside a later baseline decode, a
+ *                           pipelined call's or a chunk's)
  *   PSCL_TUNE_DL_LANE       1: a DL-SCL baseline decode (N = 128) on the lane-per-path screening
  *                           kernel; 2: on the two-lanes-per-path one (default: 1 at L = 8, 2 at
  *                           L = 4)

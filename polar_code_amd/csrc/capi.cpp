@@ -817,7 +817,8 @@ struct DlState {
     int32_t* nt;
     double* warm_metric;
     uint8_t* of;
-    int32_t *dcnt, *dlist;   // screening retry decodes: deferred entries ([NSEG * CSTRIDE] counts, [NSEG][cap])
+    int32_t *dcnt, *dlist;   // screening retry decodes: the side chain's bucket lists, one per round
+                             // ([rounds + 1][NSEG * CSTRIDE] counts, [rounds + 1][NSEG][cap])
     uint64_t* ob2;           // [cap][W] and [cap]: their exact decode's outputs (the main post pass reads
     uint8_t* of2;            //   `of` concurrently, where the deferred mark must stay)
 };
@@ -886,23 +887,27 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     H.wpg_cap = (int)h->tune[PSCL_TUNE_RETRY_WPG];
     if (pscl_decode_wpg(H) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
     int rc;
-    // screening retry decodes (tuning knob PSCL_TUNE_DL_SCREEN = 1, measured in DESIGN.md §5.1b): the forced-bit
-    // screening instance decodes the round's entries and files the ones it cannot certify in
-    // bucket lists of their own (flags PSCL_DL_DEFERRED, which the post pass skips); on the side
-    // stream the exact kernel decodes those (warm-started, as every retry decode) and a second
-    // post pass handles them, overlapping the main post pass
+    // screening retry decodes (measured in DESIGN.md §5.1b): the forced-bit screening instance
+    // decodes the round's entries and moves the ones it cannot certify to a SIDE CHAIN (flags
+    // PSCL_DL_DEFERRED, which the main post pass skips): on the side stream, round r of the side
+    // chain decodes its entries exactly (warm-started, as every retry decode) -- the ones round r
+    // of the main chain deferred plus the side chain's own survivors -- and its post pass files the
+    // survivors in the side chain's list of round r + 1.  An entry stays on the side chain once
+    // deferred, at the same attempt index as the main chain's round, so the main chain never waits
+    // for the side chain's exact decodes; the chain ends with both.  Each round has its own side
+    // list (the side chain may lag the main chain by several rounds).
     // screening retry decodes: always (1), never (2), or for chains of many entries (0): at low SNR
     // the rounds are throughput-bound and the screening decode's ~4x cheaper frames win (config 3,
     // 4.0 dB point: 10.5 -> 9.0 ms); with few entries the exact decode of the deferred ones is one
     // more latency per round (5.0 dB: 5.6 -> 6.1 ms), DESIGN.md §5.1b
-    // At L = 8 (the lane-per-path FS kernel) also every chain that runs beside a later baseline
-    // decode (the next pipelined call's, or the next chunk's): there the screened decodes' smaller
-    // GPU share wins even when the chain is short (config 3 sweep 199-201 -> 218-222 M frames/s),
-    // while a chain running alone (a single call, a join) keeps the latency-bound rule
+    // Also every chain that runs beside a later baseline decode (the next pipelined call's, or the
+    // next chunk's): there the screened decodes' smaller GPU share wins even when the chain is
+    // short (config 3 sweep 199-201 -> 218-222 M frames/s; config 4 with the side chain 3.44 ->
+    // 3.30 ms), while a chain running alone (a single call, a join) keeps the latency-bound rule
     const int64_t ds = h->tune[PSCL_TUNE_DL_SCREEN];
     const int64_t ds_min = h->tune[PSCL_TUNE_DL_SCREEN_MIN] ? h->tune[PSCL_TUNE_DL_SCREEN_MIN] : PSCL_DL_SCREEN_MIN;
     const bool dl_screen =
-        ds == 1 || (ds == 0 && (A >= ds_min || (beside && h->L >= 8 && !h->tune[PSCL_TUNE_DL_SCREEN_MIN])));
+        ds == 1 || (ds == 0 && (A >= ds_min || (beside && !h->tune[PSCL_TUNE_DL_SCREEN_MIN])));
     const bool scr = dl_screen && h->screen && S.dcnt && S.ob2 && side && pscl_screening_fs_available(H);
     pscl_decode_params HA, HX;
     pscl_post_params QD;
@@ -910,42 +915,43 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
         HA = H;
         HA.apx = 1;
         pscl_decode_layout(HA, 0);  // (no exp table in LDS)
-        HA.amb_elist = S.dlist;
-        HA.amb_count = S.dcnt;
         HA.no_lane = h->tune[PSCL_TUNE_DL_RETRY_LANE] == 2 ? 1 : 0;  // (lane-per-path FS kernel by default)
         HX = H;
-        HX.elist = S.dlist;
-        HX.bcount = S.dcnt;
         HX.best = S.ob2;
         HX.flags = S.of2;
         HX.grid_cap = (int64_t)256 * 16 / (pscl_decode_wpg(HX) > 0 ? pscl_decode_wpg(HX) : 1);
         QD = Q;
         QD.init = 0;
-        QD.in_count = S.dcnt;
-        QD.in_list = S.dlist;
         QD.ob = S.ob2;
         QD.of = S.of2;
+        HIP_TRY(hipMemsetAsync(S.dcnt, 0, (size_t)(rounds + 1) * bstride * 4, st));
     }
+    auto side_list = [&](int r) { return S.dlist + (size_t)r * PSCL_DL_NSEG * (size_t)A; };
+    auto side_cnt = [&](int r) { return S.dcnt + (size_t)r * bstride; };
     Q.init = 0;
     for (int r = 0; r < rounds; ++r) {  // no host round trips: the counts stay on the device
         H.elist = lists[r & 1];
         H.bcount = S.bcnt + (size_t)r * bstride;
         if (scr) {
-            if (r > 0) HIP_TRY(hipStreamWaitEvent(st, ev_d, 0));  // the previous round's deferred entries
-            HIP_TRY(hipMemsetAsync(S.dcnt, 0, bstride * 4, st));
             HA.elist = H.elist;
             HA.bcount = H.bcount;
+            HA.amb_elist = side_list(r);  // (the side chain's round-r list: appended beside QD(r - 1))
+            HA.amb_count = side_cnt(r);
             if ((e = pscl_launch_decode(HA, 0, st)) != hipSuccess)
                 return fail(PSCL_EDEVICE, "screening retry decode: %s", hipGetErrorString(e));
             HIP_TRY(hipEventRecord(ev_s, st));
+            // side round r: after the main round's deferrals (ev_s) and side round r - 1 (stream order)
             HIP_TRY(hipStreamWaitEvent(side, ev_s, 0));
+            HX.elist = side_list(r);
+            HX.bcount = side_cnt(r);
             if ((e = pscl_launch_decode(HX, 0, side)) != hipSuccess)
                 return fail(PSCL_EDEVICE, "exact retry re-decode: %s", hipGetErrorString(e));
-            QD.out_count = S.bcnt + (size_t)(r + 1) * bstride;
-            QD.out_list = lists[(r + 1) & 1];
+            QD.in_list = side_list(r);
+            QD.in_count = side_cnt(r);
+            QD.out_list = side_list(r + 1);
+            QD.out_count = side_cnt(r + 1);
             if ((e = pscl_launch_dl_post(QD, A, side)) != hipSuccess)
                 return fail(PSCL_EDEVICE, "dl_post launch: %s", hipGetErrorString(e));
-            HIP_TRY(hipEventRecord(ev_d, side));
         } else if ((rc = launch_decode(h, H, 0, st))) {
             return rc;
         }
@@ -956,7 +962,10 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
         if ((e = pscl_launch_dl_post(Q, A, st)) != hipSuccess)
             return fail(PSCL_EDEVICE, "dl_post launch: %s", hipGetErrorString(e));
     }
-    if (scr && rounds > 0) HIP_TRY(hipStreamWaitEvent(st, ev_d, 0));
+    if (scr && rounds > 0) {  // the chain ends with its side chain
+        HIP_TRY(hipEventRecord(ev_d, side));
+        HIP_TRY(hipStreamWaitEvent(st, ev_d, 0));
+    }
     return PSCL_OK;
 }
 
@@ -1112,7 +1121,8 @@ int dl_setup(pscl_handle* h, const pscl_dl_call& a, DlBufs& b) {
         // failing frames, which may still exceed half the chunk); chain 1 at most half
         const size_t c = (size_t)(i == 0 ? cap : cap - cap / 2);
         const size_t sz[14] = {(size_t)(rounds + 1) * NS * PSCL_DL_CSTRIDE * 4, NS * c * 4, NS * c * 4, c * 16, c * 4,
-                               c * 2 * W * 8, c * NS * 8, c * 16, c * W * 8, c, NS * PSCL_DL_CSTRIDE * 4, NS * c * 4,
+                               c * 2 * W * 8, c * NS * 8, c * 16, c * W * 8, c,
+                               (size_t)(rounds + 1) * NS * PSCL_DL_CSTRIDE * 4, (size_t)(rounds + 1) * NS * c * 4,
                                c * W * 8, c};
         static const int slot[2][14] = {{12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 8, 9, 10, 11},
                                         {40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 24, 29}};
