@@ -398,8 +398,9 @@ def extra_configs(args, ctx: Ctx, orc: Oracle | None):
                "side_stream_kernel_ms_per_step": r["side_ms"] / args.extra_steps, "side_stream_launches": r["side_launches"],
                "kernel": ("scl_lane_kernel<4> screening + scl128_kernel<4> exact re-decode (pipelined)"
                           if name.startswith("config2") else
-                          "scl128_kernel<4> baseline + scl128_kernel<4,FS> warm-started retry decodes + dl_post_kernel"
-                          " rounds" if name.startswith("config4") else
+                          "scl128_kernel<4> baseline + retry rounds beside the next step's baseline: scl_lane_kernel<4,FS>"
+                          " screened warm-started retry decodes, scl128_kernel<4,FS> exact decodes of the deferred entries"
+                          " (side chain), dl_post_kernel" if name.startswith("config4") else
                           "scl128_kernel<8,CH,CODE=2> screening (de-rate-match in staging) + exact re-decode"
                           " (pipelined)"),
                "kernel_timing": ("HIP events around each decode launch: main stream = the screening (plain) or "
