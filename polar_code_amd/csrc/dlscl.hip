@@ -227,6 +227,9 @@ __global__ void __launch_bounds__(256) replay_kernel(const pscl_replay_params R,
 #ifndef PSCL_POST_UNROLL
 #define PSCL_POST_UNROLL 4
 #endif
+#ifndef PSCL_POST_BETA32
+#define PSCL_POST_BETA32 1
+#endif
 #ifndef PSCL_POST_BETA_LDS
 #define PSCL_POST_BETA_LDS 1
 #endif
@@ -270,16 +273,19 @@ template <int NC, int KC, int PW>
 __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PSCL_POST_WPE))) dl_post_kernel(const pscl_post_params Q, int beta_lds) {
     constexpr int kPostWaves = PW, kPostChunk = PostShared<PW>::kChunk;
     __shared__ PostShared<PW> S;
-    extern __shared__ double sbeta[];  // [K][K] when beta_lds
+    extern __shared__ double sbeta[];  // [K][K]: fp64 when beta_lds == 1, fp32 when 2
+    float* const sbeta32 = reinterpret_cast<float*>(sbeta);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int hs = lane >> 5, hl = lane & 31, hb = lane & 32;  // half, lane in half, half's first lane
     const int N = NC ? NC : Q.N, K = KC ? KC : Q.K, W = KC ? (KC + 63) / 64 : Q.W, n = NC ? 7 : Q.n;
     for (int i = threadIdx.x; i < PSCL_EXP_TABLE_WORDS; i += blockDim.x) S.exp_table[i] = Q.exp_table[i];
-    if (beta_lds)
+    if (beta_lds == 1)
         for (int i = threadIdx.x; i < K * K; i += blockDim.x) sbeta[i] = Q.beta[i];
+    else if (beta_lds == 2)
+        for (int i = threadIdx.x; i < K * K; i += blockDim.x) sbeta32[i] = (float)Q.beta[i];
     if (threadIdx.x < PSCL_DL_NSEG) S.lcnt[threadIdx.x] = 0;
     if (threadIdx.x == 0) S.nst = 0;
-    const double* beta = beta_lds ? sbeta : Q.beta;
+    const double* beta = beta_lds == 1 ? sbeta : Q.beta;  // (the exact sums: fp64 beta)
     const uint64_t info0 = Q.info_mask[0], info1 = Q.info_mask[1];
     const int ninfo0 = __popcll(info0);
     int pre[PSCL_DL_NSEG + 1];
@@ -488,13 +494,24 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
                     // same index back)
 #pragma unroll
                     for (int m = 0; m < MC; ++m) qv[m] = 0.0;
-                    const double* bc = beta + hl;
+                    if (beta_lds == 2) {  // (narrow form: beta staged in LDS as fp32, see e2 below)
+                        const float* bc = sbeta32 + hl;
 #pragma unroll PSCL_POST_UNROLL
-                    for (int k = 0; k < K; ++k) {
-                        const double ak = nxt[k];
+                        for (int k = 0; k < K; ++k) {
+                            const double ak = nxt[k];
 #pragma unroll
-                        for (int m = 0; m < MC; ++m)
-                            if (hl + 32 * m < K) qv[m] = __builtin_fma(ak, bc[k * K + 32 * m], qv[m]);
+                            for (int m = 0; m < MC; ++m)
+                                if (hl + 32 * m < K) qv[m] = __builtin_fma(ak, (double)bc[k * K + 32 * m], qv[m]);
+                        }
+                    } else {
+                        const double* bc = beta + hl;
+#pragma unroll PSCL_POST_UNROLL
+                        for (int k = 0; k < K; ++k) {
+                            const double ak = nxt[k];
+#pragma unroll
+                            for (int m = 0; m < MC; ++m)
+                                if (hl + 32 * m < K) qv[m] = __builtin_fma(ak, bc[k * K + 32 * m], qv[m]);
+                        }
                     }
                     argmin();
                     double as = 0.0;
@@ -502,7 +519,10 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
                     for (int m = 0; m < MC; ++m) as = as + (hl + 32 * m < K ? nxt[hl + 32 * m] : 0.0);
 #pragma unroll
                     for (int sft = 1; sft < 32; sft <<= 1) as = as + pscl_asf64(pscl::shfl_u64(pscl_asu64(as), lane ^ sft));
-                    const double e2 = as * Q.beta_absmax * (264.0 * 0x1p-53);  // 2 E, with 1.5 % slack
+                    // 2 E, with 1.5 % slack; fp32 beta adds |beta32 - beta| <= 2^-24 |beta| + 2^-150 per
+                    // term, i.e. 2^-24 S + 2^-150 ||L0||_1 (2 % slack on the doubled bound)
+                    const double e2 = beta_lds == 2 ? as * Q.beta_absmax * (264.0 * 0x1p-53 + 2.04 * 0x1p-24) + as * 0x1p-140
+                                                    : as * Q.beta_absmax * (264.0 * 0x1p-53);
                     double qmine = qv[0];
 #pragma unroll
                     for (int m = 1; m < MC; ++m) qmine = (bj >> 5) == m ? qv[m] : qmine;
@@ -770,8 +790,13 @@ hipError_t pscl_launch_dl_post(const pscl_post_params& Q, int64_t entries, hipSt
     int64_t grid = (entries + PW * 2 * pairs - 1) / (PW * 2 * pairs);
     const int64_t gcap = Q.grid_cap >= 16 && Q.grid_cap <= 4096 ? Q.grid_cap : PSCL_POST_GRID;  // (tuning knob)
     if (grid > gcap) grid = gcap;
-    const int beta_lds = PSCL_POST_BETA_LDS && !Q.narrow && Q.beta && (size_t)Q.K * Q.K * 8 <= 32 * 1024;  // (LDS <= 64 KB)
-    const size_t lds = beta_lds ? (size_t)Q.K * Q.K * 8 : 0;
+    // beta in LDS: fp64 in the wide form (LDS <= 64 KB), fp32 in the narrow one (16 KB at K = 64, beside
+    // the next call's baseline; its rows read through L2 lost to that baseline's streaming: the flip
+    // metric measured 48 of 109 us per pass, profiles/r04p2_post_trace.txt)
+    const int beta_lds = !Q.beta ? 0
+                         : (PSCL_POST_BETA_LDS && !Q.narrow && (size_t)Q.K * Q.K * 8 <= 32 * 1024) ? 1
+                         : (PSCL_POST_BETA32 && Q.narrow && (size_t)Q.K * Q.K * 4 <= 16 * 1024) ? 2 : 0;
+    const size_t lds = beta_lds == 1 ? (size_t)Q.K * Q.K * 8 : beta_lds == 2 ? (size_t)Q.K * Q.K * 4 : 0;
     const dim3 g((unsigned)grid), b(PW * 64);
     if (Q.narrow) {
         if (Q.N == 128 && Q.K == 64)
