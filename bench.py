@@ -398,7 +398,7 @@ def extra_configs(args, ctx: Ctx, orc: Oracle | None):
                "side_stream_kernel_ms_per_step": r["side_ms"] / args.extra_steps, "side_stream_launches": r["side_launches"],
                "kernel": ("scl_lane_kernel<4> screening + scl128_kernel<4> exact re-decode (pipelined)"
                           if name.startswith("config2") else
-                          "scl128_kernel<4> baseline + retry rounds beside the next step's baseline: scl_lane_kernel<4,FS>"
+                          "scl_lane_kernel<4> baseline + retry rounds beside the next step's baseline: scl_lane_kernel<4,FS>"
                           " screened warm-started retry decodes, scl128_kernel<4,FS> exact decodes of the deferred entries"
                           " (side chain), dl_post_kernel" if name.startswith("config4") else
                           "scl128_kernel<8,CH,CODE=2> screening (de-rate-match in staging) + exact re-decode"
@@ -507,7 +507,7 @@ def launch_ranks(n: int) -> int:
 def dominant_kernel(N, K, L, E, retries):
     """The kernel the step's dominant launch runs (pscl_launch_decode's choice for a plain or
     DL-SCL baseline decode of this configuration)."""
-    if N == 128 and K == 64 and not E and (L == 8 or (L == 4 and not retries)):
+    if N == 128 and K == 64 and not E and L in (4, 8):
         return f"scl_lane_kernel<{L}> screening pass" + (" (DL-SCL baseline)" if retries else "")
     if N == 128 and L <= 8:
         return f"scl128_kernel<{L}> " + ("baseline decode" if retries else "screening pass")

@@ -313,8 +313,7 @@ int pscl_join(pscl_handle* h);
  *                           screens every chain that runs beside a later baseline decode, a
  *                           pipelined call's or a chunk's)
  *   PSCL_TUNE_DL_LANE       1: a DL-SCL baseline decode (N = 128) on the lane-per-path screening
- *                           kernel; 2: on the two-lanes-per-path one (default: 1 at L = 8, 2 at
- *                           L = 4)
+ *                           kernel (default); 2: on the two-lanes-per-path one
  *   PSCL_TUNE_DL_RETRY_LANE 2: screened retry decodes (N = 128) on the two-lanes-per-path forced-
  *                           bit instance instead of the lane-per-path one (default)
  *   PSCL_TUNE_POST_PAIRS    1..32: entry pairs per wavefront the DL-SCL post pass grid is sized for

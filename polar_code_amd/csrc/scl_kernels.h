@@ -261,9 +261,12 @@ hipError_t pscl_launch_count_reduce(int32_t* cpart, int64_t slots, int64_t* coun
 #define PSCL_DL_SCREEN_MIN 24576
 #endif
 // the DL-SCL baseline decode's screening kernel at N = 128 (PSCL_TUNE_DL_LANE default): 1 the
-// lane-per-path kernel, 2 the two-lanes-per-path one, 0 by list size (lane-per-path at L = 8)
+// lane-per-path kernel, 2 the two-lanes-per-path one, 0 by list size (lane-per-path at L = 8).
+// 1: with the lighter retry chains of round 4 (screened lane-per-path retry decodes, side chain,
+// fp32 beta in LDS) the lane kernel wins at L = 4 too (config 4: 2.86-2.91 against 3.08-3.09 ms,
+// profiles/r04k2_dl_knobs.txt)
 #ifndef PSCL_DL_LANE_DEFAULT
-#define PSCL_DL_LANE_DEFAULT 0
+#define PSCL_DL_LANE_DEFAULT 1
 #endif
 // scl_lane_long.hip: the lane-per-path screening decoder of the long codes (N = 256..1024, L = 4, 8)
 int pscl_lane_long_available(const pscl_decode_params& P);
