@@ -193,33 +193,81 @@ def host_internal_llrs(llrE: np.ndarray, N: int) -> np.ndarray:
     return np.stack([subblock_deinterleave(derate_match_polar(r, N), N) for r in llrE])
 
 
-def cpu_baseline(orc: Oracle, llr_host: np.ndarray, info, L: int, budget_s: float, retries: int = 0, beta=None):
-    """The oracle timed on the host cores on a bounded sample of the step-0 batch.  Returns the
-    baseline record and the oracle's outputs for the first pass (kept for the parity check)."""
-    n0 = min(4000, llr_host.shape[0])
+def _cpu_quota():
+    """The cgroup CPU quota of this process in CPUs (cgroup v2 cpu.max, v1 cfs files), or None."""
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read_text())
+        per = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
+def _timed_sample(fn, n0: int, n_max: int, budget_s: float):
+    """Calibrate on n0 frames, then repeat a sample sized for the budget until ~80 % of it is
+    spent.  Returns (frames done, seconds, distinct frames per pass, first pass's output)."""
     t0 = time.perf_counter()
-    orc.run(llr_host[:n0], info, L, retries, beta)  # warm-up / calibration
+    fn(n0)
     rate = n0 / max(time.perf_counter() - t0, 1e-6)
-    n = int(min(llr_host.shape[0], max(n0, rate * budget_s)))
+    n = int(min(n_max, max(n0, rate * budget_s)))
     done, dt, first = 0, 0.0, None
     t0 = time.perf_counter()
-    while dt < budget_s * 0.8 or done == 0:  # repeat the sample until the budget is spent
-        out = orc.run(llr_host[:n], info, L, retries, beta)
-        first = first or out
+    while dt < budget_s * 0.8 or done == 0:
+        out = fn(n)
+        first = first if first is not None else out
         done += n
         dt = time.perf_counter() - t0
-    what = (f"decode_with_retries (SCL L={L} + up to {retries} flips, beta)" if retries > 0
-            else f"decode_scl L={L} + CRC select")
+    return done, dt, n, first
+
+
+def cpu_baseline(orc: Oracle, llr_host: np.ndarray, info, L: int, budget_s: float, retries: int = 0, beta=None,
+                 product_s: float = 6.0):
+    """The oracle timed on the host cores on a bounded sample of the step-0 batch, with one OpenMP
+    thread per CPU of this process's affinity mask (P = the host's usable CPUs), and
+    beside it the product's own host decoder (pscl_decode_cpu, csrc/scl_cpu.cpp) on the same
+    threads.  Returns the baseline record and the oracle's outputs for the first pass (kept for the
+    parity check)."""
     try:
         aff = sorted(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         aff = None
+    P = len(aff) if aff else (os.cpu_count() or 1)
+    orc.o.set_num_threads(P)
+    n0 = min(max(4000, 8 * P), llr_host.shape[0])
+    done, dt, n, first = _timed_sample(lambda k: orc.run(llr_host[:k], info, L, retries, beta), n0,
+                                       llr_host.shape[0], budget_s)
+    what = (f"decode_with_retries (SCL L={L} + up to {retries} flips, beta)" if retries > 0
+            else f"decode_scl L={L} + CRC select")
+    quota = _cpu_quota()
     rec = {"value": done / dt, "unit": "frames/s", "cores": orc.o.num_threads(), "kind": "port",
            "threads_used": orc.o.num_threads(), "host_cpu_count": os.cpu_count(),
            "affinity_cpus": len(aff) if aff is not None else None,
            "affinity_mask": _cpu_ranges(aff) if aff is not None else None,
+           "cgroup_cpu_quota": quota,
+           "per_thread": done / dt / max(orc.o.num_threads(), 1),
+           "per_quota_cpu": done / dt / quota if quota else None,
            "sample": f"{done} frames ({n} distinct frames of the step-0 batch, same LLRs as the GPU) through "
-                     f"oracle/scl_oracle.c (C restatement of {what}), OpenMP over frames, {dt:.1f} s"}
+                     f"oracle/scl_oracle.c (C restatement of {what}), OpenMP over frames, {P} threads "
+                     f"(one per CPU of the affinity mask), {dt:.1f} s"}
+    if retries == 0:  # the product's own host decoder (no DL-SCL loop on the host path)
+        try:
+            from polar_code_amd import _native
+
+            cdec = _native.CpuDecoder(llr_host.shape[1], info, L, POLY, threads=P)
+            pdone, pdt, pn, _ = _timed_sample(
+                lambda k: cdec.decode(llr_host[:k], want_metrics=False, want_cands=False, want_info_llrs=False),
+                n0, llr_host.shape[0], product_s)
+            rec["product_cpu_decoder"] = {
+                "value": pdone / pdt, "unit": "frames/s", "threads_used": P, "per_thread": pdone / pdt / P,
+                "sample": f"{pdone} frames ({pn} distinct) through pscl_decode_cpu (csrc/scl_cpu.cpp, the "
+                          f"product's host decoder, bit-exact), std::thread over frames, {pdt:.1f} s"}
+        except Exception as ex:  # reported, never fatal to the GPU line
+            rec["product_cpu_decoder"] = {"error": str(ex)}
     return rec, first, n
 
 

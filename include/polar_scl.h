@@ -317,7 +317,7 @@ int pscl_join(pscl_handle* h);
  *   PSCL_TUNE_DL_RETRY_LANE 2: screened retry decodes (N = 128) on the two-lanes-per-path forced-
  *                           bit instance instead of the lane-per-path one (default)
  *   PSCL_TUNE_POST_PAIRS    1..32: entry pairs per wavefront the DL-SCL post pass grid is sized for
- *                           (default 4; capped by PSCL_TUNE_POST_GRID)
+ *                           (default 2, PSCL_POST_PAIRS in dlscl.hip; capped by PSCL_TUNE_POST_GRID)
  */
 #define PSCL_TUNE_DL_SCREEN 1
 #define PSCL_TUNE_DL_CHUNKS 2

@@ -36,6 +36,7 @@ def lib() -> C.CDLL:
         L.oracle_dl_batch.argtypes = [dp, C.c_int64, C.c_int, ip, C.c_int, C.c_int, C.c_int, C.c_uint64,
                                       C.POINTER(C.c_float), bp, ip, ip]
         L.oracle_num_threads.restype = C.c_int
+        L.oracle_set_num_threads.argtypes = [C.c_int]
         L.oracle_logaddexp0_batch.argtypes = [dp, C.c_int64, dp]
         _LIB = L
     return _LIB
@@ -165,6 +166,11 @@ def dl_batch(llr, info, M, retries, crc=None, beta=None):
 
 def num_threads() -> int:
     return int(lib().oracle_num_threads())
+
+
+def set_num_threads(n: int) -> None:
+    """OpenMP thread count of decode_batch / dl_batch (n > 0)."""
+    lib().oracle_set_num_threads(int(n))
 
 
 def logaddexp0(v):

@@ -555,6 +555,16 @@ int oracle_num_threads(void) {
 #endif
 }
 
+/* thread count of the batch entry points (bench.py's cpu_baseline: one per CPU of the affinity mask) */
+void oracle_set_num_threads(int n) {
+#ifdef _OPENMP
+    extern void omp_set_num_threads(int);
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}
+
 /* np.logaddexp(0, v) as the reference computes it (for host checks of the device port) */
 void oracle_logaddexp0_batch(const double* v, int64_t n, double* out) {
     for (int64_t i = 0; i < n; i++) out[i] = logaddexp0(v[i]);

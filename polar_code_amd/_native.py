@@ -407,6 +407,12 @@ class Decoder:
             if k not in TUNE:
                 raise ValueError(f"unknown tuning knob {k!r}")
             check(lib().pscl_set_tuning(self._h, TUNE[k], int(v)))
+            tun = self.__dict__.setdefault("_tuning", {})
+            tun[k] = int(v)
+
+    def get_tuning(self) -> dict:
+        """The knobs set on this handle through set_tuning (0 = default for any other knob)."""
+        return dict(self.__dict__.get("_tuning", {}))
 
     def set_screening(self, on: bool = True) -> None:
         """Screening decode for plain decodes (default on; include/polar_scl.h)."""

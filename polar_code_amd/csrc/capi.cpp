@@ -8,6 +8,8 @@
 // is the handle-free pscl_decode_cpu (scl_cpu.cpp).
 #include <hip/hip_runtime.h>
 #include <math.h>
+
+#include <cmath>
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -137,6 +139,7 @@ struct pscl_handle {
     int32_t* h_count = nullptr;          // pinned: failing-frame counts of the chunk parities
     double* d_beta = nullptr;         // [K][K] DL-SCL flip metric (null = |L0|)
     double beta_absmax = 0.0;         // max |beta| (dl_post_kernel's certificate)
+    std::vector<double> beta_host;    // staging of the last pscl_set_beta upload (stream-ordered copy)
     uint64_t* d_epi = nullptr;        // scl128 epilogue tables (gather + syndrome)
     uint64_t* d_xtab = nullptr;       // TX: codeword of each message byte value
     uint32_t* d_crctab = nullptr;     // TX: CRC remainder of each payload byte value
@@ -530,6 +533,20 @@ int pscl_create(pscl_handle** out, int device, int N, const int32_t* info_set, i
     if (K > 0) CREATE_TRY(hipMemcpy(h->d_info_set, h->info_set.data(), (size_t)K * 4, hipMemcpyHostToDevice));
     CREATE_TRY(hipMemcpy(h->d_exp_table, kExpTable, sizeof(kExpTable), hipMemcpyHostToDevice));
     {
+        // NR sub-block interleaver tables (interleaver.py:10-37: order[k] = (k % 32) nb + k / 32 over
+        // nb * 32 positions, the identity when N < 32) -- a function of N alone, so they are uploaded
+        // here once; pscl_set_rate_match only switches rate matching on or off (no device write
+        // while pipelined work may be reading them)
+        std::vector<int32_t> order((size_t)N), src((size_t)N);
+        const int nb = (N + 31) / 32;
+        for (int k = 0; k < N; ++k) order[(size_t)k] = N >= 32 ? (k % 32) * nb + k / 32 : k;
+        for (int k = 0; k < N; ++k) src[(size_t)order[(size_t)k]] = k;
+        CREATE_TRY(hipMalloc(&h->d_rm_src, (size_t)N * 4));
+        CREATE_TRY(hipMalloc(&h->d_rm_order, (size_t)N * 4));
+        CREATE_TRY(hipMemcpy(h->d_rm_src, src.data(), (size_t)N * 4, hipMemcpyHostToDevice));
+        CREATE_TRY(hipMemcpy(h->d_rm_order, order.data(), (size_t)N * 4, hipMemcpyHostToDevice));
+    }
+    {
         // scl128 epilogue: gather[k][v] = the information bits of u-byte k (value v), compacted
         // in index order; syn[m][v] = XOR of the CRC check columns of info bits 4m..4m+3 set in v
         // (N > 128: N / 8 gather tables, scl_lane_long.hip)
@@ -797,13 +814,24 @@ int pscl_set_beta(pscl_handle* h, const double* beta) {
         return PSCL_OK;
     }
     if (h->K == 0) return fail(PSCL_EINVAL, "beta must be a square matrix matching abs_l0 length");
-    const size_t bytes = (size_t)h->K * h->K * 8;
-    if (!h->d_beta) HIP_TRY(hipMalloc(&h->d_beta, bytes));
-    HIP_TRY(hipStreamSynchronize(h->stream));  // a previous round may still read the old matrix
-    HIP_TRY(hipMemcpy(h->d_beta, beta, bytes, hipMemcpyHostToDevice));
+    const size_t n = (size_t)h->K * h->K;
+    if (!h->d_beta) HIP_TRY(hipMalloc(&h->d_beta, n * 8));
+    // stream-ordered upload: enter() made the handle's stream wait for every pending pipelined
+    // round (which may still read the old matrix), so the copy lands after them and before any
+    // later launch; the host staging buffer is rewritten only once the previous upload is done
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    h->beta_host.assign(beta, beta + n);
+    HIP_TRY(hipMemcpyAsync(h->d_beta, h->beta_host.data(), n * 8, hipMemcpyHostToDevice, h->stream));
     double mx = 0.0;
-    for (size_t i = 0; i < (size_t)h->K * h->K; ++i) mx = fabs(beta[i]) > mx ? fabs(beta[i]) : mx;
-    h->beta_absmax = mx != mx ? INFINITY : mx;  // (NaN: every certificate fails, exact sums)
+    bool nan = false;
+    for (size_t i = 0; i < n; ++i) {
+        const double a = fabs(beta[i]);
+        if (std::isnan(a))
+            nan = true;
+        else if (a > mx)
+            mx = a;
+    }
+    h->beta_absmax = nan ? INFINITY : mx;  // (a NaN entry: every certificate fails, exact sums)
     return PSCL_OK;
 }
 
@@ -1609,20 +1637,10 @@ int pscl_set_rate_match(pscl_handle* h, int E) {
         h->rm_E = 0;
         return PSCL_OK;
     }
-    const int N = h->N;
-    if (E > N && N < 32)
+    if (E > h->N && h->N < 32)
         return fail(PSCL_EUNSUP, "repetition (E > N) needs N >= 32 (sub-block interleaver without padding)");
-    // interleaver.py:10-37: order[k] = (k % 32) * nb + k / 32 over nb*32 positions (identity when N < 32)
-    std::vector<int32_t> order((size_t)N), src((size_t)N);
-    const int nb = (N + 31) / 32;
-    for (int k = 0; k < N; ++k) order[(size_t)k] = N >= 32 ? (k % 32) * nb + k / 32 : k;
-    for (int k = 0; k < N; ++k) src[(size_t)order[(size_t)k]] = k;
-    int rc = enter(h);
-    if (rc) return rc;
-    if (!h->d_rm_src) HIP_TRY(hipMalloc(&h->d_rm_src, (size_t)N * 4));
-    if (!h->d_rm_order) HIP_TRY(hipMalloc(&h->d_rm_order, (size_t)N * 4));
-    HIP_TRY(hipMemcpy(h->d_rm_src, src.data(), (size_t)N * 4, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(h->d_rm_order, order.data(), (size_t)N * 4, hipMemcpyHostToDevice));
+    // (the interleaver tables depend on N only: uploaded by pscl_create; later launches read rm_E
+    // from their parameter block, so switching it never races with enqueued work)
     h->rm_E = E;
     return PSCL_OK;
 }
@@ -1685,9 +1703,9 @@ int pscl_screening_count(pscl_handle* h, int64_t* count) {
     if (!h->screened || !h->scratch[h->screened_slot].p) return PSCL_OK;
     int rc = enter(h);
     if (rc) return rc;
-    HIP_TRY(hipStreamSynchronize(h->stream));
     int32_t c = 0;
-    HIP_TRY(hipMemcpy(&c, h->scratch[h->screened_slot].p, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyAsync(&c, h->scratch[h->screened_slot].p, 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
     *count = c;
     return PSCL_OK;
 }

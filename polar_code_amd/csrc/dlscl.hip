@@ -519,10 +519,13 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
                     for (int m = 0; m < MC; ++m) as = as + (hl + 32 * m < K ? nxt[hl + 32 * m] : 0.0);
 #pragma unroll
                     for (int sft = 1; sft < 32; sft <<= 1) as = as + pscl_asf64(pscl::shfl_u64(pscl_asu64(as), lane ^ sft));
-                    // 2 E, with 1.5 % slack; fp32 beta adds |beta32 - beta| <= 2^-24 |beta| + 2^-150 per
-                    // term, i.e. 2^-24 S + 2^-150 ||L0||_1 (2 % slack on the doubled bound)
-                    const double e2 = beta_lds == 2 ? as * Q.beta_absmax * (264.0 * 0x1p-53 + 2.04 * 0x1p-24) + as * 0x1p-140
-                                                    : as * Q.beta_absmax * (264.0 * 0x1p-53);
+                    // 2 E = 2 (gamma_K + gamma_K+1) S <= (4 K + 2 + slack) u S, u = 2^-53 (K = 64:
+                    // 264 u, 2.3 % slack; the bound grows with K, so the (128,88) and runtime-K
+                    // instances get their own); fp32 beta adds |beta32 - beta| <= 2^-24 |beta| + 2^-150
+                    // per term, i.e. 2^-24 S + 2^-150 ||L0||_1 (2 % slack on the doubled bound)
+                    const double gk = (4.0 * (double)K + 8.0) * 0x1p-53;
+                    const double e2 = beta_lds == 2 ? as * Q.beta_absmax * (gk + 2.04 * 0x1p-24) + as * 0x1p-140
+                                                    : as * Q.beta_absmax * gk;
                     double qmine = qv[0];
 #pragma unroll
                     for (int m = 1; m < MC; ++m) qmine = (bj >> 5) == m ? qv[m] : qmine;

@@ -56,6 +56,13 @@ struct LaneLayout {
 #define PSCL_LANE_CREG4 1
 #endif
 
+// timing-only ablations of the plain kernel (tools/build_variant.py; 0 in the product): 1 every
+// full-list information phase ranked (outputs still exact), 2 never ranked (invalid outputs), 4 no
+// depth-1..3 recompute (invalid), 8 no epilogue table lookups (invalid)
+#ifndef PSCL_LANE_ABL
+#define PSCL_LANE_ABL 0
+#endif
+
 #ifndef PSCL_LANE_WAVES_PER_EU
 #define PSCL_LANE_WAVES_PER_EU 2
 #endif
@@ -179,7 +186,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
 #endif
 
             // ---- depths 1-3 recomputed from the channel (phi % 16 == 0)
-            if constexpr (start <= 3) {
+            if constexpr (start <= 3 && !(PSCL_LANE_ABL & 4)) {
                 constexpr bool r1 = phi >= 64, r2 = (phi >> 5) & 1, r3 = (phi >> 4) & 1;
                 if constexpr (!CREG && phi > 0) load_chan();
                 uint4* const xs = reinterpret_cast<uint4*>(Af + Ly::OFF6);
@@ -412,7 +419,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
                 atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + ((badm & vmask) == 0 ? 12 : (one ? 13 : 14)), 1ULL);
             }
 #endif
-            if ((badm & vmask) == 0) {
+            if ((PSCL_LANE_ABL & 2) || ((badm & vmask) == 0 && !(PSCL_LANE_ABL & 1))) {
                 metric = mg;
                 lastbit = gbit;
                 if (phi < 64) u0 |= (uint64_t)gbit << phi; else u1 |= (uint64_t)gbit << (phi - 64);
@@ -426,7 +433,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
             // when w and the second-largest better child are both below gmax by the margin (every
             // other worse child already clears every better child, hence w too); else the frame is
             // deferred (its boundary is within the margin, which no ranking could certify either)
-            if ((wmask(__builtin_popcount(bad8) > 1) & vmask) == 0) {
+            if (!(PSCL_LANE_ABL & 1) && (wmask(__builtin_popcount(bad8) > 1) & vmask) == 0) {
                 const uint32_t kg = hiw(mg);
                 const uint32_t gmaxh = frame_max<G>(kg);
                 const bool ismax = kg == gmaxh;
@@ -531,7 +538,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 const uint32_t byte = (uint32_t)(((k < 8 ? u0 : u1) >> (8 * (k & 7))) & 255u);
-                const uint64_t cb = GT[k * 256 + byte];
+                const uint64_t cb = (PSCL_LANE_ABL & 8) ? (uint64_t)byte : GT[k * 256 + byte];
                 if (off < 64) {
                     ib0 |= cb << off;
                     if (off > 56) ib1 |= cb >> (64 - off);
@@ -546,7 +553,8 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
             constexpr int k4 = (K + 3) >> 2;
 #pragma unroll
             for (int m = 0; m < k4; ++m)
-                syn ^= ST[m * 16 + (uint32_t)(((m < 16 ? ib0 : ib1) >> (4 * (m & 15))) & 15u)];
+                syn ^= (PSCL_LANE_ABL & 8) ? (uint32_t)(((m < 16 ? ib0 : ib1) >> (4 * (m & 15))) & 15u) << m
+                                           : ST[m * 16 + (uint32_t)(((m < 16 ? ib0 : ib1) >> (4 * (m & 15))) & 15u)];
         }
         // list position = rank of the metric among the frame's L (high words); certified when all
         // pairs are apart by the margin (then the ranks are distinct and equal the exact order).

@@ -179,7 +179,8 @@ def decode_with_retries_device(llr: np.ndarray, info_set, M: int, retries: int, 
     Returns best_bits [B, K] (final attempt), success [B], attempts [B], tried [B, R]
     (R = max(retries, 0), -1 padded), base_bits / base_pass (the baseline SCL), and with
     `msg` [B, K] the in-kernel counters {"scl": [...], "dl": [...]} (PSCL_CNT_* order).
-    `tuning`: schedule knobs for this call (Decoder.set_tuning; reset to the defaults after).
+    `tuning`: schedule knobs for this call (Decoder.set_tuning; the handle's previous values,
+    e.g. knobs a caller set on the shared decoder, are restored after).
     """
     llr = np.ascontiguousarray(llr, dtype=np.float64)
     B, N = llr.shape
@@ -189,13 +190,14 @@ def decode_with_retries_device(llr: np.ndarray, info_set, M: int, retries: int, 
     W = dec.W
     R = max(int(retries), 0)
     out = {}
+    prev = dec.get_tuning() if tuning else {}
     if tuning:
         dec.set_tuning(**tuning)
     try:
         _retries_device(dec, llr, B, W, R, K, retries, crc, beta, msg, out)
     finally:
         if tuning:
-            dec.set_tuning(**{k: 0 for k in tuning})
+            dec.set_tuning(**{k: prev.get(k, 0) for k in tuning})
     return out
 
 

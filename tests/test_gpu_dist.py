@@ -141,3 +141,47 @@ def test_world1_rccl_group_equals_no_group(tmp_path):
     assert out[True][0] == out[False][0] and out[True][0].count("\n") == 3
     assert out[True][1] == out[False][1]
     assert out[True][2] == out[False][2] and out[True][2]["frames"] == 300_000
+
+
+@pytest.mark.timeout(900)
+def test_bench_gpus2_default_extras_equal_world1():
+    """The driver's multi-GPU command with its default extras (`bench.py --gpus 2`, no --extra
+    none): every extra config and the config-3 sweep run under a 2-rank process group (rank 0's
+    oracle parity sample while the other rank waits at a collective included), rank 0's single
+    line carries extra_configs and config3_sweep_L8, and every counter equals the world-1 run
+    over the same global frames (world 1 decodes 2B frames per step, world 2 B per rank)."""
+    B, S, E = 20_000, 2, 2
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    env.update(PSCL_SHARE_GPU="1", PSCL_DIST_BACKEND="gloo")
+    line = {}
+    for gpus, frames in ((1, 2 * B), (2, B)):
+        cmd = [sys.executable, "bench.py", "--gpus", str(gpus), "--frames", str(frames), "--steps", str(S),
+               "--warmup", "1", "--extra-steps", str(E), "--extra-parity", "4000", "--cpu-seconds", "1"]
+        res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+        assert res.returncode == 0, (res.stdout + res.stderr)[-3000:]
+        lines = [x for x in res.stdout.splitlines() if x.startswith("{")]
+        assert len(lines) == 1, res.stdout[-2000:]
+        line[gpus] = json.loads(lines[0])
+    w1, w2 = line[1], line[2]
+    assert w2["n_gpus"] == 2 and w2["config"]["collective"] == "gloo"
+    assert w2["cpu_baseline"] is None and w1["cpu_baseline"] is not None  # an N = 1 figure only
+    assert w2["parity"]["mismatches"] == 0 and w1["parity"]["mismatches"] == 0
+    assert w1["fer"]["frames"] == w2["fer"]["frames"] == 2 * B * S
+    for k in ("frame_errors", "ber", "payload_fer", "payload_ber"):
+        assert w1["fer"][k] == w2["fer"][k], k
+    x1, x2 = w1["extra_configs"], w2["extra_configs"]
+    assert set(x1) == set(x2) == {"config2_scl_L4", "config4_dlscl_L4_r8_beta4", "config5_nr_E256_L8",
+                                  "config3_sweep_L8"}
+    for name in ("config2_scl_L4", "config4_dlscl_L4_r8_beta4", "config5_nr_E256_L8"):
+        assert x2[name]["fer"]["frames"] == x1[name]["fer"]["frames"] == 2 * B * E, name
+        assert x2[name]["fer"]["frame_errors"] == x1[name]["fer"]["frame_errors"], name
+        assert x2[name]["parity"]["mismatches"] == 0, name
+        if "dl_scl" in x1[name]:
+            assert x2[name]["dl_scl"]["frame_errors"] == x1[name]["dl_scl"]["frame_errors"], name
+    s1, s2 = x1["config3_sweep_L8"], x2["config3_sweep_L8"]
+    assert s1["frames_per_point"] == s2["frames_per_point"] == 2 * B
+    assert [p["snr_db"] for p in s2["points"]] == [4.0, 4.5, 5.0, 5.5, 6.0, 6.5]
+    for p1, p2 in zip(s1["points"], s2["points"]):
+        for k in ("fer_scl", "fer_dl", "fer_uncoded", "avg_retries"):
+            assert p1[k] == p2[k], (p1["snr_db"], k)

@@ -81,3 +81,14 @@ def test_philox_stream_ids_distinct_on_fine_grids():
         ids = [philox_stream_id(x) for x in grid]
         assert len(set(ids)) == len(ids), step
         assert all(0 <= i < 2 ** 32 for i in ids)
+    # negative grid points keep their historical 32-bit words (round(10 x) & 0xFFFFFFFF)
+    assert [philox_stream_id(x) for x in (-1.0, -0.5, -2.0)] == [0xFFFFFFF6, 0xFFFFFFFB, 0xFFFFFFEC]
+    # grids spanning negative and positive points, coarse and fine: no shared stream, and no
+    # off-grid word equals any grid word
+    for step in (0.1, 0.05, 0.01, 0.001):
+        grid = np.round(np.arange(-3.0, 3.0 + 1e-9, step), 6)
+        ids = [philox_stream_id(x) for x in grid]
+        assert len(set(ids)) == len(ids), step
+    on = {philox_stream_id(k / 10) for k in range(-2000, 2001)}
+    off = {philox_stream_id(x) for x in (-1e-6, -0.05, 0.05, -123.456789, 7.77)}
+    assert not (on & off)

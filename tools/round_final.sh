@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-4 final GPU pass on the frozen build: full GPU suite, smoke, default bench line,
+# Round-final GPU pass on the frozen build: full GPU suite, smoke, default bench line,
 # rocprofv3 kernel stats + PMC passes of the headline, long codes, config-3 sweep, kernel PMC of
 # configs 3 and 4.
-#   bash tools/r04_final.sh <tag>
+#   bash tools/round_final.sh <tag>
 set -o pipefail
-tag=${1:-r04z}
+tag=${1:?tag}
 bash tools/gpu_round.sh ${tag} || exit 1
 tail -3 gpurun_out/${tag}_gpu_tests.log
 python3 -c "
