@@ -44,6 +44,26 @@ __device__ __forceinline__ void rank_pair(uint32_t og, uint32_t ob, uint32_t kg,
         : "vcc");
 }
 
+// rank counts for the survivor selection (select_survivors): rg += [og < kg] + [ob < kg] (this
+// lane's better child against the other lane's two children), rbb += [ob < kb] (its worse child
+// against the other lane's worse child), the other lane read through the DPP permutation CTRL
+template <int CTRL>
+__device__ __forceinline__ void rank3(uint32_t og, uint32_t ob, uint32_t kg, uint32_t kb, uint32_t& rg, uint32_t& rbb) {
+    uint32_t t;
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_sub_co_u32_dpp %0, vcc, %3, %5 quad_perm:[%7,%8,%9,%10] row_mask:0xf bank_mask:0xf\n\t"
+        "v_addc_co_u32 %1, vcc, 0, %1, vcc\n\t"
+        "v_sub_co_u32_dpp %0, vcc, %4, %5 quad_perm:[%7,%8,%9,%10] row_mask:0xf bank_mask:0xf\n\t"
+        "v_addc_co_u32 %1, vcc, 0, %1, vcc\n\t"
+        "v_sub_co_u32_dpp %0, vcc, %4, %6 quad_perm:[%7,%8,%9,%10] row_mask:0xf bank_mask:0xf\n\t"
+        "v_addc_co_u32 %2, vcc, 0, %2, vcc"
+        : "=&v"(t), "+v"(rg), "+v"(rbb)
+        : "v"(og), "v"(ob), "v"(kg), "v"(kb), "i"(CTRL & 3), "i"((CTRL >> 2) & 3), "i"((CTRL >> 4) & 3),
+          "i"((CTRL >> 6) & 3)
+        : "vcc");
+}
+
 // max / min / sum of v over the G lanes of each frame (G = 4: two quad_perm steps; G = 8: and
 // the half-row mirror)
 template <int G>
@@ -76,6 +96,52 @@ __device__ __forceinline__ uint32_t frame_sum(uint32_t v) {
     v += dpp32<kQX2>(v);
     if constexpr (G == 8) v += dpp32<kHMIR>(v);
     return v;
+}
+
+// Survivor selection of a full list (the L smallest of each frame's 2L children): this lane's
+// better child key kg and worse child key kb (kb >= kg: the worse child pays |llr| more).  Keys are
+// counted strictly below, so with distinct keys keep_g / win_b are exact; equal keys can give a
+// wrong count, which the caller's certificate (exactly L survivors, margin between the largest
+// survivor and the smallest non-survivor) always rejects.
+//   PSCL_LANE_RANK3 = 1: rg = #{children below kg} (2L - 2 compares), d = the frame's number of
+//     dropped better children, and a worse child survives iff it is among the d smallest worse
+//     children (L - 1 compares): 3 compares per lane permutation.
+//   0: both children ranked among all 2L (4 compares per permutation).
+#ifndef PSCL_LANE_RANK3
+#define PSCL_LANE_RANK3 1
+#endif
+template <int G, int LMAX>
+__device__ __forceinline__ void select_survivors(uint32_t kg, uint32_t kb, bool& keep_g, bool& win_b) {
+#if PSCL_LANE_RANK3
+    uint32_t rg = 0, rbb = 0;
+    rank3<kQX1>(kg, kb, kg, kb, rg, rbb);
+    rank3<kQX2>(kg, kb, kg, kb, rg, rbb);
+    rank3<kQX3>(kg, kb, kg, kb, rg, rbb);
+    if constexpr (G == 8) {  // the other quad of the frame, through the half-row mirror
+        const uint32_t mkg = dpp32<kHMIR>(kg), mkb = dpp32<kHMIR>(kb);
+        rank3<kQID>(mkg, mkb, kg, kb, rg, rbb);
+        rank3<kQX1>(mkg, mkb, kg, kb, rg, rbb);
+        rank3<kQX2>(mkg, mkb, kg, kb, rg, rbb);
+        rank3<kQX3>(mkg, mkb, kg, kb, rg, rbb);
+    }
+    keep_g = rg < (uint32_t)LMAX;
+    const uint32_t d = frame_sum<G>(keep_g ? 0u : 1u);
+    win_b = rbb < d;
+#else
+    uint32_t rg = 0, rb = kg < kb ? 1u : 0u;
+    rank_pair<kQX1>(kg, kb, kg, kb, rg, rb);
+    rank_pair<kQX2>(kg, kb, kg, kb, rg, rb);
+    rank_pair<kQX3>(kg, kb, kg, kb, rg, rb);
+    if constexpr (G == 8) {
+        const uint32_t mkg = dpp32<kHMIR>(kg), mkb = dpp32<kHMIR>(kb);
+        rank_pair<kQID>(mkg, mkb, kg, kb, rg, rb);
+        rank_pair<kQX1>(mkg, mkb, kg, kb, rg, rb);
+        rank_pair<kQX2>(mkg, mkb, kg, kb, rg, rb);
+        rank_pair<kQX3>(mkg, mkb, kg, kb, rg, rb);
+    }
+    keep_g = rg < (uint32_t)LMAX;
+    win_b = rb < (uint32_t)LMAX;
+#endif
 }
 
 // position of the j-th set bit (j < popcount(m)) of a mask of at most 8 bits, branch-free

@@ -362,18 +362,8 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
                 {
                     // rank the 2L children of each frame: counts of keys (high words) strictly below each
                     const uint32_t kg = hiw(mg);
-                    uint32_t rg = 0, rb = kg < kb ? 1u : 0u;
-                    rank_pair<kQX1>(kg, kb, kg, kb, rg, rb);
-                    rank_pair<kQX2>(kg, kb, kg, kb, rg, rb);
-                    rank_pair<kQX3>(kg, kb, kg, kb, rg, rb);
-                    if constexpr (G == 8) {
-                        const uint32_t mkg = dpp32<kHMIR>(kg), mkb = dpp32<kHMIR>(kb);
-                        rank_pair<kQID>(mkg, mkb, kg, kb, rg, rb);
-                        rank_pair<kQX1>(mkg, mkb, kg, kb, rg, rb);
-                        rank_pair<kQX2>(mkg, mkb, kg, kb, rg, rb);
-                        rank_pair<kQX3>(mkg, mkb, kg, kb, rg, rb);
-                    }
-                    const bool keep_g = rg < (uint32_t)LMAX, win_b = rb < (uint32_t)LMAX;
+                    bool keep_g, win_b;
+                    select_survivors<G, LMAX>(kg, kb, keep_g, win_b);
                     const uint32_t kbu = hiw_up(mb);
                     const uint32_t su = keep_g ? (win_b ? kbu : kgu) : (win_b ? kbu : 0u);
                     const uint32_t nm = keep_g ? (win_b ? 0xffffffffu : kb) : kg;
