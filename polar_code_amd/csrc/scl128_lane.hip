@@ -94,7 +94,15 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
     const uint8_t* const GT = reinterpret_cast<const uint8_t*>(P.epi_table);   // [16][256] u-byte -> info bits
     const uint32_t* const ST = reinterpret_cast<const uint32_t*>(GT + 16 * 256);  // [K/4][16] nibble -> syndrome
     auto hiw = [](double m) { return (uint32_t)(pscl_asu64(m) >> 32); };
-    auto hiw_up = [&](double m) { return hiw(__builtin_fma(m, 1.0 + 0x1p-40, PSCL_TAIL_ABS_MARGIN)); };
+    // the margin-raised key hi(fma(m, 1 + 2^-40, MARGIN)) as one VOP3 fma with the factor in an SGPR
+    // (left to itself the compiler emits a copy of the margin register plus v_fmac_f64)
+    auto hiw_up = [&](double m) {
+        double r;
+        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(m), "s"(1.0 + 0x1p-40), "v"((double)PSCL_TAIL_ABS_MARGIN));
+        return hiw(r);
+    };
+    // this frame's G bits of a wave ballot (one 64-bit shift by the frame's first lane)
+    auto frame_bits = [&](uint64_t m) { return (uint32_t)(m >> gbase) & GM; };
 
     int cfe = 0, cbe = 0, cpe = 0, cpb = 0;  // this lane's error counts (flushed at the end)
     // frames of the launch: P.B, or (FS) the total of the round's bucket lists
@@ -321,8 +329,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
                 const bool bad = kb <= mx;
                 const uint64_t badm = wmask(bad);
                 if ((badm & fullm) != 0) {  // some full frame has a worse child within the margin
-                    const uint32_t sh = (uint32_t)gbase & 31u;
-                    const uint32_t bad8 = ((fl < F / 2 ? (uint32_t)badm : (uint32_t)(badm >> 32)) >> sh) & GM;
+                    const uint32_t bad8 = frame_bits(badm);
                     if ((wmask(__builtin_popcount(bad8) > 1) & fullm) == 0) {
                         // one swap per full frame at most (see the plain form below)
                         const uint32_t kg = hiw(mg);
@@ -348,9 +355,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
                         const uint32_t nsurv = frame_sum<G>((keep_g ? 1u : 0u) + (win_b ? 1u : 0u));
                         const uint32_t smax = frame_max<G>(su), nmin = frame_min<G>(nmk);
                         amb |= wmask(full && !(nsurv == (uint32_t)LMAX && nmin > smax)) & vmask;
-                        const uint64_t fw = wmask(!keep_g), ww = wmask(win_b);
-                        const uint32_t f8 = ((fl < F / 2 ? (uint32_t)fw : (uint32_t)(fw >> 32)) >> sh) & GM;
-                        const uint32_t w8 = ((fl < F / 2 ? (uint32_t)ww : (uint32_t)(ww >> 32)) >> sh) & GM;
+                        const uint32_t f8 = frame_bits(wmask(!keep_g)), w8 = frame_bits(wmask(win_b));
                         const uint32_t jj = __builtin_popcount(f8 & ((1u << p) - 1u));
                         const int rsrc = gbase + (int)nth_set_bit8(w8, jj);
                         if (full && !keep_g) {
@@ -404,88 +409,73 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
             const uint64_t badm = wmask(bad);
 #ifdef PSCL_STATS  // diagnostic build (tools/fastpath_stats.py): full-list info phases per wave by
                    // tier: counters[12] kept in place, [13] one swap, [14] full ranking
-            const bool one = (wmask(__builtin_popcount(((fl < F / 2 ? (uint32_t)badm : (uint32_t)(badm >> 32)) >> (gbase & 31)) & GM) > 1) & vmask) == 0;
+            const bool one = (wmask(__builtin_popcount(frame_bits(badm)) > 1) & vmask) == 0;
             if (lane == 0 && P.counters) {
                 atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + ((badm & vmask) == 0 ? 12 : (one ? 13 : 14)), 1ULL);
             }
 #endif
-            if ((PSCL_LANE_ABL & 2) || ((badm & vmask) == 0 && !(PSCL_LANE_ABL & 1))) {
-                metric = mg;
-                lastbit = gbit;
-                if (phi < 64) u0 |= (uint64_t)gbit << phi; else u1 |= (uint64_t)gbit << (phi - 64);
-                return;
-            }
-            const uint32_t sh = (uint32_t)gbase & 31u;
-            const uint32_t bad8 = ((fl < F / 2 ? (uint32_t)badm : (uint32_t)(badm >> 32)) >> sh) & GM;
+            // the better child stays in place unless a tier below makes this lane pull another
+            // path's worse child (the keep tier: no lane pulls)
+            metric = mg;
+            uint32_t b = gbit;
+            if (!(PSCL_LANE_ABL & 2) && ((badm & vmask) != 0 || (PSCL_LANE_ABL & 1))) {
+                const uint32_t bad8 = frame_bits(badm);
+                bool pull;
+                int src;
 #if PSCL_LANE_SWAP
-            // one-swap path (every frame of the wave has at most one worse child w that is not
-            // clear): the survivors are the better children but the largest, gmax, plus w -- certain
-            // when w and the second-largest better child are both below gmax by the margin (every
-            // other worse child already clears every better child, hence w too); else the frame is
-            // deferred (its boundary is within the margin, which no ranking could certify either)
-            if (!(PSCL_LANE_ABL & 1) && (wmask(__builtin_popcount(bad8) > 1) & vmask) == 0) {
-                const uint32_t kg = hiw(mg);
-                const uint32_t gmaxh = frame_max<G>(kg);
-                const bool ismax = kg == gmaxh;
-                const uint32_t nmax = frame_sum<G>(ismax ? 1u : 0u);
-                const uint32_t g2u = frame_max<G>(ismax ? 0u : kgu);
-                const uint32_t wu = frame_max<G>(bad ? hiw_up(mb) : 0u);
-                const bool swap = bad8 != 0;
-                amb |= wmask(swap && !(nmax == 1u && g2u < gmaxh && wu < gmaxh)) & vmask;
-                const int src = (gbase + (int)__builtin_ctz(bad8 | (1u << G))) & 63;  // (frames without a swap: unused)
+                // one-swap tier (every frame of the wave has at most one worse child w that is not
+                // clear): the survivors are the better children but the largest, gmax, plus w --
+                // certain when w and the second-largest better child are both below gmax by the
+                // margin (every other worse child already clears every better child, hence w too);
+                // else the frame is deferred (its boundary is within the margin, which no ranking
+                // could certify either)
+                if (!(PSCL_LANE_ABL & 1) && (wmask(__builtin_popcount(bad8) > 1) & vmask) == 0) {
+                    const uint32_t kg = hiw(mg);
+                    const uint32_t gmaxh = frame_max<G>(kg);
+                    const bool ismax = kg == gmaxh;
+                    const uint32_t nmax = frame_sum<G>(ismax ? 1u : 0u);
+                    const uint32_t g2u = frame_max<G>(ismax ? 0u : kgu);
+                    const uint32_t wu = frame_max<G>(bad ? hiw_up(mb) : 0u);
+                    const bool swap = bad8 != 0;
+                    amb |= wmask(swap && !(nmax == 1u && g2u < gmaxh && wu < gmaxh)) & vmask;
+                    src = (gbase + (int)__builtin_ctz(bad8 | (1u << G))) & 63;  // (frames without a swap: unused)
+                    pull = swap && ismax;
+                } else
+#endif
+                {
+                    // rank the 2L children of each frame (select_survivors), then certify: exactly L
+                    // survivors, and the largest survivor (raised by the margin) below the smallest
+                    // non-survivor
+                    const uint32_t kg = hiw(mg);
+                    bool keep_g, win_b;
+                    select_survivors<G, LMAX>(kg, kb, keep_g, win_b);
+                    const uint32_t kbu = hiw_up(mb);
+                    const uint32_t su = keep_g ? (win_b ? kbu : kgu) : (win_b ? kbu : 0u);
+                    const uint32_t nm = keep_g ? (win_b ? 0xffffffffu : kb) : kg;
+                    const uint32_t nsurv = frame_sum<G>((keep_g ? 1u : 0u) + (win_b ? 1u : 0u));
+                    const uint32_t smax = frame_max<G>(su), nmin = frame_min<G>(nm);
+                    amb |= wmask(!(nsurv == (uint32_t)LMAX && nmin > smax)) & vmask;
+                    // freed lanes take the surviving worse children: the j-th freed lane of a frame
+                    // pulls the j-th winner (both counted in lane order)
+                    const uint32_t f8 = frame_bits(wmask(!keep_g)), w8 = frame_bits(wmask(win_b));
+                    const uint32_t j = __builtin_popcount(f8 & ((1u << p) - 1u));
+                    src = gbase + (int)nth_set_bit8(w8, j);
+                    pull = !keep_g;
+                }
+                // the pull: metric, bits and slot table of the source lane's worse child, whose bit
+                // rides on the table word
                 const uint32_t tw = tab | ((gbit ^ 1u) << 31);
                 const uint64_t pmb = shfl_u64(pscl_asu64(mb), src);
                 const uint64_t pu0 = shfl_u64(u0, src);
                 const uint64_t pu1 = phi >= 64 ? shfl_u64(u1, src) : 0ULL;
                 const uint32_t ptw = bperm32(tw, src);
-                uint32_t b = gbit;
-                if (swap && ismax) {
+                if (pull) {
                     metric = pscl_asf64(pmb);
                     u0 = pu0;
                     u1 = pu1;
                     tab = ptw & 0x7fffffffu;
                     b = ptw >> 31;
-                } else {
-                    metric = mg;
                 }
-                if (phi < 64) u0 |= (uint64_t)b << phi; else u1 |= (uint64_t)b << (phi - 64);
-                lastbit = b;
-                return;
-            }
-#endif
-            // rank the 2L children of each frame: counts of keys (high words) strictly below each
-            const uint32_t kg = hiw(mg);
-            bool keep_g, win_b;
-            select_survivors<G, LMAX>(kg, kb, keep_g, win_b);
-            // certificate: exactly L survivors, and the largest survivor (raised by the margin)
-            // below the smallest non-survivor
-            const uint32_t kbu = hiw_up(mb);
-            const uint32_t su = keep_g ? (win_b ? kbu : kgu) : (win_b ? kbu : 0u);
-            const uint32_t nm = keep_g ? (win_b ? 0xffffffffu : kb) : kg;
-            const uint32_t nsurv = frame_sum<G>((keep_g ? 1u : 0u) + (win_b ? 1u : 0u));
-            const uint32_t smax = frame_max<G>(su), nmin = frame_min<G>(nm);
-            amb |= wmask(!(nsurv == (uint32_t)LMAX && nmin > smax)) & vmask;
-            // freed lanes take the surviving worse children: the j-th freed lane of a frame pulls
-            // the j-th winner (both counted in lane order)
-            const uint64_t fw = wmask(!keep_g), ww = wmask(win_b);
-            const uint32_t f8 = ((fl < F / 2 ? (uint32_t)fw : (uint32_t)(fw >> 32)) >> sh) & GM;
-            const uint32_t w8 = ((fl < F / 2 ? (uint32_t)ww : (uint32_t)(ww >> 32)) >> sh) & GM;
-            const uint32_t j = __builtin_popcount(f8 & ((1u << p) - 1u));
-            const int src = gbase + (int)nth_set_bit8(w8, j);
-            const uint32_t tw = tab | ((gbit ^ 1u) << 31);  // the worse child's bit rides on the table word
-            const uint64_t pmb = shfl_u64(pscl_asu64(mb), src);
-            const uint64_t pu0 = shfl_u64(u0, src);
-            const uint64_t pu1 = phi >= 64 ? shfl_u64(u1, src) : 0ULL;
-            const uint32_t ptw = bperm32(tw, src);
-            uint32_t b = gbit;
-            if (!keep_g) {
-                metric = pscl_asf64(pmb);
-                u0 = pu0;
-                u1 = pu1;
-                tab = ptw & 0x7fffffffu;
-                b = ptw >> 31;
-            } else {
-                metric = mg;
             }
             if (phi < 64) u0 |= (uint64_t)b << phi; else u1 |= (uint64_t)b << (phi - 64);
             lastbit = b;

@@ -53,7 +53,11 @@ __device__ __forceinline__ double f_minsum(double a, double b) {
     double m;
     asm("v_min_f64 %0, |%1|, |%2|" : "=v"(m) : "v"(a), "v"(b));
     const uint64_t ab = pscl_asu64(a), bb = pscl_asu64(b), mb = pscl_asu64(m);
-    const uint32_t hi = (uint32_t)(mb >> 32) | (((uint32_t)(ab >> 32) ^ (uint32_t)(bb >> 32)) & 0x80000000u);
+    const uint32_t x = (uint32_t)(ab >> 32) ^ (uint32_t)(bb >> 32);
+    // v_and_or_b32 with the sign mask in an SGPR: a VOP3 encoding takes no literal on gfx950, and
+    // left to itself the compiler splits the fold into v_and_b32 (literal) + v_or_b32
+    uint32_t hi;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(hi) : "v"(x), "s"(0x80000000u), "v"((uint32_t)(mb >> 32)));
     return pscl_asf64(((uint64_t)hi << 32) | (uint32_t)mb);
 }
 // g(a,b,c) = b + (1-2c) a  (polar.py:126-127): b + (+-a), one rounding, sign of a flipped by c
