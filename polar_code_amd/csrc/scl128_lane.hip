@@ -422,7 +422,33 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
                 const uint32_t bad8 = frame_bits(badm);
                 bool pull;
                 int src;
-#if PSCL_LANE_SWAP
+#if PSCL_LANE_G1
+                // one-swap tier, general form: in every frame at most one worse child w1 (the
+                // smallest) displaces the largest better child gmax.  Certified per frame when gmax
+                // and w1 are unique and max(second better, w1) raised by the margin is below
+                // min(gmax, second-smallest worse w2); a frame with a single near-worse child that
+                // fails it is deferred (no ranking could certify it); any other failing frame sends
+                // the wave to the ranking
+                const uint32_t kg1 = hiw(mg);
+                const uint32_t gmaxh = frame_max<G>(kg1);
+                const bool ismax = kg1 == gmaxh;
+                const uint32_t w1 = frame_min<G>(kb);
+                const bool isw1 = kb == w1;
+                const uint32_t nuniq = frame_sum<G>((ismax ? 1u : 0u) + (isw1 ? 0x100u : 0u));
+                const uint32_t g2u = frame_max<G>(ismax ? 0u : kgu);
+                const uint32_t w1u = frame_max<G>(isw1 ? hiw_up(mb) : 0u);
+                const uint32_t w2 = frame_min<G>(isw1 ? 0xffffffffu : kb);
+                const uint32_t smax1 = g2u > w1u ? g2u : w1u, nmin1 = gmaxh < w2 ? gmaxh : w2;
+                const bool cert1 = nuniq == 0x101u && smax1 < nmin1;
+                const bool any_bad = bad8 != 0;
+                const bool ok1 = !any_bad || cert1 || __builtin_popcount(bad8) == 1;
+                if (!(PSCL_LANE_ABL & 1) && (wmask(!ok1) & vmask) == 0) {
+                    amb |= wmask(any_bad && !cert1) & vmask;
+                    src = gbase + (int)__builtin_ctz(frame_bits(wmask(isw1)) | (1u << G));
+                    src &= 63;
+                    pull = any_bad && cert1 && ismax;
+                } else
+#elif PSCL_LANE_SWAP
                 // one-swap tier (every frame of the wave has at most one worse child w that is not
                 // clear): the survivors are the better children but the largest, gmax, plus w --
                 // certain when w and the second-largest better child are both below gmax by the
@@ -449,6 +475,21 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
                     const uint32_t kg = hiw(mg);
                     bool keep_g, win_b;
                     select_survivors<G, LMAX>(kg, kb, keep_g, win_b);
+#if defined(PSCL_STATS) && PSCL_STATS == 2  // diagnostic: ranked-tier frames by surviving worse children
+                    {                        // [16 + d] and near-worse count [25 + nb]; waves by max d [34 + d]
+                        const uint32_t dw = frame_sum<G>(win_b ? 1u : 0u);
+                        const uint32_t nb = __builtin_popcount(bad8);
+                        unsigned long long* C = reinterpret_cast<unsigned long long*>(P.counters);
+                        if (p == 0 && fvalid && C) {
+                            atomicAdd(C + 16 + (dw > 8u ? 8u : dw), 1ULL);
+                            atomicAdd(C + 25 + nb, 1ULL);
+                        }
+                        uint32_t md = 0;
+                        for (uint32_t k = 1; k <= 8; ++k)
+                            if (wmask(dw >= k) & vmask) md = k;
+                        if (lane == 0 && C) atomicAdd(C + 34 + md, 1ULL);
+                    }
+#endif
                     const uint32_t kbu = hiw_up(mb);
                     const uint32_t su = keep_g ? (win_b ? kbu : kgu) : (win_b ? kbu : 0u);
                     const uint32_t nm = keep_g ? (win_b ? 0xffffffffu : kb) : kg;

@@ -24,7 +24,7 @@ dec.set_stream(torch.cuda.current_stream().cuda_stream)
 llr = torch.empty((B, 128), dtype=torch.float64, device="cuda")
 msg = torch.empty((B, 1), dtype=torch.int64, device="cuda")
 best = torch.empty((B, 1), dtype=torch.int64, device="cuda")
-cnt = torch.zeros(16, dtype=torch.int64, device="cuda")  # the stats build writes slots 8..11
+cnt = torch.zeros(64, dtype=torch.int64, device="cuda")  # the stats builds write slots 8..42
 dec.channel_device(0, int(ebno * 10), ebno, 0.5, 40, 0, B, llr.data_ptr(), msg.data_ptr())
 dec.decode_device(llr.data_ptr(), B, d_best=best.data_ptr(), d_ref=msg.data_ptr(), k_payload=40,
                   d_counters=cnt.data_ptr())
@@ -36,6 +36,13 @@ tot = max(sum(c[12:16]), 1)
 if os.environ.get("PSCL_LANE_STATS"):  # the lane-per-path kernel's tiers (scl128_lane.hip)
     print("lane kernel full-list info phases (waves): " +
           ", ".join(f"{k}: {c[12 + i]} ({c[12 + i] / tot:.1%})" for i, k in enumerate(["kept", "one swap", "ranked"])))
+    if sum(c[16:25]):  # PSCL_STATS=2: the ranked tier's frames and waves
+        def hist(a):
+            t = max(sum(a), 1)
+            return ", ".join(f"{i}: {v} ({v / t:.1%})" for i, v in enumerate(a) if v)
+        print("ranked-tier frames by surviving worse children d: " + hist(c[16:25]))
+        print("ranked-tier frames by near-worse children: " + hist(c[25:34]))
+        print("ranked-tier waves by the largest d of their frames: " + hist(c[34:43]))
 else:
     print("screening full-list info phases (waves) by worst frame's near-worse children: " +
           ", ".join(f"{k}: {c[12 + i]} ({c[12 + i] / tot:.1%})" for i, k in enumerate(["0", "1", "2", ">=3"])))
