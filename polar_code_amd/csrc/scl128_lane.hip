@@ -422,33 +422,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
                 const uint32_t bad8 = frame_bits(badm);
                 bool pull;
                 int src;
-#if PSCL_LANE_G1
-                // one-swap tier, general form: in every frame at most one worse child w1 (the
-                // smallest) displaces the largest better child gmax.  Certified per frame when gmax
-                // and w1 are unique and max(second better, w1) raised by the margin is below
-                // min(gmax, second-smallest worse w2); a frame with a single near-worse child that
-                // fails it is deferred (no ranking could certify it); any other failing frame sends
-                // the wave to the ranking
-                const uint32_t kg1 = hiw(mg);
-                const uint32_t gmaxh = frame_max<G>(kg1);
-                const bool ismax = kg1 == gmaxh;
-                const uint32_t w1 = frame_min<G>(kb);
-                const bool isw1 = kb == w1;
-                const uint32_t nuniq = frame_sum<G>((ismax ? 1u : 0u) + (isw1 ? 0x100u : 0u));
-                const uint32_t g2u = frame_max<G>(ismax ? 0u : kgu);
-                const uint32_t w1u = frame_max<G>(isw1 ? hiw_up(mb) : 0u);
-                const uint32_t w2 = frame_min<G>(isw1 ? 0xffffffffu : kb);
-                const uint32_t smax1 = g2u > w1u ? g2u : w1u, nmin1 = gmaxh < w2 ? gmaxh : w2;
-                const bool cert1 = nuniq == 0x101u && smax1 < nmin1;
-                const bool any_bad = bad8 != 0;
-                const bool ok1 = !any_bad || cert1 || __builtin_popcount(bad8) == 1;
-                if (!(PSCL_LANE_ABL & 1) && (wmask(!ok1) & vmask) == 0) {
-                    amb |= wmask(any_bad && !cert1) & vmask;
-                    src = gbase + (int)__builtin_ctz(frame_bits(wmask(isw1)) | (1u << G));
-                    src &= 63;
-                    pull = any_bad && cert1 && ismax;
-                } else
-#elif PSCL_LANE_SWAP
+#if PSCL_LANE_SWAP
                 // one-swap tier (every frame of the wave has at most one worse child w that is not
                 // clear): the survivors are the better children but the largest, gmax, plus w --
                 // certain when w and the second-largest better child are both below gmax by the
@@ -633,9 +607,15 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
 // 64 / L frames per workgroup, LDS = 30 L doubles per frame (15 KB per workgroup at both sizes)
 int pscl_lane_frames_per_wg(int L) { return 64 / L; }
 
+// timing-only: unused LDS bytes added to each plain launch (occupancy experiments; 0 in the product)
+#ifndef PSCL_LANE_LDS_PAD
+#define PSCL_LANE_LDS_PAD 0
+#endif
+
 hipError_t pscl_launch_lane(const pscl_decode_params& P, int64_t grid, hipStream_t s) {
     // (pscl_lane_available: the (128,64) code on plain rows, or the rate-matched NR (128,88) code)
-    const int lds8 = LaneLayout<8>::F * LaneLayout<8>::FSTRIDE * 8, lds4 = LaneLayout<4>::F * LaneLayout<4>::FSTRIDE * 8;
+    const int lds8 = LaneLayout<8>::F * LaneLayout<8>::FSTRIDE * 8 + PSCL_LANE_LDS_PAD,
+              lds4 = LaneLayout<4>::F * LaneLayout<4>::FSTRIDE * 8 + PSCL_LANE_LDS_PAD;
     if (P.L == 8 && !P.rm_E)
         hipLaunchKernelGGL((scl_lane_kernel<8, 1>), dim3((unsigned)grid), dim3(64), lds8, s, P);
     else if (P.L == 8)

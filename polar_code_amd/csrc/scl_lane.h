@@ -9,10 +9,7 @@
 #ifndef PSCL_LANE_SWAP
 #define PSCL_LANE_SWAP 1
 #endif
-// its general form in the N = 128 lane kernel (several near-worse children, one displacing)
-#ifndef PSCL_LANE_G1
-#define PSCL_LANE_G1 0
-#endif
+
 
 namespace {
 
