@@ -348,6 +348,13 @@ int pscl_softplus_tails_device(pscl_handle* h, const double* d_v, int64_t n, dou
 int pscl_tail_abs_scan_device(pscl_handle* h, uint32_t lo, uint32_t hi, uint64_t* d_out);
 
 /*
+ * The same scan for the bits form of the screening tail (the lane kernels' plain decodes):
+ * max |pscl_tail2_f32(y32) - log1p(exp(-y32 ln 2)) / ln 2| over the fp32 bit patterns [lo, hi],
+ * the reference being the bit-exact glibc port in fp64 (glibc_softplus.h).  Same output layout.
+ */
+int pscl_tail2_scan_device(pscl_handle* h, uint32_t lo, uint32_t hi, uint64_t* d_out);
+
+/*
  * Kernel timing with HIP events recorded on the launch stream around every decode kernel
  * launch (enable = 1 starts a fresh accumulation).  pscl_timing_read returns the number of
  * timed launches and their summed duration in milliseconds (synchronizes the stream).

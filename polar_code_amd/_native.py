@@ -41,7 +41,7 @@ EXPORTS = (
     "pscl_timing_read", "pscl_launch_info", "pscl_set_rate_match", "pscl_set_beta", "pscl_dlscl_device",
     "pscl_path_llrs_device", "pscl_uncoded_device", "pscl_simulate", "pscl_set_screening", "pscl_build_hash",
     "pscl_screening_count", "pscl_softplus_tails_device", "pscl_set_pipelined", "pscl_join",
-    "pscl_tail_abs_scan_device", "pscl_set_tuning", "pscl_timing_read_split", "pscl_decode_cpu",
+    "pscl_tail_abs_scan_device", "pscl_tail2_scan_device", "pscl_set_tuning", "pscl_timing_read_split", "pscl_decode_cpu",
     "pscl_simulate_device",
 )
 
@@ -104,6 +104,7 @@ def lib() -> C.CDLL:
         "pscl_join": (C.c_int, [_vp]),
         "pscl_softplus_tails_device": (C.c_int, [_vp, _vp, _i64, _vp, _vp]),
         "pscl_tail_abs_scan_device": (C.c_int, [_vp, C.c_uint32, C.c_uint32, _vp]),
+        "pscl_tail2_scan_device": (C.c_int, [_vp, C.c_uint32, C.c_uint32, _vp]),
         "pscl_set_tuning": (C.c_int, [_vp, C.c_int, _i64]),
         "pscl_simulate_device": (C.c_int, [_vp, _u64, C.c_uint32, _dbl, _dbl, C.c_int, _i64, _i64, C.c_int, C.c_int,
                                            _vp]),
@@ -377,13 +378,15 @@ class Decoder:
             check(lib().pscl_softplus_tails_device(self._h, d_v, v.size, d_e, d_a))
             return mem.download(d_e, v.nbytes, np.float64), mem.download(d_a, v.nbytes, np.float64)
 
-    def tail_abs_scan(self, lo: int = 0, hi: int = 0x7F800000):
+    def tail_abs_scan(self, lo: int = 0, hi: int = 0x7F800000, bits: bool = False):
         """Largest |screening tail - exact tail| over the fp32 bit patterns [lo, hi] and the x32
-        where it occurs (pscl_tail_abs_scan_device; the default range is every x32 >= 0)."""
+        where it occurs (pscl_tail_abs_scan_device; the default range is every x32 >= 0).  bits:
+        the bits form of the lane kernels' plain decodes (pscl_tail2_scan_device)."""
+        fn = lib().pscl_tail2_scan_device if bits else lib().pscl_tail_abs_scan_device
         with DeviceArena(self) as mem:
             d = mem.alloc(16)
             mem.memset(d, 0, 16)
-            check(lib().pscl_tail_abs_scan_device(self._h, int(lo), int(hi), d))
+            check(fn(self._h, int(lo), int(hi), d))
             out = mem.download(d, 16, np.uint64)
         err = float(out[:1].view(np.float64)[0])
         x32 = float(np.array([int(out[1]) & 0xFFFFFFFF], np.uint32).view(np.float32)[0])

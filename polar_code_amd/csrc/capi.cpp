@@ -1722,15 +1722,26 @@ int pscl_softplus_tails_device(pscl_handle* h, const double* d_v, int64_t n, dou
     return PSCL_OK;
 }
 
-int pscl_tail_abs_scan_device(pscl_handle* h, uint32_t lo, uint32_t hi, uint64_t* d_out) {
+namespace {
+int tail_scan(pscl_handle* h, uint32_t lo, uint32_t hi, uint64_t* d_out, int bits) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
     if (!d_out) return fail(PSCL_EINVAL, "d_out is required");
     if (lo > hi) return fail(PSCL_EINVAL, "lo > hi");
     int rc = enter(h);
     if (rc) return rc;
-    hipError_t e = pscl_launch_tail_abs_scan(lo, hi, h->d_exp_table, reinterpret_cast<unsigned long long*>(d_out), h->stream);
+    hipError_t e =
+        pscl_launch_tail_abs_scan(lo, hi, h->d_exp_table, reinterpret_cast<unsigned long long*>(d_out), h->stream, bits);
     if (e != hipSuccess) return fail(PSCL_EDEVICE, "tail scan launch: %s", hipGetErrorString(e));
     return PSCL_OK;
+}
+}  // namespace
+
+int pscl_tail_abs_scan_device(pscl_handle* h, uint32_t lo, uint32_t hi, uint64_t* d_out) {
+    return tail_scan(h, lo, hi, d_out, 0);
+}
+
+int pscl_tail2_scan_device(pscl_handle* h, uint32_t lo, uint32_t hi, uint64_t* d_out) {
+    return tail_scan(h, lo, hi, d_out, 1);
 }
 
 int pscl_timing_enable(pscl_handle* h, int enable) {

@@ -534,6 +534,46 @@ PSCL_HD float pscl_tail_abs_f32(float x32) {
 }
 PSCL_HD double pscl_softplus_tail_abs(double v) { return (double)pscl_tail_abs_f32(pscl_cvt_abs_f32(v)); }
 
+/*
+ * The same tail in bits (round 5; the lane kernels' plain decodes, PSCL_LANE_BITS): with the LLR tree
+ * computed in units of log2 e (the channel LLRs multiplied by LOG2E once, as they are loaded), the
+ * metric increment logaddexp(0, -+v) / ln 2 = relu(-+v') + L2(|v'|), L2(y) = log2(1 + 2^-y), and
+ *
+ *   y32 = fl32(|v'|)                    v_cvt_f32_f64 with |.|
+ *   L2  = log2(1 + 2^-y32)              v_exp_f32 (negation as a source modifier), v_add_f32,
+ *                                       v_log_f32, v_cvt_f64_f32
+ *
+ * drops the two fp32 multiplies of pscl_tail_abs_f32.  Error, all in bits:
+ *   * the fp32 evaluation: max over EVERY non-negative fp32 y32 of |L2(y32) - log1p(exp(-y32 ln 2)) /
+ *     ln 2| (the glibc port in fp64), scanned on the device (pscl_tail2_scan_device,
+ *     tests/test_gpu_screening.py::test_tail2_exhaustive_device) = PSCL_TAIL2_SCAN;
+ *   * the conversion: |y32 - y| <= 2^-24 y and |dL2/dy| = 2^-y / (1 + 2^-y), so at most
+ *     2^-24 max_y y 2^-y / (1 + 2^-y) < 0.41 * 2^-24;
+ *   * the reference's own rounding of each increment (one ulp, < 2^-52 at these magnitudes);
+ *   * the scaled tree itself: f is 1-Lipschitz in each argument and g rounds once, so a leaf
+ *     computed from the scaled channel row differs from log2 e times the fp64 leaf of the exact
+ *     decode by at most 15 u S' (u = 2^-53, S' = the row's sum of scaled magnitudes: 8 u S' for
+ *     the scaled tree against real arithmetic -- the scaling and seven levels, each channel value
+ *     under seven g nodes -- and log2 e * 7 u S for the fp64 tree).  The kernel defers every frame
+ *     where one lane's share of the row (128 / L values, L = 4 or 8 lanes per frame) has scaled
+ *     magnitudes summing to 2^14 or more (S' < 2^17), so that term is below PSCL_TAIL2_TREE = 2^-31
+ *     per increment (15 * 2^-53 * 2^17 < 2^-32).  (h(x) = log2(1 + 2^-x) is 1-Lipschitz, so the error
+ *     of an increment is at most the error of its LLR whichever child the LLR's sign names.)
+ */
+#define PSCL_LOG2E_F64 1.4426950408889634
+#ifndef PSCL_TAIL2_SCAN
+#define PSCL_TAIL2_SCAN (4.0 / 16777216.0)
+#endif
+#define PSCL_TAIL2_TREE (1.0 / 2147483648.0)
+#define PSCL_TAIL2_DELTA (PSCL_TAIL2_SCAN + 0.41 / 16777216.0 + 2.0 * 2.220446049250313e-16 + PSCL_TAIL2_TREE)
+/* certificate margin of the bits form: two metrics' errors (2 * 128 * delta), rounded up */
+#define PSCL_TAIL2_MARGIN (2.0 * 128.0 * PSCL_TAIL2_DELTA * 1.0001)
+/* per-lane bound on the sum of the scaled channel magnitudes a lane holds (else the frame is deferred) */
+#define PSCL_TAIL2_CHAN_SUM 16384.0
+
+PSCL_HD float pscl_tail2_f32(float y32) { return pscl_log2_f32(1.0f + pscl_exp2_f32(-y32)); }
+PSCL_HD double pscl_softplus_tail2(double v) { return (double)pscl_tail2_f32(pscl_cvt_abs_f32(v)); }
+
 /* L = log1p(exp(-|v|)), the part of logaddexp(0, +-v) shared by both bit hypotheses. */
 PSCL_HD double pscl_softplus_tail(double v, const uint64_t* T) {
     double a = v < 0 ? -v : v;

@@ -63,6 +63,13 @@ struct LaneLayout {
 #define PSCL_LANE_ABL 0
 #endif
 
+// plain decodes compute the LLR tree in units of log2 e and the metrics in bits (the tail without its
+// two fp32 multiplies, glibc_softplus.h pscl_softplus_tail2); the FS retry decodes, whose warm-start
+// metrics come from the post pass in nats, keep the natural-log form
+#ifndef PSCL_LANE_BITS
+#define PSCL_LANE_BITS 1
+#endif
+
 #ifndef PSCL_LANE_WAVES_PER_EU
 #define PSCL_LANE_WAVES_PER_EU 2
 #endif
@@ -96,9 +103,11 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
     auto hiw = [](double m) { return (uint32_t)(pscl_asu64(m) >> 32); };
     // the margin-raised key hi(fma(m, 1 + 2^-40, MARGIN)) as one VOP3 fma with the factor in an SGPR
     // (left to itself the compiler emits a copy of the margin register plus v_fmac_f64)
+    constexpr bool BITS = !FS && PSCL_LANE_BITS;
+    constexpr double MARGIN = BITS ? PSCL_TAIL2_MARGIN : PSCL_TAIL_ABS_MARGIN;
     auto hiw_up = [&](double m) {
         double r;
-        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(m), "s"(1.0 + 0x1p-40), "v"((double)PSCL_TAIL_ABS_MARGIN));
+        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(m), "s"(1.0 + 0x1p-40), "v"(MARGIN));
         return hiw(r);
     };
     // this frame's G bits of a wave ballot (one 64-bit shift by the frame's first lane)
@@ -141,15 +150,17 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
 #pragma unroll
             for (int k = 0; k < EPL; ++k)
 #pragma unroll
-                for (int m = 0; m < 8; ++m) c[8 * k + m] = chan_at(p + G * k + 16 * m);
+                for (int m = 0; m < 8; ++m) c[8 * k + m] = BITS ? chan_at(p + G * k + 16 * m) * PSCL_LOG2E_F64
+                                                                : chan_at(p + G * k + 16 * m);
         };
         load_chan();
         // frames whose channel magnitudes could overflow the fp64 metric sums or carry a NaN go to
-        // the exact re-decode (the lane's values summed; NaN propagates through the sum)
+        // the exact re-decode (the lane's values summed; NaN propagates through the sum); in bits,
+        // a tighter bound keeps the scaled tree's error below PSCL_TAIL2_TREE (glibc_softplus.h)
         double cs = fabs(c[0]);
 #pragma unroll
         for (int m = 1; m < 8 * EPL; ++m) cs = cs + fabs(c[m]);
-        uint64_t amb = wmask(!(cs < 0x1p25));
+        uint64_t amb = wmask(!(cs < (BITS ? PSCL_TAIL2_CHAN_SUM : 0x1p25)));
         const uint64_t vmask = wmask(fvalid);
 
         double metric = 0.0;
@@ -300,7 +311,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
             // ---- leaf LLR and metric tail (scl.py:80-82, 102-105)
             const double2 lab = *reinterpret_cast<const double2*>(Af + Ly::OFF6 + (start <= 6 ? p : slot_at(tab, 6)) * 2);
             const double lam = (phi & 1) ? g_node(lab.x, lab.y, lastbit) : f_minsum(lab.x, lab.y);
-            const double Lt = pscl_softplus_tail_abs(lam);
+            const double Lt = BITS ? pscl_softplus_tail2(lam) : pscl_softplus_tail_abs(lam);
             if constexpr (!is_info) {  // frozen: bit 0 (scl.py:149-153)
                 metric = metric + (relu_neg(lam) + Lt);
                 lastbit = 0;

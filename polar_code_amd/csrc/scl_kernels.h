@@ -288,7 +288,7 @@ hipError_t pscl_launch_dl_compact(const uint8_t* flags, int64_t B, int64_t base,
 hipError_t pscl_launch_iota64(int64_t* out, int64_t n, hipStream_t s);
 hipError_t pscl_launch_replay(const pscl_replay_params& R, int64_t cap, hipStream_t s);
 hipError_t pscl_launch_tail_abs_scan(uint32_t lo, uint32_t hi, const uint64_t* exp_table, unsigned long long* out,
-                                     hipStream_t s);
+                                     hipStream_t s, int bits);
 hipError_t pscl_launch_softplus_tails(const double* v, int64_t n, const uint64_t* exp_table, double* exact,
                                      double* apx, hipStream_t s);
 hipError_t pscl_launch_dl_post(const pscl_post_params& Q, int64_t entries, hipStream_t s);

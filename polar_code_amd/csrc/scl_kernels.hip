@@ -787,8 +787,9 @@ __global__ void __launch_bounds__(256) softplus_tails_kernel(const double* v, in
 // [lo, hi] (the screening tail is a function of x32 = fl32(|v|) alone: glibc_softplus.h).
 // out[0] = the largest error's fp64 bits (non-negative doubles order like their bit patterns),
 // out[1] = (high word of that error << 32) | its x32 bit pattern, for the argmax.
+// bits = 1: the bits form, max |pscl_tail2_f32(y32) - log1p(exp(-y32 ln 2)) / ln 2| (glibc_softplus.h)
 __global__ void __launch_bounds__(256) tail_abs_scan_kernel(uint32_t lo, uint32_t hi, const uint64_t* exp_table,
-                                                             unsigned long long* out) {
+                                                             unsigned long long* out, int bits) {
     __shared__ uint64_t T[PSCL_EXP_TABLE_WORDS];
     for (int i = threadIdx.x; i < PSCL_EXP_TABLE_WORDS; i += blockDim.x) T[i] = exp_table[i];
     __syncthreads();
@@ -796,8 +797,9 @@ __global__ void __launch_bounds__(256) tail_abs_scan_kernel(uint32_t lo, uint32_
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= hi; i += stride) {
         const float x32 = __uint_as_float((uint32_t)i);
-        const double ex = pscl_softplus_tail_bf((double)x32, T);
-        const double ap = (double)pscl_tail_abs_f32(x32);
+        const double ex = bits ? pscl_softplus_tail_bf((double)x32 * PSCL_LOGE2, T) / PSCL_LOGE2
+                               : pscl_softplus_tail_bf((double)x32, T);
+        const double ap = bits ? (double)pscl_tail2_f32(x32) : (double)pscl_tail_abs_f32(x32);
         const unsigned long long eb = (unsigned long long)pscl_asu64(fabs(ap - ex));
         if (eb > best) {
             best = eb;
@@ -817,8 +819,8 @@ __global__ void __launch_bounds__(256) tail_abs_scan_kernel(uint32_t lo, uint32_
 }
 
 hipError_t pscl_launch_tail_abs_scan(uint32_t lo, uint32_t hi, const uint64_t* exp_table, unsigned long long* out,
-                                     hipStream_t s) {
-    hipLaunchKernelGGL(tail_abs_scan_kernel, dim3(8192), dim3(256), 0, s, lo, hi, exp_table, out);
+                                     hipStream_t s, int bits) {
+    hipLaunchKernelGGL(tail_abs_scan_kernel, dim3(8192), dim3(256), 0, s, lo, hi, exp_table, out, bits);
     return hipGetLastError();
 }
 

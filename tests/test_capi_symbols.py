@@ -12,7 +12,7 @@ HEADER = Path(__file__).resolve().parent.parent / "include" / "polar_scl.h"
 def _declared():
     text = HEADER.read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(pscl_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(pscl_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_header_matches_binding_table():

@@ -164,6 +164,35 @@ def test_screening_huge_llrs_deferred(M):
 
 
 @pytest.mark.parametrize("M", [4, 8])
+def test_screening_bits_domain_bound_deferred(M):
+    """The lane kernels' plain decodes compute the tree in units of log2 e (glibc_softplus.h,
+    pscl_softplus_tail2) and defer every frame where one lane's 16 scaled channel magnitudes sum to
+    PSCL_TAIL2_CHAN_SUM or more (the scaled tree's error bound).  Frames straddling that bound
+    (strong, noiseless-like rows scaled so the per-lane sums cross it) decode exactly as the exact
+    kernel and the oracle, deferred or not.  (A lane holds the row positions i = p mod L.)"""
+    rng = np.random.default_rng(7500 + M)
+    info = construct_info_set(128, 64)
+    B = 6000
+    llr = _frames(rng, B, info, 4.0)
+    bound = _header_const("PSCL_TAIL2_CHAN_SUM") / _header_const("PSCL_LOG2E_F64")
+    # rows scaled so the largest per-lane share (128 / L values) sits between 0.5 and 2 times the bound
+    lanes = np.abs(llr).reshape(B, 128 // M, M).sum(axis=1).max(axis=1)
+    scale = bound * np.exp2(rng.uniform(-1.0, 1.0, size=B)) / lanes
+    pick = np.arange(0, B, 3)
+    llr[pick] *= scale[pick, None]
+    scr, ex = _pair(128, info, M)
+    a = _plain(scr, llr)
+    _assert_same(a, _plain(ex, llr), "bits-domain bound")
+    over = np.abs(llr).reshape(B, 128 // M, M).sum(axis=1).max(axis=1) * _header_const("PSCL_LOG2E_F64") >= \
+        _header_const("PSCL_TAIL2_CHAN_SUM")
+    assert over.sum() > 500 and scr.screening_count() >= int(over.sum())
+    for f in pick[::40]:
+        n, c, m, il, b = oracle.decode_scl(llr[f], info, M, crc=POLY)
+        assert a["n_paths"][f] == n and a["best_idx"][f] == b, f
+        np.testing.assert_array_equal(a["best_bits"][f], c[b], err_msg=f"f={f}")
+
+
+@pytest.mark.parametrize("M", [4, 8])
 def test_pipelined_decodes_equal_stream_ordered(M):
     """pscl_set_pipelined: a stream of plain decodes whose exact re-decodes overlap the next
     call (alternate output buffers, as bench.py steps), then join: every batch's best bits and
@@ -254,6 +283,20 @@ def test_tail_abs_exhaustive_device():
     e2, x2 = dec.tail_abs_scan(0x3F800000, 0x3F800000)  # x32 = 1.0 only
     ex, ap = dec.softplus_tails(np.array([1.0]))
     assert e2 == abs(ap[0] - ex[0]) and x2 in (0.0, 1.0)
+
+
+def test_tail2_exhaustive_device():
+    """The bits form of the screening tail (the lane kernels' plain decodes) against
+    log1p(exp(-y ln 2)) / ln 2 from the bit-exact glibc port, over EVERY non-negative fp32 y32:
+    within PSCL_TAIL2_SCAN, the measured term of its margin (glibc_softplus.h); and the margin
+    covers two metrics of 128 increments of PSCL_TAIL2_DELTA."""
+    dec = _native.Decoder(128, construct_info_set(128, 64), 8, POLY)
+    err, y32 = dec.tail_abs_scan(bits=True)
+    scan = _header_const("PSCL_TAIL2_SCAN")
+    print(f"exhaustive fp32 scan (bits): max |tail2 - glibc/ln2| = {err:.4e} = 2^{np.log2(err):.3f} at "
+          f"y32 = {y32!r} (bound {scan:.4e})")
+    assert 0.0 < err <= scan
+    assert _header_const("PSCL_TAIL2_MARGIN") >= 2 * 128 * _header_const("PSCL_TAIL2_DELTA")
 
 
 def test_screening_tail_within_bound_device():
