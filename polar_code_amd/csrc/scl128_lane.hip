@@ -34,6 +34,13 @@
 
 namespace {
 
+// depths 5 and 6 (4 + 2 values per path) in the registers of the path's lane, carried along when a
+// lane takes another path's child (1), or in LDS slots with lazy copies like depths 3 and 4 (0):
+// LDS per frame 24 L doubles (+ pad) instead of 30 L, 12 wavefronts per CU instead of 10 at L = 8
+#ifndef PSCL_LANE_REG56
+#define PSCL_LANE_REG56 1
+#endif
+
 template <int LMAX>
 struct LaneLayout {
     static constexpr int G = LMAX;
@@ -41,12 +48,16 @@ struct LaneLayout {
     static constexpr int LOG_G = __builtin_ctz(G);
     static constexpr int OFF3 = 0;              // [8][L][2]
     static constexpr int OFF4 = OFF3 + 16 * LMAX;  // [4][L][2]
-    static constexpr int OFF5 = OFF4 + 8 * LMAX;   // [2][L][2]
-    static constexpr int OFF6 = OFF5 + 4 * LMAX;   // [1][L][2]; recompute phases: partial sums (16 B per path)
-    // 30 L doubles: at L = 8, 240 = 16 (mod 32), so frames start alternately on the two 128-byte
-    // halves of the 256-byte bank row and a ds_read_b128 lane group (lanes of 4 frames) touching one
-    // pair index of its paths' slots covers 4 distinct 64-byte quarters
-    static constexpr int FSTRIDE = OFF6 + 2 * LMAX;
+    static constexpr int OFF5 = OFF4 + 8 * LMAX;   // [2][L][2] (PSCL_LANE_REG56 = 0)
+    static constexpr int OFF6 = OFF5 + 4 * LMAX;   // [1][L][2] (PSCL_LANE_REG56 = 0)
+    // the depth-1..3 recompute's partial sums (16 B per path): on depth 6, or on depth 4 when depths
+    // 5 and 6 live in registers (depth 4 is rewritten after the recompute has read them)
+    static constexpr int OFFX = PSCL_LANE_REG56 ? OFF4 : OFF6;
+    static constexpr int RAW = PSCL_LANE_REG56 ? OFF5 : OFF6 + 2 * LMAX;
+    // frames at a stride = 16 (mod 32) doubles (at L = 8: 240 or, with REG56, 208): frames start
+    // alternately on the two 128-byte halves of the 256-byte bank row and a ds_read_b128 lane group
+    // (lanes of 4 frames) touching one pair index of its paths' slots covers 4 distinct 64-byte quarters
+    static constexpr int FSTRIDE = RAW + (((16 - RAW) % 32) + 32) % 32;
 };
 
 // L = 4: keep the lane's 32 channel LLRs in registers across the frame (1) or re-read them at each
@@ -167,6 +178,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
         uint64_t u0 = 0, u1 = 0;  // decided bits
         uint32_t tab = 0;          // LDS slot of depths 3..6 (4 bits each)
         uint32_t lastbit = 0;      // the bit decided at the previous phase
+        double r5[4] = {0.0, 0.0, 0.0, 0.0}, r6[2] = {0.0, 0.0};  // PSCL_LANE_REG56: depths 5 and 6 of this lane's path
         uint64_t fm0 = 0, fm1 = 0, fv0 = 0, fv1 = 0;  // FS: force mask and values (information bits)
         int lcnt = 0;                                 // FS: log2 of the frame's live paths
         if constexpr (FS) {
@@ -208,7 +220,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
             if constexpr (start <= 3 && !(PSCL_LANE_ABL & 4)) {
                 constexpr bool r1 = phi >= 64, r2 = (phi >> 5) & 1, r3 = (phi >> 4) & 1;
                 if constexpr (!CREG && phi > 0) load_chan();
-                uint4* const xs = reinterpret_cast<uint4*>(Af + Ly::OFF6);
+                uint4* const xs = reinterpret_cast<uint4*>(Af + Ly::OFFX);
                 if constexpr (r1 || r2 || r3) {
                     uint64_t X1 = 0;
                     uint32_t X2 = 0, X3 = 0;
@@ -285,22 +297,35 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
                         constexpr int OFF_OUT = D == 4 ? Ly::OFF4 : (D == 5 ? Ly::OFF5 : Ly::OFF6);
                         constexpr bool first = D == start || (D == 4 && start < 4);
                         constexpr bool is_g = D == start && phi != 0;
-                        const int sin = first ? slot_at(tab, D - 1) : p;  // (depth 3 at a recompute: own slot p)
-                        const int sin_eff = (D == 4 && start <= 3) ? p : sin;
-                        const double* in = Af + OFF_IN + sin_eff * 2;
-                        double o[W];
+                        if constexpr (PSCL_LANE_REG56 && D == 6) {
+                            // from this path's depth-5 registers (computed this phase, or carried
+                            // along with the path since)
 #pragma unroll
-                        for (int k = 0; k < W; ++k) {
-                            const double2 ab = *reinterpret_cast<const double2*>(in + k * LMAX * 2);
-                            o[k] = is_g ? g_node(ab.x, ab.y, (xsb >> k) & 1u) : f_minsum(ab.x, ab.y);
-                        }
-                        double* out = Af + OFF_OUT + p * 2;
-                        if constexpr (HW >= 1) {
+                            for (int k = 0; k < 2; ++k)
+                                r6[k] = is_g ? g_node(r5[k], r5[k + 2], (xsb >> k) & 1u) : f_minsum(r5[k], r5[k + 2]);
+                        } else {
+                            const int sin = first ? slot_at(tab, D - 1) : p;  // (depth 3 at a recompute: own slot p)
+                            const int sin_eff = (D == 4 && start <= 3) ? p : sin;
+                            const double* in = Af + OFF_IN + sin_eff * 2;
+                            double o[W];
 #pragma unroll
-                            for (int k = 0; k < (HW ? HW : 1); ++k)
-                                *reinterpret_cast<double2*>(out + k * LMAX * 2) = make_double2(o[k], o[k + HW]);
+                            for (int k = 0; k < W; ++k) {
+                                const double2 ab = *reinterpret_cast<const double2*>(in + k * LMAX * 2);
+                                o[k] = is_g ? g_node(ab.x, ab.y, (xsb >> k) & 1u) : f_minsum(ab.x, ab.y);
+                            }
+                            if constexpr (PSCL_LANE_REG56 && D == 5) {
+#pragma unroll
+                                for (int k = 0; k < 4; ++k) r5[k] = o[k];
+                            } else {
+                                double* out = Af + OFF_OUT + p * 2;
+                                if constexpr (HW >= 1) {
+#pragma unroll
+                                    for (int k = 0; k < (HW ? HW : 1); ++k)
+                                        *reinterpret_cast<double2*>(out + k * LMAX * 2) = make_double2(o[k], o[k + HW]);
+                                }
+                                wave_lds_fence();
+                            }
                         }
-                        wave_lds_fence();
                     }
                 });
                 // this path's own slot at every depth rewritten this phase
@@ -309,7 +334,28 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
                 tab = (tab & ~mask) | ((uint32_t)p * 0x1111u & mask);
             }
             // ---- leaf LLR and metric tail (scl.py:80-82, 102-105)
-            const double2 lab = *reinterpret_cast<const double2*>(Af + Ly::OFF6 + (start <= 6 ? p : slot_at(tab, 6)) * 2);
+            const double2 lab = PSCL_LANE_REG56 ? make_double2(r6[0], r6[1])
+                                                : *reinterpret_cast<const double2*>(Af + Ly::OFF6 + (start <= 6 ? p : slot_at(tab, 6)) * 2);
+            // a lane taking another path's child also takes that path's depth-6 node (needed by the
+            // next, odd, leaf: even phases) and its depth-5 node (needed by the depth-6 g node two
+            // phases on: phases 0 and 1 mod 4)
+            constexpr bool C6 = PSCL_LANE_REG56 && (t % 2 == 0), C5 = PSCL_LANE_REG56 && (t % 4 <= 1);
+            auto carry = [&](int src, double (&q5)[4], double (&q6)[2]) {
+                if constexpr (C5)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) q5[k] = shfl_f64(r5[k], src);
+                if constexpr (C6)
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) q6[k] = shfl_f64(r6[k], src);
+            };
+            auto take = [&](const double (&q5)[4], const double (&q6)[2]) {
+                if constexpr (C5)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) r5[k] = q5[k];
+                if constexpr (C6)
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) r6[k] = q6[k];
+            };
             const double lam = (phi & 1) ? g_node(lab.x, lab.y, lastbit) : f_minsum(lab.x, lab.y);
             const double Lt = BITS ? pscl_softplus_tail2(lam) : pscl_softplus_tail_abs(lam);
             if constexpr (!is_info) {  // frozen: bit 0 (scl.py:149-153)
@@ -384,12 +430,15 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
                     const uint64_t pu0 = shfl_u64(u0, src);
                     const uint64_t pu1 = phi >= 64 ? shfl_u64(u1, src) : 0ULL;
                     const uint32_t ptw = bperm32(tw, src);
+                    double q5[4], q6[2];
+                    carry(src, q5, q6);
                     if (pull) {
                         nm = pscl_asf64(pm);
                         u0 = pu0;
                         u1 = pu1;
                         tab = ptw & 0x7fffffffu;
                         b = ptw >> 31;
+                        take(q5, q6);
                     }
                 }
                 metric = nm;
@@ -408,6 +457,9 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
                 u0 = shfl_u64(u0, src);
                 if (phi >= 64) u1 = shfl_u64(u1, src);
                 tab = bperm32(tab, src);
+                double q5[4], q6[2];
+                carry(src, q5, q6);
+                take(q5, q6);
                 if (phi < 64) u0 |= (uint64_t)b << phi; else u1 |= (uint64_t)b << (phi - 64);
                 lastbit = b;
                 return;
@@ -495,12 +547,15 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
                 const uint64_t pu0 = shfl_u64(u0, src);
                 const uint64_t pu1 = phi >= 64 ? shfl_u64(u1, src) : 0ULL;
                 const uint32_t ptw = bperm32(tw, src);
+                double q5[4], q6[2];
+                carry(src, q5, q6);
                 if (pull) {
                     metric = pscl_asf64(pmb);
                     u0 = pu0;
                     u1 = pu1;
                     tab = ptw & 0x7fffffffu;
                     b = ptw >> 31;
+                    take(q5, q6);
                 }
             }
             if (phi < 64) u0 |= (uint64_t)b << phi; else u1 |= (uint64_t)b << (phi - 64);
