@@ -552,13 +552,14 @@ PSCL_HD double pscl_softplus_tail_abs(double v) { return (double)pscl_tail_abs_f
  *   * the reference's own rounding of each increment (one ulp, < 2^-52 at these magnitudes);
  *   * the scaled tree itself: f is 1-Lipschitz in each argument and g rounds once, so a leaf
  *     computed from the scaled channel row differs from log2 e times the fp64 leaf of the exact
- *     decode by at most 15 u S' (u = 2^-53, S' = the row's sum of scaled magnitudes: 8 u S' for
- *     the scaled tree against real arithmetic -- the scaling and seven levels, each channel value
- *     under seven g nodes -- and log2 e * 7 u S for the fp64 tree).  The kernel defers every frame
- *     where one lane's share of the row (128 / L values, L = 4 or 8 lanes per frame) has scaled
- *     magnitudes summing to 2^14 or more (S' < 2^17), so that term is below PSCL_TAIL2_TREE = 2^-31
- *     per increment (15 * 2^-53 * 2^17 < 2^-32).  (h(x) = log2(1 + 2^-x) is 1-Lipschitz, so the error
- *     of an increment is at most the error of its LLR whichever child the LLR's sign names.)
+ *     decode by at most (2 n + 1) u S' (u = 2^-53, S' = the row's sum of scaled magnitudes, n =
+ *     log2 N levels: (n + 1) u S' for the scaled tree against real arithmetic -- the scaling and
+ *     n levels, each channel value under n g nodes -- and log2 e * n u S for the fp64 tree).  The
+ *     kernels defer every frame where one lane's share of the row (N / L values, L = 4 or 8 lanes
+ *     per frame) has scaled magnitudes summing to 2^14 or more (S' < 2^17), so that term is below
+ *     PSCL_TAIL2_TREE = 2^-31 per increment for every N <= 1024 (21 * 2^-53 * 2^17 < 2^-31).
+ *     (h(x) = log2(1 + 2^-x) is 1-Lipschitz, so the error of an increment is at most the error of
+ *     its LLR whichever child the LLR's sign names.)
  */
 #define PSCL_LOG2E_F64 1.4426950408889634
 #ifndef PSCL_TAIL2_SCAN

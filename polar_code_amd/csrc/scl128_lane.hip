@@ -74,13 +74,6 @@ struct LaneLayout {
 #define PSCL_LANE_ABL 0
 #endif
 
-// plain decodes compute the LLR tree in units of log2 e and the metrics in bits (the tail without its
-// two fp32 multiplies, glibc_softplus.h pscl_softplus_tail2); the FS retry decodes, whose warm-start
-// metrics come from the post pass in nats, keep the natural-log form
-#ifndef PSCL_LANE_BITS
-#define PSCL_LANE_BITS 1
-#endif
-
 #ifndef PSCL_LANE_WAVES_PER_EU
 #define PSCL_LANE_WAVES_PER_EU 2
 #endif

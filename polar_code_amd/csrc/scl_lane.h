@@ -11,6 +11,13 @@
 #endif
 
 
+// plain decodes compute the LLR tree in units of log2 e and the metrics in bits (the tail without its
+// two fp32 multiplies, glibc_softplus.h pscl_softplus_tail2); the N = 128 FS retry decodes, whose
+// warm-start metrics come from the post pass in nats, keep the natural-log form
+#ifndef PSCL_LANE_BITS
+#define PSCL_LANE_BITS 1
+#endif
+
 namespace {
 
 // intra-frame lane permutations of an 8-lane group (DPP controls): quad_perm xor 1, 2, 3, and the

@@ -80,8 +80,12 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
     constexpr int EPL = 16 / G;         // depth-R elements per lane at a block start
     constexpr uint32_t GM = (1u << G) - 1u;
     constexpr bool CREG = EPL * CE <= 32;  // N = 256, L = 8: the lane's channel LLRs stay in registers
-    // every metric carries N tail terms: two metrics differ from their exact values by < 2 N DELTA
-    constexpr double MARGIN = 2.0 * N * PSCL_TAIL_ABS_DELTA * 1.0001;
+    // every metric carries N tail terms: two metrics differ from their exact values by < 2 N DELTA.
+    // Metrics in bits (PSCL_LANE_BITS, scl128_lane.hip): the channel LLRs scaled by log2 e as they
+    // are loaded, the tail without its multiplies, DELTA = PSCL_TAIL2_DELTA (glibc_softplus.h: its
+    // tree term covers n <= 10 levels, (2 n + 2) u S' < 2^-31 for S' < 2^17)
+    constexpr bool BITS = PSCL_LANE_BITS;
+    constexpr double MARGIN = 2.0 * N * (BITS ? PSCL_TAIL2_DELTA : PSCL_TAIL_ABS_DELTA) * 1.0001;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double* const A = reinterpret_cast<double*>(smem);
     const int lane = threadIdx.x & 63;
@@ -92,7 +96,13 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
     const uint32_t* const ST = reinterpret_cast<const uint32_t*>(GT + (N / 8) * 256);  // [K/4][16] nibble -> syndrome
     const int K = P.K, W = P.W;
     auto hiw = [](double m) { return (uint32_t)(pscl_asu64(m) >> 32); };
-    auto hiw_up = [&](double m) { return hiw(__builtin_fma(m, 1.0 + 0x1p-40, MARGIN)); };
+    // the margin-raised key as one VOP3 fma with the factor in an SGPR (scl128_lane.hip)
+    auto hiw_up = [&](double m) {
+        double r;
+        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(m), "s"(1.0 + 0x1p-40), "v"(MARGIN));
+        return hiw(r);
+    };
+    auto frame_bits = [&](uint64_t m) { return (uint32_t)(m >> gbase) & GM; };
     auto slot_rel = [](uint32_t tab, int dr) { return (int)((tab >> (4 * dr)) & 15u); };
 
     int cfe = 0, cbe = 0, cpe = 0, cpb = 0;  // this lane's error counts (flushed at the end)
@@ -110,11 +120,11 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
             for (int h = 0; h < EPL; ++h)
 #pragma unroll
                 for (int m = 0; m < CE; ++m) {
-                    const double v = chan[p + G * h + 16 * m];
+                    const double v = BITS ? chan[p + G * h + 16 * m] * PSCL_LOG2E_F64 : chan[p + G * h + 16 * m];
                     if constexpr (CREG) c[CE * h + m] = v;
                     cs = cs + fabs(v);
                 }
-            amb = wmask(!(cs < 0x1p25));
+            amb = wmask(!(cs < (BITS ? PSCL_TAIL2_CHAN_SUM : 0x1p25)));
         }
         const uint64_t vmask = wmask(fvalid);
 
@@ -214,7 +224,7 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
                         for (int m = 0; m < CE; ++m) ch[m] = c[CE * h + m];
                     } else {
 #pragma unroll
-                        for (int m = 0; m < CE; ++m) ch[m] = chan[e + 16 * m];
+                        for (int m = 0; m < CE; ++m) ch[m] = BITS ? chan[e + 16 * m] * PSCL_LOG2E_F64 : chan[e + 16 * m];
                     }
                     if (!r1) {
                         // depth 1 before phase N/2: the same f node for every path (the channel
@@ -304,7 +314,7 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
                 // ---- leaf LLR and metric tail (scl.py:80-82, 102-105)
                 const double2 lab = *reinterpret_cast<const double2*>(Af + Ly::OFF3 + (start <= NL - 1 ? p : slot_rel(tab, 3)) * 2);
                 const double lam = (t & 1) ? g_node(lab.x, lab.y, lastbit) : f_minsum(lab.x, lab.y);
-                const double Lt = pscl_softplus_tail_abs(lam);
+                const double Lt = BITS ? pscl_softplus_tail2(lam) : pscl_softplus_tail_abs(lam);
                 if (!is_info) {  // frozen: bit 0 (scl.py:149-153)
                     metric = metric + (relu_neg(lam) + Lt);
                     lastbit = 0;
@@ -333,70 +343,62 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
                 const uint32_t mx = frame_max<G>(kgu);
                 const bool bad = kb <= mx;
                 const uint64_t badm = wmask(bad);
-                if ((badm & vmask) == 0) {
-                    metric = mg;
-                    lastbit = gbit;
-                    ub |= gbit << t;
-                    return;
-                }
-                const uint32_t sh = (uint32_t)gbase & 31u;
-                const uint32_t bad8 = ((fl < F / 2 ? (uint32_t)badm : (uint32_t)(badm >> 32)) >> sh) & GM;
-                int src;
-                bool take;  // this lane's path becomes a pulled worse child
-#if PSCL_LANE_SWAP
-                if ((wmask(__builtin_popcount(bad8) > 1) & vmask) == 0) {
-                    // one swap per frame at most (scl128_lane.hip): the largest better child gives
-                    // way to the one unclear worse child, certified by the margin or deferred
-                    const uint32_t kg = hiw(mg);
-                    const uint32_t gmaxh = frame_max<G>(kg);
-                    const bool ismax = kg == gmaxh;
-                    const uint32_t nmax = frame_sum<G>(ismax ? 1u : 0u);
-                    const uint32_t g2u = frame_max<G>(ismax ? 0u : kgu);
-                    const uint32_t wu = frame_max<G>(bad ? hiw_up(mb) : 0u);
-                    const bool swap = bad8 != 0;
-                    amb |= wmask(swap && !(nmax == 1u && g2u < gmaxh && wu < gmaxh)) & vmask;
-                    src = (gbase + (int)__builtin_ctz(bad8 | (1u << G))) & 63;
-                    take = swap && ismax;
-                } else
-#endif
-                {
-                    // rank the 2L children of each frame: counts of keys (high words) strictly below each
-                    const uint32_t kg = hiw(mg);
-                    bool keep_g, win_b;
-                    select_survivors<G, LMAX>(kg, kb, keep_g, win_b);
-                    const uint32_t kbu = hiw_up(mb);
-                    const uint32_t su = keep_g ? (win_b ? kbu : kgu) : (win_b ? kbu : 0u);
-                    const uint32_t nm = keep_g ? (win_b ? 0xffffffffu : kb) : kg;
-                    const uint32_t nsurv = frame_sum<G>((keep_g ? 1u : 0u) + (win_b ? 1u : 0u));
-                    const uint32_t smax = frame_max<G>(su), nmin = frame_min<G>(nm);
-                    amb |= wmask(!(nsurv == (uint32_t)LMAX && nmin > smax)) & vmask;
-                    const uint64_t fw = wmask(!keep_g), ww = wmask(win_b);
-                    const uint32_t f8 = ((fl < F / 2 ? (uint32_t)fw : (uint32_t)(fw >> 32)) >> sh) & GM;
-                    const uint32_t w8 = ((fl < F / 2 ? (uint32_t)ww : (uint32_t)(ww >> 32)) >> sh) & GM;
-                    const uint32_t j = __builtin_popcount(f8 & ((1u << p) - 1u));
-                    src = gbase + (int)nth_set_bit8(w8, j);
-                    take = !keep_g;
-                }
-                // the worse child's bit rides on the table word
-                const uint32_t tw = tab | ((gbit ^ 1u) << 31);
-                const uint64_t pmb = shfl_u64(pscl_asu64(mb), src);
-                const uint32_t ptw = bperm32(tw, src);
-                const uint32_t pub = bperm32(ub, src);
-                // (word by word: one pulled word live at a time)
-#pragma unroll
-                for (int k = 0; k < NW; ++k)
-                    if (64 * k < 16 * b) {
-                        const uint64_t x = shfl_u64(u[k], src);
-                        u[k] = take ? x : u[k];
-                    }
+                metric = mg;
                 uint32_t bt = gbit;
-                if (take) {
-                    metric = pscl_asf64(pmb);
-                    ub = pub;
-                    tab = ptw & 0x7fffffffu;
-                    bt = ptw >> 31;
-                } else {
-                    metric = mg;
+                if ((badm & vmask) != 0) {
+                    const uint32_t bad8 = frame_bits(badm);
+                    int src;
+                    bool take;  // this lane's path becomes a pulled worse child
+#if PSCL_LANE_SWAP
+                    if ((wmask(__builtin_popcount(bad8) > 1) & vmask) == 0) {
+                        // one swap per frame at most (scl128_lane.hip): the largest better child gives
+                        // way to the one unclear worse child, certified by the margin or deferred
+                        const uint32_t kg = hiw(mg);
+                        const uint32_t gmaxh = frame_max<G>(kg);
+                        const bool ismax = kg == gmaxh;
+                        const uint32_t nmax = frame_sum<G>(ismax ? 1u : 0u);
+                        const uint32_t g2u = frame_max<G>(ismax ? 0u : kgu);
+                        const uint32_t wu = frame_max<G>(bad ? hiw_up(mb) : 0u);
+                        const bool swap = bad8 != 0;
+                        amb |= wmask(swap && !(nmax == 1u && g2u < gmaxh && wu < gmaxh)) & vmask;
+                        src = (gbase + (int)__builtin_ctz(bad8 | (1u << G))) & 63;
+                        take = swap && ismax;
+                    } else
+#endif
+                    {
+                        // rank the 2L children of each frame (select_survivors) and certify
+                        const uint32_t kg = hiw(mg);
+                        bool keep_g, win_b;
+                        select_survivors<G, LMAX>(kg, kb, keep_g, win_b);
+                        const uint32_t kbu = hiw_up(mb);
+                        const uint32_t su = keep_g ? (win_b ? kbu : kgu) : (win_b ? kbu : 0u);
+                        const uint32_t nm = keep_g ? (win_b ? 0xffffffffu : kb) : kg;
+                        const uint32_t nsurv = frame_sum<G>((keep_g ? 1u : 0u) + (win_b ? 1u : 0u));
+                        const uint32_t smax = frame_max<G>(su), nmin = frame_min<G>(nm);
+                        amb |= wmask(!(nsurv == (uint32_t)LMAX && nmin > smax)) & vmask;
+                        const uint32_t f8 = frame_bits(wmask(!keep_g)), w8 = frame_bits(wmask(win_b));
+                        const uint32_t j = __builtin_popcount(f8 & ((1u << p) - 1u));
+                        src = gbase + (int)nth_set_bit8(w8, j);
+                        take = !keep_g;
+                    }
+                    // the worse child's bit rides on the table word
+                    const uint32_t tw = tab | ((gbit ^ 1u) << 31);
+                    const uint64_t pmb = shfl_u64(pscl_asu64(mb), src);
+                    const uint32_t ptw = bperm32(tw, src);
+                    const uint32_t pub = bperm32(ub, src);
+                    // (word by word: one pulled word live at a time)
+#pragma unroll
+                    for (int k = 0; k < NW; ++k)
+                        if (64 * k < 16 * b) {
+                            const uint64_t x = shfl_u64(u[k], src);
+                            u[k] = take ? x : u[k];
+                        }
+                    if (take) {
+                        metric = pscl_asf64(pmb);
+                        ub = pub;
+                        tab = ptw & 0x7fffffffu;
+                        bt = ptw >> 31;
+                    }
                 }
                 ub |= bt << t;
                 lastbit = bt;
