@@ -562,8 +562,10 @@ PSCL_HD double pscl_softplus_tail_abs(double v) { return (double)pscl_tail_abs_f
  *     its LLR whichever child the LLR's sign names.)
  */
 #define PSCL_LOG2E_F64 1.4426950408889634
+/* upper bound of the exhaustive device scan: measured on MI355X 1.4155e-7 = 2.37 * 2^-24 bits, at
+ * y32 = 0.93874 (tests/test_gpu_screening.py::test_tail2_exhaustive_device, profiles/r05g_scan.txt) */
 #ifndef PSCL_TAIL2_SCAN
-#define PSCL_TAIL2_SCAN (4.0 / 16777216.0)
+#define PSCL_TAIL2_SCAN (2.5 / 16777216.0)
 #endif
 #define PSCL_TAIL2_TREE (1.0 / 2147483648.0)
 #define PSCL_TAIL2_DELTA (PSCL_TAIL2_SCAN + 0.41 / 16777216.0 + 2.0 * 2.220446049250313e-16 + PSCL_TAIL2_TREE)
