@@ -44,6 +44,9 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+#ifndef PSCL_F_ASM
+#define PSCL_F_ASM 1
+#endif
 // f(a,b) = sign(a) sign(b) min(|a|,|b|)  (polar.py:122-123).  Exact: the result is one of the
 // inputs' magnitudes with the XOR of the signs (sign(0) = 0 makes a +-0 result either way, and
 // the sign of a zero never reaches a decision or a metric).  v_min_f64 with |.| source
@@ -54,10 +57,14 @@ __device__ __forceinline__ double f_minsum(double a, double b) {
     asm("v_min_f64 %0, |%1|, |%2|" : "=v"(m) : "v"(a), "v"(b));
     const uint64_t ab = pscl_asu64(a), bb = pscl_asu64(b), mb = pscl_asu64(m);
     const uint32_t x = (uint32_t)(ab >> 32) ^ (uint32_t)(bb >> 32);
+#if PSCL_F_ASM
     // v_and_or_b32 with the sign mask in an SGPR: a VOP3 encoding takes no literal on gfx950, and
     // left to itself the compiler splits the fold into v_and_b32 (literal) + v_or_b32
     uint32_t hi;
     asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(hi) : "v"(x), "s"(0x80000000u), "v"((uint32_t)(mb >> 32)));
+#else
+    const uint32_t hi = (uint32_t)(mb >> 32) | (x & 0x80000000u);
+#endif
     return pscl_asf64(((uint64_t)hi << 32) | (uint32_t)mb);
 }
 // g(a,b,c) = b + (1-2c) a  (polar.py:126-127): b + (+-a), one rounding, sign of a flipped by c
