@@ -54,10 +54,13 @@ struct LaneLayout {
     // 5 and 6 live in registers (depth 4 is rewritten after the recompute has read them)
     static constexpr int OFFX = PSCL_LANE_REG56 ? OFF4 : OFF6;
     static constexpr int RAW = PSCL_LANE_REG56 ? OFF5 : OFF6 + 2 * LMAX;
-    // frames at a stride = 16 (mod 32) doubles (at L = 8: 240 or, with REG56, 208): frames start
+    // frame stride in doubles: = 16 (mod 32) at L = 8 (240, or 208 with REG56): frames start
     // alternately on the two 128-byte halves of the 256-byte bank row and a ds_read_b128 lane group
-    // (lanes of 4 frames) touching one pair index of its paths' slots covers 4 distinct 64-byte quarters
-    static constexpr int FSTRIDE = RAW + (((16 - RAW) % 32) + 32) % 32;
+    // (lanes of 4 frames) touching one pair index of its paths' slots covers 4 distinct 64-byte
+    // quarters; = 24 (mod 32) at L = 4 (120 either way; 112 = 16 mod 32 measured 46 % bank
+    // conflicts against 4.5 %: the L = 4 kernel's occupancy is bound by its VGPRs, not its LDS)
+    static constexpr int FRES = LMAX == 8 ? 16 : 24;
+    static constexpr int FSTRIDE = RAW + (((FRES - RAW) % 32) + 32) % 32;
 };
 
 // L = 4: keep the lane's 32 channel LLRs in registers across the frame (1) or re-read them at each
