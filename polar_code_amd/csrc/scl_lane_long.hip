@@ -54,9 +54,11 @@ struct LongLaneLayout {
 #define PSCL_LANE_LONG_WAVES_PER_EU 2
 #endif
 // N = 1024: the element recompute holds 64 channel LLRs (128 VGPRs); at 2 waves/SIMD (256 VGPRs)
-// it spills ~120 dwords, at 1 (512) none -- LDS allows 6 wavefronts per CU either way
+// it spills (592 bytes of scratch per lane), at 1 (512) none -- LDS allows 6 wavefronts per CU
+// either way.  Measured (tools/long_bench.py, profiles/r05j_long_*): 3.42 M frames/s at 1 against
+// 2.60 M at 2 (4.36 M against 3.02 M pipelined)
 #ifndef PSCL_LANE_LONG1024_WAVES_PER_EU
-#define PSCL_LANE_LONG1024_WAVES_PER_EU 2
+#define PSCL_LANE_LONG1024_WAVES_PER_EU 1
 #endif
 
 // word k of the register array u, k wave-uniform
