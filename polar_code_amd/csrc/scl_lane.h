@@ -23,6 +23,13 @@ namespace {
 // intra-frame lane permutations of an 8-lane group (DPP controls): quad_perm xor 1, 2, 3, and the
 // half-row mirror (lane i <-> 7 - i), which maps one quad onto the other
 constexpr int kQX1 = 0xB1, kQX2 = 0x4E, kQX3 = 0x1B, kQID = 0xE4, kHMIR = 0x141;
+// the permutation that maps one quad of an 8-lane frame onto the other: row_half_mirror (0x141,
+// lane i <-> 7 - i) for frames of 8 consecutive lanes; row_mirror (0x140, lane i <-> 15 - i) for the
+// N = 128 kernel's frames of the outer or the inner two quads of a row (scl128_lane.hip)
+#ifndef PSCL_LANE_FRAME_MIRROR
+#define PSCL_LANE_FRAME_MIRROR 0x141
+#endif
+constexpr int kFMIR = PSCL_LANE_FRAME_MIRROR;
 
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp32(uint32_t v) {
@@ -81,7 +88,7 @@ __device__ __forceinline__ uint32_t frame_max(uint32_t v) {
     o = dpp32<kQX2>(v);
     v = o > v ? o : v;
     if constexpr (G == 8) {
-        o = dpp32<kHMIR>(v);
+        o = dpp32<kFMIR>(v);
         v = o > v ? o : v;
     }
     return v;
@@ -93,7 +100,7 @@ __device__ __forceinline__ uint32_t frame_min(uint32_t v) {
     o = dpp32<kQX2>(v);
     v = o < v ? o : v;
     if constexpr (G == 8) {
-        o = dpp32<kHMIR>(v);
+        o = dpp32<kFMIR>(v);
         v = o < v ? o : v;
     }
     return v;
@@ -102,7 +109,7 @@ template <int G>
 __device__ __forceinline__ uint32_t frame_sum(uint32_t v) {
     v += dpp32<kQX1>(v);
     v += dpp32<kQX2>(v);
-    if constexpr (G == 8) v += dpp32<kHMIR>(v);
+    if constexpr (G == 8) v += dpp32<kFMIR>(v);
     return v;
 }
 
@@ -126,7 +133,7 @@ __device__ __forceinline__ void select_survivors(uint32_t kg, uint32_t kb, bool&
     rank3<kQX2>(kg, kb, kg, kb, rg, rbb);
     rank3<kQX3>(kg, kb, kg, kb, rg, rbb);
     if constexpr (G == 8) {  // the other quad of the frame, through the half-row mirror
-        const uint32_t mkg = dpp32<kHMIR>(kg), mkb = dpp32<kHMIR>(kb);
+        const uint32_t mkg = dpp32<kFMIR>(kg), mkb = dpp32<kFMIR>(kb);
         rank3<kQID>(mkg, mkb, kg, kb, rg, rbb);
         rank3<kQX1>(mkg, mkb, kg, kb, rg, rbb);
         rank3<kQX2>(mkg, mkb, kg, kb, rg, rbb);
@@ -141,7 +148,7 @@ __device__ __forceinline__ void select_survivors(uint32_t kg, uint32_t kb, bool&
     rank_pair<kQX2>(kg, kb, kg, kb, rg, rb);
     rank_pair<kQX3>(kg, kb, kg, kb, rg, rb);
     if constexpr (G == 8) {
-        const uint32_t mkg = dpp32<kHMIR>(kg), mkb = dpp32<kHMIR>(kb);
+        const uint32_t mkg = dpp32<kFMIR>(kg), mkb = dpp32<kFMIR>(kb);
         rank_pair<kQID>(mkg, mkb, kg, kb, rg, rb);
         rank_pair<kQX1>(mkg, mkb, kg, kb, rg, rb);
         rank_pair<kQX2>(mkg, mkb, kg, kb, rg, rb);
