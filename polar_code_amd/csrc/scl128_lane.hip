@@ -37,9 +37,11 @@
 // reads (any 8 of its 8 slots, 16 B each) never meet another frame's: no LDS bank conflicts by
 // construction (8 consecutive lanes put four frames in a group, two per half, whose parent-slot
 // reads met: 11.8-16.5 % conflict cycles).  The within-frame permutations are unchanged in p (quad
-// perms on p % 4, the mirror p <-> 7 - p).
+// perms on p % 4, the mirror p <-> 7 - p).  Measured (profiles/r05k_remap_ab.txt): conflicts 16.5 ->
+// 10.7 % of LDS cycles, but the split frame bits cost 212 VALU per wavefront more and the launch
+// 1.96-1.97 ms against 1.92-1.95: off by default.
 #ifndef PSCL_LANE_REMAP
-#define PSCL_LANE_REMAP 1
+#define PSCL_LANE_REMAP 0
 #endif
 #if PSCL_LANE_REMAP
 #define PSCL_LANE_FRAME_MIRROR 0x140
