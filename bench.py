@@ -354,14 +354,17 @@ def run_workload(ctx: Ctx, *, L: int, E: int, retries: int, beta, B: int, steps:
     nbuf = max(1, min(steps, int(48e9 // (B * n_in * 8))))
     llr = [torch.empty((B, n_in), dtype=torch.float64, device=dev) for _ in range(nbuf)]
     msg = [torch.empty((B, W), dtype=torch.int64, device=dev) for _ in range(nbuf)]
-    # plain decodes run pipelined (pscl_set_pipelined: each step's exact re-decode of its deferred
-    # frames overlaps the next step's screening launch), so consecutive steps write alternate
-    # output buffers; the final synchronize covers every pending re-decode
+    # decodes run pipelined (pscl_set_pipelined: each step's exact re-decode of its deferred frames,
+    # or its DL-SCL retry chains, overlap the next steps), so consecutive steps write rotating output
+    # buffers: 2 for plain decodes, 4 for DL-SCL steps (the pipeline depth: a step's buffers are free
+    # again at the 4th following step, so the chains of up to three steps run behind the baselines);
+    # the final join + synchronize covers every pending re-decode and chain
     pipelined = True
+    depth = 4 if retries > 0 else 2
     if pipelined:
-        dec.set_pipelined(True)
-    best_b = [torch.empty((B, W), dtype=torch.int64, device=dev) for _ in range(2)]
-    flags_b = [torch.empty((B,), dtype=torch.uint8, device=dev) for _ in range(2)]
+        dec.set_pipelined(True, depth=depth)
+    best_b = [torch.empty((B, W), dtype=torch.int64, device=dev) for _ in range(depth)]
+    flags_b = [torch.empty((B,), dtype=torch.uint8, device=dev) for _ in range(depth)]
     calls = [0]
     counters = torch.zeros(8, dtype=torch.int64, device=dev)
     counters_dl = torch.zeros(8, dtype=torch.int64, device=dev)
@@ -374,7 +377,7 @@ def run_workload(ctx: Ctx, *, L: int, E: int, retries: int, beta, B: int, steps:
     def step(j, count=True):
         c_scl = counters.data_ptr() if count else 0
         ref = msg[j].data_ptr() if count else 0
-        best, flags = best_b[calls[0] & 1], flags_b[calls[0] & 1]
+        best, flags = best_b[calls[0] % depth], flags_b[calls[0] % depth]
         calls[0] += 1
         if retries > 0:  # SCL + DL-SCL retry rounds, all on the device
             dec.dlscl_device(llr[j].data_ptr(), B, retries, beta=beta, d_best=best.data_ptr(),
@@ -407,7 +410,7 @@ def run_workload(ctx: Ctx, *, L: int, E: int, retries: int, beta, B: int, steps:
     cdl = ctx.sum_over_ranks(counters_dl)
     # untimed: the step-0 batch once more, outputs kept for the parity check
     step(0, count=False)
-    best, flags = best_b[(calls[0] - 1) & 1], flags_b[(calls[0] - 1) & 1]
+    best, flags = best_b[(calls[0] - 1) % depth], flags_b[(calls[0] - 1) % depth]
     dec.sync()
     torch.cuda.synchronize(dev)
     res = {"N": N, "K": K, "W": W, "L": L, "E": E, "B": B, "n_in": n_in, "info": info, "retries": retries,

@@ -282,10 +282,14 @@ int pscl_screening_count(pscl_handle* h, int64_t* count);
  * pipelined decode.  Consecutive pipelined decodes must not write the same output buffers.
  * pscl_dlscl_device (one chunk) likewise: a pipelined call enqueues its baseline decode, then the
  * previous pipelined call's retry rounds and DL counters (on high-priority streams, beside this
- * call's baseline), and leaves its own rounds to the next call or the join.
+ * call's baseline), and leaves its own rounds to the next call or the join.  The retry chains of
+ * consecutive calls alternate two stream sets, so they run beside each other.  enable = d in
+ * 2..4 deepens the DL-SCL pipeline: a pscl_dlscl_device call's input, output and counter buffers
+ * are free again at the d-th following pipelined call (enable = 1: the second), so a caller
+ * cycling d output buffers lets the chains of up to d - 1 calls run behind the baselines.
  * Results are bit-identical to the non-pipelined form.  enable = 0 (default) restores
  * stream-ordered completion.  Timing (pscl_timing_*) of a pipelined decode covers its
- * screening launch only.
+ * screening launch only.  PSCL_EINVAL for enable outside 0..4.
  */
 int pscl_set_pipelined(pscl_handle* h, int enable);
 /* Order the pending pipelined re-decodes into the handle's stream (no host wait on the plain

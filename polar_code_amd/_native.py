@@ -392,10 +392,11 @@ class Decoder:
         x32 = float(np.array([int(out[1]) & 0xFFFFFFFF], np.uint32).view(np.float32)[0])
         return err, x32
 
-    def set_pipelined(self, on: bool = True) -> None:
+    def set_pipelined(self, on: bool = True, depth: int = 2) -> None:
         """Throughput mode for streams of plain decodes (include/polar_scl.h): a screening
-        decode's exact re-decode overlaps the next decode; join() / sync() order it back."""
-        check(lib().pscl_set_pipelined(self._h, 1 if on else 0))
+        decode's exact re-decode overlaps the next decode; join() / sync() order it back.  depth
+        (2..4): a DL-SCL call's buffers are free again at the depth-th following call."""
+        check(lib().pscl_set_pipelined(self._h, (depth if depth > 2 else 1) if on else 0))
 
     def join(self) -> None:
         """Order pending pipelined work into the handle's stream: the plain decodes' re-decodes

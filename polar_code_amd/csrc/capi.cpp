@@ -108,6 +108,11 @@ struct pscl_dl_call {
 // the chains (2 measured 175 M frames/s on the config-3 sweep, the stream waiting on chains of the
 // low-SNR points)
 constexpr int kDlPar = 4;
+// retry-chain sets: the chains of consecutive pipelined calls (and of consecutive chunks of one
+// call) alternate two sets of streams, events and state, so a call's chains run beside the previous
+// call's instead of queueing behind them; each set holds the chain pair of one call (k = 0, 1 at
+// index 2 set + k)
+constexpr int kChainSets = 2, kChainStreams = 2 * kChainSets;
 
 struct pscl_handle {
     int device = 0;
@@ -128,14 +133,14 @@ struct pscl_handle {
     int rm_E = 0;                     // NR rate matching (0 = off)
     int32_t* d_rm_src = nullptr;      // [N] de-interleave gather index
     int32_t* d_rm_order = nullptr;    // [N] interleaver order
-    DevBuf scratch[96];
-    hipStream_t retry_stream[2] = {nullptr, nullptr};  // DL-SCL retry chains of the two chunk parities
-    hipStream_t side_stream[2] = {nullptr, nullptr};   // their deferred-entry work (PSCL_TUNE_DL_SCREEN)
+    DevBuf scratch[128];
+    hipStream_t retry_stream[kChainStreams] = {};  // DL-SCL retry chains: [2 set + k], chain k of a call
+    hipStream_t side_stream[kChainStreams] = {};   // their deferred-entry work (PSCL_TUNE_DL_SCREEN)
     // the side streams of the other pipelining mode (their priority differs, create_priority_stream),
     // kept across pscl_set_pipelined switches: a stream creation costs ~0.5 ms of host time
-    hipStream_t stash_pipe = nullptr, stash_retry[2] = {nullptr, nullptr}, stash_side[2] = {nullptr, nullptr};
-    hipEvent_t ev_scr[2] = {nullptr, nullptr}, ev_def[2] = {nullptr, nullptr};
-    hipEvent_t ev_base[kDlPar] = {}, ev_retry[kDlPar] = {}, ev_join = nullptr;
+    hipStream_t stash_pipe = nullptr, stash_retry[kChainStreams] = {}, stash_side[kChainStreams] = {};
+    hipEvent_t ev_scr[kChainStreams] = {}, ev_def[kChainStreams] = {};
+    hipEvent_t ev_base[kDlPar] = {}, ev_retry[kDlPar] = {}, ev_join[kChainSets] = {};
     int32_t* h_count = nullptr;          // pinned: failing-frame counts of the chunk parities
     double* d_beta = nullptr;         // [K][K] DL-SCL flip metric (null = |L0|)
     double beta_absmax = 0.0;         // max |beta| (dl_post_kernel's certificate)
@@ -163,9 +168,9 @@ struct pscl_handle {
     hipEvent_t ev_dl[kDlPar] = {};
     bool dl_pending[kDlPar] = {};
     int dl_par = 0;
-    // how many calls back a pipelined call's own buffers may still be in use: 2 for the caller's
-    // buffers (the pscl_set_pipelined contract: free again at the second following call),
-    // kDlPar for pscl_simulate_device's own scratch sets
+    // how many calls back a pipelined call's own buffers may still be in use: for the caller's
+    // buffers the depth of pscl_set_pipelined (2 by default: free again at the second following
+    // call), kDlPar for pscl_simulate_device's own scratch sets
     int dl_back = 2;
     pscl_dl_call dl_defer;            // the last pipelined call, its chains not yet enqueued
     bool dl_defer_valid = false;
@@ -228,7 +233,7 @@ int join_pipe(pscl_handle* h, int what = 3) {
 // freed and regrown)
 void quiesce(pscl_handle* h) {
     if (h->pipe_stream) hipStreamSynchronize(h->pipe_stream);
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kChainStreams; ++i) {
         if (h->retry_stream[i]) hipStreamSynchronize(h->retry_stream[i]);
         if (h->side_stream[i]) hipStreamSynchronize(h->side_stream[i]);
     }
@@ -240,14 +245,14 @@ void drop_side_streams(pscl_handle* h) {
     quiesce(h);
     if (h->stash_pipe) hipStreamDestroy(h->stash_pipe);
     h->stash_pipe = nullptr;
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kChainStreams; ++i) {
         if (h->stash_retry[i]) hipStreamDestroy(h->stash_retry[i]);
         if (h->stash_side[i]) hipStreamDestroy(h->stash_side[i]);
         h->stash_retry[i] = h->stash_side[i] = nullptr;
     }
     if (h->pipe_stream) hipStreamDestroy(h->pipe_stream);
     h->pipe_stream = nullptr;
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kChainStreams; ++i) {
         if (h->retry_stream[i]) hipStreamDestroy(h->retry_stream[i]);
         if (h->side_stream[i]) hipStreamDestroy(h->side_stream[i]);
         h->retry_stream[i] = h->side_stream[i] = nullptr;
@@ -646,16 +651,17 @@ int pscl_destroy(pscl_handle* h) {
     if (h->d_epi) hipFree(h->d_epi);
     if (h->d_xtab) hipFree(h->d_xtab);
     if (h->d_crctab) hipFree(h->d_crctab);
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < kChainStreams; ++i)
         if (h->retry_stream[i]) hipStreamSynchronize(h->retry_stream[i]);
     for (int i = 0; i < kDlPar; ++i) {
         if (h->ev_base[i]) hipEventDestroy(h->ev_base[i]);
         if (h->ev_retry[i]) hipEventDestroy(h->ev_retry[i]);
         if (h->ev_dl[i]) hipEventDestroy(h->ev_dl[i]);
     }
-    if (h->ev_join) hipEventDestroy(h->ev_join);
+    for (int i = 0; i < kChainSets; ++i)
+        if (h->ev_join[i]) hipEventDestroy(h->ev_join[i]);
     if (h->h_count) hipHostFree(h->h_count);
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kChainStreams; ++i) {
         if (h->side_stream[i]) hipStreamSynchronize(h->side_stream[i]);
         if (h->retry_stream[i]) hipStreamDestroy(h->retry_stream[i]);
         if (h->side_stream[i]) hipStreamDestroy(h->side_stream[i]);
@@ -668,7 +674,7 @@ int pscl_destroy(pscl_handle* h) {
     }
     if (h->pipe_stream) hipStreamDestroy(h->pipe_stream);
     if (h->stash_pipe) hipStreamDestroy(h->stash_pipe);
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kChainStreams; ++i) {
         if (h->stash_retry[i]) hipStreamDestroy(h->stash_retry[i]);
         if (h->stash_side[i]) hipStreamDestroy(h->stash_side[i]);
     }
@@ -738,16 +744,20 @@ int pscl_set_pipelined(pscl_handle* h, int enable) {
     int rc = set_device(h);
     if (rc) return rc;
     if ((rc = join_pipe(h))) return rc;
+    if (enable < 0 || enable > kDlPar) return fail(PSCL_EINVAL, "pipelined depth %d out of range 0..%d", enable, kDlPar);
     if (h->pipelined != (enable != 0)) {
         // the other mode's streams in, this mode's to the stash (drained first)
         quiesce(h);
         std::swap(h->pipe_stream, h->stash_pipe);
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < kChainStreams; ++i) {
             std::swap(h->retry_stream[i], h->stash_retry[i]);
             std::swap(h->side_stream[i], h->stash_side[i]);
         }
     }
     h->pipelined = enable != 0;
+    // DL-SCL calls: a call's buffers are free again at the depth-th following call (1 and 2: the
+    // second, the documented default); its chains run up to depth - 1 calls behind the baselines
+    h->dl_back = enable >= 2 ? enable : 2;
     return PSCL_OK;
 }
 
@@ -1082,7 +1092,7 @@ constexpr int kMinSplit = 2048;
 
 // the retry chains' state (scratch slots), sized by dl_setup
 struct DlBufs {
-    DlState S[2];         // chain state (S[k] on retry stream k)
+    DlState S[kChainStreams];  // chain state (S[2 set + k] on retry stream 2 set + k)
     DlLongState LS = {};  // (long codes)
     int32_t* cnt[kDlPar] = {};  // failing-frame count of the compaction parities
     int64_t* act[kDlPar] = {};  // their frame indices
@@ -1099,19 +1109,22 @@ int dl_setup(pscl_handle* h, const pscl_dl_call& a, DlBufs& b) {
     int rc;
     const int K = h->K, W = h->W, rounds = a.rounds;
     const int64_t cap = a.cap;
-    for (int i = 0; i < 2; ++i)
+    // chain sets: a pipelined call's chains (or an unpipelined call's chunk chains) alternate two
+    const int nsets = (h->N <= PSCL_FAST_N && (a.pipe || a.nch >= 2)) ? kChainSets : 1;
+    for (int i = 0; i < 2 * nsets; ++i)
         if (!h->retry_stream[i]) HIP_TRY(create_priority_stream(h, &h->retry_stream[i]));
     for (int i = 0; i < kDlPar; ++i) {
         if (!h->ev_base[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_base[i], hipEventDisableTiming));
         if (!h->ev_retry[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_retry[i], hipEventDisableTiming));
         if (!h->ev_dl[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_dl[i], hipEventDisableTiming));
     }
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 2 * nsets; ++i) {
         if (!h->side_stream[i]) HIP_TRY(create_priority_stream(h, &h->side_stream[i]));
         if (!h->ev_scr[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_scr[i], hipEventDisableTiming));
         if (!h->ev_def[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_def[i], hipEventDisableTiming));
     }
-    if (!h->ev_join) HIP_TRY(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+    for (int i = 0; i < nsets; ++i)
+        if (!h->ev_join[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_join[i], hipEventDisableTiming));
     if (!h->h_count) HIP_TRY(hipHostMalloc((void**)&h->h_count, 4 * kDlPar, hipHostMallocDefault));
     const size_t NS = PSCL_DL_NSEG;
     for (int i = 0; i < (a.pipe ? kDlPar : (a.nch >= 2 ? 2 : 1)); ++i) {
@@ -1144,42 +1157,53 @@ int dl_setup(pscl_handle* h, const pscl_dl_call& a, DlBufs& b) {
         if ((rc = ensure(h, kLongRetryScratch, (size_t)pscl_decode_grid(H) * (size_t)H.long_block_bytes, &d_scr)))
             return rc;
     }
-    for (int i = 0; i < a.nsplit; ++i) {
+    for (int j = 0; j < a.nsplit * nsets; ++j) {
         // chain 0 takes every entry of a call that does not split (fewer than 2 kMinSplit
         // failing frames, which may still exceed half the chunk); chain 1 at most half
+        const int i = j & 1, set = j >> 1;
         const size_t c = (size_t)(i == 0 ? cap : cap - cap / 2);
         const size_t sz[14] = {(size_t)(rounds + 1) * NS * PSCL_DL_CSTRIDE * 4, NS * c * 4, NS * c * 4, c * 16, c * 4,
                                c * 2 * W * 8, c * NS * 8, c * 16, c * W * 8, c,
                                (size_t)(rounds + 1) * NS * PSCL_DL_CSTRIDE * 4, (size_t)(rounds + 1) * NS * c * 4,
                                c * W * 8, c};
-        static const int slot[2][14] = {{12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 8, 9, 10, 11},
-                                        {40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 24, 29}};
+        static const int slot[kChainStreams][14] = {{12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 8, 9, 10, 11},
+                                                    {40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 24, 29},
+                                                    {96, 97, 98, 99, 100, 101, 102, 103, 104, 105, 106, 107, 108, 109},
+                                                    {110, 111, 112, 113, 114, 115, 116, 117, 118, 119, 120, 121, 122, 123}};
         void* q[14];
         for (int k = 0; k < 14; ++k)
-            if ((rc = ensure(h, slot[i][k], sz[k], &q[k]))) return rc;
-        b.S[i].dcnt = (int32_t*)q[10];
-        b.S[i].dlist = (int32_t*)q[11];
-        b.S[i].ob2 = (uint64_t*)q[12];
-        b.S[i].of2 = (uint8_t*)q[13];
-        b.S[i].bcnt = (int32_t*)q[0];
-        b.S[i].list0 = (int32_t*)q[1];
-        b.S[i].list1 = (int32_t*)q[2];
-        b.S[i].tried = (uint64_t*)q[3];
-        b.S[i].nt = (int32_t*)q[4];
-        b.S[i].force = (uint64_t*)q[5];
-        b.S[i].warm_metric = (double*)q[6];
-        b.S[i].warm_u = (uint64_t*)q[7];
-        b.S[i].ob = (uint64_t*)q[8];
-        b.S[i].of = (uint8_t*)q[9];
+            if ((rc = ensure(h, slot[j][k], sz[k], &q[k]))) return rc;
+        DlState& T = b.S[2 * set + i];
+        T.dcnt = (int32_t*)q[10];
+        T.dlist = (int32_t*)q[11];
+        T.ob2 = (uint64_t*)q[12];
+        T.of2 = (uint8_t*)q[13];
+        T.bcnt = (int32_t*)q[0];
+        T.list0 = (int32_t*)q[1];
+        T.list1 = (int32_t*)q[2];
+        T.tried = (uint64_t*)q[3];
+        T.nt = (int32_t*)q[4];
+        T.force = (uint64_t*)q[5];
+        T.warm_metric = (double*)q[6];
+        T.warm_u = (uint64_t*)q[7];
+        T.ob = (uint64_t*)q[8];
+        T.of = (uint8_t*)q[9];
     }
     return PSCL_OK;
 }
 
+// the chain set of chunk c: alternating by call (pipelined) or by chunk; the long codes' single
+// dense-state chain keeps set 0
+inline int dl_set(const pscl_handle* h, const pscl_dl_call& a, int64_t c) {
+    return h->N > PSCL_FAST_N ? 0 : (a.pipe ? a.pbase : (int)c) & (kChainSets - 1);
+}
+
 // the retry chains of chunk c (compaction parity p): the host reads the chunk's failing count
-// (waiting for its baseline) and enqueues the rounds on the retry streams; ev_retry[p] marks
-// their end on retry stream 0
+// (waiting for its baseline) and enqueues the rounds on the retry streams of the chunk's set;
+// ev_retry[p] marks their end on the set's first retry stream
 int dl_chain(pscl_handle* h, const pscl_dl_call& a, const DlBufs& b, int64_t c, bool beside) {
     const int p = dl_parity(a, c);
+    const int cs = 2 * dl_set(h, a, c);  // the set's first stream
     const int64_t cap = a.cap;
     HIP_TRY(hipEventSynchronize(h->ev_base[p]));
     const int A = h->h_count[p];
@@ -1201,19 +1225,19 @@ int dl_chain(pscl_handle* h, const pscl_dl_call& a, const DlBufs& b, int64_t c, 
         if (nk > capk)
             return fail(PSCL_EDEVICE, "retry chain %d: %lld entries exceed its state (%lld)", k, (long long)nk,
                         (long long)capk);
-        HIP_TRY(hipStreamWaitEvent(h->retry_stream[k], h->ev_base[p], 0));
-        DlState T = b.S[k];
+        HIP_TRY(hipStreamWaitEvent(h->retry_stream[cs + k], h->ev_base[p], 0));
+        DlState T = b.S[cs + k];
         T.act = b.act[p] + (k ? A0 : 0);
         int r2 = dl_retry_chunk(h, T, k ? A - A0 : A0, a.rounds, a.d_llr, a.d_best, a.d_flags, a.d_attempts,
-                                a.d_tried, a.tried_stride, d_cdl, h->retry_stream[k], h->side_stream[k], h->ev_scr[k],
-                                h->ev_def[k], a.pipe, beside);
+                                a.d_tried, a.tried_stride, d_cdl, h->retry_stream[cs + k], h->side_stream[cs + k],
+                                h->ev_scr[cs + k], h->ev_def[cs + k], a.pipe, beside);
         if (r2) return r2;
     }
     if (parts == 2) {  // both chains done before the parity's indices are reused
-        HIP_TRY(hipEventRecord(h->ev_join, h->retry_stream[1]));
-        HIP_TRY(hipStreamWaitEvent(h->retry_stream[0], h->ev_join, 0));
+        HIP_TRY(hipEventRecord(h->ev_join[cs >> 1], h->retry_stream[cs + 1]));
+        HIP_TRY(hipStreamWaitEvent(h->retry_stream[cs], h->ev_join[cs >> 1], 0));
     }
-    HIP_TRY(hipEventRecord(h->ev_retry[p], h->retry_stream[0]));
+    HIP_TRY(hipEventRecord(h->ev_retry[p], h->retry_stream[cs]));
     return PSCL_OK;
 }
 
@@ -1228,12 +1252,12 @@ int dl_enqueue_deferred(pscl_handle* h, bool beside) {
     int rc = dl_setup(h, a, b);  // (the sizes of the call's own setup: no allocation)
     if (rc) return rc;
     if ((rc = dl_chain(h, a, b, 0, beside))) return rc;
+    hipStream_t rs = h->retry_stream[2 * dl_set(h, a, 0)];
     if (a.d_ref) {
-        hipError_t e = pscl_launch_dl_count(a.d_best, a.d_flags, a.d_ref, a.B, h->W, a.k_payload, a.d_counters_dl,
-                                            h->retry_stream[0]);
+        hipError_t e = pscl_launch_dl_count(a.d_best, a.d_flags, a.d_ref, a.B, h->W, a.k_payload, a.d_counters_dl, rs);
         if (e != hipSuccess) return fail(PSCL_EDEVICE, "dl_count launch: %s", hipGetErrorString(e));
     }
-    HIP_TRY(hipEventRecord(h->ev_dl[a.pbase], h->retry_stream[0]));
+    HIP_TRY(hipEventRecord(h->ev_dl[a.pbase], rs));
     h->dl_pending[a.pbase] = true;
     return PSCL_OK;
 }
@@ -1357,7 +1381,9 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
     }
     if (rounds > 0) {
         if ((rc = dl_chain(h, a, bufs, nch - 1, false))) return rc;
-        HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[dl_parity(a, nch - 1)], 0));  // chains run in order on stream 0
+        // (the chunk chains alternate two sets: the last two end every chain)
+        HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[dl_parity(a, nch - 1)], 0));
+        if (nch >= 2) HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[dl_parity(a, nch - 2)], 0));
     }
     if (d_ref) {
         e = pscl_launch_dl_count(d_best, d_flags, d_ref, B, W, k_payload, d_counters_dl, s);
@@ -1536,10 +1562,11 @@ int simulate_enqueue(pscl_handle* h, uint64_t seed, uint32_t stream_id, double e
         if (include_uncoded && !unc_fused &&
             (rc = uncoded_launch(h, seed, stream_id, ebno_db, k_payload, frame0 + f, n, cs + 2 * PSCL_NCOUNT, true)))
             return rc;
+        const int back = h->dl_back;
         h->dl_back = kDlPar;  // (its own scratch set: kDlPar sets rotate with the call parity)
         rc = pscl_dlscl_device(h, (const double*)d_llr, n, retries, (uint64_t*)d_best, (uint8_t*)d_flags, nullptr, nullptr,
                                0, (const uint64_t*)d_msg, k_payload, cs, cs + PSCL_NCOUNT);
-        h->dl_back = 2;
+        h->dl_back = back;
         if (rc) return rc;
     }
     return PSCL_OK;

@@ -195,32 +195,33 @@ def test_device_retry_loop_split_chains(chunks, split):
     assert dev["counters"]["dl"][1] == int((~host["success"]).sum())
 
 
-@pytest.mark.parametrize("L", [4, 8])
-def test_pipelined_dlscl_calls_equal_stream_ordered(L):
+@pytest.mark.parametrize("L,depth", [(4, 2), (8, 2), (4, 4), (8, 3)])
+def test_pipelined_dlscl_calls_equal_stream_ordered(L, depth):
     """pscl_set_pipelined on pscl_dlscl_device: each call's retry chains and DL counters stay on
-    the retry streams and overlap the next call's baseline.  Five calls on two alternating output
-    buffers (as bench.py's steps): a call's buffers are reused by the second following call, which
-    must start after that call's chains end.  After a join the last two calls' bits, flags and
-    attempts and the SCL/DL counters of all five equal the stream-ordered calls'."""
+    the retry streams and overlap the next call's baseline (and, in the other chain set, the
+    previous call's chains).  Calls on `depth` rotating output buffers (as bench.py's steps): a
+    call's buffers are reused by the depth-th following call, which must start after that call's
+    chains end.  After a join the last `depth` calls' bits, flags and attempts and the SCL/DL
+    counters of all calls equal the stream-ordered calls'."""
     from polar_code_amd.polar.polar import construct_info_set
 
     info = construct_info_set(128, 64)
     beta = np.load(GOLDEN / f"beta_M{L}.npy")
-    B, nb, nc = 40_000, 5, _native.PSCL_NCOUNT
+    B, nb, nc = 40_000, depth + 3, _native.PSCL_NCOUNT
     res = {}
     for pipe in (True, False):
         dec = _native.Decoder(128, info, L, "0x1864CFB")
-        dec.set_pipelined(pipe)
+        dec.set_pipelined(pipe, depth=depth)
         with _native.DeviceArena(dec) as mem:
             d_llr = [mem.alloc(B * 128 * 8) for _ in range(nb)]
             d_msg = [mem.alloc(B * 8) for _ in range(nb)]
-            d_out = [(mem.alloc(B * 8), mem.alloc(B), mem.alloc(B * 4)) for _ in range(2)]
+            d_out = [(mem.alloc(B * 8), mem.alloc(B), mem.alloc(B * 4)) for _ in range(depth)]
             d_cnt = mem.alloc(2 * nc * 8)
             mem.memset(d_cnt, 0, 2 * nc * 8)
             for i in range(nb):
                 dec.channel_device(5, 60 + i, 2.5 + 0.5 * (i % 3), 0.5, 40, i * B, B, d_llr[i], d_msg[i])
             for i in range(nb):
-                o = d_out[i & 1]
+                o = d_out[i % depth]
                 dec.dlscl_device(d_llr[i], B, 8, beta=beta, d_best=o[0], d_flags=o[1], d_attempts=o[2],
                                  d_ref=d_msg[i], k_payload=40, d_counters_scl=d_cnt, d_counters_dl=d_cnt + nc * 8)
             dec.join()
@@ -228,7 +229,7 @@ def test_pipelined_dlscl_calls_equal_stream_ordered(L):
                            mem.download(a, B * 4, np.int32)) for b, f, a in d_out],
                          mem.download(d_cnt, 2 * nc * 8, np.int64).reshape(2, nc))
         dec.close()
-    for i in range(2):
+    for i in range(depth):
         for k, name in enumerate(("best", "flags", "attempts")):
             np.testing.assert_array_equal(res[True][0][i][k], res[False][0][i][k], err_msg=f"{name}, buffer {i}")
     np.testing.assert_array_equal(res[True][1], res[False][1], err_msg="counters")
