@@ -1157,10 +1157,11 @@ int dl_setup(pscl_handle* h, const pscl_dl_call& a, DlBufs& b) {
         if ((rc = ensure(h, kLongRetryScratch, (size_t)pscl_decode_grid(H) * (size_t)H.long_block_bytes, &d_scr)))
             return rc;
     }
-    for (int j = 0; j < a.nsplit * nsets; ++j) {
+    for (int j = 0; j < 2 * nsets; ++j) {
         // chain 0 takes every entry of a call that does not split (fewer than 2 kMinSplit
         // failing frames, which may still exceed half the chunk); chain 1 at most half
         const int i = j & 1, set = j >> 1;
+        if (i >= a.nsplit) continue;
         const size_t c = (size_t)(i == 0 ? cap : cap - cap / 2);
         const size_t sz[14] = {(size_t)(rounds + 1) * NS * PSCL_DL_CSTRIDE * 4, NS * c * 4, NS * c * 4, c * 16, c * 4,
                                c * 2 * W * 8, c * NS * 8, c * 16, c * W * 8, c,
