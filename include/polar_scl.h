@@ -306,7 +306,7 @@ int pscl_join(pscl_handle* h);
  *                           2 never, 0 (default) for retry chains of at least
  *                           PSCL_TUNE_DL_SCREEN_MIN entries
  *   PSCL_TUNE_DL_CHUNKS     1..64: baseline chunks of a DL-SCL call (default 1)
- *   PSCL_TUNE_DL_SPLIT      1..2: retry chains per chunk (default 2)
+ *   PSCL_TUNE_DL_SPLIT      1..2: retry chains per chunk (default 2; 1 when pipelined)
  *   PSCL_TUNE_SIDE_PRIORITY 1: a pipelined handle's side streams at normal priority (default high)
  *   PSCL_TUNE_POST_GRID     16..4096: workgroup cap of the DL-SCL post pass (default 512)
  *   PSCL_TUNE_RETRY_WPG     1..4: wavefronts per workgroup of the retry decodes (default: by LDS)

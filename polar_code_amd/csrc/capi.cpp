@@ -1294,10 +1294,13 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
     // stream; the retry entries of chunk c are split over two chains, each on its own retry
     // stream with its own state, so the two chains' rounds overlap each other (and chunk c + 1's
     // baseline decode).  A round is latency-bound (a few 10^4 entries per launch), so a second
-    // concurrent chain fills what one leaves idle.  PSCL_TUNE_DL_SPLIT (1 or 2, default 2) sets the
-    // chains per chunk; chunks below 2 * kMinSplit failing frames keep one chain.
+    // concurrent chain fills what one leaves idle.  PSCL_TUNE_DL_SPLIT (1 or 2) sets the chains per
+    // chunk; chunks below 2 * kMinSplit failing frames keep one chain.  The default is 2 for a
+    // blocking call and 1 when pipelined: there the previous call's chains already overlap this
+    // one's, and a second chain per call only doubles the host's launches (config 4 measured
+    // 2.65 -> 2.38 ms/step with one).
     a.nch = 1;
-    a.nsplit = h->N > PSCL_FAST_N ? 0 : 2;
+    a.nsplit = h->N > PSCL_FAST_N ? 0 : (h->pipelined ? 1 : 2);
     if (rounds > 0 && h->tune[PSCL_TUNE_DL_CHUNKS]) a.nch = h->tune[PSCL_TUNE_DL_CHUNKS];
     if (rounds > 0 && h->N <= PSCL_FAST_N && h->tune[PSCL_TUNE_DL_SPLIT]) a.nsplit = (int)h->tune[PSCL_TUNE_DL_SPLIT];
     a.cap = (B + a.nch - 1) / a.nch;

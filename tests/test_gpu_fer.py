@@ -195,11 +195,11 @@ def test_device_retry_loop_split_chains(chunks, split):
     assert dev["counters"]["dl"][1] == int((~host["success"]).sum())
 
 
-@pytest.mark.parametrize("L,depth", [(4, 2), (8, 2), (4, 4), (8, 3)])
-def test_pipelined_dlscl_calls_equal_stream_ordered(L, depth):
+@pytest.mark.parametrize("L,depth,split", [(4, 2, 0), (8, 2, 0), (4, 4, 0), (8, 3, 0), (4, 3, 2)])
+def test_pipelined_dlscl_calls_equal_stream_ordered(L, depth, split):
     """pscl_set_pipelined on pscl_dlscl_device: each call's retry chains and DL counters stay on
     the retry streams and overlap the next call's baseline (and, in the other chain set, the
-    previous call's chains).  Calls on `depth` rotating output buffers (as bench.py's steps): a
+    previous call's chains); split 0 = the pipelined default (one chain per call), 2 = two.  Calls on `depth` rotating output buffers (as bench.py's steps): a
     call's buffers are reused by the depth-th following call, which must start after that call's
     chains end.  After a join the last `depth` calls' bits, flags and attempts and the SCL/DL
     counters of all calls equal the stream-ordered calls'."""
@@ -212,6 +212,8 @@ def test_pipelined_dlscl_calls_equal_stream_ordered(L, depth):
     for pipe in (True, False):
         dec = _native.Decoder(128, info, L, "0x1864CFB")
         dec.set_pipelined(pipe, depth=depth)
+        if split:
+            dec.set_tuning(dl_split=split)
         with _native.DeviceArena(dec) as mem:
             d_llr = [mem.alloc(B * 128 * 8) for _ in range(nb)]
             d_msg = [mem.alloc(B * 8) for _ in range(nb)]
