@@ -271,6 +271,20 @@ def cpu_baseline(orc: Oracle, llr_host: np.ndarray, info, L: int, budget_s: floa
     return rec, first, n
 
 
+def complete_ref(orc: Oracle, host: np.ndarray, ref, info, L: int, retries: int, beta):
+    """The oracle's outputs for the whole step-0 batch, so that parity covers every frame: the
+    frames the timed sample did not reach are decoded untimed, on one thread per CPU of the cgroup
+    quota (more threads than the quota only slow the oracle down)."""
+    n = ref[0].shape[0]
+    if n >= host.shape[0]:
+        return ref
+    q = _cpu_quota()
+    if q:
+        orc.o.set_num_threads(max(1, min(orc.o.num_threads(), int(math.ceil(q)))))
+    rest = orc.run(host[n:], info, L, retries, beta)
+    return tuple(None if a is None else np.concatenate([a, b]) for a, b in zip(ref, rest))
+
+
 def _cpu_ranges(cpus):
     """Compact '0-15,32-47' form of a CPU list."""
     out, i = [], 0
@@ -674,6 +688,7 @@ def main():
             host = host_internal_llrs(host[: min(host.shape[0], 100_000)], N)
         if world == 1:
             cpu, ref, n = cpu_baseline(orc, host, info, L, args.cpu_seconds, args.retries, beta)
+            ref = complete_ref(orc, host, ref, info, L, args.retries, beta)
         else:  # the CPU baseline is an N = 1 figure; the step-0 parity check stays (untimed)
             ref = orc.run(host, info, L, args.retries, beta)
         par = parity(r["best0"], r["flags0"], ref, K, check_idx=args.retries == 0)

@@ -1552,8 +1552,17 @@ int simulate_enqueue(pscl_handle* h, uint64_t seed, uint32_t stream_id, double e
             h->dl_pending[par] = false;
         }
         static const int kSimSlot[kDlPar] = {30, 66, 84, 88};
-        const int base = kSimSlot[par];
         void *d_llr, *d_msg, *d_best, *d_flags;
+        // (pipelined: every parity's set sized at once, so the first call warms all of them and no
+        // later call of a sweep allocates -- ~130 us of hipMalloc on the host per new set)
+        for (int q = h->pipelined ? 0 : par; q <= (h->pipelined ? kDlPar - 1 : par); ++q) {
+            const int base = kSimSlot[q];
+            if ((rc = ensure(h, base, (size_t)chunk * N * 8, &d_llr))) return rc;
+            if ((rc = ensure(h, base + 1, (size_t)chunk * W * 8, &d_msg))) return rc;
+            if ((rc = ensure(h, base + 2, (size_t)chunk * W * 8, &d_best))) return rc;
+            if ((rc = ensure(h, base + 3, (size_t)chunk, &d_flags))) return rc;
+        }
+        const int base = kSimSlot[par];
         if ((rc = ensure(h, base, (size_t)chunk * N * 8, &d_llr))) return rc;
         if ((rc = ensure(h, base + 1, (size_t)chunk * W * 8, &d_msg))) return rc;
         if ((rc = ensure(h, base + 2, (size_t)chunk * W * 8, &d_best))) return rc;

@@ -220,9 +220,12 @@ __global__ void __launch_bounds__(256) replay_kernel(const pscl_replay_params R,
 #endif
 // unroll of the flip metric's sums over k: beta rows in flight per lane (read through L2 in the
 // narrow form)
-// occupancy hint of the post pass (waves per SIMD; 4 caps it at 128 VGPRs)
+// occupancy hint of the post pass (waves per SIMD): 3 (168 VGPRs) -- at 4 (128 VGPRs) it spilled
+// 5 VGPRs to scratch (24 B per lane), and a kernel with scratch stalls its first dispatch on each
+// queue while the runtime allocates that queue's scratch; a pass's grid (512 workgroups of 4 or 8
+// wavefronts) is resident either way
 #ifndef PSCL_POST_WPE
-#define PSCL_POST_WPE 4
+#define PSCL_POST_WPE 3
 #endif
 #ifndef PSCL_POST_UNROLL
 #define PSCL_POST_UNROLL 4

@@ -206,6 +206,14 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 #ifndef PSCL_WAVES_PER_EU
 #define PSCL_WAVES_PER_EU 4
 #endif
+// the exact plain and forced-bit instances (the re-decode of deferred frames, the DL-SCL retry
+// decodes: few frames per launch, latency-bound): 3 waves/SIMD, i.e. up to 168 VGPRs -- at 4
+// (128 VGPRs) they spilled 4-16 VGPRs and 20-60 B per lane to scratch, and a kernel with scratch
+// makes the runtime (re)allocate a queue's scratch at its first launch there (a ~130 us dispatch
+// stall measured on a retry stream, rocprofv3 scratch-memory trace)
+#ifndef PSCL_EXACT_WAVES_PER_EU
+#define PSCL_EXACT_WAVES_PER_EU 3
+#endif
 
 // FS: the launch may carry forced bits or SC hard decisions (P.force / P.sc_hard).  Without
 // them (every plain SCL decode) the per-frame force words and their tests compile away.
@@ -214,7 +222,9 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 // words and must clear a margin of PSCL_SCR_H units (glibc_softplus.h: proven to exceed twice
 // the metric error), else the frame is appended to P.amb_list for an exact re-decode.
 template <int LMAX, bool HIST, bool CH, bool FS, int CODE, bool APX = false>
-__global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64, PSCL_WAVES_PER_EU) scl128_kernel(const pscl_decode_params P) {
+__global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * 64)
+__attribute__((amdgpu_waves_per_eu((APX || HIST) ? PSCL_WAVES_PER_EU : PSCL_EXACT_WAVES_PER_EU)))
+scl128_kernel(const pscl_decode_params P) {
     using Ly = Layout128<LMAX, CH>;
     const uint64_t* const force = FS ? P.force : nullptr;
     const bool sc_hard = FS && P.sc_hard;

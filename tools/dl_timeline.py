@@ -2,7 +2,7 @@
 with its queue, start offset from the first baseline decode of the window and duration (us), for a
 window of consecutive steps in the middle of the timed region.
 
-    python tools/dl_timeline.py <trace dir> [first step] [steps]
+    python tools/dl_timeline.py <trace dir> [first step] [steps]   (steps 0: to the trace's end)
 """
 import csv
 import glob
@@ -23,9 +23,11 @@ def short(n):
 
 
 base = [r for r in rows if "scl_lane_kernel<4, 1, false>" in r[2] or "scl_lane_kernel<8, 1, false>" in r[2]]
-if len(base) < first + nsteps + 1:
+if len(base) < first + max(nsteps, 1) + (nsteps > 0):
     sys.exit(f"only {len(base)} baseline decodes")
-t0, t1 = base[first][0], base[first + nsteps][0]
+# steps 0: from baseline decode `first` to the end of the trace (a standalone sweep point)
+t0, t1 = base[first][0], base[first + nsteps][0] if nsteps else max(r[1] for r in rows)
+nsteps = max(nsteps, 1)
 print(f"window: baseline decodes {first}..{first + nsteps - 1}, {(t1 - t0) / 1e3:.1f} us "
       f"({(t1 - t0) / 1e3 / nsteps:.1f} us per step)")
 busy = {}
