@@ -302,20 +302,17 @@ int pscl_join(pscl_handle* h);
  * schedule).  The library reads no environment variables: a knob changes only
  * the handle it is set on, never a result (every schedule is bit-identical).  Pending pipelined
  * work is ordered first.  PSCL_EINVAL for an unknown knob or a value out of range.
- *   PSCL_TUNE_DL_SCREEN     DL-SCL retry decodes on the forced-bit screening instance: 1 always,
- *                           2 never, 0 (default) for retry chains of at least
- *                           PSCL_TUNE_DL_SCREEN_MIN entries
+ *   PSCL_TUNE_DL_SCREEN     DL-SCL retry decodes on the forced-bit screening instance (where the
+ *                           code has one): 1 always, 2 never, 0 (default) every retry chain, or
+ *                           with PSCL_TUNE_DL_SCREEN_MIN set the chains it selects
  *   PSCL_TUNE_DL_CHUNKS     1..64: baseline chunks of a DL-SCL call (default 1)
  *   PSCL_TUNE_DL_SPLIT      1..2: retry chains per chunk (default 2; 1 when pipelined)
  *   PSCL_TUNE_SIDE_PRIORITY 1: a pipelined handle's side streams at normal priority (default high)
  *   PSCL_TUNE_POST_GRID     16..4096: workgroup cap of the DL-SCL post pass (default 512)
  *   PSCL_TUNE_RETRY_WPG     1..4: wavefronts per workgroup of the retry decodes (default: by LDS)
- *   PSCL_TUNE_DL_SCREEN_MIN 1..2^30: entries of a retry chain from which PSCL_TUNE_DL_SCREEN = 0
- *                           screens its retry decodes (default 24576: the throughput regime of
- *                           low-SNR points -- fewer entries take the exact decode, whose deferred-
- *                           entry latency would otherwise sit on every round; the default also
- *                           screens every chain that runs beside a later baseline decode, a
- *                           pipelined call's or a chunk's)
+ *   PSCL_TUNE_DL_SCREEN_MIN 1..2^30: with PSCL_TUNE_DL_SCREEN = 0, screen only the retry chains of
+ *                           at least this many entries and those beside a later baseline decode (a
+ *                           pipelined call's or a chunk's); 0 (default): no threshold
  *   PSCL_TUNE_DL_LANE       1: a DL-SCL baseline decode (N = 128) on the lane-per-path screening
  *                           kernel (default); 2: on the two-lanes-per-path one
  *   PSCL_TUNE_DL_RETRY_LANE 2: screened retry decodes (N = 128) on the two-lanes-per-path forced-

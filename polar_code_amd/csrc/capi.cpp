@@ -934,18 +934,15 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     // deferred, at the same attempt index as the main chain's round, so the main chain never waits
     // for the side chain's exact decodes; the chain ends with both.  Each round has its own side
     // list (the side chain may lag the main chain by several rounds).
-    // screening retry decodes: always (1), never (2), or for chains of many entries (0): at low SNR
-    // the rounds are throughput-bound and the screening decode's ~4x cheaper frames win (config 3,
-    // 4.0 dB point: 10.5 -> 9.0 ms); with few entries the exact decode of the deferred ones is one
-    // more latency per round (5.0 dB: 5.6 -> 6.1 ms), DESIGN.md §5.1b
-    // Also every chain that runs beside a later baseline decode (the next pipelined call's, or the
-    // next chunk's): there the screened decodes' smaller GPU share wins even when the chain is
-    // short (config 3 sweep 199-201 -> 218-222 M frames/s; config 4 with the side chain 3.44 ->
-    // 3.30 ms), while a chain running alone (a single call, a join) keeps the latency-bound rule
+    // screening retry decodes: always (1), never (2), or by default (0) every chain, unless
+    // PSCL_TUNE_DL_SCREEN_MIN sets a size threshold (chains of at least that many entries, and every
+    // chain beside a later baseline decode).  With the deferred entries on the side chain the main
+    // chain never waits for an exact decode, so screening wins alone too: the standalone config-3
+    // 5 dB point (~10^4 entries per round) 4.61-4.62 -> 4.32 ms, the sweep 283.7 -> 285.1 M frames/s
+    // (profiles/r05v_screen_ab.txt; round 4, before the side chain, it lost alone: 5.6 -> 6.1 ms)
     const int64_t ds = h->tune[PSCL_TUNE_DL_SCREEN];
-    const int64_t ds_min = h->tune[PSCL_TUNE_DL_SCREEN_MIN] ? h->tune[PSCL_TUNE_DL_SCREEN_MIN] : PSCL_DL_SCREEN_MIN;
-    const bool dl_screen =
-        ds == 1 || (ds == 0 && (A >= ds_min || (beside && !h->tune[PSCL_TUNE_DL_SCREEN_MIN])));
+    const int64_t ds_min = h->tune[PSCL_TUNE_DL_SCREEN_MIN];
+    const bool dl_screen = ds == 1 || (ds == 0 && (!ds_min || A >= ds_min || beside));
     const bool scr = dl_screen && h->screen && S.dcnt && S.ob2 && side && pscl_screening_fs_available(H);
     pscl_decode_params HA, HX;
     pscl_post_params QD;

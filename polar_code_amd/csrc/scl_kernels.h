@@ -254,12 +254,6 @@ int64_t pscl_decode_count_slots(const pscl_decode_params& P, int hist);
 // counters[FRAME_ERR, BIT_ERR, PAYLOAD_ERR, PAYLOAD_BIT] += the sums of cpart[slots][4], which it
 // leaves zero (the kernels store only the slots of wavefronts with errors)
 hipError_t pscl_launch_count_reduce(int32_t* cpart, int64_t slots, int64_t* counters, hipStream_t s);
-// retry-chain entries from which the DL-SCL retry decodes screen (PSCL_TUNE_DL_SCREEN_MIN default;
-// at L = 8 also every chain beside a later baseline, capi.cpp dl_retry_chunk): config 4 (L = 4,
-// chains of ~19k entries) 3.43-3.47 ms against 3.79-3.85 screened, profiles/r04q_lane_fs_ab.txt
-#ifndef PSCL_DL_SCREEN_MIN
-#define PSCL_DL_SCREEN_MIN 24576
-#endif
 // the DL-SCL baseline decode's screening kernel at N = 128 (PSCL_TUNE_DL_LANE default): 1 the
 // lane-per-path kernel, 2 the two-lanes-per-path one, 0 by list size (lane-per-path at L = 8).
 // 1: with the lighter retry chains of round 4 (screened lane-per-path retry decodes, side chain,

@@ -75,14 +75,16 @@ def test_device_retry_loop_golden(golden):
 @pytest.mark.parametrize("M,retries,ebno,screen", [(4, 8, 3.0, "0"), (8, 8, 3.5, "0"), (2, 3, 3.0, "0"), (1, 70, 4.0, "0"),
                                                    (4, 8, 1.5, "0"), (4, 8, 2.0, "1"), (8, 8, 2.5, "1"),
                                                    (8, 8, 2.5, "2"), (4, 8, 2.0, "adaptive"), (8, 8, 3.5, "1"),
-                                                   (4, 8, 3.0, "1"), (8, 8, 2.5, "1/2lane"), (4, 8, 2.0, "1/2lane")])
+                                                   (4, 8, 3.0, "1"), (8, 8, 2.5, "1/2lane"), (4, 8, 2.0, "1/2lane"),
+                                                   (4, 8, 3.0, "2")])
 def test_device_retry_loop_equals_host_ranking(monkeypatch, M, retries, ebno, screen):
     """Device retry loop == numpy-ranked retries, frame by frame (3000 frames, ~30% failing);
     screen = 1: the retry decodes on the forced-bit screening instance (lane per path: per-frame
     forced / growing / full list) plus the exact decode of the entries it defers (tuning knob
     dl_screen = 1); "1/2lane": the same on the two-lanes-per-path instance (dl_retry_lane = 2);
-    2: never; "adaptive": the default rule with a threshold every chain here exceeds
-    (dl_screen_min = 1)."""
+    2: never (the exact forced-bit kernel); 0: the default (every chain screened where the list size
+    has a screening instance, L = 4 and 8); "adaptive": the size-threshold rule with a threshold
+    every chain here exceeds (dl_screen_min = 1)."""
     from polar_code_amd.polar.polar import construct_info_set, encode
     from polar_code_amd.polar.crc import attach_crc
 
