@@ -1,6 +1,8 @@
 """The bench's config-3 sweep alone (bench.py config3_sweep): run_fer_sweep --rng philox, L = 8,
-4.0-6.5 dB, 10^6 frames per point, after an untimed 4.0-4.5 dB warm-up at another seed; prints the
-wall time of the timed pass (for rocprofv3 traces of the product path).
+4.0-6.5 dB, 10^6 frames per point, after an untimed 4.0-5.5 dB warm-up at another seed (four
+pipelined calls: every scratch set and chain set of the handle used once, as in the bench, whose
+5 dB point follows its 6-point sweep); prints the wall time of the timed pass (for rocprofv3
+traces of the product path).
 
     python tools/config3_run.py [frames] [lo] [hi] [k=v,k=v] [batch]   (handle tuning knobs and the
     frames per pscl_simulate_device call, run_fer_sweep --batch: A/B only; "-" for no knobs)
@@ -45,7 +47,7 @@ def run(a_lo, a_hi, seed, td):
 
 
 with tempfile.TemporaryDirectory() as td:
-    run(4.0, 4.5, 1, td)
+    run(4.0, 5.5, 1, td)
     rows, t = run(lo, hi, 0, td)
 print(f"config 3 sweep {lo:g}-{hi:g} dB{' ' + str(tune) if tune else ''}{f' batch {batch}' if batch else ''}: {len(rows)} points x {frames} frames in {t * 1e3:.2f} ms = "
       f"{len(rows) * frames / t / 1e6:.1f} M frames/s", flush=True)
