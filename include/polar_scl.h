@@ -299,7 +299,7 @@ int pscl_join(pscl_handle* h);
 
 /*
  * Tuning and test knobs of one handle (value 0 restores the default, which is the measured best
- * schedule, DESIGN.md §5.1b).  The library reads no environment variables: a knob changes only
+ * schedule, DESIGN.md §5.4).  The library reads no environment variables: a knob changes only
  * the handle it is set on, never a result (every schedule is bit-identical).  Pending pipelined
  * work is ordered first.  PSCL_EINVAL for an unknown knob or a value out of range.
  *   PSCL_TUNE_DL_SCREEN     DL-SCL retry decodes on the forced-bit screening instance (where the
@@ -314,7 +314,7 @@ int pscl_join(pscl_handle* h);
  *                           at least this many entries and those beside a later baseline decode (a
  *                           pipelined call's or a chunk's); 0 (default): no threshold
  *   PSCL_TUNE_DL_LANE       1: a DL-SCL baseline decode (N = 128) on the lane-per-path screening
- *                           kernel (default); 2: on the two-lanes-per-path one (DESIGN.md §5.1b)
+ *                           kernel (default); 2: on the two-lanes-per-path one (DESIGN.md §5.4)
  *   PSCL_TUNE_DL_RETRY_LANE 2: screened retry decodes (N = 128) on the two-lanes-per-path forced-
  *                           bit instance instead of the lane-per-path one (default)
  *   PSCL_TUNE_POST_PAIRS    1..32: entry pairs per wavefront the DL-SCL post pass grid is sized for

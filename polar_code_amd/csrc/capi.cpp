@@ -106,7 +106,7 @@ struct pscl_dl_call {
 // pscl_simulate_device, its TX buffers are one of kDlPar sets, rewritten only after the retry chains
 // of the call kDlPar back have ended -- the handle's stream runs up to kDlPar - 1 calls ahead of
 // the chains (2 measured 175 M frames/s on the config-3 sweep, the stream waiting on chains of the
-// low-SNR points; DESIGN.md §5.3)
+// low-SNR points; DESIGN.md §5.4)
 constexpr int kDlPar = 4;
 // retry-chain sets: the chains of consecutive pipelined calls (and of consecutive chunks of one
 // call) alternate two sets of streams, events and state, so a call's chains run beside the previous
@@ -303,7 +303,7 @@ void fill_decode_params(const pscl_handle* h, pscl_decode_params& P, int hist) {
 // on its own stream by its count-reduce launch)
 // A (re)allocated buffer is zeroed on the decode's own stream st: a plain hipMemset runs on the null
 // stream, which the handle's non-blocking streams do not wait for -- the decode could store (and its
-// reduce read) partials before the zeroing lands (an intermittent counter mismatch, DESIGN.md §5.6)
+// reduce read) partials before the zeroing lands (an intermittent counter mismatch, DESIGN.md §5.8)
 int with_count_slots(pscl_handle* h, pscl_decode_params& P, int hist, int slot, hipStream_t st) {
     P.cpart = nullptr;
     const int64_t slots = pscl_decode_count_slots(P, hist);
@@ -925,7 +925,7 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     H.wpg_cap = (int)h->tune[PSCL_TUNE_RETRY_WPG];
     if (pscl_decode_wpg(H) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
     int rc;
-    // screening retry decodes (measured in DESIGN.md §5.1b): the forced-bit screening instance
+    // screening retry decodes (measured in DESIGN.md §5.4): the forced-bit screening instance
     // decodes the round's entries and moves the ones it cannot certify to a SIDE CHAIN (flags
     // PSCL_DL_DEFERRED, which the main post pass skips): on the side stream, round r of the side
     // chain decodes its entries exactly (warm-started, as every retry decode) -- the ones round r
@@ -1352,7 +1352,7 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
         P.counters = d_counters_scl;
         // (N = 128: the DL-SCL baseline's screening kernel, PSCL_TUNE_DL_LANE; by default the
         // lane-per-path one at L = 8 and the two-lanes-per-path one at L = 4, which measured faster
-        // beside the retry chains, DESIGN.md §5.1b)
+        // beside the retry chains, DESIGN.md §5.4)
         if (rounds > 0) {
             const int64_t dl_lane = h->tune[PSCL_TUNE_DL_LANE] ? h->tune[PSCL_TUNE_DL_LANE]
                                                                : (PSCL_DL_LANE_DEFAULT ? PSCL_DL_LANE_DEFAULT : (h->L == 8 ? 1 : 2));

@@ -508,7 +508,7 @@ PSCL_HD double pscl_softplus_tail_scr(double v) { return pscl_softplus_tail_scr_
 #define PSCL_LOG2E_F32 1.44269504088896341f
 #define PSCL_LN2_F32 0.693147180559945309f
 /* upper bound of the exhaustive device scan: measured on MI355X 1.2338e-7 = 2.07 * 2^-24, at
- * x32 = 0.28314 (tests/test_gpu_screening.py, profiles/r04c_screening_tests.txt; DESIGN.md §5.1a) */
+ * x32 = 0.28314 (tests/test_gpu_screening.py, profiles/r04c_screening_tests.txt; DESIGN.md §5.2) */
 #ifndef PSCL_TAIL_ABS_SCAN
 #define PSCL_TAIL_ABS_SCAN (3.0 / 16777216.0)
 #endif

@@ -199,7 +199,7 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 #define PSCL_TAIL_NC 1
 #endif
 
-// diagnostic builds only: the history instances with the aggregated counters
+// diagnostic builds only: the history instances with the aggregated counters (docs/HISTORY.md §5.6)
 #ifndef PSCL_HIST_AGG
 #define PSCL_HIST_AGG 0
 #endif
@@ -970,7 +970,7 @@ scl128_kernel(const pscl_decode_params P) {
                     if constexpr (HIST && !PSCL_HIST_AGG) {
                         // (the history instances keep per-frame atomics: their register budget is
                         // spent -- four more live counters spill further, and the rate-matched L = 8
-                        // history instance then measured wrong decision LLRs)
+                        // history instance then measured wrong decision LLRs; see docs/HISTORY.md §5.6)
                         count_errors(P.counters, ib0, ib1, P.ref[fo * PW], PW > 1 ? P.ref[fo * PW + 1] : 0, P.k_payload,
                                      bpass);
                     } else {

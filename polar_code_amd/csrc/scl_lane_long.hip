@@ -1,7 +1,7 @@
 // scl_lane_long.hip -- the lane-per-path screening decoder for the longer codes (N = 256, 512,
 // 1024; L = 4, 8; any information set) and its launch.
 //
-// The long-code form of scl128_lane.hip (DESIGN.md §5.1b, §9.3): a plain decode whose path
+// The long-code form of scl128_lane.hip (DESIGN.md §5.6, §9): a plain decode whose path
 // metrics carry the bounded-error tail (pscl_softplus_tail_abs), every ordering decision
 // certified by the absolute margin of an N-phase metric (2 N DELTA), a frame with an uncertain
 // decision appended to P.amb_list and re-decoded exactly by scl_long_kernel (capi.cpp).  Results

@@ -1,4 +1,4 @@
-// xlane_probe.hip -- root-cause probe of the two cross-lane workarounds (DESIGN.md §5.1a,
+// xlane_probe.hip -- root-cause probe of the two cross-lane workarounds (DESIGN.md §5.2,
 // §5.4): what ds_bpermute and DPP return when their source lane is inactive, and what the
 // compiler makes of a DPP row_shr:1 move that feeds a subtract right after a ds_bpermute.
 //
