@@ -39,6 +39,11 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
+# OpenMP workers (the oracle's cpu_baseline and parity runs) sleep as soon as a parallel region
+# ends: spinning workers -- one per CPU of the affinity mask -- otherwise eat the process's cgroup
+# CPU quota and slow the host-bound GPU legs that follow (config 4's launches, the sweep's Python).
+# Set before libgomp loads (torch or the oracle), so it applies to both.
+os.environ.setdefault("OMP_WAIT_POLICY", "PASSIVE")
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 POLY = "0x1864CFB"
