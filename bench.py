@@ -455,7 +455,7 @@ def extra_configs(args, ctx: Ctx, orc: Oracle | None):
     out = {}
     for name, kw, ref_kind, ref_L in cfgs:
         beta = np.load(ROOT / "tests" / "golden" / "beta_M4.npy") if kw["retries"] else None
-        r = run_workload(ctx, **kw, beta=beta, B=args.frames, steps=args.extra_steps, warmup=1, ebno=args.ebno,
+        r = run_workload(ctx, **kw, beta=beta, B=args.frames, steps=args.extra_steps, warmup=2, ebno=args.ebno,
                          seed=args.seed, keep_buffers=orc is not None)
         if ctx.rank != 0:
             continue
