@@ -241,7 +241,10 @@ __global__ void __launch_bounds__(256) replay_kernel(const pscl_replay_params R,
 #ifndef PSCL_POST_FMA
 #define PSCL_POST_FMA 1
 #endif
-constexpr int kPostWavesWide = 8, kPostWavesNarrow = 4;
+#ifndef PSCL_POST_WAVES_NARROW
+#define PSCL_POST_WAVES_NARROW 4
+#endif
+constexpr int kPostWavesWide = 8, kPostWavesNarrow = PSCL_POST_WAVES_NARROW;
 constexpr int kPostIters = 32;  // entry pairs per wavefront between flushes
 
 template <int PW>

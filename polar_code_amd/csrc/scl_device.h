@@ -471,7 +471,8 @@ __device__ __forceinline__ void flush_counts(int64_t* counters, int fe, int be, 
 __device__ __forceinline__ void tally_errors(const uint64_t* ib, const uint64_t* ref, int W, int k_payload, bool pass,
                                              int& fe, int& be, int& pe, int& pb) {
     int bit_err = 0, pay_err = 0;
-    for (int w = 0; w < W; ++w) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) {  // (unrolled: callers with a compile-time W keep ib in registers)
         const uint64_t dff = ib[w] ^ ref[w];
         const int kp = k_payload - 64 * w;
         const uint64_t pm = kp >= 64 ? ~0ULL : (kp > 0 ? ((1ULL << kp) - 1) : 0ULL);

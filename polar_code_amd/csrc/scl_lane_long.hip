@@ -61,13 +61,22 @@ struct LongLaneLayout {
 #define PSCL_LANE_LONG1024_WAVES_PER_EU 1
 #endif
 
-// word k of the register array u, k wave-uniform
+// word k of the register array u, k wave-uniform.  The selects are inline asm (v_cndmask with the
+// wave-uniform condition in an SGPR pair): left as C, the compiler turned the select chain into a
+// load from a private copy of u indexed by k, i.e. u kept in scratch and stored on every pull
+// (48 / 80 / 144 B of scratch per lane at N = 256 / 512 / 1024)
 template <int NW>
 __device__ __forceinline__ uint64_t uword(const uint64_t (&u)[NW], int k) {
-    uint64_t r = u[0];
+    uint32_t lo = (uint32_t)u[0], hi = (uint32_t)(u[0] >> 32);
+    const int ku = __builtin_amdgcn_readfirstlane(k);  // (uniform: the condition lives in SGPRs)
 #pragma unroll
-    for (int i = 1; i < NW; ++i) r = k == i ? u[i] : r;
-    return r;
+    for (int i = 1; i < NW; ++i) {
+        const uint32_t c = __builtin_amdgcn_readfirstlane(ku == i ? 0xffffffffu : 0u);
+        const uint64_t m = ((uint64_t)c << 32) | c;
+        asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(lo) : "v"(lo), "v"((uint32_t)u[i]), "s"(m));
+        asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(hi) : "v"(hi), "v"((uint32_t)(u[i] >> 32)), "s"(m));
+    }
+    return ((uint64_t)hi << 32) | lo;
 }
 
 template <int NL, int LMAX>
@@ -406,10 +415,21 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
                 lastbit = bt;
             };
             static_for<16>([&](auto TC) { phase(TC); });
-            // the block's bits into their word
+            // the block's bits into their word (a uniform branch per word, the OR in asm: as plain
+            // C the compiler made this a store into a private copy of u indexed by b / 4, which
+            // kept u in scratch at N = 1024)
+            {
+                const int kb = __builtin_amdgcn_readfirstlane(b >> 2);
+                const uint64_t add = (uint64_t)ub << (16 * (b & 3));
 #pragma unroll
-            for (int k = 0; k < NW; ++k)
-                if (k == (b >> 2)) u[k] |= (uint64_t)ub << (16 * (b & 3));
+                for (int k = 0; k < NW; ++k)
+                    if (k == kb) {
+                        uint32_t lo = (uint32_t)u[k], hi = (uint32_t)(u[k] >> 32);
+                        asm volatile("v_or_b32 %0, %0, %1" : "+v"(lo) : "v"((uint32_t)add));
+                        asm volatile("v_or_b32 %0, %0, %1" : "+v"(hi) : "v"((uint32_t)(add >> 32)));
+                        u[k] = ((uint64_t)hi << 32) | lo;
+                    }
+            }
             ub = 0;
         }
 
@@ -420,17 +440,23 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
         for (int k = 0; k < NW; ++k) ib[k] = 0;
         {
             int off = 0;  // information bits before byte k (wave-uniform)
+            // words of u by a compile-time index (the byte loop inside may stay rolled: at N = 1024
+            // a rolled loop over all N / 8 bytes indexed u by k / 8, which put u in scratch)
 #pragma unroll
-            for (int k = 0; k < N / 8; ++k) {
-                const uint32_t byte = (uint32_t)((u[k >> 3] >> (8 * (k & 7))) & 255u);
-                const uint64_t cb = GT[k * 256 + byte];
-                const int wi = off >> 6, sb = off & 63;
+            for (int kw = 0; kw < NW; ++kw) {
+                const uint64_t uw = u[kw], iw = P.info_words[kw];
+                for (int j = 0; j < 8; ++j) {
+                    const int k = 8 * kw + j;
+                    const uint32_t byte = (uint32_t)((uw >> (8 * j)) & 255u);
+                    const uint64_t cb = GT[k * 256 + byte];
+                    const int wi = off >> 6, sb = off & 63;
 #pragma unroll
-                for (int w = 0; w < NW; ++w) {
-                    if (w == wi) ib[w] |= cb << sb;
-                    if (w == wi + 1 && sb > 56) ib[w] |= cb >> (64 - sb);
+                    for (int w = 0; w < NW; ++w) {
+                        if (w == wi) ib[w] |= cb << sb;
+                        if (w == wi + 1 && sb > 56) ib[w] |= cb >> (64 - sb);
+                    }
+                    off += __builtin_popcount((uint32_t)((iw >> (8 * j)) & 255u));
                 }
-                off += __builtin_popcount((uint32_t)((P.info_words[k >> 3] >> (8 * (k & 7))) & 255u));
             }
         }
         uint32_t syn = 0;
