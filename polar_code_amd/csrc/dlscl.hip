@@ -287,8 +287,17 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
     for (int i = threadIdx.x; i < PSCL_EXP_TABLE_WORDS; i += blockDim.x) S.exp_table[i] = Q.exp_table[i];
     if (beta_lds == 1)
         for (int i = threadIdx.x; i < K * K; i += blockDim.x) sbeta[i] = Q.beta[i];
-    else if (beta_lds == 2)
-        for (int i = threadIdx.x; i < K * K; i += blockDim.x) sbeta32[i] = (float)Q.beta[i];
+    else if (beta_lds == 2) {
+        if constexpr (KC == 64) {  // pair layout [k][hl][2] = (beta[k][hl], beta[k][hl + 32]): one
+                                   // 8-byte read gives a lane both of its candidates (kPostPk)
+            for (int i = threadIdx.x; i < K * K; i += blockDim.x) {
+                const int k = i >> 6, j = i & 63;
+                sbeta32[(k * 32 + (j & 31)) * 2 + (j >> 5)] = (float)Q.beta[i];
+            }
+        } else {
+            for (int i = threadIdx.x; i < K * K; i += blockDim.x) sbeta32[i] = (float)Q.beta[i];
+        }
+    }
     if (threadIdx.x < PSCL_DL_NSEG) S.lcnt[threadIdx.x] = 0;
     if (threadIdx.x == 0) S.nst = 0;
     const double* beta = beta_lds == 1 ? sbeta : Q.beta;  // (the exact sums: fp64 beta)
@@ -438,9 +447,14 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
                     }
                 }
                 // ---- |L0| at the information phases (flip.py:97-102, 127-132), in nxt
+                // (K = 64, narrow form: an fp32 copy too, in nxt's upper half -- free until the tails)
+                float* const l32 = reinterpret_cast<float*>(nxt + 64);
 #pragma unroll
                 for (int m = 0; m < 4; ++m)
-                    if (jpos[m] >= 0) nxt[jpos[m]] = fabs(cur[hl + 32 * m]);
+                    if (jpos[m] >= 0) {
+                        nxt[jpos[m]] = fabs(cur[hl + 32 * m]);
+                        if (KC == 64 && beta_lds == 2) l32[jpos[m]] = (float)fabs(cur[hl + 32 * m]);
+                    }
                 pscl::wave_lds_fence();
                 // ---- next flip: argmin over untried (q, index), q = |L0| @ beta summed in
                 // index order (flip.py:104-108), q = |L0| without beta
@@ -500,7 +514,27 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
                     // same index back)
 #pragma unroll
                     for (int m = 0; m < MC; ++m) qv[m] = 0.0;
-                    if (beta_lds == 2) {  // (narrow form: beta staged in LDS as fp32, see e2 below)
+                    constexpr bool PK = KC == 64;  // packed fp32 sums (narrow form, K = 64; e2 below)
+                    if (PK && beta_lds == 2) {
+                        // both candidates of the lane in one v_pk_fma_f32 per k: |L0| read 4 at a time
+                        // (fp32 copy), beta pairs from the pair layout; summed in fp32 and certified
+                        // against the fp32 bound below (the exact fp64 sums when uncertified)
+                        typedef float f2 __attribute__((ext_vector_type(2)));
+                        typedef float f4 __attribute__((ext_vector_type(4)));
+                        const f2* bp = reinterpret_cast<const f2*>(sbeta32) + hl;
+                        const f4* lp = reinterpret_cast<const f4*>(l32);
+                        f2 acc = {0.0f, 0.0f};
+#pragma unroll 4
+                        for (int k4 = 0; k4 < 16; ++k4) {
+                            const f4 a = lp[k4];
+                            acc = __builtin_elementwise_fma((f2){a.x, a.x}, bp[(4 * k4 + 0) * 32], acc);
+                            acc = __builtin_elementwise_fma((f2){a.y, a.y}, bp[(4 * k4 + 1) * 32], acc);
+                            acc = __builtin_elementwise_fma((f2){a.z, a.z}, bp[(4 * k4 + 2) * 32], acc);
+                            acc = __builtin_elementwise_fma((f2){a.w, a.w}, bp[(4 * k4 + 3) * 32], acc);
+                        }
+                        qv[0] = (double)acc.x;  // (exact widening; MC = 2 here)
+                        qv[1] = (double)acc.y;
+                    } else if (beta_lds == 2) {  // (narrow form: beta staged in LDS as fp32, see e2 below)
                         const float* bc = sbeta32 + hl;
 #pragma unroll PSCL_POST_UNROLL
                         for (int k = 0; k < K; ++k) {
@@ -530,8 +564,17 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
                     // instances get their own); fp32 beta adds |beta32 - beta| <= 2^-24 |beta| + 2^-150
                     // per term, i.e. 2^-24 S + 2^-150 ||L0||_1 (2 % slack on the doubled bound)
                     const double gk = (4.0 * (double)K + 8.0) * 0x1p-53;
-                    const double e2 = beta_lds == 2 ? as * Q.beta_absmax * (gk + 2.04 * 0x1p-24) + as * 0x1p-140
-                                                    : as * Q.beta_absmax * gk;
+                    // packed fp32 sums: |L0| and beta each rounded to fp32 (u = 2^-24 relative per
+                    // factor), K fp32 fma roundings (gamma_K), the exact sums' own gamma_K (fp64):
+                    // |q32 - q_exact| <= ((K + 2.01) 2^-24 + gk / 2) S + K 2^-149 (fp32 underflow);
+                    // doubled, 2 % slack.  A non-finite or huge ||L0||_1 (fp32 overflow) leaves the
+                    // certificate false: the exact sums decide
+                    const double e2 = (PK && beta_lds == 2)
+                                          ? (as * Q.beta_absmax < 0x1p100 ? 2.04 * (as * Q.beta_absmax * (((double)K + 2.01) * 0x1p-24 + 0.5 * gk)
+                                                                    + (double)K * 0x1p-149)
+                                                          : __builtin_inf())
+                                      : beta_lds == 2 ? as * Q.beta_absmax * (gk + 2.04 * 0x1p-24) + as * 0x1p-140
+                                                      : as * Q.beta_absmax * gk;
                     double qmine = qv[0];
 #pragma unroll
                     for (int m = 1; m < MC; ++m) qmine = (bj >> 5) == m ? qv[m] : qmine;
