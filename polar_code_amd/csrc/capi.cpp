@@ -351,7 +351,9 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
     pscl_decode_params T = P;
     T.apx = 1;
     const bool screen = h->screen && !hist && !P.metrics && !P.cands && !P.force && !P.sc_hard && !P.fidx &&
-                        !P.d_count && (P.fast ? pscl_screening_available(P) != 0 : pscl_lane_long_available(T) != 0);
+                        !P.d_count &&
+                        (P.fast ? (pscl_screening_available(P) != 0 || pscl_lane_long128_available(T) != 0)
+                                : pscl_lane_long_available(T) != 0);
     hipError_t err;
     if (!(screen && pipe)) {
         const int rc = join_pipe(h, 1);

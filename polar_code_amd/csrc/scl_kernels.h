@@ -264,6 +264,8 @@ hipError_t pscl_launch_count_reduce(int32_t* cpart, int64_t slots, int64_t* coun
 #endif
 // scl_lane_long.hip: the lane-per-path screening decoder of the long codes (N = 256..1024, L = 4, 8)
 int pscl_lane_long_available(const pscl_decode_params& P);
+// an N = 128 screening launch that runs it (codes without a compiled-in screening kernel)
+int pscl_lane_long128_available(const pscl_decode_params& P);
 hipError_t pscl_launch_lane_long(const pscl_decode_params& P, hipStream_t s);
 int64_t pscl_lane_long_grid(const pscl_decode_params& P);
 int pscl_screening_fs_available(const pscl_decode_params& P);  // forced-bit screening (DL-SCL retries)

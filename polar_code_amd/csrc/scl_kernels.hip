@@ -564,6 +564,14 @@ void pscl_decode_layout(pscl_decode_params& P, int hist) {
     }
 }
 
+// the screening launch of an N = 128 code without a compiled-in screening kernel (any information
+// set, L = 4 or 8): the runtime-information-set lane-per-path kernel (scl_lane_long.hip at n = 7)
+static bool lane_long128(const pscl_decode_params& P) {
+    return P.fast && P.apx && !pscl_screening_available(P) && pscl_lane_long_available(P);
+}
+
+int pscl_lane_long128_available(const pscl_decode_params& P) { return lane_long128(P) ? 1 : 0; }
+
 hipError_t pscl_launch_decode(const pscl_decode_params& P, int hist, hipStream_t s) {
     if (P.long_mode) {
         if (!hist && P.apx) return pscl_launch_lane_long(P, s);  // (screening: lane-per-path only)
@@ -582,6 +590,7 @@ hipError_t pscl_launch_decode(const pscl_decode_params& P, int hist, hipStream_t
         const int64_t g = (P.B + fw - 1) / fw;
         return pscl_launch_lane_fs(P, g < 1 ? 1 : (g > (1 << 20) ? (1 << 20) : g), s);
     }
+    if (!hist && lane_long128(P)) return pscl_launch_lane_long(P, s);
     if (pscl_decode_wpg(P) < 1) return hipErrorInvalidValue;
     const int64_t grid = pscl_decode_grid(P);
     if (P.fast) return pscl_launch_decode128(P, hist, pscl_decode_wpg(P), grid, decode_lds_bytes(P, hist), s);
@@ -607,6 +616,7 @@ int64_t pscl_decode_count_slots(const pscl_decode_params& P0, int hist) {
         const int64_t g = (P.B + fw - 1) / fw;
         return g < 1 ? 1 : (g > (1 << 20) ? (1 << 20) : g);
     }
+    if (lane_long128(P)) return pscl_lane_long_grid(P);
     if (!P.fast || pscl_decode_wpg(P) < 1) return 0;  // (the generic kernel adds per frame)
     return pscl_decode_grid(P) * pscl_decode_wpg(P);
 }

@@ -83,7 +83,7 @@ template <int NL, int LMAX>
 __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU : PSCL_LANE_LONG_WAVES_PER_EU)
     scl_lane_long_kernel(const pscl_decode_params P) {
     static_assert(LMAX == 4 || LMAX == 8, "the lane-per-path decoder is built for L = 4 and 8");
-    static_assert(NL >= 8 && NL <= 10, "N = 256 .. 1024");
+    static_assert(NL >= 7 && NL <= 10, "N = 128 .. 1024");
     using Ly = LongLaneLayout<NL, LMAX>;
     constexpr int N = Ly::N, R = Ly::R, G = Ly::G, F = Ly::F, LOG_G = Ly::LOG_G;
     constexpr int CE = 1 << R;          // channel LLRs per depth-R element
@@ -541,13 +541,15 @@ hipError_t launch_lane_long(const pscl_decode_params& P, hipStream_t s) {
 #define PSCL_LANE_LONG 1
 #endif
 
-// the screening launch of this plain long-code decode runs the lane-per-path kernel: N = 256,
-// 512 or 1024, L = 4 or 8, plain channel rows, at least log2 L information bits (a full list)
+// the screening launch of this plain decode can run the runtime-information-set lane-per-path
+// kernel: N = 256, 512 or 1024 (every long code), or N = 128 (the codes without a compiled-in
+// screening kernel: pscl_launch_decode takes the compiled-in ones first); L = 4 or 8, plain
+// channel rows, at least log2 L information bits (a full list)
 int pscl_lane_long_available(const pscl_decode_params& P) {
     if (!PSCL_LANE_LONG || !P.apx || P.force || P.sc_hard || P.rm_E || P.fidx || P.d_count || P.elist) return 0;
     if (!P.info_words || !P.epi_table || P.out_by_row) return 0;
     if (P.L != 8 && P.L != 4) return 0;
-    if (P.N != 256 && P.N != 512 && P.N != 1024) return 0;
+    if (P.N != 128 && P.N != 256 && P.N != 512 && P.N != 1024) return 0;
     return P.K >= (P.L == 8 ? 3 : 2);
 }
 
@@ -556,6 +558,7 @@ int64_t pscl_lane_long_grid(const pscl_decode_params& P) { return lane_long_grid
 hipError_t pscl_launch_lane_long(const pscl_decode_params& P, hipStream_t s) {
     if (!pscl_lane_long_available(P)) return hipErrorInvalidValue;
     switch (P.N) {
+        case 128: return P.L == 8 ? launch_lane_long<7, 8>(P, s) : launch_lane_long<7, 4>(P, s);
         case 256: return P.L == 8 ? launch_lane_long<8, 8>(P, s) : launch_lane_long<8, 4>(P, s);
         case 512: return P.L == 8 ? launch_lane_long<9, 8>(P, s) : launch_lane_long<9, 4>(P, s);
         default: return P.L == 8 ? launch_lane_long<10, 8>(P, s) : launch_lane_long<10, 4>(P, s);

@@ -140,3 +140,31 @@ def test_lane_long_bits_domain_bound_deferred(N, L):
     a, n_def = _screened_vs_exact(N, info, L, POLY, llr)
     over = int(np.sum(share(llr) >= bound))
     assert over > B // 8 and n_def >= over, (over, n_def)
+
+
+@pytest.mark.parametrize("K,L,ebno", [(32, 8, 1.5), (100, 8, 4.5), (32, 4, 1.5), (100, 4, 4.5), (64, 8, "custom")])
+def test_lane_n128_runtime_info_set(K, L, ebno):
+    """N = 128 codes without a compiled-in screening kernel (K other than 64 and 88, or K = 64 with
+    another information set): the runtime-information-set lane kernel at n = 7 screens them.  Bit for
+    bit the exact kernel's outputs; the reference algorithm on a sample; integer LLRs (exact metric
+    ties) deferred -- which also shows that the screening pass ran."""
+    B = 6000
+    if ebno == "custom":  # K = 64 on every other position from 32 on: not construct_info_set(128, 64)
+        rng = np.random.default_rng(5)
+        info = np.sort(np.concatenate([np.arange(33, 128, 2), rng.choice(np.arange(32, 128, 2), 16, replace=False)]))
+        _, llr = _frames(128, 64, B, 5.0, seed=11)
+        msg = attach_crc(rng.integers(0, 2, size=(B, 40), dtype=np.int8), POLY)
+        u = np.zeros((B, 128), np.int8)
+        u[:, info] = msg
+        nv = 1.0 / (2.0 * 0.5 * 10 ** (5.0 / 10))
+        llr = 2.0 * ((1.0 - 2.0 * _polar_transform(u)) + rng.normal(0.0, np.sqrt(nv), size=(B, 128))) / nv
+    else:
+        info, llr = _frames(128, K, B, ebno, seed=128 * 7 + K + L)
+    a, n_def = _screened_vs_exact(128, info, L, POLY, llr)
+    assert n_def < B // 4
+    for f in range(0, B, B // 6):
+        n, c, m, il, bi = oracle.decode_scl(llr[f], info, L, crc=POLY)
+        np.testing.assert_array_equal(a["best_bits"][f], c[bi], err_msg=f"frame {f}")
+    ties = np.round(llr[:600] / 4.0)
+    _, n_tie = _screened_vs_exact(128, info, L, POLY, ties)
+    assert n_tie > 0

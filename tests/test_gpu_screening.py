@@ -91,8 +91,9 @@ def test_screening_nr_rate_matched(M):
 @pytest.mark.parametrize("K,E,M", [(64, 256, 4), (64, 100, 8), (88, 0, 8), (60, 0, 4), (64, 0, 3)])
 def test_plain_decode_without_screening_form(K, E, M):
     """Codes and modes with no compiled-in screening kernel ((128,64) rate matched, (128,88)
-    unmatched, other information sets, L below its power of two) decode exactly: plain
-    outputs equal the oracle's and no screening pass runs."""
+    unmatched, other information sets, L below its power of two): plain outputs equal the
+    oracle's.  Rate-matched rows and L = 3 run no screening pass; unmatched rows at L = 4 and 8
+    are screened by the runtime-information-set lane kernel (scl_lane_long.hip at n = 7)."""
     from polar_code_amd.nr.polar import derate_match_polar, subblock_deinterleave
 
     rng = np.random.default_rng(7400 + K + E + M)
@@ -104,7 +105,8 @@ def test_plain_decode_without_screening_form(K, E, M):
     if E:
         dec.set_rate_match(E)
     a = _plain(dec, llr)
-    assert dec.screening_count() == 0
+    if E or M not in (4, 8):
+        assert dec.screening_count() == 0
     for f in range(0, B, 5):
         x = subblock_deinterleave(derate_match_polar(llr[f], 128), 128) if E else llr[f]
         n, c, m, il, b = oracle.decode_scl(x, info, M, crc=POLY)

@@ -79,8 +79,10 @@ def dl_bench():
 if "--dl" in sys.argv:
     dl_bench()
     sys.exit(0)
-for N, K, L, B, snr in [(256, 128, 8, 200_000, 4.0), (512, 256, 8, 100_000, 5.0), (1024, 512, 8, 50_000, 6.0),
-                        (1024, 512, 32, 20_000, 6.0)]:
+# (N = 128, K = 100: a code without a compiled-in screening kernel -- the runtime-information-set
+# lane kernel at n = 7 -- timed against the exact kernel alone too)
+for N, K, L, B, snr in [(128, 100, 8, 500_000, 4.5), (256, 128, 8, 200_000, 4.0), (512, 256, 8, 100_000, 5.0),
+                        (1024, 512, 8, 50_000, 6.0), (1024, 512, 32, 20_000, 6.0)]:
     rng = np.random.default_rng(N + L)
     info = construct_info_set(N, K)
     msg = attach_crc(rng.integers(0, 2, size=(B, K - 24), dtype=np.int8), POLY)
@@ -108,6 +110,17 @@ for N, K, L, B, snr in [(256, 128, 8, 200_000, 4.0), (512, 256, 8, 100_000, 5.0)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / steps
     fer = float(((flags.cpu().numpy() & 0x80) == 0).mean())
+    exact_note = ""
+    if N == 128:  # the same decode on the exact kernel alone (screening off)
+        dec.set_screening(False)
+        e0.record(stream)
+        for _ in range(steps):
+            dec.decode_device(d_llr.data_ptr(), B, d_best=best2.data_ptr(), d_flags=flags2.data_ptr())
+        e1.record(stream)
+        torch.cuda.synchronize()
+        exact_note = (f", exact kernel alone {B / (e0.elapsed_time(e1) / steps) * 1e3 / 1e6:.2f} M frames/s "
+                      f"(outputs equal {bool(torch.equal(best, best2) and torch.equal(flags, flags2))})")
+        dec.set_screening(True)
     # pipelined handle (as bench.py): each call's exact re-decode of its deferred frames overlaps
     # the next call's screening pass; alternating output buffers, the last re-decode inside the
     # timed region (join)
@@ -128,6 +141,7 @@ for N, K, L, B, snr in [(256, 128, 8, 200_000, 4.0), (512, 256, 8, 100_000, 5.0)
     same = bool(torch.equal(best, best2) and torch.equal(flags, flags2))
     print(f"N={N} K={K} L={L} {snr:g} dB: {B / ms * 1e3 / 1e6:.2f} M frames/s ({ms:.2f} ms per {B} frames), "
           f"pipelined {B / pms * 1e3 / 1e6:.2f} M frames/s ({pms:.2f} ms), input {B * N * 8 / pms / 1e6:.1f} GB/s, "
-          f"FER {fer:.4f}, deferred to the exact kernel {n_def} ({100.0 * n_def / B:.2f} %), outputs equal {same}",
+          f"FER {fer:.4f}, deferred to the exact kernel {n_def} ({100.0 * n_def / B:.2f} %), outputs equal {same}"
+          f"{exact_note}",
           flush=True)
     dec.close()
