@@ -81,6 +81,8 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
         // f indexes the force words and outputs: the frame index, or a bucket list's entry id
         const int64_t f = P.elist ? pscl_elist_entry(P, fsafe, bpre) : fi;
         const int64_t frow = P.fidx ? P.fidx[P.elist ? f : fsafe] : fsafe;
+        // best / flags / counts at the frame's own row (the exact re-decode of screened frames) or at f
+        const int64_t fo = P.out_by_row ? frow : f;
         if (P.rm_E == 0) {  // stage this frame's channel LLRs in LDS (read at every depth-1 use)
             const double* src = P.llr + frow * N;
             for (int x = g; x < N; x += G) Af[x] = src[x];
@@ -297,13 +299,13 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
                     }
                 }
                 if (P.best) {
-                    P.best[f * W] = ib0;
-                    if (W > 1) P.best[f * W + 1] = ib1;
+                    P.best[fo * W] = ib0;
+                    if (W > 1) P.best[fo * W + 1] = ib1;
                 }
-                if (P.flags) P.flags[f] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
-                if (P.n_paths) P.n_paths[f] = cnt;
+                if (P.flags) P.flags[fo] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
+                if (P.n_paths) P.n_paths[fo] = cnt;
                 if (P.ref) {
-                    const uint64_t r0 = P.ref[f * W], r1 = (W > 1) ? P.ref[f * W + 1] : 0;
+                    const uint64_t r0 = P.ref[fo * W], r1 = (W > 1) ? P.ref[fo * W + 1] : 0;
                     const uint64_t d0 = ib0 ^ r0, d1 = ib1 ^ r1;
                     const int bit_err = __popcll(d0) + __popcll(d1);
                     const int kp = P.k_payload;
@@ -322,7 +324,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
         }
         wave_lds_fence();  // the next frames reuse this wave's LDS
     }
-    if (P.ref && blockIdx.x == 0 && threadIdx.x == 0)
+    if (P.ref && !P.out_by_row && blockIdx.x == 0 && threadIdx.x == 0)  // (a re-decode's frames were counted)
         atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
 }
 
@@ -565,9 +567,9 @@ void pscl_decode_layout(pscl_decode_params& P, int hist) {
 }
 
 // the screening launch of an N = 128 code without a compiled-in screening kernel (any information
-// set, L = 4 or 8): the runtime-information-set lane-per-path kernel (scl_lane_long.hip at n = 7)
+// set, L = 4, 8 or 16): the runtime-information-set lane-per-path kernel (scl_lane_long.hip at n = 7)
 static bool lane_long128(const pscl_decode_params& P) {
-    return P.fast && P.apx && !pscl_screening_available(P) && pscl_lane_long_available(P);
+    return P.N == 128 && !P.long_mode && P.apx && !pscl_screening_available(P) && pscl_lane_long_available(P);
 }
 
 int pscl_lane_long128_available(const pscl_decode_params& P) { return lane_long128(P) ? 1 : 0; }

@@ -79,16 +79,24 @@ __device__ __forceinline__ void rank3(uint32_t og, uint32_t ob, uint32_t kg, uin
         : "vcc");
 }
 
+// lane i <-> 15 - i within a row: maps one 8-lane half of a 16-lane frame (G = 16, a whole row)
+// onto the other
+constexpr int kRMIR = 0x140;
+
 // max / min / sum of v over the G lanes of each frame (G = 4: two quad_perm steps; G = 8: and
-// the half-row mirror)
+// the half-row mirror; G = 16: and the row mirror)
 template <int G>
 __device__ __forceinline__ uint32_t frame_max(uint32_t v) {
     uint32_t o = dpp32<kQX1>(v);
     v = o > v ? o : v;
     o = dpp32<kQX2>(v);
     v = o > v ? o : v;
-    if constexpr (G == 8) {
-        o = dpp32<kFMIR>(v);
+    if constexpr (G >= 8) {
+        o = dpp32<G == 16 ? kHMIR : kFMIR>(v);
+        v = o > v ? o : v;
+    }
+    if constexpr (G == 16) {
+        o = dpp32<kRMIR>(v);
         v = o > v ? o : v;
     }
     return v;
@@ -99,8 +107,12 @@ __device__ __forceinline__ uint32_t frame_min(uint32_t v) {
     v = o < v ? o : v;
     o = dpp32<kQX2>(v);
     v = o < v ? o : v;
-    if constexpr (G == 8) {
-        o = dpp32<kFMIR>(v);
+    if constexpr (G >= 8) {
+        o = dpp32<G == 16 ? kHMIR : kFMIR>(v);
+        v = o < v ? o : v;
+    }
+    if constexpr (G == 16) {
+        o = dpp32<kRMIR>(v);
         v = o < v ? o : v;
     }
     return v;
@@ -109,7 +121,8 @@ template <int G>
 __device__ __forceinline__ uint32_t frame_sum(uint32_t v) {
     v += dpp32<kQX1>(v);
     v += dpp32<kQX2>(v);
-    if constexpr (G == 8) v += dpp32<kFMIR>(v);
+    if constexpr (G >= 8) v += dpp32<G == 16 ? kHMIR : kFMIR>(v);
+    if constexpr (G == 16) v += dpp32<kRMIR>(v);
     return v;
 }
 
@@ -132,12 +145,25 @@ __device__ __forceinline__ void select_survivors(uint32_t kg, uint32_t kb, bool&
     rank3<kQX1>(kg, kb, kg, kb, rg, rbb);
     rank3<kQX2>(kg, kb, kg, kb, rg, rbb);
     rank3<kQX3>(kg, kb, kg, kb, rg, rbb);
-    if constexpr (G == 8) {  // the other quad of the frame, through the half-row mirror
-        const uint32_t mkg = dpp32<kFMIR>(kg), mkb = dpp32<kFMIR>(kb);
+    if constexpr (G >= 8) {  // the other quad of the frame's 8-lane half, through the half-row mirror
+        const uint32_t mkg = dpp32<G == 16 ? kHMIR : kFMIR>(kg), mkb = dpp32<G == 16 ? kHMIR : kFMIR>(kb);
         rank3<kQID>(mkg, mkb, kg, kb, rg, rbb);
         rank3<kQX1>(mkg, mkb, kg, kb, rg, rbb);
         rank3<kQX2>(mkg, mkb, kg, kb, rg, rbb);
         rank3<kQX3>(mkg, mkb, kg, kb, rg, rbb);
+    }
+    if constexpr (G == 16) {  // the other half's two quads: the row mirror (lane 15 - i), and the row
+                              // mirror of the half-row mirror (lane i + 8 or i - 8)
+        const uint32_t rkg = dpp32<kRMIR>(kg), rkb = dpp32<kRMIR>(kb);
+        rank3<kQID>(rkg, rkb, kg, kb, rg, rbb);
+        rank3<kQX1>(rkg, rkb, kg, kb, rg, rbb);
+        rank3<kQX2>(rkg, rkb, kg, kb, rg, rbb);
+        rank3<kQX3>(rkg, rkb, kg, kb, rg, rbb);
+        const uint32_t xkg = dpp32<kRMIR>(dpp32<kHMIR>(kg)), xkb = dpp32<kRMIR>(dpp32<kHMIR>(kb));
+        rank3<kQID>(xkg, xkb, kg, kb, rg, rbb);
+        rank3<kQX1>(xkg, xkb, kg, kb, rg, rbb);
+        rank3<kQX2>(xkg, xkb, kg, kb, rg, rbb);
+        rank3<kQX3>(xkg, xkb, kg, kb, rg, rbb);
     }
     keep_g = rg < (uint32_t)LMAX;
     const uint32_t d = frame_sum<G>(keep_g ? 0u : 1u);
@@ -157,6 +183,24 @@ __device__ __forceinline__ void select_survivors(uint32_t kg, uint32_t kb, bool&
     keep_g = rg < (uint32_t)LMAX;
     win_b = rb < (uint32_t)LMAX;
 #endif
+}
+
+// position of the j-th set bit (j < popcount(m)) of a mask of at most 16 bits, branch-free
+__device__ __forceinline__ uint32_t nth_set_bit16(uint32_t m, uint32_t j) {
+    const uint32_t c8 = __builtin_popcount(m & 255u);
+    const bool h8 = j >= c8;
+    j = h8 ? j - c8 : j;
+    m = h8 ? (m >> 8) : (m & 255u);
+    const uint32_t c4 = __builtin_popcount(m & 15u);
+    const bool h4 = j >= c4;
+    j = h4 ? j - c4 : j;
+    m = h4 ? (m >> 4) : (m & 15u);
+    const uint32_t c2 = __builtin_popcount(m & 3u);
+    const bool h2 = j >= c2;
+    j = h2 ? j - c2 : j;
+    m = h2 ? (m >> 2) : m;
+    const bool h1 = j >= (m & 1u);
+    return (h8 ? 8u : 0u) + (h4 ? 4u : 0u) + (h2 ? 2u : 0u) + (h1 ? 1u : 0u);
 }
 
 // position of the j-th set bit (j < popcount(m)) of a mask of at most 8 bits, branch-free

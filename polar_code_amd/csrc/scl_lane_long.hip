@@ -82,7 +82,7 @@ __device__ __forceinline__ uint64_t uword(const uint64_t (&u)[NW], int k) {
 template <int NL, int LMAX>
 __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU : PSCL_LANE_LONG_WAVES_PER_EU)
     scl_lane_long_kernel(const pscl_decode_params P) {
-    static_assert(LMAX == 4 || LMAX == 8, "the lane-per-path decoder is built for L = 4 and 8");
+    static_assert(LMAX == 4 || LMAX == 8 || LMAX == 16, "the lane-per-path decoder is built for L = 4, 8 and 16");
     static_assert(NL >= 7 && NL <= 10, "N = 128 .. 1024");
     using Ly = LongLaneLayout<NL, LMAX>;
     constexpr int N = Ly::N, R = Ly::R, G = Ly::G, F = Ly::F, LOG_G = Ly::LOG_G;
@@ -389,7 +389,7 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
                         amb |= wmask(!(nsurv == (uint32_t)LMAX && nmin > smax)) & vmask;
                         const uint32_t f8 = frame_bits(wmask(!keep_g)), w8 = frame_bits(wmask(win_b));
                         const uint32_t j = __builtin_popcount(f8 & ((1u << p) - 1u));
-                        src = gbase + (int)nth_set_bit8(w8, j);
+                        src = gbase + (int)(G == 16 ? nth_set_bit16(w8, j) : nth_set_bit8(w8, j));
                         take = !keep_g;
                     }
                     // the worse child's bit rides on the table word
@@ -482,12 +482,18 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
         cmp_perm(dpp32<kQX1>(kh), dpp32<kQX1>(ku));
         cmp_perm(dpp32<kQX2>(kh), dpp32<kQX2>(ku));
         cmp_perm(dpp32<kQX3>(kh), dpp32<kQX3>(ku));
-        if constexpr (G == 8) {
-            const uint32_t mh = dpp32<kHMIR>(kh), mu = dpp32<kHMIR>(ku);
+        // the other quads of the frame: G = 8 the half-row mirror's; G = 16 also the row mirror's and
+        // the row mirror of the half-row mirror's (select_survivors, scl_lane.h)
+        auto cmp_quad = [&](uint32_t mh, uint32_t mu) {
             cmp_perm(mh, mu);
             cmp_perm(dpp32<kQX1>(mh), dpp32<kQX1>(mu));
             cmp_perm(dpp32<kQX2>(mh), dpp32<kQX2>(mu));
             cmp_perm(dpp32<kQX3>(mh), dpp32<kQX3>(mu));
+        };
+        if constexpr (G >= 8) cmp_quad(dpp32<kHMIR>(kh), dpp32<kHMIR>(ku));
+        if constexpr (G == 16) {
+            cmp_quad(dpp32<kRMIR>(kh), dpp32<kRMIR>(ku));
+            cmp_quad(dpp32<kRMIR>(dpp32<kHMIR>(kh)), dpp32<kRMIR>(dpp32<kHMIR>(ku)));
         }
         amb |= wmask(near) & vmask;
         const bool famb = ((amb >> gbase) & (uint64_t)GM) != 0;
@@ -548,19 +554,22 @@ hipError_t launch_lane_long(const pscl_decode_params& P, hipStream_t s) {
 int pscl_lane_long_available(const pscl_decode_params& P) {
     if (!PSCL_LANE_LONG || !P.apx || P.force || P.sc_hard || P.rm_E || P.fidx || P.d_count || P.elist) return 0;
     if (!P.info_words || !P.epi_table || P.out_by_row) return 0;
-    if (P.L != 8 && P.L != 4) return 0;
+    if (P.L != 16 && P.L != 8 && P.L != 4) return 0;
     if (P.N != 128 && P.N != 256 && P.N != 512 && P.N != 1024) return 0;
-    return P.K >= (P.L == 8 ? 3 : 2);
+    return P.K >= __builtin_ctz((unsigned)P.L);
 }
 
 int64_t pscl_lane_long_grid(const pscl_decode_params& P) { return lane_long_grid(P); }
 
 hipError_t pscl_launch_lane_long(const pscl_decode_params& P, hipStream_t s) {
     if (!pscl_lane_long_available(P)) return hipErrorInvalidValue;
+#define PSCL_LL(NL_) (P.L == 16 ? launch_lane_long<NL_, 16>(P, s) : P.L == 8 ? launch_lane_long<NL_, 8>(P, s) \
+                                                                   : launch_lane_long<NL_, 4>(P, s))
     switch (P.N) {
-        case 128: return P.L == 8 ? launch_lane_long<7, 8>(P, s) : launch_lane_long<7, 4>(P, s);
-        case 256: return P.L == 8 ? launch_lane_long<8, 8>(P, s) : launch_lane_long<8, 4>(P, s);
-        case 512: return P.L == 8 ? launch_lane_long<9, 8>(P, s) : launch_lane_long<9, 4>(P, s);
-        default: return P.L == 8 ? launch_lane_long<10, 8>(P, s) : launch_lane_long<10, 4>(P, s);
+        case 128: return PSCL_LL(7);
+        case 256: return PSCL_LL(8);
+        case 512: return PSCL_LL(9);
+        default: return PSCL_LL(10);
     }
+#undef PSCL_LL
 }

@@ -1,4 +1,5 @@
-"""GPU: the long-code screening decoder (csrc/scl_lane_long.hip, N = 256..1024, L = 4 and 8)
+"""GPU: the runtime-information-set screening decoder (csrc/scl_lane_long.hip, N = 128..1024,
+L = 4, 8 and 16)
 against the exact long-code kernel (scl_long.hip, screening off) and the oracle.
 
 A plain decode (best bits and CRC flags only) of a long code runs the lane-per-path screening
@@ -50,7 +51,9 @@ def _screened_vs_exact(N, info, L, crc, llr):
 @pytest.mark.parametrize("N,K,L,ebno,B", [(256, 128, 8, 4.0, 6000), (256, 128, 4, 4.0, 6000),
                                           (512, 256, 8, 5.0, 3000), (512, 256, 4, 5.0, 3000),
                                           (1024, 512, 8, 6.0, 1500), (1024, 512, 4, 6.0, 1500),
-                                          (256, 100, 8, 2.5, 3000), (512, 300, 8, 3.0, 1500)])
+                                          (256, 100, 8, 2.5, 3000), (512, 300, 8, 3.0, 1500),
+                                          (256, 128, 16, 4.0, 3000), (1024, 512, 16, 6.0, 800),
+                                          (128, 64, 16, 4.0, 6000), (512, 256, 16, 5.0, 1500)])
 def test_lane_long_equals_exact(N, K, L, ebno, B):
     info, llr = _frames(N, K, B, ebno, seed=N * 7 + K + L)
     a, n_def = _screened_vs_exact(N, info, L, POLY, llr)
@@ -73,7 +76,7 @@ def test_lane_long_no_crc(N, L):
         np.testing.assert_array_equal(a["best_bits"][f], c[bi], err_msg=f"frame {f}")
 
 
-@pytest.mark.parametrize("N,L", [(256, 8), (512, 4)])
+@pytest.mark.parametrize("N,L", [(256, 8), (512, 4), (256, 16), (128, 16)])
 def test_lane_long_ties_and_extremes_defer(N, L):
     """Integer LLRs (exact metric ties through the stable sort), noiseless +-1 rows and rows with
     LLRs beyond 2^25 must reach the exact kernel; the outputs equal it everywhere."""
@@ -142,7 +145,8 @@ def test_lane_long_bits_domain_bound_deferred(N, L):
     assert over > B // 8 and n_def >= over, (over, n_def)
 
 
-@pytest.mark.parametrize("K,L,ebno", [(32, 8, 1.5), (100, 8, 4.5), (32, 4, 1.5), (100, 4, 4.5), (64, 8, "custom")])
+@pytest.mark.parametrize("K,L,ebno", [(32, 8, 1.5), (100, 8, 4.5), (32, 4, 1.5), (100, 4, 4.5), (64, 8, "custom"),
+                                      (100, 16, 4.0)])
 def test_lane_n128_runtime_info_set(K, L, ebno):
     """N = 128 codes without a compiled-in screening kernel (K other than 64 and 88, or K = 64 with
     another information set): the runtime-information-set lane kernel at n = 7 screens them.  Bit for
