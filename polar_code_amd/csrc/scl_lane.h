@@ -85,6 +85,9 @@ constexpr int kRMIR = 0x140;
 
 // max / min / sum of v over the G lanes of each frame (G = 4: two quad_perm steps; G = 8: and
 // the half-row mirror; G = 16: and the row mirror)
+// the other row of a 32-lane frame (G = 32: two rows; DPP does not cross rows)
+__device__ __forceinline__ uint32_t xrow32(uint32_t v) { return (uint32_t)__shfl_xor((int)v, 16); }
+
 template <int G>
 __device__ __forceinline__ uint32_t frame_max(uint32_t v) {
     uint32_t o = dpp32<kQX1>(v);
@@ -92,11 +95,15 @@ __device__ __forceinline__ uint32_t frame_max(uint32_t v) {
     o = dpp32<kQX2>(v);
     v = o > v ? o : v;
     if constexpr (G >= 8) {
-        o = dpp32<G == 16 ? kHMIR : kFMIR>(v);
+        o = dpp32<G >= 16 ? kHMIR : kFMIR>(v);
         v = o > v ? o : v;
     }
-    if constexpr (G == 16) {
+    if constexpr (G >= 16) {
         o = dpp32<kRMIR>(v);
+        v = o > v ? o : v;
+    }
+    if constexpr (G == 32) {
+        o = xrow32(v);
         v = o > v ? o : v;
     }
     return v;
@@ -108,11 +115,15 @@ __device__ __forceinline__ uint32_t frame_min(uint32_t v) {
     o = dpp32<kQX2>(v);
     v = o < v ? o : v;
     if constexpr (G >= 8) {
-        o = dpp32<G == 16 ? kHMIR : kFMIR>(v);
+        o = dpp32<G >= 16 ? kHMIR : kFMIR>(v);
         v = o < v ? o : v;
     }
-    if constexpr (G == 16) {
+    if constexpr (G >= 16) {
         o = dpp32<kRMIR>(v);
+        v = o < v ? o : v;
+    }
+    if constexpr (G == 32) {
+        o = xrow32(v);
         v = o < v ? o : v;
     }
     return v;
@@ -121,8 +132,9 @@ template <int G>
 __device__ __forceinline__ uint32_t frame_sum(uint32_t v) {
     v += dpp32<kQX1>(v);
     v += dpp32<kQX2>(v);
-    if constexpr (G >= 8) v += dpp32<G == 16 ? kHMIR : kFMIR>(v);
-    if constexpr (G == 16) v += dpp32<kRMIR>(v);
+    if constexpr (G >= 8) v += dpp32<G >= 16 ? kHMIR : kFMIR>(v);
+    if constexpr (G >= 16) v += dpp32<kRMIR>(v);
+    if constexpr (G == 32) v += xrow32(v);
     return v;
 }
 
@@ -146,29 +158,37 @@ __device__ __forceinline__ void select_survivors(uint32_t kg, uint32_t kb, bool&
     rank3<kQX2>(kg, kb, kg, kb, rg, rbb);
     rank3<kQX3>(kg, kb, kg, kb, rg, rbb);
     if constexpr (G >= 8) {  // the other quad of the frame's 8-lane half, through the half-row mirror
-        const uint32_t mkg = dpp32<G == 16 ? kHMIR : kFMIR>(kg), mkb = dpp32<G == 16 ? kHMIR : kFMIR>(kb);
+        const uint32_t mkg = dpp32<G >= 16 ? kHMIR : kFMIR>(kg), mkb = dpp32<G >= 16 ? kHMIR : kFMIR>(kb);
         rank3<kQID>(mkg, mkb, kg, kb, rg, rbb);
         rank3<kQX1>(mkg, mkb, kg, kb, rg, rbb);
         rank3<kQX2>(mkg, mkb, kg, kb, rg, rbb);
         rank3<kQX3>(mkg, mkb, kg, kb, rg, rbb);
     }
-    if constexpr (G == 16) {  // the other half's two quads: the row mirror (lane 15 - i), and the row
-                              // mirror of the half-row mirror (lane i + 8 or i - 8)
-        const uint32_t rkg = dpp32<kRMIR>(kg), rkb = dpp32<kRMIR>(kb);
-        rank3<kQID>(rkg, rkb, kg, kb, rg, rbb);
-        rank3<kQX1>(rkg, rkb, kg, kb, rg, rbb);
-        rank3<kQX2>(rkg, rkb, kg, kb, rg, rbb);
-        rank3<kQX3>(rkg, rkb, kg, kb, rg, rbb);
-        const uint32_t xkg = dpp32<kRMIR>(dpp32<kHMIR>(kg)), xkb = dpp32<kRMIR>(dpp32<kHMIR>(kb));
-        rank3<kQID>(xkg, xkb, kg, kb, rg, rbb);
-        rank3<kQX1>(xkg, xkb, kg, kb, rg, rbb);
-        rank3<kQX2>(xkg, xkb, kg, kb, rg, rbb);
-        rank3<kQX3>(xkg, xkb, kg, kb, rg, rbb);
+    // the row's other half (G >= 16): the row mirror (lane 15 - i) and the row mirror of the half-row
+    // mirror (lane i + 8 or i - 8), each with the quad permutations; G = 32: then the other row's 16
+    // lanes, brought over by a bpermute (xor 16), the same way
+    auto quads16 = [&](uint32_t ok, uint32_t ob) {
+        rank3<kQID>(ok, ob, kg, kb, rg, rbb);
+        rank3<kQX1>(ok, ob, kg, kb, rg, rbb);
+        rank3<kQX2>(ok, ob, kg, kb, rg, rbb);
+        rank3<kQX3>(ok, ob, kg, kb, rg, rbb);
+    };
+    if constexpr (G >= 16) {
+        quads16(dpp32<kRMIR>(kg), dpp32<kRMIR>(kb));
+        quads16(dpp32<kRMIR>(dpp32<kHMIR>(kg)), dpp32<kRMIR>(dpp32<kHMIR>(kb)));
+    }
+    if constexpr (G == 32) {
+        const uint32_t xg = xrow32(kg), xb = xrow32(kb);
+        quads16(xg, xb);
+        quads16(dpp32<kHMIR>(xg), dpp32<kHMIR>(xb));
+        quads16(dpp32<kRMIR>(xg), dpp32<kRMIR>(xb));
+        quads16(dpp32<kRMIR>(dpp32<kHMIR>(xg)), dpp32<kRMIR>(dpp32<kHMIR>(xb)));
     }
     keep_g = rg < (uint32_t)LMAX;
     const uint32_t d = frame_sum<G>(keep_g ? 0u : 1u);
     win_b = rbb < d;
 #else
+    static_assert(G <= 8, "the two-rank selection is built for frames of at most 8 lanes");
     uint32_t rg = 0, rb = kg < kb ? 1u : 0u;
     rank_pair<kQX1>(kg, kb, kg, kb, rg, rb);
     rank_pair<kQX2>(kg, kb, kg, kb, rg, rb);
@@ -183,6 +203,14 @@ __device__ __forceinline__ void select_survivors(uint32_t kg, uint32_t kb, bool&
     keep_g = rg < (uint32_t)LMAX;
     win_b = rb < (uint32_t)LMAX;
 #endif
+}
+
+// position of the j-th set bit (j < popcount(m)) of a mask of at most 32 bits, branch-free
+__device__ __forceinline__ uint32_t nth_set_bit16(uint32_t m, uint32_t j);
+__device__ __forceinline__ uint32_t nth_set_bit32(uint32_t m, uint32_t j) {
+    const uint32_t c16 = __builtin_popcount(m & 0xffffu);
+    const bool h16 = j >= c16;
+    return (h16 ? 16u : 0u) + nth_set_bit16(h16 ? (m >> 16) : (m & 0xffffu), h16 ? j - c16 : j);
 }
 
 // position of the j-th set bit (j < popcount(m)) of a mask of at most 16 bits, branch-free

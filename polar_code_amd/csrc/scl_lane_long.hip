@@ -53,9 +53,9 @@ struct LongLaneLayout {
 #ifndef PSCL_LANE_LONG_WAVES_PER_EU
 #define PSCL_LANE_LONG_WAVES_PER_EU 2
 #endif
-// N = 1024: the element recompute holds 64 channel LLRs (128 VGPRs); at 2 waves/SIMD (256 VGPRs)
-// it spills (592 bytes of scratch per lane), at 1 (512) none -- LDS allows 6 wavefronts per CU
-// either way.  Measured (tools/long_bench.py, profiles/r05j_long_*): 3.42 M frames/s at 1 against
+// N = 1024 (and N = 512 at L = 16, 32): the element recompute holds 64 channel LLRs (128 VGPRs); at
+// 2 waves/SIMD (256 VGPRs) it spills (592 bytes of scratch per lane at N = 1024, 120-168 at N = 512,
+// L >= 16), at 1 (512) none -- LDS allows 6 wavefronts per CU either way.  Measured (tools/long_bench.py, profiles/r05j_long_*): 3.42 M frames/s at 1 against
 // 2.60 M at 2 (4.36 M against 3.02 M pipelined)
 #ifndef PSCL_LANE_LONG1024_WAVES_PER_EU
 #define PSCL_LANE_LONG1024_WAVES_PER_EU 1
@@ -80,16 +80,23 @@ __device__ __forceinline__ uint64_t uword(const uint64_t (&u)[NW], int k) {
 }
 
 template <int NL, int LMAX>
-__global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU : PSCL_LANE_LONG_WAVES_PER_EU)
+__global__ void __launch_bounds__(64, (NL == 10 || (NL == 9 && LMAX >= 16)) ? PSCL_LANE_LONG1024_WAVES_PER_EU
+                                                                           : PSCL_LANE_LONG_WAVES_PER_EU)
     scl_lane_long_kernel(const pscl_decode_params P) {
-    static_assert(LMAX == 4 || LMAX == 8 || LMAX == 16, "the lane-per-path decoder is built for L = 4, 8 and 16");
+    static_assert(LMAX == 4 || LMAX == 8 || LMAX == 16 || LMAX == 32,
+                  "the lane-per-path decoder is built for L = 4, 8, 16 and 32");
     static_assert(NL >= 7 && NL <= 10, "N = 128 .. 1024");
     using Ly = LongLaneLayout<NL, LMAX>;
     constexpr int N = Ly::N, R = Ly::R, G = Ly::G, F = Ly::F, LOG_G = Ly::LOG_G;
     constexpr int CE = 1 << R;          // channel LLRs per depth-R element
     constexpr int NW = N / 64;          // decided-bit words per path
-    constexpr int EPL = 16 / G;         // depth-R elements per lane at a block start
-    constexpr uint32_t GM = (1u << G) - 1u;
+    // depth-R elements per lane at a block start; G = 32: the lanes p and p + 16 share element p % 16,
+    // each recomputing it for half of the paths (those of parity p / 16)
+    constexpr int EPL = G == 32 ? 1 : 16 / G;
+    constexpr uint32_t GM = G == 32 ? 0xffffffffu : (1u << G) - 1u;
+    // slot-table fields: 4 bits per stored depth (L <= 16) or 5 (L = 32)
+    constexpr int SB = LMAX > 16 ? 5 : 4;
+    constexpr uint32_t SFULL = (1u << (4 * SB)) - 1u, SREP = SB == 4 ? 0x1111u : 0x8421u;
     constexpr bool CREG = EPL * CE <= 32;  // N = 256, L = 8: the lane's channel LLRs stay in registers
     // every metric carries N tail terms: two metrics differ from their exact values by < 2 N DELTA.
     // Metrics in bits (PSCL_LANE_BITS, scl128_lane.hip): the channel LLRs scaled by log2 e as they
@@ -101,6 +108,7 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
     double* const A = reinterpret_cast<double*>(smem);
     const int lane = threadIdx.x & 63;
     const int fl = lane >> LOG_G, p = lane & (G - 1), gbase = lane & ~(G - 1);
+    const int pe = G == 32 ? (p & 15) : p;  // the lane's first depth-R element (EPL above)
     double* const Af = A + fl * Ly::FSTRIDE;
     uint32_t* const XS = reinterpret_cast<uint32_t*>(Af + Ly::OFFX);
     const uint8_t* const GT = reinterpret_cast<const uint8_t*>(P.epi_table);        // [N/8][256] u-byte -> info bits
@@ -114,7 +122,7 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
         return hiw(r);
     };
     auto frame_bits = [&](uint64_t m) { return (uint32_t)(m >> gbase) & GM; };
-    auto slot_rel = [](uint32_t tab, int dr) { return (int)((tab >> (4 * dr)) & 15u); };
+    auto slot_rel = [](uint32_t tab, int dr) { return (int)((tab >> (SB * dr)) & ((1u << SB) - 1u)); };
 
     int cfe = 0, cbe = 0, cpe = 0, cpb = 0;  // this lane's error counts (flushed at the end)
     for (int64_t f0 = (int64_t)blockIdx.x * F; f0 < P.B; f0 += (int64_t)gridDim.x * F) {
@@ -131,7 +139,7 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
             for (int h = 0; h < EPL; ++h)
 #pragma unroll
                 for (int m = 0; m < CE; ++m) {
-                    const double v = BITS ? chan[p + G * h + 16 * m] * PSCL_LOG2E_F64 : chan[p + G * h + 16 * m];
+                    const double v = BITS ? chan[pe + G * h + 16 * m] * PSCL_LOG2E_F64 : chan[pe + G * h + 16 * m];
                     if constexpr (CREG) c[CE * h + m] = v;
                     cs = cs + fabs(v);
                 }
@@ -196,12 +204,13 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
                 const bool r2 = (b >> (R - 2)) & 1;
                 auto elem = [&](auto HC) {
                     const int h = HC;
-                    const uint32_t e = (uint32_t)(p + G * h);
+                    const uint32_t e = (uint32_t)(pe + G * h);
                     // every path of the element: depths 1-2 by first(q, xq, v), then depths 3..R
                     auto paths = [&](auto&& first) {
                         auto path = [&](int q0) {
                             // lane p takes path (q0 + p) mod L: the lanes' stores hit distinct bank groups
-                            const int q = cnt == LMAX ? ((q0 + p) & (LMAX - 1)) : q0;
+                            // (G = 32: q0 of the lane's parity, rotated by 2 (p % 16), keeping it)
+                            const int q = cnt == LMAX ? ((q0 + (G == 32 ? 2 * (p & 15) : p)) & (LMAX - 1)) : q0;
                             const uint32_t* xq = XS + q * Ly::XWORDS;
                             double v[CE / 4];  // depth-2 values at e + 16 m
                             first(xq, v);
@@ -220,7 +229,11 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
                             // element e of slot q: pair index e & 7, half e >> 3 ([8][L][2] layout)
                             Af[Ly::OFF0 + ((e & 7) * LMAX + q) * 2 + (e >> 3)] = v[0];
                         };
-                        if constexpr (CREG) {
+                        if constexpr (G == 32) {  // the paths of parity p / 16
+#pragma unroll
+                            for (int i = 0; i < LMAX / 2; ++i)
+                                if (2 * i + (p >> 4) < cnt) path(2 * i + (p >> 4));
+                        } else if constexpr (CREG) {
 #pragma unroll
                             for (int q0 = 0; q0 < LMAX; ++q0)
                                 if (q0 < cnt) path(q0);
@@ -319,8 +332,8 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
                     });
                     // this path's own slot at every depth rewritten this phase
                     constexpr int s0 = start - R;
-                    constexpr uint32_t mask = (0xffffu << (4 * s0)) & 0xffffu;
-                    tab = (tab & ~mask) | ((uint32_t)p * 0x1111u & mask);
+                    constexpr uint32_t mask = (SFULL << (SB * s0)) & SFULL;
+                    tab = (tab & ~mask) | ((uint32_t)p * SREP & mask);
                 }
                 // ---- leaf LLR and metric tail (scl.py:80-82, 102-105)
                 const double2 lab = *reinterpret_cast<const double2*>(Af + Ly::OFF3 + (start <= NL - 1 ? p : slot_rel(tab, 3)) * 2);
@@ -372,7 +385,7 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
                         const uint32_t wu = frame_max<G>(bad ? hiw_up(mb) : 0u);
                         const bool swap = bad8 != 0;
                         amb |= wmask(swap && !(nmax == 1u && g2u < gmaxh && wu < gmaxh)) & vmask;
-                        src = (gbase + (int)__builtin_ctz(bad8 | (1u << G))) & 63;
+                        src = (gbase + (int)__builtin_ctzll((uint64_t)bad8 | (1ull << G))) & 63;
                         take = swap && ismax;
                     } else
 #endif
@@ -389,7 +402,7 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
                         amb |= wmask(!(nsurv == (uint32_t)LMAX && nmin > smax)) & vmask;
                         const uint32_t f8 = frame_bits(wmask(!keep_g)), w8 = frame_bits(wmask(win_b));
                         const uint32_t j = __builtin_popcount(f8 & ((1u << p) - 1u));
-                        src = gbase + (int)(G == 16 ? nth_set_bit16(w8, j) : nth_set_bit8(w8, j));
+                        src = gbase + (int)(G == 32 ? nth_set_bit32(w8, j) : G == 16 ? nth_set_bit16(w8, j) : nth_set_bit8(w8, j));
                         take = !keep_g;
                     }
                     // the worse child's bit rides on the table word
@@ -491,9 +504,16 @@ __global__ void __launch_bounds__(64, NL == 10 ? PSCL_LANE_LONG1024_WAVES_PER_EU
             cmp_perm(dpp32<kQX3>(mh), dpp32<kQX3>(mu));
         };
         if constexpr (G >= 8) cmp_quad(dpp32<kHMIR>(kh), dpp32<kHMIR>(ku));
-        if constexpr (G == 16) {
+        if constexpr (G >= 16) {
             cmp_quad(dpp32<kRMIR>(kh), dpp32<kRMIR>(ku));
             cmp_quad(dpp32<kRMIR>(dpp32<kHMIR>(kh)), dpp32<kRMIR>(dpp32<kHMIR>(ku)));
+        }
+        if constexpr (G == 32) {  // the frame's other row
+            const uint32_t xh = xrow32(kh), xu = xrow32(ku);
+            cmp_quad(xh, xu);
+            cmp_quad(dpp32<kHMIR>(xh), dpp32<kHMIR>(xu));
+            cmp_quad(dpp32<kRMIR>(xh), dpp32<kRMIR>(xu));
+            cmp_quad(dpp32<kRMIR>(dpp32<kHMIR>(xh)), dpp32<kRMIR>(dpp32<kHMIR>(xu)));
         }
         amb |= wmask(near) & vmask;
         const bool famb = ((amb >> gbase) & (uint64_t)GM) != 0;
@@ -554,7 +574,7 @@ hipError_t launch_lane_long(const pscl_decode_params& P, hipStream_t s) {
 int pscl_lane_long_available(const pscl_decode_params& P) {
     if (!PSCL_LANE_LONG || !P.apx || P.force || P.sc_hard || P.rm_E || P.fidx || P.d_count || P.elist) return 0;
     if (!P.info_words || !P.epi_table || P.out_by_row) return 0;
-    if (P.L != 16 && P.L != 8 && P.L != 4) return 0;
+    if (P.L != 32 && P.L != 16 && P.L != 8 && P.L != 4) return 0;
     if (P.N != 128 && P.N != 256 && P.N != 512 && P.N != 1024) return 0;
     return P.K >= __builtin_ctz((unsigned)P.L);
 }
@@ -563,8 +583,9 @@ int64_t pscl_lane_long_grid(const pscl_decode_params& P) { return lane_long_grid
 
 hipError_t pscl_launch_lane_long(const pscl_decode_params& P, hipStream_t s) {
     if (!pscl_lane_long_available(P)) return hipErrorInvalidValue;
-#define PSCL_LL(NL_) (P.L == 16 ? launch_lane_long<NL_, 16>(P, s) : P.L == 8 ? launch_lane_long<NL_, 8>(P, s) \
-                                                                   : launch_lane_long<NL_, 4>(P, s))
+#define PSCL_LL(NL_)                                                                                        \
+    (P.L == 32 ? launch_lane_long<NL_, 32>(P, s) : P.L == 16 ? launch_lane_long<NL_, 16>(P, s)                \
+                                                 : P.L == 8 ? launch_lane_long<NL_, 8>(P, s) : launch_lane_long<NL_, 4>(P, s))
     switch (P.N) {
         case 128: return PSCL_LL(7);
         case 256: return PSCL_LL(8);

@@ -1,5 +1,5 @@
 """GPU: the runtime-information-set screening decoder (csrc/scl_lane_long.hip, N = 128..1024,
-L = 4, 8 and 16)
+L = 4, 8, 16 and 32)
 against the exact long-code kernel (scl_long.hip, screening off) and the oracle.
 
 A plain decode (best bits and CRC flags only) of a long code runs the lane-per-path screening
@@ -53,7 +53,9 @@ def _screened_vs_exact(N, info, L, crc, llr):
                                           (1024, 512, 8, 6.0, 1500), (1024, 512, 4, 6.0, 1500),
                                           (256, 100, 8, 2.5, 3000), (512, 300, 8, 3.0, 1500),
                                           (256, 128, 16, 4.0, 3000), (1024, 512, 16, 6.0, 800),
-                                          (128, 64, 16, 4.0, 6000), (512, 256, 16, 5.0, 1500)])
+                                          (128, 64, 16, 4.0, 6000), (512, 256, 16, 5.0, 1500),
+                                          (128, 64, 32, 4.0, 3000), (256, 128, 32, 4.0, 1500),
+                                          (1024, 512, 32, 6.0, 400)])
 def test_lane_long_equals_exact(N, K, L, ebno, B):
     info, llr = _frames(N, K, B, ebno, seed=N * 7 + K + L)
     a, n_def = _screened_vs_exact(N, info, L, POLY, llr)
@@ -76,7 +78,7 @@ def test_lane_long_no_crc(N, L):
         np.testing.assert_array_equal(a["best_bits"][f], c[bi], err_msg=f"frame {f}")
 
 
-@pytest.mark.parametrize("N,L", [(256, 8), (512, 4), (256, 16), (128, 16)])
+@pytest.mark.parametrize("N,L", [(256, 8), (512, 4), (256, 16), (128, 16), (128, 32), (512, 32)])
 def test_lane_long_ties_and_extremes_defer(N, L):
     """Integer LLRs (exact metric ties through the stable sort), noiseless +-1 rows and rows with
     LLRs beyond 2^25 must reach the exact kernel; the outputs equal it everywhere."""
