@@ -687,16 +687,11 @@ def main():
 
     cpu = par = None
     orc = Oracle() if (rank == 0 and not args.no_cpu_baseline) else None
+    host = None
     if orc is not None:
         host = r["llr0"][: min(B, 1_000_000)].cpu().numpy()
         if E:
             host = host_internal_llrs(host[: min(host.shape[0], 100_000)], N)
-        if world == 1:
-            cpu, ref, n = cpu_baseline(orc, host, info, L, args.cpu_seconds, args.retries, beta)
-            ref = complete_ref(orc, host, ref, info, L, args.retries, beta)
-        else:  # the CPU baseline is an N = 1 figure; the step-0 parity check stays (untimed)
-            ref = orc.run(host, info, L, args.retries, beta)
-        par = parity(r["best0"], r["flags0"], ref, K, check_idx=args.retries == 0)
     r.pop("llr0", None)
     torch.cuda.empty_cache()
     extra = None
@@ -705,6 +700,17 @@ def main():
         sweep = config3_sweep(args, ctx)
         if rank == 0:
             extra["config3_sweep_L8"] = sweep
+    # the CPU legs after every timed GPU leg: the oracle's workers (one per CPU of the affinity mask,
+    # on a cgroup quota of fewer CPUs) measured to slow the host-bound legs that followed them (the
+    # config-3 sweep 281 -> 271 M frames/s, its 5 dB point 4.54 -> 4.72 ms)
+    if orc is not None:
+        if world == 1:
+            cpu, ref, n = cpu_baseline(orc, host, info, L, args.cpu_seconds, args.retries, beta)
+            ref = complete_ref(orc, host, ref, info, L, args.retries, beta)
+        else:  # the CPU baseline is an N = 1 figure; the step-0 parity check stays (untimed)
+            ref = orc.run(host, info, L, args.retries, beta)
+        par = parity(r["best0"], r["flags0"], ref, K, check_idx=args.retries == 0)
+        host = None
 
     if rank == 0:
         launches, kern_ms = r["launches"], r["kern_ms"]
