@@ -620,6 +620,9 @@ def config3_sweep(args, ctx: Ctx):
         run(4.0, 4.5, args.seed + 1, td)
         rows, total_t = run(4.0, 6.5, args.seed, td)
         rows5, t5 = run(5.0, 5.0, args.seed, td)
+    from polar_code_amd import _native
+
+    _native.release_decoders()  # (the sweep's handle and its streams: the next legs start clean)
     pts = []
     for row in rows:
         pt = {"snr_db": row["snr_db"], "frames": frames, "fer_scl": row["fer_scl"], "fer_dl": row["fer_dl"],
@@ -696,8 +699,10 @@ def main():
     torch.cuda.empty_cache()
     extra = None
     if args.extra == "auto" and not E and args.retries == 0 and L == 8:
-        extra = extra_configs(args, ctx, orc)
+        # (the sweep first: the extra configs' oracle parity checks run the oracle on every CPU of
+        # the affinity mask, after which the host-timed sweep measured ~4 % slower)
         sweep = config3_sweep(args, ctx)
+        extra = extra_configs(args, ctx, orc)
         if rank == 0:
             extra["config3_sweep_L8"] = sweep
     # the CPU legs after every timed GPU leg: the oracle's workers (one per CPU of the affinity mask,

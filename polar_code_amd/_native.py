@@ -523,6 +523,17 @@ def get_decoder(N: int, info_set, L: int, crc=None, device: int = 0, E: int = 0,
         return dec
 
 
+def release_decoders() -> None:
+    """Close every cached decoder (get_decoder): their handles, streams and device scratch go.  A
+    long-lived process that is done with a workload calls this so that the next one's streams are
+    not spread over hardware queues shared with idle ones."""
+    with _CACHE_LOCK:
+        decs = list(_CACHE.values())
+        _CACHE.clear()
+    for d in decs:
+        d.close()
+
+
 class DeviceArena:
     """Device buffers owned through the C ABI (pscl_device_alloc), freed on exit.  Lets the
     host layer drive the device path without PyTorch."""
