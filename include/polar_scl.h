@@ -317,6 +317,8 @@ int pscl_join(pscl_handle* h);
  *                           kernel (default); 2: on the two-lanes-per-path one
  *   PSCL_TUNE_DL_RETRY_LANE 2: screened retry decodes (N = 128) on the two-lanes-per-path forced-
  *                           bit instance instead of the lane-per-path one (default)
+ *   PSCL_TUNE_DL_STREAMS    0..3 (bit mask): 1 the side chain on its main chain's stream, 2 one chain
+ *                           set (consecutive calls' chains on the same streams, in call order)
  *   PSCL_TUNE_POST_PAIRS    1..32: entry pairs per wavefront the DL-SCL post pass grid is sized for
  *                           (default 2, PSCL_POST_PAIRS in dlscl.hip; capped by PSCL_TUNE_POST_GRID)
  */
@@ -330,7 +332,8 @@ int pscl_join(pscl_handle* h);
 #define PSCL_TUNE_DL_SCREEN_MIN 8
 #define PSCL_TUNE_DL_RETRY_LANE 9
 #define PSCL_TUNE_POST_PAIRS 10
-#define PSCL_TUNE_COUNT 11
+#define PSCL_TUNE_DL_STREAMS 11
+#define PSCL_TUNE_COUNT 12
 int pscl_set_tuning(pscl_handle* h, int knob, int64_t value);
 
 /*

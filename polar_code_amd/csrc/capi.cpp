@@ -766,7 +766,7 @@ int pscl_set_pipelined(pscl_handle* h, int enable) {
 int pscl_set_tuning(pscl_handle* h, int knob, int64_t value) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
     static const int64_t lim[PSCL_TUNE_COUNT][2] = {{0, 0}, {0, 2}, {0, 64}, {0, 2}, {0, 1}, {0, 4096}, {0, PSCL_MAX_WAVES_PER_WG}, {0, 2},
-                                                    {0, (int64_t)1 << 30}, {0, 2}, {0, 32}};
+                                                    {0, (int64_t)1 << 30}, {0, 2}, {0, 32}, {0, 3}};
     if (knob < 1 || knob >= PSCL_TUNE_COUNT) return fail(PSCL_EINVAL, "unknown tuning knob %d", knob);
     if (value < lim[knob][0] || value > lim[knob][1] || (knob == PSCL_TUNE_POST_GRID && value && value < 16))
         return fail(PSCL_EINVAL, "tuning knob %d: value %lld out of range", knob, (long long)value);
@@ -1110,14 +1110,17 @@ int dl_setup(pscl_handle* h, const pscl_dl_call& a, DlBufs& b) {
     const int64_t cap = a.cap;
     // chain sets: a pipelined call's chains (or an unpipelined call's chunk chains) alternate two
     const int nsets = (h->N <= PSCL_FAST_N && (a.pipe || a.nch >= 2)) ? kChainSets : 1;
+    // (only the streams of the chains this call runs: chain i of set s is stream 2 s + i, i < nsplit;
+    // every extra stream of the process shifts how the runtime spreads streams over its hardware queues)
     for (int i = 0; i < 2 * nsets; ++i)
-        if (!h->retry_stream[i]) HIP_TRY(create_priority_stream(h, &h->retry_stream[i]));
+        if (!h->retry_stream[i] && (i & 1) < (a.nsplit > 0 ? a.nsplit : 1)) HIP_TRY(create_priority_stream(h, &h->retry_stream[i]));
     for (int i = 0; i < kDlPar; ++i) {
         if (!h->ev_base[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_base[i], hipEventDisableTiming));
         if (!h->ev_retry[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_retry[i], hipEventDisableTiming));
         if (!h->ev_dl[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_dl[i], hipEventDisableTiming));
     }
     for (int i = 0; i < 2 * nsets; ++i) {
+        if ((i & 1) >= (a.nsplit > 0 ? a.nsplit : 1)) continue;
         if (!h->side_stream[i]) HIP_TRY(create_priority_stream(h, &h->side_stream[i]));
         if (!h->ev_scr[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_scr[i], hipEventDisableTiming));
         if (!h->ev_def[i]) HIP_TRY(hipEventCreateWithFlags(&h->ev_def[i], hipEventDisableTiming));
@@ -1195,6 +1198,7 @@ int dl_setup(pscl_handle* h, const pscl_dl_call& a, DlBufs& b) {
 // the chain set of chunk c: alternating by call (pipelined) or by chunk; the long codes' single
 // dense-state chain keeps set 0
 inline int dl_set(const pscl_handle* h, const pscl_dl_call& a, int64_t c) {
+    if (h->tune[PSCL_TUNE_DL_STREAMS] & 2) return 0;  // (one set: chains in call order on its streams)
     return h->N > PSCL_FAST_N ? 0 : (a.pipe ? a.pbase : (int)c) & (kChainSets - 1);
 }
 
@@ -1229,7 +1233,8 @@ int dl_chain(pscl_handle* h, const pscl_dl_call& a, const DlBufs& b, int64_t c, 
         DlState T = b.S[cs + k];
         T.act = b.act[p] + (k ? A0 : 0);
         int r2 = dl_retry_chunk(h, T, k ? A - A0 : A0, a.rounds, a.d_llr, a.d_best, a.d_flags, a.d_attempts,
-                                a.d_tried, a.tried_stride, d_cdl, h->retry_stream[cs + k], h->side_stream[cs + k],
+                                a.d_tried, a.tried_stride, d_cdl, h->retry_stream[cs + k],
+                                (h->tune[PSCL_TUNE_DL_STREAMS] & 1) ? h->retry_stream[cs + k] : h->side_stream[cs + k],
                                 h->ev_scr[cs + k], h->ev_def[cs + k], a.pipe, beside);
         if (r2) return r2;
     }
