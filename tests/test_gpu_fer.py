@@ -108,6 +108,30 @@ def test_device_retry_loop_equals_host_ranking(monkeypatch, M, retries, ebno, sc
         np.testing.assert_array_equal(dev["success"], host["success"])
 
 
+@pytest.mark.parametrize("K,M,ebno", [(100, 8, 3.0), (48, 16, 1.0)])
+def test_device_retry_loop_runtime_info_set(K, M, ebno):
+    """DL-SCL on an N = 128 code without a compiled-in kernel (its baseline screened by the runtime-
+    information-set lane kernel; exact forced-bit retry decodes) equals the
+    numpy-ranked retries frame for frame, beta = None (the checkpoints are K = 64)."""
+    from polar_code_amd.polar.polar import construct_info_set
+    from polar_code_amd.polar.crc import attach_crc
+
+    rng = np.random.default_rng(K + M)
+    info = construct_info_set(128, K)
+    B = 2000
+    msg = attach_crc(rng.integers(0, 2, size=(B, K - 24), dtype=np.int8), "0x1864CFB")
+    u = np.zeros((B, 128), np.int8)
+    u[:, info] = msg
+    from polar_code_amd.polar.polar import _polar_transform
+    var = 1.0 / (2.0 * K / 128 * 10 ** (ebno / 10))
+    llr = 2.0 * ((1.0 - 2.0 * _polar_transform(u)) + rng.normal(0, math.sqrt(var), size=(B, 128))) / var
+    dev = decode_with_retries_device(llr, info, M, 6, crc="0x1864CFB", beta=None)
+    host = decode_with_retries_batch(llr, info, M, 6, crc="0x1864CFB", beta=None)
+    assert 0.02 < (~dev["base_pass"]).mean() < 0.95
+    for k in ("tried", "attempts", "best_bits", "success"):
+        np.testing.assert_array_equal(dev[k], host[k], err_msg=k)
+
+
 def test_philox_device_and_host_dl_engines_agree(tmp_path):
     rows = {}
     for engine in ("device", "host"):
