@@ -56,8 +56,16 @@ __device__ __forceinline__ void wave_mem_fence() {
 #ifndef PSCL_LONG_WAVES_PER_EU
 #define PSCL_LONG_WAVES_PER_EU 8
 #endif
+// The history instances and L = 16 spill 6-10 VGPRs at 64 (scratch: private-memory traffic and
+// the per-queue scratch allocation at the first dispatch); they build for one wave fewer (the
+// L = 16 history instance for two)
+#ifndef PSCL_LONG_SPILL_WAVES_PER_EU
+#define PSCL_LONG_SPILL_WAVES_PER_EU 7
+#endif
 #if PSCL_LONG_WAVES_PER_EU
-#define PSCL_LONG_BOUNDS __launch_bounds__(64, PSCL_LONG_WAVES_PER_EU)
+#define PSCL_LONG_BOUNDS \
+    __launch_bounds__(64, (HIST && LMAX == 16) ? PSCL_LONG_SPILL_WAVES_PER_EU - 1 \
+                          : (HIST || LMAX == 16) ? PSCL_LONG_SPILL_WAVES_PER_EU : PSCL_LONG_WAVES_PER_EU)
 #else
 #define PSCL_LONG_BOUNDS __launch_bounds__(64)
 #endif
