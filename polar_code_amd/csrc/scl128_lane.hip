@@ -258,7 +258,10 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
                         constexpr int lo = phi - 16;
                         X3 = polar_transform16((uint32_t)((lo >= 64 ? u1 : u0) >> (lo & 63)) & 0xffffu);
                     }
-                    xs[p] = make_uint4((uint32_t)X1, (uint32_t)(X1 >> 32), X2, X3);
+                    // (X2 with X3 as the 64-bit word [X2, X2 >> 16 | X3 << 16]: bit e of X2 and bit e + 16
+                    // land on bit 31 of the two halves by one 64-bit shift, bit e of X3 is bit e + 16
+                    // of the high half)
+                    xs[p] = make_uint4((uint32_t)X1, (uint32_t)(X1 >> 32), X2, (X2 >> 16) | (X3 << 16));
                     wave_lds_fence();
                 }
                 // the depth-1 f node is the same for every path before phase 64, and depth 2 too
@@ -277,28 +280,32 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
                 for (int q0 = 0; q0 < npaths; ++q0) {
                     // lane p takes path (q0 + p) mod L: the 8 lanes' stores hit 8 distinct bank groups
                     const int q = npaths == LMAX ? ((q0 + p) & (LMAX - 1)) : q0;
-                    uint64_t x1 = 0;
-                    uint32_t x2 = 0, x3 = 0;
+                    uint64_t x1 = 0, x23 = 0;
                     if constexpr (r1 || r2 || r3) {
                         const uint4 xv = xs[q];
                         x1 = ((uint64_t)xv.y << 32) | xv.x;
-                        x2 = xv.z;
-                        x3 = xv.w;
+                        x23 = ((uint64_t)xv.w << 32) | xv.z;
                     }
                     double d3[EPL];
 #pragma unroll
                     for (int h = 0; h < EPL; ++h) {
                         const uint32_t e = (uint32_t)(p + G * h);
+                        // the g nodes' bits moved to bit 31 of a 32-bit half by 64-bit shifts, each
+                        // serving two nodes: bits e + 16 s and e + 16 s + 32 of X1 (depth 1), bits e and
+                        // e + 16 of X2 (depth 2)
+                        const uint64_t s1[2] = {r1 ? x1 << (31u - e) : 0ULL, r1 ? x1 << (15u - e) : 0ULL};
+                        const uint64_t s2w = r2 ? x23 << (31u - e) : 0ULL;
                         double d1[4];
 #pragma unroll
                         for (int m = 0; m < 4; ++m)
-                            d1[m] = r1 ? g_node_wbit(c[8 * h + m], c[8 * h + m + 4], (uint32_t)(x1 >> (32 * (m >> 1))), e + 16 * (m & 1))
+                            d1[m] = r1 ? g_node_bit31(c[8 * h + m], c[8 * h + m + 4], (uint32_t)(s1[m & 1] >> (32 * (m >> 1))))
                                        : d1l[h][m];
                         double d2[2];
 #pragma unroll
                         for (int s2 = 0; s2 < 2; ++s2)
-                            d2[s2] = shared2 ? d2s[h][s2] : (r2 ? g_node_wbit(d1[s2], d1[s2 + 2], x2, e + 16 * s2) : f_minsum(d1[s2], d1[s2 + 2]));
-                        d3[h] = r3 ? g_node_wbit(d2[0], d2[1], x3, e) : f_minsum(d2[0], d2[1]);
+                            d2[s2] = shared2 ? d2s[h][s2]
+                                             : (r2 ? g_node_bit31(d1[s2], d1[s2 + 2], (uint32_t)(s2w >> (32 * s2))) : f_minsum(d1[s2], d1[s2 + 2]));
+                        d3[h] = r3 ? g_node_wbit(d2[0], d2[1], (uint32_t)(x23 >> 32), e + 16) : f_minsum(d2[0], d2[1]);
                     }
                     // elements e_k and e_k + 8 = e_{k + EPL/2} of slot q: one pair ([8][L][2] layout)
 #pragma unroll

@@ -83,6 +83,16 @@ __device__ __forceinline__ double g_node_wbit(double a, double b, uint32_t w, ui
     return b + pscl_asf64(((uint64_t)hi << 32) | (uint32_t)ab);
 }
 
+// g(a, b, c) with c = bit 31 of w (the bit already moved there, e.g. by a 64-bit shift serving two
+// nodes): a's sign ^= w & 0x80000000 in one v_bitop3 (written out: the compiler splits it into
+// v_and + v_xor once the shift is not part of the pattern)
+__device__ __forceinline__ double g_node_bit31(double a, double b, uint32_t w) {
+    const uint64_t ab = pscl_asu64(a);
+    uint32_t hi;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6c" : "=v"(hi) : "v"(w), "v"((uint32_t)(ab >> 32)), "s"(0x80000000u));
+    return b + pscl_asf64(((uint64_t)hi << 32) | (uint32_t)ab);
+}
+
 // max(-v, 0): the part of np.logaddexp(0, -v) beyond the shared tail (bit 0 pays |v| when
 // v < 0); one v_max_f64 with the negation as a source modifier (fmax would canonicalise)
 __device__ __forceinline__ double relu_neg(double v) {
