@@ -88,7 +88,7 @@ struct Layout128 {
     static constexpr int OFF4 = OFF3 + 16 * LMAX;   // [4][LMAX][2]
     static constexpr int OFF5 = OFF4 + 8 * LMAX;    // [2][LMAX][2]
     static constexpr int OFF6 = OFF5 + 4 * LMAX;    // [1][LMAX][2]
-    // the paths' left-sibling partial sums {X1 lo, X1 hi, X2, X3} at a depth-1..3 recompute,
+    // the paths' left-sibling partial sums {X1 lo, X1 hi, X2, X2 >> 16 | X3 << 16} at a depth-1..3 recompute,
     // 16 B per path: every lane reads them for all paths with ds_read_b128
     static constexpr int OFFX = OFF6 + 2 * LMAX;
     // doubles per frame, padded to 256 B: the frames of a wave then start on bank 0.  (With 8-lane
@@ -474,7 +474,9 @@ scl128_kernel(const pscl_decode_params P) {
                     // the path it works on (one ds_read_b128 instead of four ds_bpermute)
                     uint4* xs_lds = reinterpret_cast<uint4*>(Af + Ly::OFFX);
                     if (q == 0 && (r1 || r2 || r3)) {
-                        if (path_lane) xs_lds[g] = make_uint4((uint32_t)X1, (uint32_t)(X1 >> 32), X2, X3);
+                        // (X2 beside X2 >> 16 | X3 << 16: one 64-bit shift brings bits e and e + 16 of X2
+                        // to bit 31 of the two halves -- scl128_lane.hip's recompute)
+                        if (path_lane) xs_lds[g] = make_uint4((uint32_t)X1, (uint32_t)(X1 >> 32), X2, (X2 >> 16) | (X3 << 16));
                         wave_lds_fence();
                     }
                     // left-left quarter (phi = 0, 16): depth 2 = f(depth 1) is the same for every path
@@ -491,25 +493,25 @@ scl128_kernel(const pscl_decode_params P) {
                         // then store to 16 distinct bank pairs (the same path for every lane put
                         // the 16 stores on 2 bank pairs: 8-way conflicts)
                         const int p = npaths == LMAX ? (p0 + e) & (LMAX - 1) : p0;
-                        uint64_t x1 = 0;
-                        uint32_t x2 = 0, x3 = 0;
+                        uint64_t x1 = 0, x23 = 0;
                         if (r1 || r2 || r3) {
                             const uint4 xv = xs_lds[p];
                             x1 = ((uint64_t)xv.y << 32) | xv.x;
-                            x2 = xv.z;
-                            x3 = xv.w;
+                            x23 = ((uint64_t)xv.w << 32) | xv.z;
                         }
+                        // the g nodes' bits at bit 31 of a half of a 64-bit shift (two nodes per shift)
+                        const uint64_t s1[2] = {r1 ? x1 << (31u - (uint32_t)e) : 0ULL, r1 ? x1 << (15u - (uint32_t)e) : 0ULL};
+                        const uint64_t s2w = r2 ? x23 << (31u - (uint32_t)e) : 0ULL;
                         double d1[4];
 #pragma unroll
                         for (int m = 0; m < 4; ++m)
-                            d1[m] = r1 ? g_node_wbit(c[m], c[m + 4], (uint32_t)(x1 >> (32 * (m >> 1))), (uint32_t)(e + 16 * (m & 1)))
-                                       : d1l[m];
+                            d1[m] = r1 ? g_node_bit31(c[m], c[m + 4], (uint32_t)(s1[m & 1] >> (32 * (m >> 1)))) : d1l[m];
                         double d2[2];
 #pragma unroll
                         for (int s2 = 0; s2 < 2; ++s2)
                             d2[s2] = shared2 ? d2s[s2]
-                                     : (r2 ? g_node_wbit(d1[s2], d1[s2 + 2], x2, (uint32_t)(e + 16 * s2)) : f_minsum(d1[s2], d1[s2 + 2]));
-                        const double d3 = r3 ? g_node_wbit(d2[0], d2[1], x3, (uint32_t)e) : f_minsum(d2[0], d2[1]);
+                                     : (r2 ? g_node_bit31(d1[s2], d1[s2 + 2], (uint32_t)(s2w >> (32 * s2))) : f_minsum(d1[s2], d1[s2 + 2]));
+                        const double d3 = r3 ? g_node_wbit(d2[0], d2[1], (uint32_t)(x23 >> 32), (uint32_t)e + 16u) : f_minsum(d2[0], d2[1]);
                         Af[Ly::OFF3 + Ly::at(16, e, p)] = d3;
                     }
                 }

@@ -79,6 +79,27 @@ __device__ __forceinline__ uint64_t uword(const uint64_t (&u)[NW], int k) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// the bits of NV g nodes of element e (node m: bit e + 16 (m & 1) of word wb[m >> 1]) moved to bit 31
+// of o[m]: one 64-bit shift of a word pair serves two nodes (bit e of words 2k and 2k + 1, or bit
+// e + 16), for g_node_bit31 -- half the shifts of g_node_wbit
+template <int NV>
+__device__ __forceinline__ void bits31(const uint32_t* wb, uint32_t e, uint32_t (&o)[NV]) {
+    if constexpr (NV >= 4) {
+#pragma unroll
+        for (int k = 0; k < NV / 4; ++k) {
+            const uint64_t pr = ((uint64_t)wb[2 * k + 1] << 32) | wb[2 * k];
+            const uint64_t a = pr << (31u - e), c = pr << (15u - e);
+            o[4 * k] = (uint32_t)a;
+            o[4 * k + 1] = (uint32_t)c;
+            o[4 * k + 2] = (uint32_t)(a >> 32);
+            o[4 * k + 3] = (uint32_t)(c >> 32);
+        }
+    } else {
+#pragma unroll
+        for (int m = 0; m < NV; ++m) o[m] = wb[m >> 1] << (31u - e - 16u * (m & 1));
+    }
+}
+
 template <int NL, int LMAX>
 __global__ void __launch_bounds__(64, (NL == 10 || (NL == 9 && LMAX >= 16)) ? PSCL_LANE_LONG1024_WAVES_PER_EU
                                                                            : PSCL_LANE_LONG_WAVES_PER_EU)
@@ -218,9 +239,10 @@ __global__ void __launch_bounds__(64, (NL == 10 || (NL == 9 && LMAX >= 16)) ? PS
                                 constexpr int l = 3 + decltype(LI)::value;
                                 constexpr int nl = CE >> l;  // values per element at depth l
                                 if ((b >> (R - l)) & 1) {
+                                    uint32_t o[nl];
+                                    bits31<nl>(xq + Ly::template xoff<l>, e, o);
 #pragma unroll
-                                    for (int m = 0; m < nl; ++m)
-                                        v[m] = g_node_wbit(v[m], v[m + nl], xq[Ly::template xoff<l> + (m >> 1)], e + 16 * (m & 1));
+                                    for (int m = 0; m < nl; ++m) v[m] = g_node_bit31(v[m], v[m + nl], o[m]);
                                 } else {
 #pragma unroll
                                     for (int m = 0; m < nl; ++m) v[m] = f_minsum(v[m], v[m + nl]);
@@ -258,9 +280,10 @@ __global__ void __launch_bounds__(64, (NL == 10 || (NL == 9 && LMAX >= 16)) ? PS
                         for (int m = 0; m < CE / 2; ++m) v1s[m] = f_minsum(ch[m], ch[m + CE / 2]);
                         if (r2)
                             paths([&](const uint32_t* xq, double* v) {
+                                uint32_t o[CE / 4];
+                                bits31<CE / 4>(xq + Ly::template xoff<2>, e, o);
 #pragma unroll
-                                for (int m = 0; m < CE / 4; ++m)
-                                    v[m] = g_node_wbit(v1s[m], v1s[m + CE / 4], xq[Ly::template xoff<2> + (m >> 1)], e + 16 * (m & 1));
+                                for (int m = 0; m < CE / 4; ++m) v[m] = g_node_bit31(v1s[m], v1s[m + CE / 4], o[m]);
                             });
                         else
                             paths([&](const uint32_t* xq, double* v) {
@@ -269,19 +292,21 @@ __global__ void __launch_bounds__(64, (NL == 10 || (NL == 9 && LMAX >= 16)) ? PS
                             });
                     } else {
                         // depths 1 and 2 together from the channel (depth-1 pair (m, m + CE/4))
-                        auto d1 = [&](const uint32_t* xq, int m) {
-                            return g_node_wbit(ch[m], ch[m + CE / 2], xq[Ly::template xoff<1> + (m >> 1)], e + 16 * (m & 1));
-                        };
+                        auto d1 = [&](const uint32_t (&o1)[CE / 2], int m) { return g_node_bit31(ch[m], ch[m + CE / 2], o1[m]); };
                         if (r2)
                             paths([&](const uint32_t* xq, double* v) {
+                                uint32_t o1[CE / 2], o2[CE / 4];
+                                bits31<CE / 2>(xq + Ly::template xoff<1>, e, o1);
+                                bits31<CE / 4>(xq + Ly::template xoff<2>, e, o2);
 #pragma unroll
-                                for (int m = 0; m < CE / 4; ++m)
-                                    v[m] = g_node_wbit(d1(xq, m), d1(xq, m + CE / 4), xq[Ly::template xoff<2> + (m >> 1)], e + 16 * (m & 1));
+                                for (int m = 0; m < CE / 4; ++m) v[m] = g_node_bit31(d1(o1, m), d1(o1, m + CE / 4), o2[m]);
                             });
                         else
                             paths([&](const uint32_t* xq, double* v) {
+                                uint32_t o1[CE / 2];
+                                bits31<CE / 2>(xq + Ly::template xoff<1>, e, o1);
 #pragma unroll
-                                for (int m = 0; m < CE / 4; ++m) v[m] = f_minsum(d1(xq, m), d1(xq, m + CE / 4));
+                                for (int m = 0; m < CE / 4; ++m) v[m] = f_minsum(d1(o1, m), d1(o1, m + CE / 4));
                             });
                     }
                 };
