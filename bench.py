@@ -471,8 +471,8 @@ def extra_configs(args, ctx: Ctx, orc: Oracle | None):
                           "scl_lane_kernel<4> baseline + retry rounds beside the next step's baseline: scl_lane_kernel<4,FS>"
                           " screened warm-started retry decodes, scl128_kernel<4,FS> exact decodes of the deferred entries"
                           " (side chain), dl_post_kernel" if name.startswith("config4") else
-                          "scl128_kernel<8,CH,CODE=2> screening (de-rate-match in staging) + exact re-decode"
-                          " (pipelined)"),
+                          "scl_lane_kernel<8,NR> screening (de-rate-match as the rows are loaded) +"
+                          " scl128_kernel<8,CH,CODE=2> exact re-decode (pipelined)"),
                "kernel_timing": ("HIP events around each decode launch: main stream = the screening (plain) or "
                                  "baseline (DL-SCL) decode of each step; side streams = DL-SCL retry decodes, "
                                  "which overlap the main stream (the sums are not additive in wall time)"),
@@ -577,11 +577,12 @@ def launch_ranks(n: int) -> int:
 def dominant_kernel(N, K, L, E, retries):
     """The kernel the step's dominant launch runs (pscl_launch_decode's choice for a plain or
     DL-SCL baseline decode of this configuration)."""
-    if N == 128 and K == 64 and not E and L in (4, 8):
-        return f"scl_lane_kernel<{L}> screening pass" + (" (DL-SCL baseline)" if retries else "")
-    if N == 128 and L <= 8:
+    if N == 128 and L in (4, 8) and ((K == 64 and not E) or (K == 88 and E)):  # (pscl_lane_available)
+        return (f"scl_lane_kernel<{L}{'' if K == 64 else ',NR'}> screening pass"
+                + (" (DL-SCL baseline)" if retries else ""))
+    if N == 128 and L <= 8 and (E or retries):
         return f"scl128_kernel<{L}> " + ("baseline decode" if retries else "screening pass")
-    if N > 128 and L in (4, 8) and not E and not retries:
+    if L in (4, 8, 16, 32) and not E and not retries:  # (any other information set, N = 128..1024)
         return f"scl_lane_long_kernel<N={N},{L}> screening pass"
     return "scl_long_kernel" if N > 128 else "scl_decode_kernel"
 
