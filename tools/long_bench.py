@@ -81,9 +81,14 @@ if "--dl" in sys.argv:
     sys.exit(0)
 # (N = 128, K = 100, and every L = 16 / 32 decode: the runtime-information-set lane kernel -- no
 # compiled-in screening kernel -- timed against the exact kernel alone too)
-for N, K, L, B, snr in [(128, 100, 8, 500_000, 4.5), (256, 128, 8, 200_000, 4.0), (512, 256, 8, 100_000, 5.0),
-                        (1024, 512, 8, 50_000, 6.0), (128, 64, 16, 200_000, 4.0), (256, 128, 16, 100_000, 4.0),
-                        (1024, 512, 16, 20_000, 6.0), (128, 64, 32, 100_000, 4.0), (1024, 512, 32, 20_000, 6.0)]:
+CASES = [(128, 100, 8, 500_000, 4.5), (256, 128, 8, 200_000, 4.0), (512, 256, 8, 100_000, 5.0),
+         (1024, 512, 8, 50_000, 6.0), (128, 64, 16, 200_000, 4.0), (256, 128, 16, 100_000, 4.0),
+         (1024, 512, 16, 20_000, 6.0), (128, 64, 32, 100_000, 4.0), (1024, 512, 32, 20_000, 6.0)]
+# --big: the N = 1024 rows at 4x the batch (the 50 000-frame batch at L = 8 is 6.1 waves per SIMD
+# slot: its last wave round runs a tenth full)
+if "--big" in sys.argv:
+    CASES = [(1024, 512, 8, 200_000, 6.0), (1024, 512, 16, 80_000, 6.0), (1024, 512, 32, 80_000, 6.0)]
+for N, K, L, B, snr in CASES:
     rng = np.random.default_rng(N + L)
     info = construct_info_set(N, K)
     msg = attach_crc(rng.integers(0, 2, size=(B, K - 24), dtype=np.int8), POLY)
