@@ -49,6 +49,12 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 POLY = "0x1864CFB"
 # reference CRC-fail frame errors out of 2000 at 5 dB, seed 0 (results/fer_M{8,4}.csv:2)
 REF_ERRS = {("scl", 8): 26, ("dl", 8): 20, ("scl", 4): 91, ("dl", 4): 71}
+# multi-rank bounds: the process group's own timeout (a rank that never joins fails the others'
+# init and collectives instead of hanging to the library default), and launch_ranks' watchdog --
+# no rank finishing a stage for this long ends the job (the first `import torch` on a fresh box
+# takes 1-2 minutes; the longest stage, the oracle legs on rank 0, well under one)
+PG_TIMEOUT_S = 600
+RANK_STALL_S = 480.0
 
 # VALU issue peak of MI355X per instruction class (MI355X_MICROARCH.md, constants table):
 # 256 CUs x 4 SIMD-32 at 2.4 GHz; a wave64 instruction takes 2 SIMD cycles (fp32/int/logic,
@@ -67,7 +73,7 @@ def parse():
     ap.add_argument("--list", type=int, default=8)
     ap.add_argument("--ebno", type=float, default=5.0)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=16.0, help="budget for the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--retries", type=int, default=0,
                     help="DL-SCL flip retries per CRC-failing frame (BASELINE config 4: --list 4 --retries 8)")
@@ -232,37 +238,56 @@ def _timed_sample(fn, n0: int, n_max: int, budget_s: float):
 
 def cpu_baseline(orc: Oracle, llr_host: np.ndarray, info, L: int, budget_s: float, retries: int = 0, beta=None,
                  product_s: float = 6.0):
-    """The oracle timed on the host cores on a bounded sample of the step-0 batch, with one OpenMP
-    thread per CPU of this process's affinity mask (P = the host's usable CPUs), and
-    beside it the product's own host decoder (pscl_decode_cpu, csrc/scl_cpu.cpp) on the same
-    threads.  Returns the baseline record and the oracle's outputs for the first pass (kept for the
-    parity check)."""
+    """The oracle timed on the host cores on a bounded sample of the step-0 batch, OpenMP over
+    frames, at two thread counts: one per CPU of this process's affinity mask (P = the
+    host's usable CPUs) and one per CPU of its cgroup CPU quota (rounded up) when that is fewer --
+    more threads than the quota only time-slice (a 256-CPU mask on a 16-CPU quota measured 1.9x
+    below the 16-thread figure).  `value` is the faster leg, with its `threads_used`; both legs are
+    kept in `legs`.  Beside it the product's own host decoder (pscl_decode_cpu,
+    csrc/scl_cpu.cpp) at the winning thread count.  Returns the baseline record and the oracle's
+    outputs for the first pass of the larger sample (kept for the parity check)."""
     try:
         aff = sorted(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         aff = None
-    P = len(aff) if aff else (os.cpu_count() or 1)
-    orc.o.set_num_threads(P)
-    n0 = min(max(4000, 8 * P), llr_host.shape[0])
-    done, dt, n, first = _timed_sample(lambda k: orc.run(llr_host[:k], info, L, retries, beta), n0,
-                                       llr_host.shape[0], budget_s)
+    P_aff = len(aff) if aff else (os.cpu_count() or 1)
+    quota = _cpu_quota()
+    Ps = [P_aff]
+    if quota and int(math.ceil(quota)) < P_aff:
+        Ps.append(max(1, int(math.ceil(quota))))
     what = (f"decode_with_retries (SCL L={L} + up to {retries} flips, beta)" if retries > 0
             else f"decode_scl L={L} + CRC select")
-    quota = _cpu_quota()
-    rec = {"value": done / dt, "unit": "frames/s", "cores": orc.o.num_threads(), "kind": "port",
-           "threads_used": orc.o.num_threads(), "host_cpu_count": os.cpu_count(),
+    legs, best, keep = [], None, None
+    for P in Ps:
+        orc.o.set_num_threads(P)
+        n0 = min(max(4000, 8 * P), llr_host.shape[0])
+        done, dt, n, first = _timed_sample(lambda k: orc.run(llr_host[:k], info, L, retries, beta), n0,
+                                           llr_host.shape[0], budget_s / len(Ps))
+        leg = {"value": done / dt, "threads_used": orc.o.num_threads(), "per_thread": done / dt / max(orc.o.num_threads(), 1),
+               "why": "one per CPU of the affinity mask" if P == P_aff else "one per CPU of the cgroup quota (ceil)",
+               "sample": f"{done} frames ({n} distinct), {dt:.1f} s"}
+        legs.append(leg)
+        if best is None or leg["value"] > best["value"]:
+            best = leg
+        if keep is None or n > keep[1]:
+            keep = (first, n)
+    rec = {"value": best["value"], "unit": "frames/s", "cores": best["threads_used"], "kind": "port",
+           "threads_used": best["threads_used"], "host_cpu_count": os.cpu_count(),
            "affinity_cpus": len(aff) if aff is not None else None,
            "affinity_mask": _cpu_ranges(aff) if aff is not None else None,
            "cgroup_cpu_quota": quota,
-           "per_thread": done / dt / max(orc.o.num_threads(), 1),
-           "per_quota_cpu": done / dt / quota if quota else None,
-           "sample": f"{done} frames ({n} distinct frames of the step-0 batch, same LLRs as the GPU) through "
-                     f"oracle/scl_oracle.c (C restatement of {what}), OpenMP over frames, {P} threads "
-                     f"(one per CPU of the affinity mask), {dt:.1f} s"}
+           "per_thread": best["per_thread"],
+           "per_quota_cpu": best["value"] / quota if quota else None,
+           "legs": legs,
+           "sample": f"{best['sample']} of the step-0 batch (same LLRs as the GPU) through oracle/scl_oracle.c "
+                     f"(C restatement of {what}), OpenMP over frames, {best['threads_used']} threads ({best['why']}; "
+                     f"the faster of {len(legs)} thread count(s), see legs)"}
+    P = best["threads_used"]
     if retries == 0:  # the product's own host decoder (no DL-SCL loop on the host path)
         try:
             from polar_code_amd import _native
 
+            n0 = min(max(4000, 8 * P), llr_host.shape[0])
             cdec = _native.CpuDecoder(llr_host.shape[1], info, L, POLY, threads=P)
             pdone, pdt, pn, _ = _timed_sample(
                 lambda k: cdec.decode(llr_host[:k], want_metrics=False, want_cands=False, want_info_llrs=False),
@@ -273,7 +298,7 @@ def cpu_baseline(orc: Oracle, llr_host: np.ndarray, info, L: int, budget_s: floa
                           f"product's host decoder, bit-exact), std::thread over frames, {pdt:.1f} s"}
         except Exception as ex:  # reported, never fatal to the GPU line
             rec["product_cpu_decoder"] = {"error": str(ex)}
-    return rec, first, n
+    return rec, keep[0], keep[1]
 
 
 def complete_ref(orc: Oracle, host: np.ndarray, ref, info, L: int, retries: int, beta):
@@ -457,6 +482,7 @@ def extra_configs(args, ctx: Ctx, orc: Oracle | None):
         beta = np.load(ROOT / "tests" / "golden" / "beta_M4.npy") if kw["retries"] else None
         r = run_workload(ctx, **kw, beta=beta, B=args.frames, steps=args.extra_steps, warmup=2, ebno=args.ebno,
                          seed=args.seed, keep_buffers=orc is not None)
+        heartbeat(name)
         if ctx.rank != 0:
             continue
         c, cdl = r["c"], r["cdl"]
@@ -537,14 +563,43 @@ def launch_ranks(n: int) -> int:
     import signal
     import subprocess
 
+    import tempfile
+
     port = free_port()
+    hb_dir = tempfile.mkdtemp(prefix="pscl_bench_hb_")
+    stall_s = float(os.environ.get("PSCL_RANK_STALL_S", str(RANK_STALL_S)))
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PSCL_BENCH_CHILD="1")
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PSCL_BENCH_CHILD="1",
+                   PSCL_BENCH_HEARTBEAT=hb_dir)
         procs.append(subprocess.Popen([sys.executable, "-u", str(Path(__file__).resolve()), *sys.argv[1:]],
                                       env=env, stdout=None if r == 0 else subprocess.DEVNULL))
     rcs = [None] * n
+    t_launch = time.time()
+
+    def last_progress() -> float:
+        """Newest heartbeat of any rank (heartbeat(): one per finished stage), else the launch."""
+        t = t_launch
+        for f in Path(hb_dir).glob("rank*"):
+            try:
+                t = max(t, f.stat().st_mtime)
+            except OSError:
+                pass
+        return t
+
+    def stop_all():
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                p.send_signal(signal.SIGTERM)
+        for i, p in enumerate(procs):
+            try:
+                rcs[i] = p.wait(timeout=30) if rcs[i] is None else rcs[i]
+            except subprocess.TimeoutExpired:
+                p.kill()
+                rcs[i] = p.wait()
+
+    stalled = False
     try:
         while any(rc is None for rc in rcs):
             for i, p in enumerate(procs):
@@ -552,26 +607,43 @@ def launch_ranks(n: int) -> int:
                     rcs[i] = p.poll()
             bad = [i for i, rc in enumerate(rcs) if rc not in (None, 0)]
             if bad:  # one rank failed: the others would wait in a collective forever
-                for i, p in enumerate(procs):
-                    if rcs[i] is None:
-                        p.send_signal(signal.SIGTERM)
-                for i, p in enumerate(procs):
-                    try:
-                        rcs[i] = p.wait(timeout=30) if rcs[i] is None else rcs[i]
-                    except subprocess.TimeoutExpired:
-                        p.kill()
-                        rcs[i] = p.wait()
+                stop_all()
+                break
+            # no rank finished a stage within the bound: a rank that never joined the process group
+            # (or hangs in a collective) holds every other one in a collective -- end the job
+            if any(rc is None for rc in rcs) and time.time() - last_progress() > stall_s:
+                stalled = True
+                stop_all()
                 break
             time.sleep(0.2)
     except KeyboardInterrupt:
         for p in procs:
             p.kill()
         raise
+    finally:
+        import shutil
+
+        shutil.rmtree(hb_dir, ignore_errors=True)
+    if stalled:
+        sys.stderr.write(f"bench.py: no rank progressed for {stall_s:g} s (PSCL_RANK_STALL_S); ranks stopped: "
+                         f"{rcs}\n")
+        return 1
     failed = [(i, rc) for i, rc in enumerate(rcs) if rc != 0]
     if failed:
         sys.stderr.write(f"bench.py: rank(s) failed: {failed}\n")
         return 1
     return 0
+
+
+def heartbeat(stage: str) -> None:
+    """A rank finished a stage: touch its heartbeat file for launch_ranks' stall watchdog (no-op
+    outside bench.py's own launcher)."""
+    d = os.environ.get("PSCL_BENCH_HEARTBEAT")
+    if d:
+        try:
+            Path(d, f"rank{os.environ.get('RANK', '0')}").write_text(f"{time.time():.3f} {stage}\n")
+        except OSError:
+            pass
 
 
 def dominant_kernel(N, K, L, E, retries):
@@ -658,24 +730,39 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (one rank per GPU)")
+    if os.environ.get("PSCL_BENCH_STALL_RANK") == str(rank):  # (test hook: a rank that never joins)
+        time.sleep(1e6)
+    import datetime
+
     import torch
 
-    # one process per GPU; PSCL_SHARE_GPU=1 lets a rehearsal put several ranks on fewer GPUs
-    ndev = torch.cuda.device_count()
-    device_index = local % ndev if os.environ.get("PSCL_SHARE_GPU") == "1" else local
-    torch.cuda.set_device(device_index)
-    dev = torch.device("cuda", device_index)
+    # PSCL_BENCH_DIST_ONLY=1 (launcher tests on CPU): the process group and one barrier, no GPU
+    dist_only = os.environ.get("PSCL_BENCH_DIST_ONLY") == "1"
+    dev, device_index = None, 0
+    if not dist_only:
+        # one process per GPU; PSCL_SHARE_GPU=1 lets a rehearsal put several ranks on fewer GPUs
+        ndev = torch.cuda.device_count()
+        device_index = local % ndev if os.environ.get("PSCL_SHARE_GPU") == "1" else local
+        torch.cuda.set_device(device_index)
+        dev = torch.device("cuda", device_index)
     dist = None
     # a process group under any launcher, world 1 included (the RCCL collectives then run on one
     # GPU exactly as on eight); none for a plain `python bench.py`
     if world > 1 or ("MASTER_ADDR" in os.environ and "WORLD_SIZE" in os.environ):
         import torch.distributed as dist
 
-        backend = os.environ.get("PSCL_DIST_BACKEND", "nccl")  # nccl == RCCL over xGMI
+        backend = os.environ.get("PSCL_DIST_BACKEND", "gloo" if dist_only else "nccl")  # nccl == RCCL over xGMI
+        timeout = datetime.timedelta(seconds=float(os.environ.get("PSCL_PG_TIMEOUT_S", str(PG_TIMEOUT_S))))
         if backend == "nccl":
-            dist.init_process_group(backend="nccl", device_id=dev)
+            dist.init_process_group(backend="nccl", device_id=dev, timeout=timeout)
         else:
-            dist.init_process_group(backend=backend)
+            dist.init_process_group(backend=backend, timeout=timeout)
+        heartbeat("process group")
+    if dist_only:
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     ctx = Ctx(torch, dev, device_index, dist, rank, world)
 
     E, L, B = args.nr_E, args.list, args.frames
@@ -685,6 +772,7 @@ def main():
         beta = np.load(bp) if bp.exists() else None
     r = run_workload(ctx, L=L, E=E, retries=args.retries, beta=beta, B=B, steps=args.steps, warmup=args.warmup,
                      ebno=args.ebno, seed=args.seed, keep_buffers=(rank == 0))
+    heartbeat("headline")
     N, K, W, n_in, info, kp = r["N"], r["K"], r["W"], r["n_in"], r["info"], r["kp"]
     c, cdl, elapsed = r["c"], r["cdl"], r["elapsed"]
     frames_total = B * args.steps * world
@@ -703,7 +791,9 @@ def main():
         # (the sweep first: the extra configs' oracle parity checks run the oracle on every CPU of
         # the affinity mask, after which the host-timed sweep measured ~4 % slower)
         sweep = config3_sweep(args, ctx)
+        heartbeat("config3 sweep")
         extra = extra_configs(args, ctx, orc)
+        heartbeat("extra configs")
         if rank == 0:
             extra["config3_sweep_L8"] = sweep
     # the CPU legs after every timed GPU leg: the oracle's workers (one per CPU of the affinity mask,
@@ -717,6 +807,7 @@ def main():
             ref = orc.run(host, info, L, args.retries, beta)
         par = parity(r["best0"], r["flags0"], ref, K, check_idx=args.retries == 0)
         host = None
+        heartbeat("cpu baseline + parity")
 
     if rank == 0:
         launches, kern_ms = r["launches"], r["kern_ms"]

@@ -206,7 +206,7 @@ class Decoder:
         h = _vp()
         check(lib().pscl_create(C.byref(h), self.device, self.N, info.ctypes.data_as(C.POINTER(_i32)), self.K,
                                 self.L, self.crc_poly))
-        self._h = h
+        self._hraw = h
         self._lock = threading.Lock()
         self.E = 0
         self._beta = None
@@ -217,13 +217,24 @@ class Decoder:
         self.E = int(E)
 
     @property
+    def _h(self):
+        h = getattr(self, "_hraw", None)
+        if h is None:
+            raise RuntimeError("Decoder is closed (close(), or release_decoders() on a get_decoder() handle)")
+        return h
+
+    @property
     def handle(self):
         return self._h
 
+    @property
+    def closed(self) -> bool:
+        return getattr(self, "_hraw", None) is None
+
     def close(self) -> None:
-        if getattr(self, "_h", None):
-            lib().pscl_destroy(self._h)
-            self._h = None
+        if getattr(self, "_hraw", None):
+            lib().pscl_destroy(self._hraw)
+            self._hraw = None
 
     def __del__(self):
         try:
@@ -395,8 +406,12 @@ class Decoder:
     def set_pipelined(self, on: bool = True, depth: int = 2) -> None:
         """Throughput mode for streams of plain decodes (include/polar_scl.h): a screening
         decode's exact re-decode overlaps the next decode; join() / sync() order it back.  depth
-        (2..4): a DL-SCL call's buffers are free again at the depth-th following call."""
-        check(lib().pscl_set_pipelined(self._h, (depth if depth > 2 else 1) if on else 0))
+        (1..4): a DL-SCL call's buffers are free again at the depth-th following call -- at the
+        second at the earliest, so depth 1 behaves as 2 (a call's chains always overlap the next
+        call's baseline)."""
+        if not 1 <= int(depth) <= 4:
+            raise ValueError(f"pipelined depth must be 1..4 (got {depth})")
+        check(lib().pscl_set_pipelined(self._h, (int(depth) if depth > 2 else 1) if on else 0))
 
     def join(self) -> None:
         """Order pending pipelined work into the handle's stream: the plain decodes' re-decodes
@@ -526,7 +541,9 @@ def get_decoder(N: int, info_set, L: int, crc=None, device: int = 0, E: int = 0,
 def release_decoders() -> None:
     """Close every cached decoder (get_decoder): their handles, streams and device scratch go.  A
     long-lived process that is done with a workload calls this so that the next one's streams are
-    not spread over hardware queues shared with idle ones."""
+    not spread over hardware queues shared with idle ones.  Every Decoder an earlier get_decoder()
+    returned is closed too (flip.decode_with_retries_device and the sweeps share them): using one
+    afterwards raises RuntimeError; call get_decoder() again for a fresh handle."""
     with _CACHE_LOCK:
         decs = list(_CACHE.values())
         _CACHE.clear()

@@ -1324,8 +1324,13 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
     if (a.pipe) {
         // the chains of the call dl_back calls back may still write their call's outputs (and, kDlPar
         // back, read this parity's compaction output): they end before this call starts (the
-        // contract of pscl_set_pipelined: a call's buffers are free again at the second following
-        // call; the chains run in call order, so the later call's end covers the earlier one's)
+        // contract of pscl_set_pipelined: a call's buffers are free again at the dl_back-th following
+        // call).  Consecutive calls' chains run concurrently (two chain sets, dl_set), so one call's
+        // end does not cover another's; the invariant is by induction instead: every call makes the
+        // handle's stream wait for the chains dl_back calls back (ev_dl, here), so any call further
+        // back was already waited for by an earlier call; and calls whose pbase has the same parity
+        // share one set's streams and DlState, which stream order keeps apart.
+        // (PSCL_TUNE_DL_STREAMS bit 2 collapses everything to one set: chains then run in call order.)
         const int q = (a.pbase + kDlPar - h->dl_back) % kDlPar;
         if (h->dl_pending[q]) {
             HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_dl[q], 0));
@@ -1677,14 +1682,15 @@ int pscl_channel_device(pscl_handle* h, uint64_t seed, uint32_t stream_id, doubl
 int pscl_set_rate_match(pscl_handle* h, int E) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
     if (E < 0) return fail(PSCL_EINVAL, "E must be >= 0");
-    if (E == 0) {
-        h->rm_E = 0;
-        return PSCL_OK;
-    }
-    if (E > h->N && h->N < 32)
+    if (E > 0 && E > h->N && h->N < 32)
         return fail(PSCL_EUNSUP, "repetition (E > N) needs N >= 32 (sub-block interleaver without padding)");
-    // (the interleaver tables depend on N only: uploaded by pscl_create; later launches read rm_E
-    // from their parameter block, so switching it never races with enqueued work)
+    if (E == h->rm_E) return PSCL_OK;
+    // (the interleaver tables depend on N only: uploaded by pscl_create; enqueued launches carry
+    // rm_E in their parameter block.  A pipelined DL-SCL call's retry chains are not enqueued yet --
+    // they are built from the handle at the next call or join -- so they are enqueued here first,
+    // with the rate matching their call's LLR rows were written for)
+    const int rc = enter(h);
+    if (rc) return rc;
     h->rm_E = E;
     return PSCL_OK;
 }

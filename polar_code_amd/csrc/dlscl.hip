@@ -565,14 +565,22 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
                     // per term, i.e. 2^-24 S + 2^-150 ||L0||_1 (2 % slack on the doubled bound)
                     const double gk = (4.0 * (double)K + 8.0) * 0x1p-53;
                     // packed fp32 sums: |L0| and beta each rounded to fp32 (u = 2^-24 relative per
-                    // factor), K fp32 fma roundings (gamma_K), the exact sums' own gamma_K (fp64):
-                    // |q32 - q_exact| <= ((K + 2.01) 2^-24 + gk / 2) S + K 2^-149 (fp32 underflow);
-                    // doubled, 2 % slack.  A non-finite or huge ||L0||_1 (fp32 overflow) leaves the
-                    // certificate false: the exact sums decide
+                    // factor, plus 2^-150 absolute where the value lands in fp32's subnormal range),
+                    // K fp32 fma roundings (gamma_K, plus 2^-149 each in the subnormal range), the
+                    // exact sums' own gamma_K (fp64):
+                    //   |q32 - q_exact| <= ((K + 2.01) 2^-24 + gk / 2) S + K 2^-149
+                    //                      + ||L0||_1 2^-150 + K max|beta| 2^-150
+                    // (S <= ||L0||_1 max|beta|; the last two terms: a subnormal beta32 or |L0|32 times
+                    // the other factor, summed over k); doubled, 2 % slack.  Trusted only when every
+                    // |L0_k| and product is far inside fp32 range (||L0||_1 < 2^100 and ||L0||_1
+                    // max|beta| < 2^100): a larger, infinite or NaN ||L0||_1 (an fp32 copy of inf, and
+                    // inf * 0 = NaN sums) leaves the certificate false and the exact sums decide
                     const double e2 = (PK && beta_lds == 2)
-                                          ? (as * Q.beta_absmax < 0x1p100 ? 2.04 * (as * Q.beta_absmax * (((double)K + 2.01) * 0x1p-24 + 0.5 * gk)
-                                                                    + (double)K * 0x1p-149)
-                                                          : __builtin_inf())
+                                          ? ((as < 0x1p100 && as * Q.beta_absmax < 0x1p100)
+                                                 ? 2.04 * (as * Q.beta_absmax * (((double)K + 2.01) * 0x1p-24 + 0.5 * gk)
+                                                           + (double)K * 0x1p-149 + as * 0x1p-150
+                                                           + (double)K * Q.beta_absmax * 0x1p-150)
+                                                 : __builtin_inf())
                                       : beta_lds == 2 ? as * Q.beta_absmax * (gk + 2.04 * 0x1p-24) + as * 0x1p-140
                                                       : as * Q.beta_absmax * gk;
                     double qmine = qv[0];

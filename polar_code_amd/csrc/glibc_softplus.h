@@ -555,9 +555,11 @@ PSCL_HD double pscl_softplus_tail_abs(double v) { return (double)pscl_tail_abs_f
  *     decode by at most (2 n + 1) u S' (u = 2^-53, S' = the row's sum of scaled magnitudes, n =
  *     log2 N levels: (n + 1) u S' for the scaled tree against real arithmetic -- the scaling and
  *     n levels, each channel value under n g nodes -- and log2 e * n u S for the fp64 tree).  The
- *     kernels defer every frame where one lane's share of the row (N / L values, L = 4 or 8 lanes
- *     per frame) has scaled magnitudes summing to 2^14 or more (S' < 2^17), so that term is below
- *     PSCL_TAIL2_TREE = 2^-31 per increment for every N <= 1024 (21 * 2^-53 * 2^17 < 2^-31).
+ *     kernels defer every frame where one lane's share of the row has scaled magnitudes summing to
+ *     PSCL_TAIL2_CHAN_SUM_G(G) or more: 2^14 with G = 4 or 8 lanes per frame (G distinct shares, S' <
+ *     2^17), 2^13 with G = 16 or 32 (16 distinct shares -- at G = 32 lanes p and p + 16 hold the same
+ *     elements -- so again S' < 2^17).  That term is then below PSCL_TAIL2_TREE = 2^-31 per increment
+ *     for every N <= 1024 (21 * 2^-53 * 2^17 < 2^-31).
  *     (h(x) = log2(1 + 2^-x) is 1-Lipschitz, so the error of an increment is at most the error of
  *     its LLR whichever child the LLR's sign names.)
  */
@@ -571,8 +573,10 @@ PSCL_HD double pscl_softplus_tail_abs(double v) { return (double)pscl_tail_abs_f
 #define PSCL_TAIL2_DELTA (PSCL_TAIL2_SCAN + 0.41 / 16777216.0 + 2.0 * 2.220446049250313e-16 + PSCL_TAIL2_TREE)
 /* certificate margin of the bits form: two metrics' errors (2 * 128 * delta), rounded up */
 #define PSCL_TAIL2_MARGIN (2.0 * 128.0 * PSCL_TAIL2_DELTA * 1.0001)
-/* per-lane bound on the sum of the scaled channel magnitudes a lane holds (else the frame is deferred) */
+/* per-lane bound on the sum of the scaled channel magnitudes a lane holds (else the frame is deferred):
+ * G lanes per frame, at most 16 distinct shares, S' < 2^17 in every case (see above) */
 #define PSCL_TAIL2_CHAN_SUM 16384.0
+#define PSCL_TAIL2_CHAN_SUM_G(G) ((G) >= 16 ? 0.5 * PSCL_TAIL2_CHAN_SUM : PSCL_TAIL2_CHAN_SUM)
 
 PSCL_HD float pscl_tail2_f32(float y32) { return pscl_log2_f32(1.0f + pscl_exp2_f32(-y32)); }
 PSCL_HD double pscl_softplus_tail2(double v) { return (double)pscl_tail2_f32(pscl_cvt_abs_f32(v)); }

@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(64, (NL == 10 || (NL == 9 && LMAX >= 16)) ? PS
                     if constexpr (CREG) c[CE * h + m] = v;
                     cs = cs + fabs(v);
                 }
-            amb = wmask(!(cs < (BITS ? PSCL_TAIL2_CHAN_SUM : 0x1p25)));
+            amb = wmask(!(cs < (BITS ? PSCL_TAIL2_CHAN_SUM_G(G) : 0x1p25)));
         }
         const uint64_t vmask = wmask(fvalid);
 

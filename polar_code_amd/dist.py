@@ -63,11 +63,16 @@ def init(backend: str | None = None) -> Context:
         if backend is None:  # PSCL_DIST_BACKEND overrides (gloo rehearsals on a shared GPU)
             backend = os.environ.get("PSCL_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if not dist.is_initialized():
+            # an explicit bound: a rank that never joins fails the others' init and collectives
+            # instead of holding them to the library default (PSCL_PG_TIMEOUT_S, default 600 s)
+            import datetime
+
+            timeout = datetime.timedelta(seconds=float(os.environ.get("PSCL_PG_TIMEOUT_S", "600")))
             if backend == "nccl":
                 torch.cuda.set_device(local)
-                dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+                dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local), timeout=timeout)
             else:
-                dist.init_process_group(backend=backend)
+                dist.init_process_group(backend=backend, timeout=timeout)
         group = True
         import sys
 

@@ -30,3 +30,27 @@ def test_launcher_fails_when_ranks_fail():
     assert res.returncode != 0
     assert "rank(s) failed" in res.stderr
     assert not [x for x in res.stdout.splitlines() if x.startswith("{")]
+
+
+def test_launcher_ranks_join_and_exit():
+    """The process-group path of the launcher on CPU (PSCL_BENCH_DIST_ONLY: gloo init with the
+    explicit timeout, one barrier, no GPU): both ranks join and the job exits 0."""
+    res = subprocess.run([sys.executable, "bench.py", "--gpus", "2"], cwd=ROOT, capture_output=True, text=True,
+                         env=_env(PSCL_BENCH_DIST_ONLY="1", PSCL_RANK_STALL_S="120"), timeout=300)
+    assert res.returncode == 0, res.stderr[-2000:]
+
+
+def test_launcher_ends_job_when_a_rank_never_joins():
+    """Rank 1 never joins the process group (PSCL_BENCH_STALL_RANK): rank 0 waits in
+    init_process_group, no rank finishes a stage, and the launcher's watchdog stops both ranks and
+    exits non-zero within the stall bound (plus the 30 s SIGTERM grace), never hanging."""
+    import time
+
+    t0 = time.time()
+    res = subprocess.run([sys.executable, "bench.py", "--gpus", "2"], cwd=ROOT, capture_output=True, text=True,
+                         env=_env(PSCL_BENCH_DIST_ONLY="1", PSCL_BENCH_STALL_RANK="1", PSCL_RANK_STALL_S="10",
+                                  PSCL_PG_TIMEOUT_S="3600"), timeout=240)
+    dt = time.time() - t0
+    assert res.returncode != 0
+    assert "no rank progressed" in res.stderr, res.stderr[-2000:]
+    assert dt < 10 + 30 + 60, dt  # (bound + SIGTERM grace + interpreter start-up)

@@ -265,6 +265,39 @@ def test_pipelined_dlscl_calls_equal_stream_ordered(L, depth, split):
     assert c[0][0] == nb * B and c[1][1] <= c[0][1] and (res[True][0][0][2] > 1).sum() > 1000
 
 
+@pytest.mark.parametrize("E_after", [0, 192])
+def test_rate_match_switch_orders_pipelined_chains(E_after):
+    """pscl_set_rate_match between a pipelined DL-SCL call on rate-matched rows ([B][E], E = 256,
+    the (128, 88) NR code) and its join: the call's retry chains, still deferred, are enqueued
+    with the E their rows were written for before the switch, so the outputs, attempts and
+    counters equal the stream-ordered call's (the chains used to read the new E)."""
+    from polar_code_amd.polar.polar import construct_info_set
+
+    info = construct_info_set(128, 88)
+    B, E, nc = 20_000, 256, _native.PSCL_NCOUNT
+    res = {}
+    for pipe in (True, False):
+        dec = _native.Decoder(128, info, 4, "0x1864CFB")
+        dec.set_pipelined(pipe)
+        dec.set_rate_match(E)
+        with _native.DeviceArena(dec) as mem:
+            d_llr, d_msg = mem.alloc(B * E * 8), mem.alloc(B * 16)
+            d_out = (mem.alloc(B * 16), mem.alloc(B), mem.alloc(B * 4))
+            d_cnt = mem.alloc(2 * nc * 8)
+            mem.memset(d_cnt, 0, 2 * nc * 8)
+            dec.channel_device(3, 17, 1.5, 64.0 / E, 64, 0, B, d_llr, d_msg)
+            dec.dlscl_device(d_llr, B, 8, d_best=d_out[0], d_flags=d_out[1], d_attempts=d_out[2], d_ref=d_msg,
+                             k_payload=64, d_counters_scl=d_cnt, d_counters_dl=d_cnt + nc * 8)
+            dec.set_rate_match(E_after)  # (the pipelined call's chains are still deferred here)
+            dec.join()
+            res[pipe] = [mem.download(d_out[0], B * 16, np.uint64), mem.download(d_out[1], B, np.uint8),
+                         mem.download(d_out[2], B * 4, np.int32), mem.download(d_cnt, 2 * nc * 8, np.int64)]
+        dec.close()
+    for k, name in enumerate(("best", "flags", "attempts", "counters")):
+        np.testing.assert_array_equal(res[True][k], res[False][k], err_msg=name)
+    assert (res[True][2] > 1).sum() > 100  # retries ran
+
+
 def test_device_free_orders_pipelined_chains():
     """pscl_device_free on the buffers of a pipelined DL-SCL call whose retry chains are still
     deferred (no join): the free first enqueues and completes those chains, so freeing the call's

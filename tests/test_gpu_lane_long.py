@@ -127,19 +127,23 @@ def test_lane_long_device_counters_equal_exact():
     assert c1[0] == B and c1[1] > 0
 
 
-@pytest.mark.parametrize("N,L", [(256, 8), (512, 4), (1024, 8)])
+@pytest.mark.parametrize("N,L", [(256, 8), (512, 4), (1024, 8), (256, 16), (1024, 16), (256, 32), (1024, 32)])
 def test_lane_long_bits_domain_bound_deferred(N, L):
     """The long-code lanes decode in bits too (channel LLRs scaled by log2 e, glibc_softplus.h
-    pscl_softplus_tail2) and defer a frame whose lane share (N / L values, positions = p mod L)
-    has scaled magnitudes summing to PSCL_TAIL2_CHAN_SUM or more.  Rows scaled to straddle that
+    pscl_softplus_tail2) and defer a frame whose lane share (positions = p mod G, G = min(L, 16)
+    distinct shares: at L = 32 lanes p and p + 16 hold the same elements) has scaled magnitudes
+    summing to PSCL_TAIL2_CHAN_SUM_G(L) or more -- PSCL_TAIL2_CHAN_SUM at L <= 8, half of it at
+    L = 16 and 32, so the frame's sum stays below 2^17 either way.  Rows scaled to straddle that
     bound decode exactly as the exact kernel, deferred or not."""
     from test_gpu_screening import _header_const
 
-    B = {256: 3000, 512: 1500, 1024: 800}[N]
+    B = {256: 3000, 512: 1500, 1024: 800}[N] // (1 if L <= 8 else 2 if L == 16 else 4)
     info, llr = _frames(N, N // 2, B, {256: 4.0, 512: 5.0, 1024: 6.0}[N], seed=9100 + N + L)
     rng = np.random.default_rng(N + L)
-    log2e, bound = _header_const("PSCL_LOG2E_F64"), _header_const("PSCL_TAIL2_CHAN_SUM")
-    share = lambda x: np.abs(x).reshape(x.shape[0], N // L, L).sum(axis=1).max(axis=1) * log2e  # noqa: E731
+    G = min(L, 16)
+    log2e = _header_const("PSCL_LOG2E_F64")
+    bound = _header_const("PSCL_TAIL2_CHAN_SUM") * (0.5 if L >= 16 else 1.0)
+    share = lambda x: np.abs(x).reshape(x.shape[0], N // G, G).sum(axis=1).max(axis=1) * log2e  # noqa: E731
     pick = np.arange(0, B, 2)
     llr[pick] *= (bound * np.exp2(rng.uniform(-1.0, 1.0, size=pick.size)) / share(llr[pick]))[:, None]
     a, n_def = _screened_vs_exact(N, info, L, POLY, llr)

@@ -92,3 +92,25 @@ def test_philox_stream_ids_distinct_on_fine_grids():
     on = {philox_stream_id(k / 10) for k in range(-2000, 2001)}
     off = {philox_stream_id(x) for x in (-1e-6, -0.05, 0.05, -123.456789, 7.77)}
     assert not (on & off)
+
+
+def test_closed_decoder_raises_clearly():
+    """A Decoder closed by close() or release_decoders() (get_decoder results are shared) raises a
+    clear RuntimeError on use instead of passing a NULL handle to the library; set_pipelined
+    rejects depths outside 1..4 in Python."""
+    import pytest
+
+    from polar_code_amd import _native
+
+    d = object.__new__(_native.Decoder)  # (no GPU here: a handle-less object, as after close())
+    d._hraw = None
+    assert d.closed
+    for call in (lambda: d.join(), lambda: d.set_pipelined(True), lambda: d.handle, lambda: d.sync()):
+        with pytest.raises(RuntimeError, match="closed"):
+            call()
+    d.close()  # idempotent
+    d._hraw = object()  # (a stand-in handle: the depth check runs before any library call)
+    for depth in (0, 5, -1):
+        with pytest.raises(ValueError, match="depth"):
+            d.set_pipelined(True, depth=depth)
+    d._hraw = None

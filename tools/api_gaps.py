@@ -32,3 +32,22 @@ for s, e, n in ev:
 print("API totals (us, calls >= threshold):")
 for n, v in sorted(tot.items(), key=lambda x: -x[1]):
     print(f"  {v:10.1f}  {n}")
+
+# busy host time: every HIP API call's duration summed by function, the blocking waits
+# (hipEventSynchronize, hipStreamSynchronize, hipDeviceSynchronize) listed apart
+calls = {}
+for f in glob.glob(d + "/**/*hip_api_trace.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        du = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        c = calls.setdefault(r["Function"], [0, 0.0])
+        c[0] += 1
+        c[1] += du
+wait = {k: v for k, v in calls.items() if "Synchronize" in k}
+busy = {k: v for k, v in calls.items() if k not in wait}
+print("API busy time (all calls, us):  total %.1f over %d calls" % (sum(v[1] for v in busy.values()),
+                                                                      sum(v[0] for v in busy.values())))
+for k, v in sorted(busy.items(), key=lambda x: -x[1][1])[:15]:
+    print(f"  {v[1]:10.1f} {v[0]:7d}  {k}  ({v[1] / max(v[0], 1):.1f} us/call)")
+print("API waits:")
+for k, v in wait.items():
+    print(f"  {v[1]:10.1f} {v[0]:7d}  {k}")
