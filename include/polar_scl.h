@@ -373,6 +373,15 @@ int pscl_timing_read_split(pscl_handle* h, int64_t* main_launches, double* main_
                            double* side_ms);
 
 /*
+ * Host-side cost of the DL-SCL calls (pscl_dlscl_device, also through pscl_simulate[_device]):
+ * the calls' summed wall time on the host, the part of it spent blocked in the one host wait a
+ * call may make (its previous pipelined call's failing-frame count, a finished baseline decode),
+ * and the number of calls -- so busy (enqueue) time = call_ms - wait_ms.  reset = 1 zeroes the
+ * accumulators after reading.  Any output pointer may be NULL.
+ */
+int pscl_host_stats(pscl_handle* h, double* call_ms, double* wait_ms, int64_t* calls, int reset);
+
+/*
  * The product's host (CPU) decoder: pscl_decode's contract and outputs (bit-identical) without a
  * GPU or a handle -- decode_scl (dl_scl_polar/polar/scl.py:108-209) for the reference's
  * CPU-only runs (BASELINE config 1: run_fer_sweep on CPU).  Any power-of-two N <= PSCL_MAX_N,

@@ -42,6 +42,7 @@ EXPORTS = (
     "pscl_path_llrs_device", "pscl_uncoded_device", "pscl_simulate", "pscl_set_screening", "pscl_build_hash",
     "pscl_screening_count", "pscl_softplus_tails_device", "pscl_set_pipelined", "pscl_join",
     "pscl_tail_abs_scan_device", "pscl_tail2_scan_device", "pscl_set_tuning", "pscl_timing_read_split", "pscl_decode_cpu",
+    "pscl_host_stats",
     "pscl_simulate_device",
 )
 
@@ -111,6 +112,7 @@ def lib() -> C.CDLL:
         "pscl_decode_cpu": (C.c_int, [C.c_int, P(_i32), C.c_int, C.c_int, _u64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
                                       _vp, _vp, C.c_int]),
         "pscl_timing_read_split": (C.c_int, [_vp, P(_i64), P(_dbl), P(_i64), P(_dbl)]),
+        "pscl_host_stats": (C.c_int, [_vp, P(_dbl), P(_dbl), P(_i64), C.c_int]),
         "pscl_device_count": (C.c_int, []),
         "pscl_create": (C.c_int, [P(_vp), C.c_int, C.c_int, P(_i32), C.c_int, C.c_int, _u64]),
         "pscl_destroy": (C.c_int, [_vp]),
@@ -450,6 +452,12 @@ class Decoder:
         n0, t0, n1, t1 = _i64(), _dbl(), _i64(), _dbl()
         check(lib().pscl_timing_read_split(self._h, C.byref(n0), C.byref(t0), C.byref(n1), C.byref(t1)))
         return (int(n0.value), float(t0.value)), (int(n1.value), float(t1.value))
+
+    def host_stats(self, reset: bool = False):
+        """(call ms, wait ms, calls) of the DL-SCL calls on the host (pscl_host_stats)."""
+        c, w, n = _dbl(), _dbl(), _i64()
+        check(lib().pscl_host_stats(self._h, C.byref(c), C.byref(w), C.byref(n), 1 if reset else 0))
+        return float(c.value), float(w.value), int(n.value)
 
     def launch_info(self, B: int):
         w, g, lds = C.c_int(), _i64(), C.c_int()

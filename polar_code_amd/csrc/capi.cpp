@@ -16,6 +16,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <string>
 #include <utility>
 #include <vector>
@@ -178,6 +179,8 @@ struct pscl_handle {
     std::vector<uint8_t> ev_main;     // per timed launch: 1 if it ran on the handle's stream
     size_t ev_used = 0;
     int64_t tune[PSCL_TUNE_COUNT] = {};  // pscl_set_tuning knobs (0 = the default schedule)
+    double host_call_ms = 0.0, host_wait_ms = 0.0;  // pscl_host_stats
+    int64_t host_calls = 0;
 };
 
 namespace {
@@ -1209,7 +1212,9 @@ int dl_chain(pscl_handle* h, const pscl_dl_call& a, const DlBufs& b, int64_t c, 
     const int p = dl_parity(a, c);
     const int cs = 2 * dl_set(h, a, c);  // the set's first stream
     const int64_t cap = a.cap;
+    const auto w0 = std::chrono::steady_clock::now();
     HIP_TRY(hipEventSynchronize(h->ev_base[p]));
+    h->host_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
     const int A = h->h_count[p];
     int64_t* d_cdl = a.d_ref ? a.d_counters_dl : nullptr;
     if (h->N > PSCL_FAST_N) {
@@ -1280,6 +1285,14 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
     const int rounds = h->crc_poly && retries > 0 ? (retries < h->K ? retries : h->K) : 0;
     if (d_tried && tried_stride < rounds) return fail(PSCL_EINVAL, "tried_stride < min(retries, K)");
     if (B > INT32_MAX) return fail(PSCL_EUNSUP, "B exceeds 2^31-1");
+    struct HostClock {  // pscl_host_stats: this call's wall time on the host
+        pscl_handle* h;
+        std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+        ~HostClock() {
+            h->host_call_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            h->host_calls++;
+        }
+    } host_clock{h};
     int rc = set_device(h);
     if (rc) return rc;
     pscl_dl_call a;
@@ -1832,6 +1845,18 @@ int pscl_timing_read(pscl_handle* h, int64_t* launches, double* total_ms) {
     if (rc) return rc;
     *launches = n0 + n1;
     *total_ms = t0 + t1;
+    return PSCL_OK;
+}
+
+int pscl_host_stats(pscl_handle* h, double* call_ms, double* wait_ms, int64_t* calls, int reset) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    if (call_ms) *call_ms = h->host_call_ms;
+    if (wait_ms) *wait_ms = h->host_wait_ms;
+    if (calls) *calls = h->host_calls;
+    if (reset) {
+        h->host_call_ms = h->host_wait_ms = 0.0;
+        h->host_calls = 0;
+    }
     return PSCL_OK;
 }
 

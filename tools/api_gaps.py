@@ -51,3 +51,23 @@ for k, v in sorted(busy.items(), key=lambda x: -x[1][1])[:15]:
 print("API waits:")
 for k, v in wait.items():
     print(f"  {v[1]:10.1f} {v[0]:7d}  {k}")
+
+# per-call host busy time of pscl_dlscl_device calls: API time between consecutive
+# hipEventSynchronize calls (one per pipelined call: the previous call's baseline), waits excluded
+if len(sys.argv) > 3 and sys.argv[3] == "--per-call":
+    rows = []
+    for f in glob.glob(d + "/**/*hip_api_trace.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Function"]))
+    rows.sort()
+    cur, calls = None, []
+    for s, e, fn in rows:
+        if fn == "hipEventSynchronize":
+            if cur:
+                calls.append(cur)
+            cur = {"busy": 0.0, "n": 0, "wait": (e - s) / 1e3, "t0": s}
+        elif cur is not None and "Synchronize" not in fn:
+            cur["busy"] += (e - s) / 1e3
+            cur["n"] += 1
+    for c in calls[-12:]:
+        print(f"call: busy {c['busy']:8.1f} us over {c['n']:4d} API calls, then waited {c['wait']:8.1f} us")
