@@ -321,6 +321,11 @@ int pscl_join(pscl_handle* h);
  *                           set (consecutive calls' chains on the same streams, in call order)
  *   PSCL_TUNE_POST_PAIRS    1..32: entry pairs per wavefront the DL-SCL post pass grid is sized for
  *                           (default 2, PSCL_POST_PAIRS in dlscl.hip; capped by PSCL_TUNE_POST_GRID)
+ *   PSCL_TUNE_TX_FUSED      pscl_simulate[_device] of the (128,64) code at L = 4, 8: 1 the baseline
+ *                           decode draws its channel rows itself (the TX chain fused into the lane
+ *                           kernel: no channel_kernel launch, no LLR rows written but those of
+ *                           failing or deferred frames), 2 the separate TX launch; 0 (default):
+ *                           the measured faster of the two
  */
 #define PSCL_TUNE_DL_SCREEN 1
 #define PSCL_TUNE_DL_CHUNKS 2
@@ -333,7 +338,8 @@ int pscl_join(pscl_handle* h);
 #define PSCL_TUNE_DL_RETRY_LANE 9
 #define PSCL_TUNE_POST_PAIRS 10
 #define PSCL_TUNE_DL_STREAMS 11
-#define PSCL_TUNE_COUNT 12
+#define PSCL_TUNE_TX_FUSED 12
+#define PSCL_TUNE_COUNT 13
 int pscl_set_tuning(pscl_handle* h, int knob, int64_t value);
 
 /*

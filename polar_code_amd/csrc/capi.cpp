@@ -394,7 +394,20 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
         // (pipelined: the count buffers alternate with the call parity, and the reduce runs on the
         // side stream after the re-decode, off the handle's stream)
         if ((rc = with_count_slots(h, S, hist, pipe ? 92 + p : 92, st))) return rc;
+        S.tx_upart = nullptr;
+        if (S.tx && S.tx_unc_counters) {  // fused TX: the uncoded baseline's per-wavefront partials
+            const int64_t slots = pscl_decode_count_slots(S, hist);
+            void* du;
+            const size_t had = h->scratch[94].n;
+            if ((rc = ensure(h, 94, (size_t)(slots > 0 ? slots : 1) * 16, &du))) return rc;
+            if (h->scratch[94].n != had) HIP_TRY(hipMemsetAsync(du, 0, h->scratch[94].n, st));  // (then kept zero by the reduces)
+            S.tx_upart = (int32_t*)du;
+        }
         err = pscl_launch_decode(S, hist, st);
+        if (err == hipSuccess && S.tx_upart)
+            err = pscl_launch_count_reduce(S.tx_upart, pscl_decode_count_slots(S, hist), S.tx_unc_counters, st);
+        if (err == hipSuccess && S.tx)  // fused TX: the deferred frames' rows, read by the exact re-decode
+            err = pscl_launch_tx_rows(S, (const int64_t*)d_list, (const int32_t*)d_cnt, S.B, S.tx_rows, S.tx_frame0, st);
         h->screened = true;
         h->screened_slot = s_cnt;
 #ifdef PSCL_APX_ABLATE
@@ -408,6 +421,7 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
             err = pscl_launch_count_reduce(S.cpart, pscl_decode_count_slots(S, hist), S.counters, st);
         if (err == hipSuccess && !screen_only) {
             pscl_decode_params X = P;  // exact decode of the listed frames, outputs at their rows
+            X.tx = 0;                  // (its rows are in HBM: loaded, or written by tx_rows_kernel)
             X.fidx = (const int64_t*)d_list;
             X.d_count = (const int32_t*)d_cnt;
             X.out_by_row = 1;
@@ -769,7 +783,7 @@ int pscl_set_pipelined(pscl_handle* h, int enable) {
 int pscl_set_tuning(pscl_handle* h, int knob, int64_t value) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
     static const int64_t lim[PSCL_TUNE_COUNT][2] = {{0, 0}, {0, 2}, {0, 64}, {0, 2}, {0, 1}, {0, 4096}, {0, PSCL_MAX_WAVES_PER_WG}, {0, 2},
-                                                    {0, (int64_t)1 << 30}, {0, 2}, {0, 32}, {0, 3}};
+                                                    {0, (int64_t)1 << 30}, {0, 2}, {0, 32}, {0, 3}, {0, 2}};
     if (knob < 1 || knob >= PSCL_TUNE_COUNT) return fail(PSCL_EINVAL, "unknown tuning knob %d", knob);
     if (value < lim[knob][0] || value > lim[knob][1] || (knob == PSCL_TUNE_POST_GRID && value && value < 16))
         return fail(PSCL_EINVAL, "tuning knob %d: value %lld out of range", knob, (long long)value);
@@ -1273,9 +1287,35 @@ int dl_enqueue_deferred(pscl_handle* h, bool beside) {
 }
 }  // namespace
 
+namespace {
+// the fused TX of a pscl_simulate_device block (PSCL_TUNE_TX_FUSED): the baseline decode draws the
+// rows it decodes (scl128_lane.hip TXF), writes the message words to d_ref's buffer and the rows of
+// failing and deferred frames to d_llr's, and counts the uncoded baseline into unc
+struct TxSpec {
+    uint32_t k0 = 0, k1 = 0;
+    int64_t frame0 = 0;
+    double sigma = 0.0, scale = 0.0, unc_sigma = 0.0;
+    int kp = 0;
+    double* rows = nullptr;
+    uint64_t* msg = nullptr;
+    int64_t* unc = nullptr;  // [PSCL_NCOUNT] or null
+};
+int dlscl_impl(pscl_handle* h, const double* d_llr, int64_t B, int retries, uint64_t* d_best, uint8_t* d_flags,
+               int32_t* d_attempts, int32_t* d_tried, int tried_stride, const uint64_t* d_ref, int k_payload,
+               int64_t* d_counters_scl, int64_t* d_counters_dl, const TxSpec* tx);
+}  // namespace
+
 int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retries, uint64_t* d_best, uint8_t* d_flags,
                       int32_t* d_attempts, int32_t* d_tried, int tried_stride, const uint64_t* d_ref, int k_payload,
                       int64_t* d_counters_scl, int64_t* d_counters_dl) {
+    return dlscl_impl(h, d_llr, B, retries, d_best, d_flags, d_attempts, d_tried, tried_stride, d_ref, k_payload,
+                      d_counters_scl, d_counters_dl, nullptr);
+}
+
+namespace {
+int dlscl_impl(pscl_handle* h, const double* d_llr, int64_t B, int retries, uint64_t* d_best, uint8_t* d_flags,
+               int32_t* d_attempts, int32_t* d_tried, int tried_stride, const uint64_t* d_ref, int k_payload,
+               int64_t* d_counters_scl, int64_t* d_counters_dl, const TxSpec* tx) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
     if (B < 0) return fail(PSCL_EINVAL, "B must be >= 0");
     if (B == 0) return PSCL_OK;
@@ -1383,6 +1423,23 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
                                                                : (PSCL_DL_LANE_DEFAULT ? PSCL_DL_LANE_DEFAULT : (h->L == 8 ? 1 : 2));
             P.no_lane = dl_lane != 1;
         }
+        if (tx) {  // the fused TX: the lane kernel draws the chunk's rows (simulate_enqueue checked it applies)
+            P.no_lane = 0;
+            P.tx = 1;
+            P.tx_k0 = tx->k0;
+            P.tx_k1 = tx->k1;
+            P.tx_kp = tx->kp;
+            P.tx_crc_deg = h->crc_deg;
+            P.tx_frame0 = tx->frame0 + c0;
+            P.tx_sigma = tx->sigma;
+            P.tx_scale = tx->scale;
+            P.tx_unc_sigma = tx->unc_sigma;
+            P.tx_crctab = h->d_crctab;
+            P.tx_xtab = h->d_xtab;
+            P.tx_rows = tx->rows + c0 * row;
+            P.tx_msg = tx->msg + c0 * W;
+            P.tx_unc_counters = tx->unc;
+        }
         if (pscl_decode_wpg(P) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
         if ((rc = launch_decode(h, P, 0))) return rc;
         if (rounds > 0) {
@@ -1391,6 +1448,10 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
             HIP_TRY(hipMemsetAsync(bufs.cnt[p], 0, 4, s));
             if ((e = pscl_launch_dl_compact(d_flags + c0, nc, c0, bufs.act[p], nullptr, bufs.cnt[p], s)) != hipSuccess)
                 return fail(PSCL_EDEVICE, "dl_compact launch: %s", hipGetErrorString(e));
+            // fused TX: the failing frames' rows, read by the retry chain (entries hold call-level frame
+            // indices c0 + f)
+            if (tx && (e = pscl_launch_tx_rows(P, bufs.act[p], bufs.cnt[p], nc, tx->rows, tx->frame0, s)) != hipSuccess)
+                return fail(PSCL_EDEVICE, "tx_rows launch: %s", hipGetErrorString(e));
             HIP_TRY(hipMemcpyAsync(h->h_count + p, bufs.cnt[p], 4, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipEventRecord(h->ev_base[p], s));
             if (c >= 1 && (rc = dl_chain(h, a, bufs, c - 1, true))) return rc;
@@ -1417,6 +1478,7 @@ int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retrie
     }
     return PSCL_OK;
 }
+}  // namespace
 
 static int decode_host(pscl_handle* h, const double* llr, int64_t B, const int8_t* forced, int32_t* n_paths,
                        int8_t* best_bits, uint8_t* crc_pass, int32_t* best_idx, double* metrics, int8_t* cands,
@@ -1555,6 +1617,23 @@ namespace {
 int channel_launch(pscl_handle* h, uint64_t seed, uint32_t stream_id, double ebno_db, double rate, int k_payload,
                    int64_t frame0, int64_t B, double* d_llr, uint64_t* d_msg, int64_t* d_unc, bool no_enter = false);
 
+#ifndef PSCL_TX_FUSED_DEFAULT
+#define PSCL_TX_FUSED_DEFAULT 0
+#endif
+// whether a pscl_simulate[_device] block takes the fused TX (PSCL_TUNE_TX_FUSED, default
+// PSCL_TX_FUSED_DEFAULT): its baseline decode must be the screening lane kernel of the (128,64) code
+// on plain rows (L = 4 or 8), which then draws the rows itself
+bool tx_fused_applies(const pscl_handle* h, int k_payload) {
+    const int64_t k = h->tune[PSCL_TUNE_TX_FUSED];
+    if (!(k == 1 || (k == 0 && PSCL_TX_FUSED_DEFAULT))) return false;
+    if (h->N != 128 || h->rm_E || !h->screen || (h->L != 8 && h->L != 4) || k_payload + h->crc_deg != h->K) return false;
+    pscl_decode_params T;
+    fill_decode_params(h, T, 0);
+    T.B = 1;
+    T.apx = 1;
+    return pscl_lane_available(T) != 0;
+}
+
 // One SNR point of run_sweep enqueued (pscl_simulate / pscl_simulate_device): chunks of at most
 // 2^20 frames through handle scratch (N * 8 bytes of LLRs per frame: about 1 GiB per chunk at
 // N = 128), each = TX (+ the uncoded baseline) + pscl_dlscl_device.  On a pipelined handle every
@@ -1589,18 +1668,37 @@ int simulate_enqueue(pscl_handle* h, uint64_t seed, uint32_t stream_id, double e
         if ((rc = ensure(h, base + 1, (size_t)chunk * W * 8, &d_msg))) return rc;
         if ((rc = ensure(h, base + 2, (size_t)chunk * W * 8, &d_best))) return rc;
         if ((rc = ensure(h, base + 3, (size_t)chunk, &d_flags))) return rc;
-        // N <= 128: the uncoded baseline is counted by the TX launch itself (same payload draw)
-        const bool unc_fused = include_uncoded && N <= PSCL_FAST_N;
-        if ((rc = channel_launch(h, seed, stream_id, ebno_db, rate, k_payload, frame0 + f, n, (double*)d_llr,
-                                 (uint64_t*)d_msg, unc_fused ? cs + 2 * PSCL_NCOUNT : nullptr, true)))
-            return rc;
-        if (include_uncoded && !unc_fused &&
-            (rc = uncoded_launch(h, seed, stream_id, ebno_db, k_payload, frame0 + f, n, cs + 2 * PSCL_NCOUNT, true)))
-            return rc;
+        // the fused TX (PSCL_TUNE_TX_FUSED): the baseline decode draws the rows itself -- where its
+        // screening launch is the lane kernel of the (128,64) code on plain rows
+        TxSpec tx;
+        const bool fused = tx_fused_applies(h, k_payload);
+        if (fused) {
+            tx.k0 = (uint32_t)seed;
+            tx.k1 = (uint32_t)(seed >> 32) ^ (stream_id * 0x85EBCA6Bu);  // (channel_kernel's key)
+            tx.frame0 = frame0 + f;
+            const double ebno = pow(10.0, ebno_db / 10.0);
+            const double nv = 1.0 / (2.0 * rate * ebno);  // (channel_launch's parameters)
+            tx.sigma = sqrt(nv);
+            tx.scale = 2.0 / nv;
+            tx.unc_sigma = sqrt(1.0 / (2.0 * ebno));
+            tx.kp = k_payload;
+            tx.rows = (double*)d_llr;
+            tx.msg = (uint64_t*)d_msg;
+            tx.unc = include_uncoded ? cs + 2 * PSCL_NCOUNT : nullptr;
+        } else {
+            // N <= 128: the uncoded baseline is counted by the TX launch itself (same payload draw)
+            const bool unc_fused = include_uncoded && N <= PSCL_FAST_N;
+            if ((rc = channel_launch(h, seed, stream_id, ebno_db, rate, k_payload, frame0 + f, n, (double*)d_llr,
+                                     (uint64_t*)d_msg, unc_fused ? cs + 2 * PSCL_NCOUNT : nullptr, true)))
+                return rc;
+            if (include_uncoded && !unc_fused &&
+                (rc = uncoded_launch(h, seed, stream_id, ebno_db, k_payload, frame0 + f, n, cs + 2 * PSCL_NCOUNT, true)))
+                return rc;
+        }
         const int back = h->dl_back;
         h->dl_back = kDlPar;  // (its own scratch set: kDlPar sets rotate with the call parity)
-        rc = pscl_dlscl_device(h, (const double*)d_llr, n, retries, (uint64_t*)d_best, (uint8_t*)d_flags, nullptr, nullptr,
-                               0, (const uint64_t*)d_msg, k_payload, cs, cs + PSCL_NCOUNT);
+        rc = dlscl_impl(h, (const double*)d_llr, n, retries, (uint64_t*)d_best, (uint8_t*)d_flags, nullptr, nullptr, 0,
+                        (const uint64_t*)d_msg, k_payload, cs, cs + PSCL_NCOUNT, fused ? &tx : nullptr);
         h->dl_back = back;
         if (rc) return rc;
     }

@@ -108,9 +108,56 @@ struct LaneLayout {
 // ordering decision), growing (every child survives) or full (the keep / one-swap / ranked
 // tiers, their certificates restricted to the full frames).  Frames it cannot certify go to
 // the deferred bucket lists (P.amb_elist, flags PSCL_DL_DEFERRED) for the exact FS kernel.
-template <int LMAX, int CODE, bool FS = false>
-__global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(const pscl_decode_params P) {
+// channel_kernel's phase A for frame counter fr (scl_kernels.hip): the payload draw (raw, for the
+// uncoded baseline), the message (payload + CRC remainder, crc.py:19-37) and the codeword
+// (polar.py:17-29,106-119) by the handle's byte tables
+__device__ __forceinline__ void tx_frame_words(const pscl_decode_params& P, uint64_t fr, uint64_t (&m)[2],
+                                               uint64_t (&raw)[2], uint64_t (&x)[2]) {
+    const u32x4 rb = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), 0xffffffffu, 0u}, P.tx_k0, P.tx_k1);
+    raw[0] = ((uint64_t)rb.y << 32) | rb.x;
+    raw[1] = ((uint64_t)rb.w << 32) | rb.z;
+    const int kp = P.tx_kp, nbp = (kp + 7) >> 3, nb = (P.K + 7) >> 3;
+    m[0] = kp >= 64 ? raw[0] : (raw[0] & ((1ULL << kp) - 1));
+    m[1] = kp > 64 ? (raw[1] & ((kp >= 128) ? ~0ULL : ((1ULL << (kp - 64)) - 1))) : 0;
+    uint32_t rem = 0;
+    for (int k = 0; k < nbp; ++k) rem ^= P.tx_crctab[k * 256 + (uint32_t)((m[k >> 3] >> (8 * (k & 7))) & 255u)];
+    if (P.tx_crc_deg) {
+        const uint64_t rw = (uint64_t)rem;
+        if (kp < 64) {
+            m[0] |= rw << kp;
+            if (kp + P.tx_crc_deg > 64) m[1] |= rw >> (64 - kp);
+        } else {
+            m[1] |= rw << (kp - 64);
+        }
+    }
+    x[0] = x[1] = 0;
+    for (int k = 0; k < nb; ++k) {
+        const uint32_t v = (uint32_t)((m[k >> 3] >> (8 * (k & 7))) & 255u);
+        x[0] ^= P.tx_xtab[(k * 256 + v) * 2];
+        x[1] ^= P.tx_xtab[(k * 256 + v) * 2 + 1];
+    }
+}
+
+// occupancy hint of the fused TX instance at L = 8: 3 waves per SIMD (168 VGPRs), the plain kernel's
+// occupancy (its LDS allows no more); its draws would otherwise take it to ~177 VGPRs and 2 waves
+#ifndef PSCL_TX_WAVES
+#define PSCL_TX_WAVES 3
+#endif
+// TXF: the fused TX instance (pscl_simulate_device, PSCL_TUNE_TX_FUSED; P.tx and the tx_* fields of
+// pscl_decode_params): each frame's channel row is drawn here from channel_kernel's Philox stream
+// -- the same draws, the same fp64 expression, so the decode sees bit for bit the row
+// channel_kernel would have written -- instead of being loaded.  The 8 (L = 8) or 4 (L = 4) lanes of
+// a frame hold exactly the positions of 8 or 16 whole Box-Muller pairs (pair c gives positions c and
+// c + 64; lane p needs p + G k + 16 m), so the frame draws its 64 pairs once, as channel_kernel does;
+// every lane of the frame forms the payload, CRC and codeword itself (channel_kernel's phase A,
+// byte tables).  Epilogue: the message words of every frame (the reference of the counts and of
+// the DL-SCL counter pass), the rows of the frames whose best candidate fails the CRC or that are
+// deferred (the retry and exact decodes read them; regenerated, ~1 % of frames at 5 dB), and the
+// uncoded BPSK baseline of the same payloads (channel_kernel's draws 0x40000000 + c).
+template <int LMAX, int CODE, bool FS = false, bool TXF = false>
+__global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(const pscl_decode_params P) {
     static_assert(LMAX == 4 || LMAX == 8, "the lane-per-path decoder is built for L = 4 and 8");
+    static_assert(!TXF || (!FS && CODE == 1), "fused TX: plain decodes of the (128,64) code");
     using Ly = LaneLayout<LMAX>;
     constexpr int G = Ly::G, F = Ly::F, LOG_G = Ly::LOG_G;
     constexpr int EPL = 16 / G;                 // depth-3 elements per lane at a recompute
@@ -150,6 +197,7 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
     };
 
     int cfe = 0, cbe = 0, cpe = 0, cpb = 0;  // this lane's error counts (flushed at the end)
+    int tufe = 0, tube = 0;                  // TXF: the uncoded baseline's errors
     // frames of the launch: P.B, or (FS) the total of the round's bucket lists
     int bpre[PSCL_DL_NSEG + 1];
     int64_t Bn = P.B;
@@ -180,16 +228,75 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
         // need c[8 k + m] = chan[e_k + 16 m] -- the same at all 8 depth-1..3 recomputes
         // (CREG = false, an L = 4 build option: the 32 values are re-read from the L2-resident row at
         // each recompute instead, which keeps them out of the registers of the other phases)
-        constexpr bool CREG = G == 8 || PSCL_LANE_CREG4;
+        constexpr bool CREG = G == 8 || PSCL_LANE_CREG4 || TXF;
         double c[8 * EPL];
-        auto load_chan = [&]() {
+        // fused TX: the frame's payload draw, message and codeword words (channel_kernel phase A)
+        uint64_t tm[2] = {0, 0}, traw[2] = {0, 0}, tx[2] = {0, 0};
+        const uint64_t tfr = TXF ? (uint64_t)(P.tx_frame0 + fsafe) : 0ULL;
+        if constexpr (TXF) tx_frame_words(P, tfr, tm, traw, tx);
+        // the channel values of this lane's positions e = p + G k + 16 m, unscaled (the fused TX
+        // instance; channel_kernel's row[e]): pair blk = p + G k + 16 j gives m = j and m = j + 4
+        auto gen_chan = [&](double* v, uint64_t fr) {
 #pragma unroll
             for (int k = 0; k < EPL; ++k)
 #pragma unroll
-                for (int m = 0; m < 8; ++m) c[8 * k + m] = BITS ? chan_at(p + G * k + 16 * m) * PSCL_LOG2E_F64
-                                                                : chan_at(p + G * k + 16 * m);
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t blk = (uint32_t)(p + G * k + 16 * j);
+                    const u32x4 rn = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), blk, 0u}, P.tx_k0, P.tx_k1);
+                    double z[2];
+                    bm_pair(((uint64_t)rn.y << 32) | rn.x, ((uint64_t)rn.w << 32) | rn.z, z[0], z[1]);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const double sym = ((tx[h] >> blk) & 1ULL) ? -1.0 : 1.0;
+                        v[8 * k + j + 4 * h] = (sym + P.tx_sigma * z[h]) * P.tx_scale;
+                    }
+                    // one pair at a time: interleaved, the 8 (16) Philox chains' temporaries raise the
+                    // kernel's register peak above the decode's own
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+        };
+        auto load_chan = [&]() {
+            if constexpr (TXF) {
+                gen_chan(c, tfr);
+                if constexpr (BITS)
+#pragma unroll
+                    for (int m = 0; m < 8 * EPL; ++m) c[m] = c[m] * PSCL_LOG2E_F64;
+            } else {
+#pragma unroll
+                for (int k = 0; k < EPL; ++k)
+#pragma unroll
+                    for (int m = 0; m < 8; ++m) c[8 * k + m] = BITS ? chan_at(p + G * k + 16 * m) * PSCL_LOG2E_F64
+                                                                    : chan_at(p + G * k + 16 * m);
+            }
         };
         load_chan();
+        if constexpr (TXF) {
+            // the uncoded BPSK baseline of the same payload (channel_kernel phase A: noise pairs
+            // 0x40000000 + cb), counted here while the decode's registers are still free
+            if (P.tx_upart) {
+                uint32_t berr = 0;
+                for (int cb = p; 2 * cb < P.tx_kp; cb += G) {
+                    const u32x4 rn = philox4x32(u32x4{(uint32_t)tfr, (uint32_t)(tfr >> 32), 0x40000000u + (uint32_t)cb, 0u},
+                                                P.tx_k0, P.tx_k1);
+                    double z[2];
+                    bm_pair(((uint64_t)rn.y << 32) | rn.x, ((uint64_t)rn.w << 32) | rn.z, z[0], z[1]);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int q = 2 * cb + h;
+                        if (q < P.tx_kp) {
+                            const uint32_t bit = (uint32_t)((traw[q >> 6] >> (q & 63)) & 1ULL);
+                            const double y = (bit ? -1.0 : 1.0) + P.tx_unc_sigma * z[h];
+                            berr += ((y < 0.0) ? 1u : 0u) != bit ? 1u : 0u;
+                        }
+                    }
+                }
+                berr = frame_sum<G>(berr);
+                if (fvalid && p == 0) {
+                    tufe += berr ? 1 : 0;
+                    tube += (int)berr;
+                }
+            }
+        }
         // frames whose channel magnitudes could overflow the fp64 metric sums or carry a NaN go to
         // the exact re-decode (the lane's values summed; NaN propagates through the sum); in bits,
         // a tighter bound keeps the scaled tree's error below PSCL_TAIL2_TREE (glibc_softplus.h)
@@ -613,6 +720,14 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
             static_for<kN>([&](auto PC) { phase(PC); });
         }
 
+        // fused TX: the message words formed again for the epilogue from an opaque copy of the frame
+        // counter -- left to itself the compiler reuses the frame start's draws and keeps them live
+        // across the whole decode (with the rows' draws: +75 VGPRs, 2 waves/SIMD instead of 3)
+        uint64_t tfr2 = tfr;
+        if constexpr (TXF) {
+            asm volatile("" : "+v"(tfr2));
+            tx_frame_words(P, tfr2, tm, traw, tx);
+        }
         // ---- epilogue: candidates u[info_set], CRC syndrome, final list order certified,
         // best = first CRC pass in list order (scl.py:176-209)
         uint64_t ib0 = 0, ib1 = 0;
@@ -687,7 +802,15 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
             if (P.n_paths) P.n_paths[f] = FS ? (1 << lcnt) : LMAX;
             if (!FS && P.ref) {
                 const uint64_t ibw[2] = {ib0, ib1};
-                tally_errors(ibw, P.ref + fi * PW, PW, P.k_payload, bpass, cfe, cbe, cpe, cpb);
+                tally_errors(ibw, TXF ? tm : P.ref + fi * PW, PW, P.k_payload, bpass, cfe, cbe, cpe, cpb);
+            }
+        }
+        if constexpr (TXF) {
+            // the message words of every frame (the counts' reference; the rows of the frames the exact
+            // re-decode or the retry chain will read are written by tx_rows_kernel, scl_kernels.hip)
+            if (fvalid && p == 0) {
+                P.tx_msg[fi * PW] = tm[0];
+                if (PW > 1) P.tx_msg[fi * PW + 1] = tm[1];
             }
         }
         wave_lds_fence();
@@ -696,6 +819,14 @@ __global__ void __launch_bounds__(64, PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(co
         flush_counts_p(P, blockIdx.x, cfe, cbe, cpe, cpb);
         if (blockIdx.x == 0 && threadIdx.x == 0)
             atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
+    }
+    if constexpr (TXF) {
+        if (P.tx_upart && __builtin_amdgcn_ballot_w64((tufe | tube) != 0)) {
+            const int fe = wave_sum(tufe), be = wave_sum(tube);
+            if (lane == 0) reinterpret_cast<int4*>(P.tx_upart)[blockIdx.x] = make_int4(fe, be, 0, 0);
+        }
+        if (P.tx_unc_counters && blockIdx.x == 0 && threadIdx.x == 0)
+            atomicAdd(reinterpret_cast<unsigned long long*>(P.tx_unc_counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
     }
 }
 
@@ -714,6 +845,16 @@ hipError_t pscl_launch_lane(const pscl_decode_params& P, int64_t grid, hipStream
     // (pscl_lane_available: the (128,64) code on plain rows, or the rate-matched NR (128,88) code)
     const int lds8 = LaneLayout<8>::F * LaneLayout<8>::FSTRIDE * 8 + PSCL_LANE_LDS_PAD,
               lds4 = LaneLayout<4>::F * LaneLayout<4>::FSTRIDE * 8 + PSCL_LANE_LDS_PAD;
+    if (P.tx) {  // the fused TX instance (plain rows of the (128,64) code, pscl_simulate_device)
+        if (P.rm_E) return hipErrorInvalidValue;
+        if (P.L == 8)
+            hipLaunchKernelGGL((scl_lane_kernel<8, 1, false, true>), dim3((unsigned)grid), dim3(64), lds8, s, P);
+        else if (P.L == 4)
+            hipLaunchKernelGGL((scl_lane_kernel<4, 1, false, true>), dim3((unsigned)grid), dim3(64), lds4, s, P);
+        else
+            return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
     if (P.L == 8 && !P.rm_E)
         hipLaunchKernelGGL((scl_lane_kernel<8, 1>), dim3((unsigned)grid), dim3(64), lds8, s, P);
     else if (P.L == 8)

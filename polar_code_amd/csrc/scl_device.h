@@ -495,6 +495,39 @@ __device__ __forceinline__ void tally_errors(const uint64_t* ib, const uint64_t*
     pb += pay_err;
 }
 
+// ---- the TX stream (channel_kernel, scl_kernels.hip; the fused-TX lane kernel, scl128_lane.hip)
+
+struct u32x4 {
+    uint32_t x, y, z, w;
+};
+
+// Philox4x32-10 (Salmon et al., SC'11)
+__device__ __forceinline__ u32x4 philox4x32(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+        c = u32x4{(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0};
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+// Box-Muller pair from one Philox block (a, bb): u1 in (0, 1] from the top 53 bits of a, u2 in
+// [0, 1) from the top 24 bits of bb; radius and angle with the fp32 hardware transcendentals
+// (v_log_f32, v_sqrt_f32, v_sin/cos_f32 in revolutions), the pair widened to fp64.  u1 keeps
+// all 53 bits (its fp32 image is normal down to 2^-53), so the tail reaches 8.57 sigma like an
+// fp64 draw; the fp32 roundings perturb a normal by ~1e-6 sigma, far below Monte-Carlo error
+// (tests/test_gpu_channel.py states the tolerance).  One fp64 log and sincospi per pair took
+// most of the TX kernel's time.
+__device__ __forceinline__ void bm_pair(uint64_t a, uint64_t bb, double& z0, double& z1) {
+    const float u1 = (float)(((double)(a >> 11) + 1.0) * 0x1p-53);
+    const float u2 = (float)(uint32_t)(bb >> 40) * 0x1p-24f;
+    const float rad = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // -2 ln u1
+    z0 = (double)(rad * __builtin_amdgcn_cosf(u2));
+    z1 = (double)(rad * __builtin_amdgcn_sinf(u2));
+}
+
 }  // namespace pscl
 
 #endif

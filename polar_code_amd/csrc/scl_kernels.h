@@ -83,6 +83,24 @@ struct pscl_decode_params {
     // below 16 k (the forced prefix's single path, replayed exactly by dl_post_kernel)
     const double* warm_metric;   // [entries][PSCL_DL_NSEG]
     const uint64_t* warm_u;      // [entries][2]
+    // fused TX (pscl_simulate_device, PSCL_TUNE_TX_FUSED; the lane kernel of the (128,64) code): the
+    // kernel draws frame b's channel row from channel_kernel's Philox stream (key tx_k0/tx_k1, frame
+    // counter tx_frame0 + b) instead of loading it, bit for bit the row channel_kernel writes; it
+    // writes the transmitted message of every frame to tx_msg (the launch's reference words: P.ref ==
+    // tx_msg for the exact re-decode), the rows of the frames that fail the CRC or are deferred to
+    // tx_rows (the retry and exact decodes read those), and the uncoded BPSK baseline of the same
+    // payloads (channel_kernel's phase A) as per-wavefront partials tx_upart, like cpart
+    int tx;
+    uint32_t tx_k0, tx_k1;
+    int tx_kp, tx_crc_deg;
+    int64_t tx_frame0;
+    double tx_sigma, tx_scale, tx_unc_sigma;
+    const uint32_t* tx_crctab;   // [ceil(kp / 8)][256] CRC remainder of each payload byte value
+    const uint64_t* tx_xtab;     // [ceil(K / 8)][256][2] codeword of each message byte value
+    double* tx_rows;             // [B][N]
+    uint64_t* tx_msg;            // [B][W]
+    int32_t* tx_upart;           // [slots][4] (frame, bit errors, 0, 0) of the uncoded baseline, or null
+    int64_t* tx_unc_counters;    // its counters (the frame count is added here)
 };
 
 #define PSCL_DL_NSEG 8     // 16-phase segments of N = 128: warm-start buckets
@@ -278,6 +296,10 @@ int pscl_decode_wpg(const pscl_decode_params& P);
 int pscl_decode_lds(const pscl_decode_params& P, int hist);
 hipError_t pscl_launch_decode(const pscl_decode_params& P, int hist, hipStream_t s);
 hipError_t pscl_launch_channel(const pscl_channel_params& P, hipStream_t s);
+// fused TX: channel_kernel's rows of the listed frames (list[0, min(*count, cap)), frame counter
+// frame0 + list[i], row rows + 128 list[i]); P carries the tx_* stream parameters
+hipError_t pscl_launch_tx_rows(const pscl_decode_params& P, const int64_t* list, const int32_t* count, int64_t cap,
+                               double* rows, int64_t frame0, hipStream_t s);
 hipError_t pscl_launch_uncoded(const pscl_channel_params& P, int64_t* counters, hipStream_t s);
 hipError_t pscl_launch_dl_compact(const uint8_t* flags, int64_t B, int64_t base, int64_t* act, int32_t* list,
                                   int32_t* count, hipStream_t s);

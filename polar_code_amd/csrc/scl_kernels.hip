@@ -330,36 +330,7 @@ __global__ void __launch_bounds__(PSCL_MAX_WAVES_PER_WG * kWave)
 
 // ------------------------------------------------------------------------ channel (TX)
 
-struct u32x4 {
-    uint32_t x, y, z, w;
-};
-
-// Philox4x32-10 (Salmon et al., SC'11)
-__device__ __forceinline__ u32x4 philox4x32(u32x4 c, uint32_t k0, uint32_t k1) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
-        c = u32x4{(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0};
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-    }
-    return c;
-}
-
-// Box-Muller pair from one Philox block (a, bb): u1 in (0, 1] from the top 53 bits of a, u2 in
-// [0, 1) from the top 24 bits of bb; radius and angle with the fp32 hardware transcendentals
-// (v_log_f32, v_sqrt_f32, v_sin/cos_f32 in revolutions), the pair widened to fp64.  u1 keeps
-// all 53 bits (its fp32 image is normal down to 2^-53), so the tail reaches 8.57 sigma like an
-// fp64 draw; the fp32 roundings perturb a normal by ~1e-6 sigma, far below Monte-Carlo error
-// (tests/test_gpu_channel.py states the tolerance).  One fp64 log and sincospi per pair took
-// most of the TX kernel's time.
-__device__ __forceinline__ void bm_pair(uint64_t a, uint64_t bb, double& z0, double& z1) {
-    const float u1 = (float)(((double)(a >> 11) + 1.0) * 0x1p-53);
-    const float u2 = (float)(uint32_t)(bb >> 40) * 0x1p-24f;
-    const float rad = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // -2 ln u1
-    z0 = (double)(rad * __builtin_amdgcn_cosf(u2));
-    z1 = (double)(rad * __builtin_amdgcn_sinf(u2));
-}
+// (u32x4, philox4x32, bm_pair: scl_device.h, shared with the fused-TX lane kernel)
 
 // TX chain, two phases per wavefront of 64 frames:
 //   A  lane = frame: Philox payload, CRC remainder and codeword from byte tables (both maps
@@ -480,7 +451,65 @@ __global__ void __launch_bounds__(256) channel_kernel(const pscl_channel_params 
 
 }  // namespace
 
+// Rows of the fused TX (scl128_lane.hip TXF, pscl_simulate_device): the lane kernel draws the rows it
+// decodes without writing them; the frames other decodes read again -- the deferred ones (exact
+// re-decode) and the failing ones (DL-SCL retry chain) -- get channel_kernel's row written here,
+// one wavefront per listed frame (lane c = Box-Muller pair c: positions c and c + 64), the codeword
+// formed by every lane (channel_kernel phase A).  list[i] < count frames, at frame counter
+// frame0 + list[i], row rows + list[i] * 128.
+__global__ void __launch_bounds__(256) tx_rows_kernel(const pscl_decode_params P, const int64_t* __restrict__ list,
+                                                      const int32_t* __restrict__ count, int64_t cap, double* rows,
+                                                      int64_t frame0) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int64_t n = *count;
+    if (n > cap) n = cap;
+    for (int64_t i = (int64_t)blockIdx.x * 4 + wave; i < n; i += (int64_t)gridDim.x * 4) {  // wave-uniform
+        const int64_t b = list[i];
+        const uint64_t fr = (uint64_t)(frame0 + b);
+        const u32x4 rb = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), 0xffffffffu, 0u}, P.tx_k0, P.tx_k1);
+        const uint64_t r0 = ((uint64_t)rb.y << 32) | rb.x, r1 = ((uint64_t)rb.w << 32) | rb.z;
+        const int kp = P.tx_kp, nbp = (kp + 7) >> 3, nb = (P.K + 7) >> 3;
+        uint64_t m0 = kp >= 64 ? r0 : (r0 & ((1ULL << kp) - 1));
+        uint64_t m1 = kp > 64 ? (r1 & ((kp >= 128) ? ~0ULL : ((1ULL << (kp - 64)) - 1))) : 0;
+        uint32_t rem = 0;
+        for (int k = 0; k < nbp; ++k) rem ^= P.tx_crctab[k * 256 + (uint32_t)(((k < 8 ? m0 : m1) >> (8 * (k & 7))) & 255u)];
+        if (P.tx_crc_deg) {
+            const uint64_t rw = (uint64_t)rem;
+            if (kp < 64) {
+                m0 |= rw << kp;
+                if (kp + P.tx_crc_deg > 64) m1 |= rw >> (64 - kp);
+            } else {
+                m1 |= rw << (kp - 64);
+            }
+        }
+        uint64_t x0 = 0, x1 = 0;
+        for (int k = 0; k < nb; ++k) {
+            const uint32_t v = (uint32_t)(((k < 8 ? m0 : m1) >> (8 * (k & 7))) & 255u);
+            x0 ^= P.tx_xtab[(k * 256 + v) * 2];
+            x1 ^= P.tx_xtab[(k * 256 + v) * 2 + 1];
+        }
+        const u32x4 rn = philox4x32(u32x4{(uint32_t)fr, (uint32_t)(fr >> 32), (uint32_t)lane, 0u}, P.tx_k0, P.tx_k1);
+        double z[2];
+        bm_pair(((uint64_t)rn.y << 32) | rn.x, ((uint64_t)rn.w << 32) | rn.z, z[0], z[1]);
+        double* row = rows + b * 128;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const double sym = (((h ? x1 : x0) >> lane) & 1ULL) ? -1.0 : 1.0;
+            row[lane + 64 * h] = (sym + P.tx_sigma * z[h]) * P.tx_scale;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------- launchers
+
+hipError_t pscl_launch_tx_rows(const pscl_decode_params& P, const int64_t* list, const int32_t* count, int64_t cap,
+                               double* rows, int64_t frame0, hipStream_t s) {
+    if (cap <= 0) return hipSuccess;
+    int64_t grid = (cap + 3) / 4;
+    if (grid > 1024) grid = 1024;  // (the count is read on the device; few frames in practice)
+    hipLaunchKernelGGL(tx_rows_kernel, dim3((unsigned)grid), dim3(256), 0, s, P, list, count, cap, rows, frame0);
+    return hipGetLastError();
+}
 
 // wavefronts per workgroup: the choice that keeps the most wavefronts resident per CU
 // under the 160 KB LDS budget (each workgroup also holds the 2 KB exp table); 0 if none fits
