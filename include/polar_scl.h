@@ -326,6 +326,10 @@ int pscl_join(pscl_handle* h);
  *                           kernel: no channel_kernel launch, no LLR rows written but those of
  *                           failing or deferred frames), 2 the separate TX launch; 0 (default):
  *                           the measured faster of the two
+ *   PSCL_TUNE_DL_FUSED_POST 1: a screened retry round of the (128,64) code at L = 4, 8 runs its post
+ *                           pass in the decode kernel (one launch per round; warm-start metrics
+ *                           from the screening tail, deferred entries exact from phase 0); 2: the
+ *                           separate dl_post_kernel; 0 (default): the measured faster
  */
 #define PSCL_TUNE_DL_SCREEN 1
 #define PSCL_TUNE_DL_CHUNKS 2
@@ -339,7 +343,8 @@ int pscl_join(pscl_handle* h);
 #define PSCL_TUNE_POST_PAIRS 10
 #define PSCL_TUNE_DL_STREAMS 11
 #define PSCL_TUNE_TX_FUSED 12
-#define PSCL_TUNE_COUNT 13
+#define PSCL_TUNE_DL_FUSED_POST 13
+#define PSCL_TUNE_COUNT 14
 int pscl_set_tuning(pscl_handle* h, int knob, int64_t value);
 
 /*
@@ -386,6 +391,14 @@ int pscl_timing_read_split(pscl_handle* h, int64_t* main_launches, double* main_
  * accumulators after reading.  Any output pointer may be NULL.
  */
 int pscl_host_stats(pscl_handle* h, double* call_ms, double* wait_ms, int64_t* calls, int reset);
+
+/*
+ * Which schedules this handle has enqueued since it was created (tests assert the path they
+ * mean to exercise ran): DL-SCL retry rounds whose post pass ran inside the screened retry
+ * decode (PSCL_TUNE_DL_FUSED_POST), rounds with the separate dl_post_kernel, and pscl_simulate
+ * blocks whose TX was fused into the baseline decode (PSCL_TUNE_TX_FUSED).  Any pointer may be NULL.
+ */
+int pscl_path_stats(pscl_handle* h, int64_t* fused_post_rounds, int64_t* post_rounds, int64_t* fused_tx_blocks);
 
 /*
  * The product's host (CPU) decoder: pscl_decode's contract and outputs (bit-identical) without a

@@ -144,6 +144,8 @@ struct pscl_handle {
     hipEvent_t ev_base[kDlPar] = {}, ev_retry[kDlPar] = {}, ev_join[kChainSets] = {};
     int32_t* h_count = nullptr;          // pinned: failing-frame counts of the chunk parities
     double* d_beta = nullptr;         // [K][K] DL-SCL flip metric (null = |L0|)
+    float* d_beta32g[2] = {nullptr, nullptr};  // K = 64: fp32 beta, [K][G][K / G] for G = 8, 4 (fused post)
+    std::vector<float> beta32g_host;
     double beta_absmax = 0.0;         // max |beta| (dl_post_kernel's certificate)
     std::vector<double> beta_host;    // staging of the last pscl_set_beta upload (stream-ordered copy)
     uint64_t* d_epi = nullptr;        // scl128 epilogue tables (gather + syndrome)
@@ -181,6 +183,7 @@ struct pscl_handle {
     int64_t tune[PSCL_TUNE_COUNT] = {};  // pscl_set_tuning knobs (0 = the default schedule)
     double host_call_ms = 0.0, host_wait_ms = 0.0;  // pscl_host_stats
     int64_t host_calls = 0;
+    int64_t n_fpost_rounds = 0, n_post_rounds = 0, n_fused_tx = 0;  // pscl_path_stats
 };
 
 namespace {
@@ -667,6 +670,8 @@ int pscl_destroy(pscl_handle* h) {
     if (h->d_rm_src) hipFree(h->d_rm_src);
     if (h->d_rm_order) hipFree(h->d_rm_order);
     if (h->d_beta) hipFree(h->d_beta);
+    for (int i = 0; i < 2; ++i)
+        if (h->d_beta32g[i]) hipFree(h->d_beta32g[i]);
     if (h->d_epi) hipFree(h->d_epi);
     if (h->d_xtab) hipFree(h->d_xtab);
     if (h->d_crctab) hipFree(h->d_crctab);
@@ -783,7 +788,7 @@ int pscl_set_pipelined(pscl_handle* h, int enable) {
 int pscl_set_tuning(pscl_handle* h, int knob, int64_t value) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
     static const int64_t lim[PSCL_TUNE_COUNT][2] = {{0, 0}, {0, 2}, {0, 64}, {0, 2}, {0, 1}, {0, 4096}, {0, PSCL_MAX_WAVES_PER_WG}, {0, 2},
-                                                    {0, (int64_t)1 << 30}, {0, 2}, {0, 32}, {0, 3}, {0, 2}};
+                                                    {0, (int64_t)1 << 30}, {0, 2}, {0, 32}, {0, 3}, {0, 2}, {0, 2}};
     if (knob < 1 || knob >= PSCL_TUNE_COUNT) return fail(PSCL_EINVAL, "unknown tuning knob %d", knob);
     if (value < lim[knob][0] || value > lim[knob][1] || (knob == PSCL_TUNE_POST_GRID && value && value < 16))
         return fail(PSCL_EINVAL, "tuning knob %d: value %lld out of range", knob, (long long)value);
@@ -840,6 +845,10 @@ int pscl_set_beta(pscl_handle* h, const double* beta) {
     if (!beta) {
         if (h->d_beta) HIP_TRY(hipFree(h->d_beta));
         h->d_beta = nullptr;
+        for (int i = 0; i < 2; ++i) {
+            if (h->d_beta32g[i]) HIP_TRY(hipFree(h->d_beta32g[i]));
+            h->d_beta32g[i] = nullptr;
+        }
         return PSCL_OK;
     }
     if (h->K == 0) return fail(PSCL_EINVAL, "beta must be a square matrix matching abs_l0 length");
@@ -851,6 +860,20 @@ int pscl_set_beta(pscl_handle* h, const double* beta) {
     HIP_TRY(hipStreamSynchronize(h->stream));
     h->beta_host.assign(beta, beta + n);
     HIP_TRY(hipMemcpyAsync(h->d_beta, h->beta_host.data(), n * 8, hipMemcpyHostToDevice, h->stream));
+    if (h->K == 64) {  // the fused post pass's layouts: lane p's candidates p + G i contiguous per row k
+        const int K = h->K;
+        h->beta32g_host.assign(2 * n, 0.0f);
+        for (int gi = 0; gi < 2; ++gi) {
+            const int G = gi ? 4 : 8, NC = K / G;
+            for (int k = 0; k < K; ++k)
+                for (int pp = 0; pp < G; ++pp)
+                    for (int i = 0; i < NC; ++i)
+                        h->beta32g_host[(size_t)gi * n + ((size_t)k * G + pp) * NC + i] = (float)beta[(size_t)k * K + pp + G * i];
+            if (!h->d_beta32g[gi]) HIP_TRY(hipMalloc(&h->d_beta32g[gi], n * 4));
+            HIP_TRY(hipMemcpyAsync(h->d_beta32g[gi], h->beta32g_host.data() + (size_t)gi * n, n * 4, hipMemcpyHostToDevice,
+                                   h->stream));
+        }
+    }
     double mx = 0.0;
     bool nan = false;
     for (size_t i = 0; i < n; ++i) {
@@ -865,6 +888,9 @@ int pscl_set_beta(pscl_handle* h, const double* beta) {
 }
 
 // retry rounds of one chunk on the retry stream (state sized for the largest chunk)
+#ifndef PSCL_DL_FUSED_POST_DEFAULT
+#define PSCL_DL_FUSED_POST_DEFAULT 0
+#endif
 namespace {
 struct DlState {
     int64_t* act;     // [cap] frame index of each entry (a slice of the chunk's dl_compact output)
@@ -965,11 +991,26 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     const bool scr = dl_screen && h->screen && S.dcnt && S.ob2 && side && pscl_screening_fs_available(H);
     pscl_decode_params HA, HX;
     pscl_post_params QD;
+    bool fpost = false;  // the main chain's post pass inside its screened retry decodes
     if (scr) {
         HA = H;
         HA.apx = 1;
         pscl_decode_layout(HA, 0);  // (no exp table in LDS)
         HA.no_lane = h->tune[PSCL_TUNE_DL_RETRY_LANE] == 2 ? 1 : 0;  // (lane-per-path FS kernel by default)
+        const int64_t fk = h->tune[PSCL_TUNE_DL_FUSED_POST];
+        pscl_decode_params T = HA;  // (the rounds' launches: bucket lists in and deferred lists out)
+        T.elist = lists[0];
+        T.bcount = S.bcnt;
+        T.amb_elist = S.dlist;
+        T.amb_count = S.dcnt;
+        fpost = (fk == 1 || (fk == 0 && PSCL_DL_FUSED_POST_DEFAULT)) && !HA.no_lane && pscl_lane_fs_available(T) &&
+                h->K == 64 && (!h->d_beta || h->d_beta32g[h->L == 8 ? 0 : 1]);
+        if (fpost) {
+            HA.fpost = 1;
+            HA.fp = Q;
+            HA.fp.init = 0;
+            HA.fp_beta32g = h->d_beta ? h->d_beta32g[h->L == 8 ? 0 : 1] : nullptr;
+        }
         HX = H;
         HX.best = S.ob2;
         HX.flags = S.of2;
@@ -991,6 +1032,12 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
             HA.bcount = H.bcount;
             HA.amb_elist = side_list(r);  // (the side chain's round-r list: appended beside QD(r - 1))
             HA.amb_count = side_cnt(r);
+            if (fpost) {  // the round's survivors to the next round's lists, filed by the decode itself
+                HA.fp.in_count = H.bcount;
+                HA.fp.in_list = lists[r & 1];
+                HA.fp.out_count = S.bcnt + (size_t)(r + 1) * bstride;
+                HA.fp.out_list = lists[(r + 1) & 1];
+            }
             if ((e = pscl_launch_decode(HA, 0, st)) != hipSuccess)
                 return fail(PSCL_EDEVICE, "screening retry decode: %s", hipGetErrorString(e));
             HIP_TRY(hipEventRecord(ev_s, st));
@@ -1009,6 +1056,11 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
         } else if ((rc = launch_decode(h, H, 0, st))) {
             return rc;
         }
+        if (fpost) {  // (the decode ran the main chain's post pass)
+            h->n_fpost_rounds++;
+            continue;
+        }
+        h->n_post_rounds++;
         Q.in_count = H.bcount;
         Q.in_list = lists[r & 1];
         Q.out_count = S.bcnt + (size_t)(r + 1) * bstride;
@@ -1673,6 +1725,7 @@ int simulate_enqueue(pscl_handle* h, uint64_t seed, uint32_t stream_id, double e
         TxSpec tx;
         const bool fused = tx_fused_applies(h, k_payload);
         if (fused) {
+            h->n_fused_tx++;
             tx.k0 = (uint32_t)seed;
             tx.k1 = (uint32_t)(seed >> 32) ^ (stream_id * 0x85EBCA6Bu);  // (channel_kernel's key)
             tx.frame0 = frame0 + f;
@@ -1955,6 +2008,14 @@ int pscl_host_stats(pscl_handle* h, double* call_ms, double* wait_ms, int64_t* c
         h->host_call_ms = h->host_wait_ms = 0.0;
         h->host_calls = 0;
     }
+    return PSCL_OK;
+}
+
+int pscl_path_stats(pscl_handle* h, int64_t* fused_post_rounds, int64_t* post_rounds, int64_t* fused_tx_blocks) {
+    if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    if (fused_post_rounds) *fused_post_rounds = h->n_fpost_rounds;
+    if (post_rounds) *post_rounds = h->n_post_rounds;
+    if (fused_tx_blocks) *fused_tx_blocks = h->n_fused_tx;
     return PSCL_OK;
 }
 

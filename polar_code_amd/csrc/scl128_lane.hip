@@ -78,7 +78,17 @@ struct LaneLayout {
     // conflicts against 4.5 %: the L = 4 kernel's occupancy is bound by its VGPRs, not its LDS)
     static constexpr int FRES = LMAX == 8 ? 16 : 24;
     static constexpr int FSTRIDE = RAW + (((FRES - RAW) % 32) + 32) % 32;
+    // the fused post pass's FS instance replays the best path's 128 leaves in the frame's region
+    // (208 doubles at L = 8; at L = 4 the stride grows 120 -> 152, still = 24 mod 32)
+    static constexpr int FSTRIDE_FS = FSTRIDE >= 128 ? FSTRIDE : FSTRIDE + 32;
 };
+
+// monotone map of an fp64 to uint64 (total order of non-NaN values, -0 == +0), as dlscl.hip
+__device__ __forceinline__ uint64_t flip_order_key(double q) {
+    if (q == 0.0) q = 0.0;
+    const uint64_t u = pscl_asu64(q);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
+}
 
 // L = 4: keep the lane's 32 channel LLRs in registers across the frame (1) or re-read them at each
 // depth-1..3 recompute (0).  Measured (tools/ab_bench.sh, config 2, two rounds): 1.649 / 1.655 ms
@@ -154,10 +164,14 @@ __device__ __forceinline__ void tx_frame_words(const pscl_decode_params& P, uint
 // the DL-SCL counter pass), the rows of the frames whose best candidate fails the CRC or that are
 // deferred (the retry and exact decodes read them; regenerated, ~1 % of frames at 5 dB), and the
 // uncoded BPSK baseline of the same payloads (channel_kernel's draws 0x40000000 + c).
-template <int LMAX, int CODE, bool FS = false, bool TXF = false>
+// FP: the FS instance with the fused post pass (P.fpost; its own instantiation -- compiled into the
+// plain FS instance behind a runtime flag, the post's registers raised that kernel's peak too,
+// L = 8 173 -> 226 VGPRs, L = 4 240 -> 256 + 26 spilled)
+template <int LMAX, int CODE, bool FS = false, bool TXF = false, bool FP = false>
 __global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(const pscl_decode_params P) {
     static_assert(LMAX == 4 || LMAX == 8, "the lane-per-path decoder is built for L = 4 and 8");
     static_assert(!TXF || (!FS && CODE == 1), "fused TX: plain decodes of the (128,64) code");
+    static_assert(!FP || (FS && CODE == 1), "fused post pass: the FS instance of the (128,64) code");
     using Ly = LaneLayout<LMAX>;
     constexpr int G = Ly::G, F = Ly::F, LOG_G = Ly::LOG_G;
     constexpr int EPL = 16 / G;                 // depth-3 elements per lane at a recompute
@@ -177,7 +191,7 @@ __global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PS
     const int lane_hi = REMAP ? (lane & ~15) + (inner ? 4 : 12) : lane_lo + 4;
     // the lane of path index q of this frame
     auto lane_of = [&](uint32_t q) -> int { return REMAP ? (q < 4u ? lane_lo + (int)q : lane_hi + (int)q - 4) : lane_lo + (int)q; };
-    double* const Af = A + fl * Ly::FSTRIDE;
+    double* const Af = A + fl * (FP ? Ly::FSTRIDE_FS : Ly::FSTRIDE);
     const uint8_t* const GT = reinterpret_cast<const uint8_t*>(P.epi_table);   // [16][256] u-byte -> info bits
     const uint32_t* const ST = reinterpret_cast<const uint32_t*>(GT + 16 * 256);  // [K/4][16] nibble -> syndrome
     auto hiw = [](double m) { return (uint32_t)(pscl_asu64(m) >> 32); };
@@ -198,6 +212,7 @@ __global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PS
 
     int cfe = 0, cbe = 0, cpe = 0, cpb = 0;  // this lane's error counts (flushed at the end)
     int tufe = 0, tube = 0;                  // TXF: the uncoded baseline's errors
+    int pdecodes = 0;                        // FS with the fused post pass: attempts recorded
     // frames of the launch: P.B, or (FS) the total of the round's bucket lists
     int bpre[PSCL_DL_NSEG + 1];
     int64_t Bn = P.B;
@@ -720,6 +735,281 @@ __global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PS
             static_for<kN>([&](auto PC) { phase(PC); });
         }
 
+        // ---- the fused post pass of a screened retry round (P.fpost; dl_post_kernel's work, dlscl.hip,
+        // for this wavefront's entries, G lanes each: flip.py:97-136).  Per frame: the attempt's
+        // best bits, flags and attempt count to the frame (the attempt just decoded is its latest,
+        // flip.py:123-136); for a failing frame with flips left, the leaves of its best path replayed
+        // top-down in place in the frame's LDS region (bit-identical to the decode's own: f/g of the
+        // same values), the next flip -- q = |L0| @ beta, argmin over the untried (q, index),
+        // flip.py:104-111, by the packed fp32 sums with dl_post_kernel's certificate, else the exact
+        // fp64 sums in index order -- its force words (flip.py:30-34), the warm-start state of its
+        // forced prefix (bits, and metrics summed from the screening tail: a screened decode's own,
+        // whose per-increment error the certificate already covers), and the append
+        // to the next round's bucket list (one atomic per bucket and wavefront).
+        auto fused_post = [&](bool x_amb, bool x_live, uint32_t x_keyb, uint32_t x_kbest, uint64_t x_ib0, uint64_t x_ib1,
+                              uint64_t x_u0, uint64_t x_u1, int64_t x_frow, int64_t e, bool x_valid) {
+            static_assert(!REMAP, "the fused post pass assumes frames of G consecutive lanes");
+            const pscl_post_params& Q = P.fp;
+            constexpr int NC = K / G;  // flip candidates per lane: j = p + G i
+            const uint32_t fl = (x_kbest < (uint32_t)LMAX ? PSCL_FLAG_CRC_PASS : 0u) | (x_kbest & (uint32_t)(LMAX - 1));
+            const bool mine = x_valid && !x_amb;  // (deferred frames: the side chain's)
+            int nt = 0;
+            uint64_t t0 = 0, t1 = 0;
+            if (mine) {
+                nt = Q.ntried[e];
+                t0 = Q.tried[2 * e];
+                t1 = Q.tried[2 * e + 1];
+            }
+            // the best path's lane: its information bits and path bits to every lane of the frame
+            const uint32_t bfb = frame_bits(wmask(x_live && x_keyb == x_kbest));
+            const int bsrc = lane_lo + (bfb ? __builtin_ctz(bfb) : 0);
+            const uint64_t bi0 = shfl_u64(x_ib0, bsrc), bi1 = PW > 1 ? shfl_u64(x_ib1, bsrc) : 0ULL;
+            const uint64_t bu0 = shfl_u64(x_u0, bsrc), bu1 = shfl_u64(x_u1, bsrc);
+            if (mine && p == 0) {
+                Q.best[x_frow * PW] = bi0;
+                if (PW > 1) Q.best[x_frow * PW + 1] = bi1;
+                Q.flags[x_frow] = (uint8_t)fl;
+                if (Q.attempts) Q.attempts[x_frow] = nt + 1;
+                ++pdecodes;
+            }
+            const bool more = mine && !(fl & PSCL_FLAG_CRC_PASS) && nt < Q.rounds;
+            if (wmask(more) == 0) return;
+            // ---- replay: level d maps the pair (q, q + w) of depth d - 1 to (f, g) in place.  The
+            // channel row is read again (L2): kept in the registers c[] until here, it would stay
+            // live through the last 16 phases and raise the kernel's register peak by its size
+            wave_lds_fence();  // (the decode's last reads of the region)
+            {
+                const double* crow = P.llr + x_frow * kN;
+#pragma unroll
+                for (int j = 0; j < kN / G; ++j) Af[p + G * j] = crow[p + G * j];
+            }
+            wave_lds_fence();
+            auto stage = [](uint64_t x, int st) {
+                const uint64_t M = st == 1 ? 0x5555555555555555ULL : st == 2 ? 0x3333333333333333ULL
+                                 : st == 4 ? 0x0f0f0f0f0f0f0f0fULL : st == 8 ? 0x00ff00ff00ff00ffULL
+                                 : st == 16 ? 0x0000ffff0000ffffULL : 0x00000000ffffffffULL;
+                return x ^ ((x >> st) & M);
+            };
+            uint64_t X0 = bu0, X1 = bu1;  // X_lw = u after butterfly stages 1 .. 2^(lw - 1) (dlscl.hip)
+#pragma unroll
+            for (int mm = 1; mm < kn; ++mm) {
+                X0 = stage(X0, 1 << (mm - 1));
+                X1 = stage(X1, 1 << (mm - 1));
+            }
+            // (rolled loops below: unrolled, the compiler issues a whole level's LDS reads before its
+            // writes and the kernel's register peak moves here -- 256 VGPRs and spills)
+            static_for<kn>([&](auto DC) {
+                constexpr int lw2 = kn - 1 - decltype(DC)::value, w2 = 1 << lw2;
+                const bool act_l = w2 >= G || (p & w2) == 0;  // (w2 < G: the lane of the pair's first half)
+                if (act_l) {
+#pragma unroll 2
+                    for (int j = 0; j < kN / G; ++j) {
+                        const int q = p + G * j;
+                        if (w2 >= G && (q & w2)) continue;  // (the pair's second half)
+                        const double a = Af[q], b = Af[q + w2];
+                        const uint32_t bit = (uint32_t)(((q >> 6) ? X1 : X0) >> (q & 63)) & 1u;
+                        Af[q] = f_minsum(a, b);
+                        Af[q + w2] = g_node(a, b, bit);
+                    }
+                }
+                wave_lds_fence();
+                if constexpr (lw2 > 0) {
+                    X0 = stage(X0, w2 >> 1);
+                    X1 = stage(X1, w2 >> 1);
+                }
+            });
+            // ---- next flip: q_j = |L0| @ beta (packed fp32, certified) or |L0|
+            float qv[NC];  // (fp32 sums, exactly widened; the exact fallback keeps its own fp64 sums)
+            double as = 0.0;
+            uint64_t bk = ~0ULL;
+            int bj = 0x7fffffff;
+            auto seen_j = [&](int j) { return (((j < 64 ? t0 : t1) >> (j & 63)) & 1ULL) != 0; };
+            auto argmin = [&]() {
+                bk = ~0ULL;
+                bj = 0x7fffffff;
+#pragma unroll
+                for (int i = 0; i < NC; ++i) {
+                    const int j = p + G * i;
+                    const uint64_t key = seen_j(j) ? ~0ULL : flip_order_key((double)qv[i]);
+                    if (key < bk) {  // (increasing j: ties keep the lower index)
+                        bk = key;
+                        bj = j;
+                    }
+                }
+#pragma unroll
+                for (int sft = 1; sft < G; sft <<= 1) {
+                    const uint64_t ok = shfl_u64(bk, lane ^ sft);
+                    const int oj = __shfl(bj, lane ^ sft);
+                    if (ok < bk || (ok == bk && oj < bj)) {
+                        bk = ok;
+                        bj = oj;
+                    }
+                }
+            };
+            // exact fallback: index-order sums, each product and sum rounded (numpy's abs_l0 @ beta), and
+            // the argmin over them (its own fp64 keys)
+            auto argmin_exact = [&]() {
+                bk = ~0ULL;
+                bj = 0x7fffffff;
+#pragma unroll 1
+                for (int i = 0; i < NC; ++i) {
+                    const int j = p + G * i;
+                    double qx = 0.0;
+#pragma unroll 1
+                    for (int k = 0; k < K; ++k) qx = qx + fabs(Af[Q.info_set[k]]) * Q.beta[k * K + j];
+                    const uint64_t key = seen_j(j) ? ~0ULL : flip_order_key(qx);
+                    if (key < bk) {
+                        bk = key;
+                        bj = j;
+                    }
+                }
+#pragma unroll
+                for (int sft = 1; sft < G; sft <<= 1) {
+                    const uint64_t ok = shfl_u64(bk, lane ^ sft);
+                    const int oj = __shfl(bj, lane ^ sft);
+                    if (ok < bk || (ok == bk && oj < bj)) {
+                        bk = ok;
+                        bj = oj;
+                    }
+                }
+            };
+            if (Q.beta) {
+                typedef float f2 __attribute__((ext_vector_type(2)));
+                // candidates in blocks of 8 (L = 4: two passes over k), each k's |L0| read from the
+                // leaves: fewer accumulators and loads in flight (registers, see the replay)
+                constexpr int CB = NC < 8 ? NC : 8;
+                const f2* bg = reinterpret_cast<const f2*>(P.fp_beta32g) + p * (NC / 2);
+#pragma unroll
+                for (int cb = 0; cb < NC / CB; ++cb) {
+                    f2 acc[CB / 2];
+#pragma unroll
+                    for (int i = 0; i < CB / 2; ++i) acc[i] = (f2){0.0f, 0.0f};
+#pragma unroll 2
+                    for (int k = 0; k < K; ++k) {
+                        const double ad = fabs(Af[Q.info_set[k]]);
+                        if (cb == 0) as = as + ad;
+                        const float a32 = (float)ad;
+#pragma unroll
+                        for (int i = 0; i < CB / 2; ++i)
+                            acc[i] = __builtin_elementwise_fma((f2){a32, a32}, bg[k * G * (NC / 2) + cb * (CB / 2) + i], acc[i]);
+                    }
+#pragma unroll
+                    for (int i = 0; i < CB / 2; ++i) {
+                        qv[cb * CB + 2 * i] = acc[i].x;
+                        qv[cb * CB + 2 * i + 1] = acc[i].y;
+                    }
+                }
+                argmin();
+                // dl_post_kernel's certificate of the packed fp32 sums (dlscl.hip): every other untried
+                // candidate's sum above the best one's by twice the error bound, else the exact sums
+                const double gk = (4.0 * (double)K + 8.0) * 0x1p-53;
+                const double e2 = (as < 0x1p100 && as * Q.beta_absmax < 0x1p100)
+                                      ? 2.04 * (as * Q.beta_absmax * (((double)K + 2.01) * 0x1p-24 + 0.5 * gk)
+                                                + (double)K * 0x1p-149 + as * 0x1p-150 + (double)K * Q.beta_absmax * 0x1p-150)
+                                      : __builtin_inf();
+                double qmine = qv[0];
+#pragma unroll
+                for (int i = 1; i < NC; ++i) qmine = (bj >> LOG_G) == i ? (double)qv[i] : qmine;
+                const double qb = pscl_asf64(shfl_u64(pscl_asu64(qmine), lane_lo + (bj & (G - 1))));
+                const double thr = qb + e2 * (1.0 + 0x1p-40);
+                bool near = false;
+#pragma unroll
+                for (int i = 0; i < NC; ++i) {
+                    const int j = p + G * i;
+                    near = near || (j != bj && !seen_j(j) && !((double)qv[i] > thr));
+                }
+                const bool fnear = frame_bits(wmask(near)) != 0;
+                if (wmask(fnear && more) != 0) {
+                    const int bj0 = bj;
+                    argmin_exact();
+                    if (!(fnear && more)) bj = bj0;  // (frames whose certificate held keep theirs)
+                }
+            } else {
+                // (|L0| itself: argmin over the fp64 values, flip.py:107)
+                bk = ~0ULL;
+                bj = 0x7fffffff;
+#pragma unroll 1
+                for (int i = 0; i < NC; ++i) {
+                    const int j = p + G * i;
+                    const uint64_t key = seen_j(j) ? ~0ULL : flip_order_key(fabs(Af[Q.info_set[j]]));
+                    if (key < bk) {
+                        bk = key;
+                        bj = j;
+                    }
+                }
+#pragma unroll
+                for (int sft = 1; sft < G; sft <<= 1) {
+                    const uint64_t ok = shfl_u64(bk, lane ^ sft);
+                    const int oj = __shfl(bj, lane ^ sft);
+                    if (ok < bk || (ok == bk && oj < bj)) {
+                        bk = ok;
+                        bj = oj;
+                    }
+                }
+            }
+            const int idx = bj;  // (frame-uniform) an untried index exists: rounds <= min(retries, K)
+            int seg = Q.info_set[idx < K ? idx : 0] >> 4;
+            if (seg > PSCL_DL_NSEG - 1) seg = PSCL_DL_NSEG - 1;
+            // ---- warm state: the forced prefix's metric at each 16-phase boundary, from the screening
+            // tail (this kernel's own increments: good child + L, bad child + |lam| + L)
+            double bs[PSCL_DL_NSEG];
+#pragma unroll
+            for (int b = 0; b < PSCL_DL_NSEG; ++b) {  // block b: the lane's phases q = p + G j in [16 b, 16 b + 16)
+                double acc_b = 0.0;
+#pragma unroll
+                for (int jj = 0; jj < 16 / G; ++jj) {
+                    const int q = p + G * (b * (16 / G) + jj);
+                    const double lam = Af[q];
+                    const uint32_t ubit = (uint32_t)(((q >> 6) ? bu1 : bu0) >> (q & 63)) & 1u;
+                    const double Lt = pscl_softplus_tail_abs(lam);
+                    const bool good = ubit == sign_bit(lam);
+                    acc_b = acc_b + (good ? Lt : fabs(lam) + Lt);
+                }
+                bs[b] = acc_b;
+            }
+#pragma unroll
+            for (int b = 0; b < PSCL_DL_NSEG; ++b)
+#pragma unroll
+                for (int sft = 1; sft < G; sft <<= 1) bs[b] = bs[b] + pscl_asf64(shfl_u64(pscl_asu64(bs[b]), lane ^ sft));
+            if (more && p == 0) {
+                double mt = 0.0;
+                double* wm = Q.warm_metric + e * PSCL_DL_NSEG;
+#pragma unroll
+                for (int k = 0; k < PSCL_DL_NSEG; ++k) {
+                    if (k <= seg) wm[k] = mt;
+                    mt = mt + bs[k];
+                }
+                Q.warm_u[2 * e] = bu0;
+                Q.warm_u[2 * e + 1] = bu1;
+                Q.tried[2 * e] = idx < 64 ? (t0 | (1ULL << idx)) : t0;
+                Q.tried[2 * e + 1] = idx >= 64 ? (t1 | (1ULL << (idx - 64))) : t1;
+                Q.ntried[e] = nt + 1;
+                if (Q.tried_out) Q.tried_out[x_frow * Q.tried_stride + nt] = idx;
+                // _force_vector (flip.py:30-34): bits [0, idx) = reference, bit idx flipped, rest free
+                uint64_t* fr = Q.force + e * 2 * PW;
+#pragma unroll
+                for (int w = 0; w < PW; ++w) {
+                    const int lo = 64 * w, nb = idx - lo + 1;
+                    const uint64_t mask = nb <= 0 ? 0ULL : (nb >= 64 ? ~0ULL : ((1ULL << nb) - 1ULL));
+                    uint64_t val = (w ? bi1 : bi0) & mask;
+                    if (idx >= lo && idx < lo + 64) val ^= 1ULL << (idx - lo);
+                    fr[w] = mask;
+                    fr[PW + w] = val;
+                }
+            }
+            // ---- append to bucket seg of the next round: one atomic per (bucket, wavefront)
+#pragma unroll
+            for (int sg = 0; sg < PSCL_DL_NSEG; ++sg) {
+                const uint64_t mm = wmask(more && p == 0 && seg == sg);
+                if (mm == 0) continue;
+                int base = 0;
+                if (lane == (int)__builtin_ctzll(mm)) base = atomicAdd(Q.out_count + sg * PSCL_DL_CSTRIDE, __popcll(mm));
+                base = __shfl(base, (int)__builtin_ctzll(mm));
+                if ((mm >> lane) & 1ULL)
+                    Q.out_list[(int64_t)sg * Q.cap + base + __popcll(mm & ((1ULL << lane) - 1ULL))] = (int32_t)e;
+            }
+            wave_lds_fence();  // (the next frame's decode rewrites the region)
+        };
         // fused TX: the message words formed again for the epilogue from an opaque copy of the frame
         // counter -- left to itself the compiler reuses the frame start's draws and keeps them live
         // across the whole decode (with the rows' draws: +75 VGPRs, 2 waves/SIMD instead of 3)
@@ -778,8 +1068,9 @@ __global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PS
         amb |= wmask(near && live) & vmask;
         const bool famb = frame_bits(amb) != 0;
         if (famb && p == 0 && fvalid) {
-            if constexpr (FS) {  // DL-SCL retry round: into the entry's deferred bucket
-                const int fseg = pscl_bucket_of(fsafe, bpre);
+            if constexpr (FS) {  // DL-SCL retry round: into the entry's deferred bucket (with the
+                                 // fused post pass bucket 0: its warm metric is a screening one)
+                const int fseg = FP ? 0 : pscl_bucket_of(fsafe, bpre);
                 const int slot = atomicAdd(P.amb_count + fseg * PSCL_DL_CSTRIDE, 1);
                 P.amb_elist[(int64_t)fseg * P.bcap + slot] = (int32_t)f;
                 P.flags[f] = PSCL_DL_DEFERRED;
@@ -805,6 +1096,9 @@ __global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PS
                 tally_errors(ibw, TXF ? tm : P.ref + fi * PW, PW, P.k_payload, bpass, cfe, cbe, cpe, cpb);
             }
         }
+        if constexpr (FS) {
+            if constexpr (FP) fused_post(famb, live, keyb, kbest, ib0, ib1, u0, u1, frow, f, fvalid);
+        }
         if constexpr (TXF) {
             // the message words of every frame (the counts' reference; the rows of the frames the exact
             // re-decode or the retry chain will read are written by tx_rows_kernel, scl_kernels.hip)
@@ -819,6 +1113,12 @@ __global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PS
         flush_counts_p(P, blockIdx.x, cfe, cbe, cpe, cpb);
         if (blockIdx.x == 0 && threadIdx.x == 0)
             atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
+    }
+    if constexpr (FS) {
+        if (FP && P.fp.counters && __builtin_amdgcn_ballot_w64(pdecodes != 0)) {
+            const int d = wave_sum(pdecodes);
+            if (lane == 0) atomicAdd(reinterpret_cast<unsigned long long*>(P.fp.counters) + PSCL_CNT_RETRIES, (unsigned long long)d);
+        }
     }
     if constexpr (TXF) {
         if (P.tx_upart && __builtin_amdgcn_ballot_w64((tufe | tube) != 0)) {
@@ -870,11 +1170,19 @@ hipError_t pscl_launch_lane(const pscl_decode_params& P, int64_t grid, hipStream
 
 // the lane-per-path forced-bit screening launch of a DL-SCL retry round (pscl_lane_fs_available)
 hipError_t pscl_launch_lane_fs(const pscl_decode_params& P, int64_t grid, hipStream_t s) {
-    const int lds8 = LaneLayout<8>::F * LaneLayout<8>::FSTRIDE * 8, lds4 = LaneLayout<4>::F * LaneLayout<4>::FSTRIDE * 8;
+    const int lds8 = LaneLayout<8>::F * (P.fpost ? LaneLayout<8>::FSTRIDE_FS : LaneLayout<8>::FSTRIDE) * 8,
+              lds4 = LaneLayout<4>::F * (P.fpost ? LaneLayout<4>::FSTRIDE_FS : LaneLayout<4>::FSTRIDE) * 8;
+    if (P.fpost && (P.K != 64 || (P.fp.beta && !P.fp_beta32g))) return hipErrorInvalidValue;
     if (P.L == 8)
-        hipLaunchKernelGGL((scl_lane_kernel<8, 1, true>), dim3((unsigned)grid), dim3(64), lds8, s, P);
+        if (P.fpost)
+            hipLaunchKernelGGL((scl_lane_kernel<8, 1, true, false, true>), dim3((unsigned)grid), dim3(64), lds8, s, P);
+        else
+            hipLaunchKernelGGL((scl_lane_kernel<8, 1, true>), dim3((unsigned)grid), dim3(64), lds8, s, P);
     else if (P.L == 4)
-        hipLaunchKernelGGL((scl_lane_kernel<4, 1, true>), dim3((unsigned)grid), dim3(64), lds4, s, P);
+        if (P.fpost)
+            hipLaunchKernelGGL((scl_lane_kernel<4, 1, true, false, true>), dim3((unsigned)grid), dim3(64), lds4, s, P);
+        else
+            hipLaunchKernelGGL((scl_lane_kernel<4, 1, true>), dim3((unsigned)grid), dim3(64), lds4, s, P);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();

@@ -17,6 +17,46 @@
 #define PSCL_EPI_LDS 1
 #endif
 
+// DL-SCL retry rounds (dlscl.hip, dl_post_kernel): entry e = one failing frame's retry state.
+// One pass per round over the entries just decoded: replay of the attempt's best path (its
+// leaf LLRs), final-attempt bookkeeping and the CRC stop rule, then for the survivors the next
+// flip (q = |L0| @ beta), its force words, the warm-start state of its forced prefix and the
+// append to the next round's bucket list.  init = 1: the first pass, over the baseline.
+struct pscl_post_params {
+    const double* llr;           // channel LLRs [.][N] (or [.][E] with rate matching)
+    int N, n, K, W, rm_E;
+    const int32_t* rm_src;
+    uint64_t info_mask[2];
+    const int32_t* info_set;     // [K] (device)
+    const uint64_t* exp_table;   // glibc exp table (exact metric tails)
+    int rounds;                  // min(retries, K)
+    int narrow;                  // small workgroups, beta through L2 (pipelined calls, dl_post_kernel)
+    int64_t grid_cap;            // 0, or the workgroup cap of a launch (tuning knob; default PSCL_POST_GRID)
+    int64_t pairs;               // 0, or the entry pairs per wavefront the grid is sized for (tuning knob)
+    int init;
+    const int32_t* in_count;     // bucket counts of this round (init: unused, cap entries)
+    const int32_t* in_list;      // bucket lists of this round ([NSEG][cap] entry ids)
+    int64_t cap;
+    int32_t* out_count;          // next round's bucket counts (zeroed)
+    int32_t* out_list;           // [NSEG][cap]
+    const int64_t* act;          // [cap] frame index (LLR row) of each entry
+    uint64_t* tried;             // [cap][2] tried-index bit sets
+    int32_t* ntried;             // [cap]
+    const double* beta;          // [K][K] or null
+    double beta_absmax;          // max |beta| (the flip metric certificate's bound)
+    uint64_t* force;             // [cap][2][W]
+    double* warm_metric;         // [cap][NSEG]
+    uint64_t* warm_u;            // [cap][2]
+    const uint64_t* ob;          // [cap][W] this round's best bits, by entry
+    const uint8_t* of;           // [cap]
+    uint64_t* best;              // [B][W] final best bits (per frame)
+    uint8_t* flags;              // [B]
+    int32_t* attempts;           // [B] or null
+    int32_t* tried_out;          // [B][tried_stride] or null
+    int tried_stride;
+    int64_t* counters;           // or null: PSCL_CNT_RETRIES += decodes
+};
+
 struct pscl_decode_params {
     const double* llr;  // [B][N]
     int64_t B;
@@ -101,6 +141,15 @@ struct pscl_decode_params {
     uint64_t* tx_msg;            // [B][W]
     int32_t* tx_upart;           // [slots][4] (frame, bit errors, 0, 0) of the uncoded baseline, or null
     int64_t* tx_unc_counters;    // its counters (the frame count is added here)
+    // fused post pass (scl_lane_kernel FS, PSCL_TUNE_DL_FUSED_POST): a screened retry
+    // round's kernel runs dl_post_kernel's work for its own entries after decoding them -- bookkeeping,
+    // the CRC stop rule, the replay of the best path, the next flip and its warm state -- and files
+    // the survivors in fp.out_list; fp holds the post pass's state arrays exactly as for
+    // dl_post_kernel.  Warm-start metrics are then the screening tail's (a screened decode's own);
+    // entries the round defers go to bucket 0 of the side list (their exact decode starts at phase 0).
+    int fpost;
+    pscl_post_params fp;
+    const float* fp_beta32g;     // beta in fp32, [K][G][K / G] (lane p's candidates p + G i contiguous), or null
 };
 
 #define PSCL_DL_NSEG 8     // 16-phase segments of N = 128: warm-start buckets
@@ -143,46 +192,6 @@ struct pscl_replay_params {
     const uint64_t* bits;        // info bits, [.][W] words
     int bits_by_row;             // 1: bits row = act[entry]; 0: bits row = list position
     double* out;                 // [entries][K] decision LLRs (signed), row = entry
-};
-
-// DL-SCL retry rounds (dlscl.hip, dl_post_kernel): entry e = one failing frame's retry state.
-// One pass per round over the entries just decoded: replay of the attempt's best path (its
-// leaf LLRs), final-attempt bookkeeping and the CRC stop rule, then for the survivors the next
-// flip (q = |L0| @ beta), its force words, the warm-start state of its forced prefix and the
-// append to the next round's bucket list.  init = 1: the first pass, over the baseline.
-struct pscl_post_params {
-    const double* llr;           // channel LLRs [.][N] (or [.][E] with rate matching)
-    int N, n, K, W, rm_E;
-    const int32_t* rm_src;
-    uint64_t info_mask[2];
-    const int32_t* info_set;     // [K] (device)
-    const uint64_t* exp_table;   // glibc exp table (exact metric tails)
-    int rounds;                  // min(retries, K)
-    int narrow;                  // small workgroups, beta through L2 (pipelined calls, dl_post_kernel)
-    int64_t grid_cap;            // 0, or the workgroup cap of a launch (tuning knob; default PSCL_POST_GRID)
-    int64_t pairs;               // 0, or the entry pairs per wavefront the grid is sized for (tuning knob)
-    int init;
-    const int32_t* in_count;     // bucket counts of this round (init: unused, cap entries)
-    const int32_t* in_list;      // bucket lists of this round ([NSEG][cap] entry ids)
-    int64_t cap;
-    int32_t* out_count;          // next round's bucket counts (zeroed)
-    int32_t* out_list;           // [NSEG][cap]
-    const int64_t* act;          // [cap] frame index (LLR row) of each entry
-    uint64_t* tried;             // [cap][2] tried-index bit sets
-    int32_t* ntried;             // [cap]
-    const double* beta;          // [K][K] or null
-    double beta_absmax;          // max |beta| (the flip metric certificate's bound)
-    uint64_t* force;             // [cap][2][W]
-    double* warm_metric;         // [cap][NSEG]
-    uint64_t* warm_u;            // [cap][2]
-    const uint64_t* ob;          // [cap][W] this round's best bits, by entry
-    const uint8_t* of;           // [cap]
-    uint64_t* best;              // [B][W] final best bits (per frame)
-    uint8_t* flags;              // [B]
-    int32_t* attempts;           // [B] or null
-    int32_t* tried_out;          // [B][tried_stride] or null
-    int tried_stride;
-    int64_t* counters;           // or null: PSCL_CNT_RETRIES += decodes
 };
 
 // DL-SCL post pass of the long codes (N > PSCL_FAST_N, dlscl.hip dl_post_long_kernel): the

@@ -138,6 +138,11 @@ def _dl_config(L, beta_name, ebno, nb, seed, tuning=None):
         dec.dlscl_device(d_llr, nb, R, beta=beta, d_best=d_best, d_flags=d_flags, d_attempts=d_att, d_ref=d_msg,
                          k_payload=kp, d_counters_scl=d_cs, d_counters_dl=d_cd)
         dec.sync()
+        paths = dec.path_stats()
+        if tuning and tuning.get("dl_fused_post") == 1:  # (the schedule under test ran)
+            assert paths["fused_post_rounds"] > 0 and paths["post_rounds"] == 0, paths
+        if tuning and tuning.get("dl_fused_post") == 2:
+            assert paths["fused_post_rounds"] == 0 and paths["post_rounds"] > 0, paths
         best = mem.download(d_best, nb * 8, np.uint64).reshape(nb, 1)
         flags = mem.download(d_flags, nb, np.uint8)
         att = mem.download(d_att, nb * 4, np.int32)
@@ -171,6 +176,9 @@ def test_config4_dlscl_L4_r8_beta4_1e6_frames_vs_oracle():
     (8, "M8", 4.5, 200_000, {"dl_screen": 1}),   # config 3's DL-SCL point (L = 8: lane-per-path FS retry decodes)
     (8, "M8", 4.0, 100_000, {"dl_screen": 1, "dl_retry_lane": 2}),  # the two-lanes-per-path screening instance
     (4, "M4", 5.0, 1_000_000, {"dl_screen": 1}),  # config 4 with every retry decode screened (L = 4 lane FS)
+    (8, "M8", 4.5, 200_000, {"dl_screen": 1, "dl_fused_post": 1}),  # the post pass fused into the retry decodes
+    (4, "M4", 5.0, 1_000_000, {"dl_screen": 1, "dl_fused_post": 1}),
+    (8, "M8", 4.5, 200_000, {"dl_screen": 1, "dl_fused_post": 2}),  # the separate post pass
 ])
 def test_dlscl_screened_retry_decodes_vs_oracle(L, beta, ebno, nb, tuning):
     """Screened DL-SCL retry rounds (forced-bit screening decodes + exact decodes of the entries

@@ -76,7 +76,9 @@ def test_device_retry_loop_golden(golden):
                                                    (4, 8, 1.5, "0"), (4, 8, 2.0, "1"), (8, 8, 2.5, "1"),
                                                    (8, 8, 2.5, "2"), (4, 8, 2.0, "adaptive"), (8, 8, 3.5, "1"),
                                                    (4, 8, 3.0, "1"), (8, 8, 2.5, "1/2lane"), (4, 8, 2.0, "1/2lane"),
-                                                   (4, 8, 3.0, "2")])
+                                                   (4, 8, 3.0, "2"), (8, 8, 2.5, "1/fp"), (4, 8, 2.0, "1/fp"),
+                                                   (8, 8, 3.5, "1/fp"), (4, 8, 3.0, "1/fp"), (8, 3, 1.5, "1/fp"),
+                                                   (8, 8, 2.5, "1/nofp"), (4, 8, 2.0, "1/nofp")])
 def test_device_retry_loop_equals_host_ranking(monkeypatch, M, retries, ebno, screen):
     """Device retry loop == numpy-ranked retries, frame by frame (3000 frames, ~30% failing);
     screen = 1: the retry decodes on the forced-bit screening instance (lane per path: per-frame
@@ -84,7 +86,8 @@ def test_device_retry_loop_equals_host_ranking(monkeypatch, M, retries, ebno, sc
     dl_screen = 1); "1/2lane": the same on the two-lanes-per-path instance (dl_retry_lane = 2);
     2: never (the exact forced-bit kernel); 0: the default (every chain screened where the list size
     has a screening instance, L = 4 and 8); "adaptive": the size-threshold rule with a threshold
-    every chain here exceeds (dl_screen_min = 1)."""
+    every chain here exceeds (dl_screen_min = 1); "1/fp" / "1/nofp": screened with the post pass
+    fused into the retry decodes or the separate dl_post_kernel (dl_fused_post = 1 / 2)."""
     from polar_code_amd.polar.polar import construct_info_set, encode
     from polar_code_amd.polar.crc import attach_crc
 
@@ -95,11 +98,19 @@ def test_device_retry_loop_equals_host_ranking(monkeypatch, M, retries, ebno, sc
     var = 1.0 / (2.0 * 0.5 * 10 ** (ebno / 10))
     llr = 2.0 * ((1.0 - 2.0 * encode(msg)) + rng.normal(0, math.sqrt(var), size=(3000, 128))) / var
     beta = np.load(GOLDEN / "beta_M4.npy")
+    shared = _native.get_decoder(128, info, M, "0x1864CFB")  # (the handle the device loop uses)
     for b in (beta, None):
+        p0 = shared.path_stats()
         dev = decode_with_retries_device(llr, info, M, retries, crc="0x1864CFB", beta=b,
                                          tuning=({"dl_screen": int(screen)} if screen.isdigit() else
                                                  {"dl_screen": 1, "dl_retry_lane": 2} if screen == "1/2lane" else
+                                                 {"dl_screen": 1, "dl_fused_post": 1} if screen == "1/fp" else
+                                                 {"dl_screen": 1, "dl_fused_post": 2} if screen == "1/nofp" else
                                                  {"dl_screen": 0, "dl_screen_min": 1}))
+        p1 = shared.path_stats()
+        if screen in ("1/fp", "1/nofp"):  # (the schedule under test ran)
+            fused, sep = p1["fused_post_rounds"] - p0["fused_post_rounds"], p1["post_rounds"] - p0["post_rounds"]
+            assert (fused > 0 and sep == 0) if screen == "1/fp" else (fused == 0 and sep > 0), (screen, fused, sep)
         host = decode_with_retries_batch(llr, info, M, retries, crc="0x1864CFB", beta=b)
         assert 0.05 < (~dev["base_pass"]).mean() < (0.97 if ebno < 2 else 0.9)
         np.testing.assert_array_equal(dev["tried"], host["tried"])

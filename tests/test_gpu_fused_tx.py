@@ -36,6 +36,7 @@ def test_fused_tx_simulate_equals_unfused(L, ebno):
     for fused in (True, False):
         dec = _decoder(L, fused, beta)
         out[fused] = dec.simulate(0, philox_stream_id(ebno), ebno, 0.5, 40, 7_777, B, 8, include_uncoded=True)
+        assert (dec.path_stats()["fused_tx_blocks"] > 0) == fused  # (the schedule under test ran)
         dec.close()
     np.testing.assert_array_equal(out[True], out[False])
     c = out[True]
@@ -64,6 +65,7 @@ def test_fused_tx_pipelined_sweep_equals_unfused(L):
                 dec.simulate_device(0, philox_stream_id(x), x, 0.5, 40, 0, B, 8, True, d)
             dec.join()
             dec.sync()
+            assert (dec.path_stats()["fused_tx_blocks"] >= len(pts)) == fused
             res[fused] = [mem.download(d, 3 * nc * 8, np.int64).reshape(3, nc) for d in d_cnt]
         dec.close()
     for i, x in enumerate(pts):

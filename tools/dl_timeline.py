@@ -22,7 +22,7 @@ def short(n):
     return n.split("(")[0][:48]
 
 
-base = [r for r in rows if "scl_lane_kernel<4, 1, false>" in r[2] or "scl_lane_kernel<8, 1, false>" in r[2]]
+base = [r for r in rows if "scl_lane_kernel<4, 1, false" in r[2] or "scl_lane_kernel<8, 1, false" in r[2]]
 if len(base) < first + max(nsteps, 1) + (nsteps > 0):
     sys.exit(f"only {len(base)} baseline decodes")
 # steps 0: from baseline decode `first` to the end of the trace (a standalone sweep point)
