@@ -15,8 +15,10 @@ READELF = Path("/opt/rocm/lib/llvm/bin/llvm-readelf")
 # mangled-name patterns of the hot kernels: the lane-per-path screening kernels (plain and forced
 # bits at N = 128; the runtime-information-set kernel at N = 128..1024, L = 4..32), the exact
 # N = 128 re-decode / forced-bit instances (HIST = CH = APX = false, compiled-in code 1 or 2), the
-# DL-SCL post pass, the exact long-code kernel (the re-decode of deferred N >= 256 frames)
-HOT = [r"scl_lane_kernelILi[48]ELi[12]ELb[01]E",
+# DL-SCL post pass, the exact long-code kernel (the re-decode of deferred N >= 256 frames).  The
+# opt-in fused instances of the lane kernel (TXF: fused TX, FP: fused post pass; off by default,
+# DESIGN.md §5.4-5.5) are not on a default path: they spill (profiles/r06e, r06l)
+HOT = [r"scl_lane_kernelILi[48]ELi[12]ELb[01]ELb0ELb0E",
        r"scl_lane_long_kernelILi(7|8|9|10)ELi(4|8|16|32)E",
        r"scl128_kernelILi[48]ELb0ELb0ELb[01]ELi1ELb0E",
        r"dl_post_kernelILi128ELi(64|88)ELi4E",
