@@ -778,27 +778,31 @@ __global__ void __launch_bounds__(256) dl_post_long_kernel(const pscl_post_long_
         atomicAdd(reinterpret_cast<unsigned long long*>(Q.counters) + PSCL_CNT_RETRIES, decodes);
 }
 
-// FER/BER statistics of the final results against the transmitted words: wavefront sums,
-// then one atomic per counter per 1024-thread block
-__global__ void __launch_bounds__(1024) dl_count_kernel(const uint64_t* __restrict__ best, const uint8_t* __restrict__ flags,
-                                                        const uint64_t* __restrict__ ref, int64_t B, int W, int k_payload,
-                                                        int64_t* counters) {
-    __shared__ int part[16][4];
-    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// FER/BER statistics of the final results against the transmitted words: per-thread sums over a
+// grid stride, wavefront sums, then one atomic per counter per 256-thread block.  (Blocks of 1024
+// threads -- 16 wavefronts that must start on one CU together -- waited up to ~350 us for a CU to
+// drain beside the next call's baseline decode in the pipelined sweep, r06m.)
+__global__ void __launch_bounds__(256) dl_count_kernel(const uint64_t* __restrict__ best, const uint8_t* __restrict__ flags,
+                                                       const uint64_t* __restrict__ ref, int64_t B, int W, int k_payload,
+                                                       int64_t* counters) {
+    __shared__ int part[4][4];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     unsigned long long* C = reinterpret_cast<unsigned long long*>(counters);
-    if (f == 0) atomicAdd(C + PSCL_CNT_FRAMES, (unsigned long long)B);
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(C + PSCL_CNT_FRAMES, (unsigned long long)B);
     int v[4] = {0, 0, 0, 0};  // frame errors, bit errors, payload frame errors, payload bit errors
-    if (f < B) {
-        v[0] = (flags[f] & PSCL_FLAG_CRC_PASS) ? 0 : 1;
+    for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < B; f += (int64_t)gridDim.x * blockDim.x) {
+        v[0] += (flags[f] & PSCL_FLAG_CRC_PASS) ? 0 : 1;
+        int be = 0, pb = 0;
         for (int w = 0; w < W; ++w) {  // payload = the first k_payload information bits
             const uint64_t d = best[f * W + w] ^ ref[f * W + w];
             const int kp = k_payload - 64 * w;
             const uint64_t pm = kp >= 64 ? ~0ULL : (kp > 0 ? ((1ULL << kp) - 1) : 0ULL);
-            v[1] += __popcll(d);
-            v[3] += __popcll(d & pm);
+            be += __popcll(d);
+            pb += __popcll(d & pm);
         }
-        v[2] = v[3] ? 1 : 0;
+        v[1] += be;
+        v[2] += pb ? 1 : 0;
+        v[3] += pb;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = wave_sum(v[i]);
@@ -877,8 +881,10 @@ hipError_t pscl_launch_dl_post(const pscl_post_params& Q, int64_t entries, hipSt
 
 hipError_t pscl_launch_dl_count(const uint64_t* best, const uint8_t* flags, const uint64_t* ref, int64_t B, int W,
                                 int k_payload, int64_t* counters, hipStream_t s) {
-    const int64_t grid = (B + 1023) / 1024;
-    hipLaunchKernelGGL(dl_count_kernel, dim3((unsigned)grid), dim3(1024), 0, s, best, flags, ref, B, W, k_payload,
+    int64_t grid = (B + 1023) / 1024;  // (four frames per thread)
+    if (grid > 1024) grid = 1024;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(dl_count_kernel, dim3((unsigned)grid), dim3(256), 0, s, best, flags, ref, B, W, k_payload,
                        counters);
     return hipGetLastError();
 }
