@@ -183,7 +183,7 @@ struct pscl_handle {
     int64_t tune[PSCL_TUNE_COUNT] = {};  // pscl_set_tuning knobs (0 = the default schedule)
     double host_call_ms = 0.0, host_wait_ms = 0.0;  // pscl_host_stats
     int64_t host_calls = 0;
-    int64_t n_fpost_rounds = 0, n_post_rounds = 0, n_fused_tx = 0;  // pscl_path_stats
+    int64_t n_fpost_rounds = 0, n_post_rounds = 0, n_fused_tx = 0, n_post_epw4 = 0;  // pscl_path_stats
 };
 
 namespace {
@@ -788,9 +788,11 @@ int pscl_set_pipelined(pscl_handle* h, int enable) {
 int pscl_set_tuning(pscl_handle* h, int knob, int64_t value) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
     static const int64_t lim[PSCL_TUNE_COUNT][2] = {{0, 0}, {0, 2}, {0, 64}, {0, 2}, {0, 1}, {0, 4096}, {0, PSCL_MAX_WAVES_PER_WG}, {0, 2},
-                                                    {0, (int64_t)1 << 30}, {0, 2}, {0, 32}, {0, 3}, {0, 2}, {0, 2}};
+                                                    {0, (int64_t)1 << 30}, {0, 2}, {0, 32}, {0, 3}, {0, 2}, {0, 2}, {0, 4}};
     if (knob < 1 || knob >= PSCL_TUNE_COUNT) return fail(PSCL_EINVAL, "unknown tuning knob %d", knob);
     if (value < lim[knob][0] || value > lim[knob][1] || (knob == PSCL_TUNE_POST_GRID && value && value < 16))
+        return fail(PSCL_EINVAL, "tuning knob %d: value %lld out of range", knob, (long long)value);
+    if (knob == PSCL_TUNE_POST_EPW && value != 0 && value != 2 && value != 4)
         return fail(PSCL_EINVAL, "tuning knob %d: value %lld out of range", knob, (long long)value);
     int rc = set_device(h);
     if (rc) return rc;
@@ -906,6 +908,11 @@ struct DlState {
     uint8_t* of2;            //   `of` concurrently, where the deferred mark must stay)
 };
 
+hipError_t launch_post(pscl_handle* h, const pscl_post_params& Q, int64_t A, hipStream_t s) {
+    if (pscl_post_epw(Q) == 4) h->n_post_epw4++;
+    return pscl_launch_dl_post(Q, A, s);
+}
+
 int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const double* d_llr, uint64_t* d_best,
                    uint8_t* d_flags, int32_t* d_attempts, int32_t* d_tried, int tried_stride, int64_t* d_cnt_dl,
                    hipStream_t st, hipStream_t side, hipEvent_t ev_s, hipEvent_t ev_d, bool narrow, bool beside) {
@@ -930,6 +937,7 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     Q.narrow = narrow ? 1 : 0;  // (pipelined calls: beside the next call's baseline)
     Q.grid_cap = h->tune[PSCL_TUNE_POST_GRID];
     Q.pairs = h->tune[PSCL_TUNE_POST_PAIRS];
+    Q.epw = (int)h->tune[PSCL_TUNE_POST_EPW];
     Q.cap = A;
     Q.act = S.act;
     Q.tried = S.tried;
@@ -953,7 +961,7 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     Q.in_count = nullptr;
     Q.out_count = S.bcnt;
     Q.out_list = lists[0];
-    if ((e = pscl_launch_dl_post(Q, A, st)) != hipSuccess) return fail(PSCL_EDEVICE, "dl_post launch: %s", hipGetErrorString(e));
+    if ((e = launch_post(h, Q, A, st)) != hipSuccess) return fail(PSCL_EDEVICE, "dl_post launch: %s", hipGetErrorString(e));
     // the retry decodes: entries bucket by bucket, LLR rows by indirection, forced prefixes,
     // warm-started past them (the compiled-in FS kernels; others decode from phase 0)
     pscl_decode_params H;
@@ -1051,7 +1059,7 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
             QD.in_count = side_cnt(r);
             QD.out_list = side_list(r + 1);
             QD.out_count = side_cnt(r + 1);
-            if ((e = pscl_launch_dl_post(QD, A, side)) != hipSuccess)
+            if ((e = launch_post(h, QD, A, side)) != hipSuccess)
                 return fail(PSCL_EDEVICE, "dl_post launch: %s", hipGetErrorString(e));
         } else if ((rc = launch_decode(h, H, 0, st))) {
             return rc;
@@ -1065,7 +1073,7 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
         Q.in_list = lists[r & 1];
         Q.out_count = S.bcnt + (size_t)(r + 1) * bstride;
         Q.out_list = lists[(r + 1) & 1];
-        if ((e = pscl_launch_dl_post(Q, A, st)) != hipSuccess)
+        if ((e = launch_post(h, Q, A, st)) != hipSuccess)
             return fail(PSCL_EDEVICE, "dl_post launch: %s", hipGetErrorString(e));
     }
     if (scr && rounds > 0) {  // the chain ends with its side chain
@@ -2011,8 +2019,10 @@ int pscl_host_stats(pscl_handle* h, double* call_ms, double* wait_ms, int64_t* c
     return PSCL_OK;
 }
 
-int pscl_path_stats(pscl_handle* h, int64_t* fused_post_rounds, int64_t* post_rounds, int64_t* fused_tx_blocks) {
+int pscl_path_stats(pscl_handle* h, int64_t* fused_post_rounds, int64_t* post_rounds, int64_t* fused_tx_blocks,
+                    int64_t* post_epw4_launches) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    if (post_epw4_launches) *post_epw4_launches = h->n_post_epw4;
     if (fused_post_rounds) *fused_post_rounds = h->n_fpost_rounds;
     if (post_rounds) *post_rounds = h->n_post_rounds;
     if (fused_tx_blocks) *fused_tx_blocks = h->n_fused_tx;

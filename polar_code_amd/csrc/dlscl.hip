@@ -245,12 +245,24 @@ __global__ void __launch_bounds__(256) replay_kernel(const pscl_replay_params R,
 #define PSCL_POST_WAVES_NARROW 4
 #endif
 constexpr int kPostWavesWide = 8, kPostWavesNarrow = PSCL_POST_WAVES_NARROW;
+// entries per wavefront at a time (dl_post_kernel EPW): the narrow form (pipelined calls, beside the
+// next baseline: its cost is the wave slots it holds) and the wide one (a chain alone: latency)
+#ifndef PSCL_POST_EPW_NARROW
+#define PSCL_POST_EPW_NARROW 2  // (K = 64; PSCL_TUNE_POST_EPW)
+#endif
+#ifndef PSCL_POST_WPE_Q  // (occupancy hint of the 4-entry form)
+#define PSCL_POST_WPE_Q 3
+#endif
+#ifndef PSCL_POST_EPW_WIDE
+#define PSCL_POST_EPW_WIDE 2
+#endif
+constexpr int kPostEpwNarrow = PSCL_POST_EPW_NARROW, kPostEpwWide = PSCL_POST_EPW_WIDE;
 constexpr int kPostIters = 32;  // entry pairs per wavefront between flushes
 
-template <int PW>
+template <int PW, int EPW>
 struct PostShared {
-    static constexpr int kChunk = PW * 2 * kPostIters;  // entries per workgroup between flushes
-    double lvl[PW][2][2][PSCL_FAST_N];  // [wave][half][buffer][element]
+    static constexpr int kChunk = PW * 2 * kPostIters;  // entries per workgroup between flushes (64 per wavefront)
+    double lvl[PW][EPW][2][PSCL_FAST_N];  // [wave][entry slot][buffer][element]
     uint64_t exp_table[PSCL_EXP_TABLE_WORDS];
     int32_t st_e[kChunk];
     uint16_t st_pos[kChunk];
@@ -260,39 +272,48 @@ struct PostShared {
     int32_t nst;
 };
 
-// Channel LLRs p = hl + 32 m (m = 0..3) of a frame row, N <= 128
-__device__ __forceinline__ void load_row4(const double* row, int rm_E, const int32_t* rm_src, int N, int hl, double* c) {
+// Channel LLRs p = hl + HLN m (m < 128 / HLN) of a frame row, N <= 128 (HLN lanes per entry)
+template <int HLN>
+__device__ __forceinline__ void load_rowq(const double* row, int rm_E, const int32_t* rm_src, int N, int hl, double* c) {
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        const int p = hl + 32 * m;
+    for (int m = 0; m < PSCL_FAST_N / HLN; ++m) {
+        const int p = hl + HLN * m;
         c[m] = p < N ? (rm_E == 0 ? row[p] : pscl::nr_stage(row, rm_src[p], rm_E, N)) : 0.0;
     }
 }
 
-// per-half broadcast of lane l's value (ds_bpermute; l differs between the halves)
+// per-entry broadcast of lane l's value (ds_bpermute; l differs between the entry slots)
 __device__ __forceinline__ uint64_t bcast64(uint64_t v, int l) {
     return ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), l) << 32) | (uint32_t)__shfl((int)(uint32_t)v, l);
 }
 
-// NC, KC: N and K compiled in (128 and 64 / 88: the BASELINE codes) or 0 (from Q)
-template <int NC, int KC, int PW>
-__global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PSCL_POST_WPE))) dl_post_kernel(const pscl_post_params Q, int beta_lds) {
-    constexpr int kPostWaves = PW, kPostChunk = PostShared<PW>::kChunk;
-    __shared__ PostShared<PW> S;
+// NC, KC: N and K compiled in (128 and 64 / 88: the BASELINE codes) or 0 (from Q).  EPW: entries a
+// wavefront works on at a time, HLN = 64 / EPW lanes each (2: halves of 32 lanes, 4 elements and 2
+// candidates per lane; 4: quarters of 16 lanes, 8 elements and 4 candidates per lane -- the same
+// instructions per entry, twice the entries per wavefront latency)
+template <int NC, int KC, int PW, int EPW = 2>
+__global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(EPW == 4 ? PSCL_POST_WPE_Q : PSCL_POST_WPE))) dl_post_kernel(const pscl_post_params Q, int beta_lds) {
+    static_assert(EPW == 2 || EPW == 4, "entries per wavefront");
+    constexpr int kPostWaves = PW, kPostChunk = PostShared<PW, EPW>::kChunk;
+    constexpr int HLN = 64 / EPW, EL = PSCL_FAST_N / HLN;  // lanes per entry, tree elements per lane
+    constexpr bool K1 = KC > 0 && KC <= 64;                 // one word of information bits
+    // (sums unrolled less in the 4-entry form: its twice as many candidates per lane hold the loads)
+    constexpr int kSumUnroll = EPW == 4 ? 2 : PSCL_POST_UNROLL, kPkUnroll = EPW == 4 ? 2 : 4;
+    __shared__ PostShared<PW, EPW> S;
     extern __shared__ double sbeta[];  // [K][K]: fp64 when beta_lds == 1, fp32 when 2
     float* const sbeta32 = reinterpret_cast<float*>(sbeta);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int hs = lane >> 5, hl = lane & 31, hb = lane & 32;  // half, lane in half, half's first lane
+    const int hs = lane / HLN, hl = lane % HLN, hb = lane & ~(HLN - 1);  // entry slot, lane in slot, slot's first lane
     const int N = NC ? NC : Q.N, K = KC ? KC : Q.K, W = KC ? (KC + 63) / 64 : Q.W, n = NC ? 7 : Q.n;
     for (int i = threadIdx.x; i < PSCL_EXP_TABLE_WORDS; i += blockDim.x) S.exp_table[i] = Q.exp_table[i];
     if (beta_lds == 1)
         for (int i = threadIdx.x; i < K * K; i += blockDim.x) sbeta[i] = Q.beta[i];
     else if (beta_lds == 2) {
-        if constexpr (KC == 64) {  // pair layout [k][hl][2] = (beta[k][hl], beta[k][hl + 32]): one
-                                   // 8-byte read gives a lane both of its candidates (kPostPk)
+        if constexpr (KC == 64) {  // lane layout [k][hl][m] = beta[k][hl + HLN m]: one 8- (16-) byte read
+                                   // gives a lane all of its 2 (4) candidates (the packed sums below)
             for (int i = threadIdx.x; i < K * K; i += blockDim.x) {
                 const int k = i >> 6, j = i & 63;
-                sbeta32[(k * 32 + (j & 31)) * 2 + (j >> 5)] = (float)Q.beta[i];
+                sbeta32[(k * HLN + (j % HLN)) * (64 / HLN) + (j / HLN)] = (float)Q.beta[i];
             }
         } else {
             for (int i = threadIdx.x; i < K * K; i += blockDim.x) sbeta32[i] = (float)Q.beta[i];
@@ -317,17 +338,24 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
     unsigned long long decodes = 0;
     double* buf0 = S.lvl[wave][hs][0];
     double* buf1 = S.lvl[wave][hs][1];
-    // info index of each of the lane's tree positions p = hl + 32 m (-1: frozen or beyond N)
-    int jpos[4];
+    // info index of each of the lane's tree positions p = hl + HLN m (-1: frozen or beyond N),
+    // packed a byte each (0xff: -1) -- 2 registers for the 8 positions of the quarter layout
+    uint32_t jpk[(EL + 3) / 4];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        const int p = hl + 32 * m;
+    for (int i = 0; i < (EL + 3) / 4; ++i) jpk[i] = 0xffffffffu;
+#pragma unroll
+    for (int m = 0; m < EL; ++m) {
+        const int p = hl + HLN * m;
         const uint64_t w = p < 64 ? info0 : info1;
         const bool inf = p < N && ((w >> (p & 63)) & 1ULL);
-        jpos[m] = inf ? (p < 64 ? __popcll(info0 & ((1ULL << p) - 1ULL))
-                                : ninfo0 + __popcll(info1 & ((1ULL << (p - 64)) - 1ULL)))
-                      : -1;
+        const int j = p < 64 ? __popcll(info0 & ((1ULL << p) - 1ULL))
+                             : ninfo0 + __popcll(info1 & ((1ULL << (p - 64)) - 1ULL));
+        if (inf) jpk[m >> 2] = (jpk[m >> 2] & ~(0xffu << (8 * (m & 3)))) | ((uint32_t)j << (8 * (m & 3)));
     }
+    auto jpos = [&](int m) -> int {
+        const uint32_t v = (jpk[m >> 2] >> (8 * (m & 3))) & 0xffu;
+        return v == 0xffu ? -1 : (int)v;
+    };
     __syncthreads();
     for (int64_t cbase = i_begin; cbase < i_end; cbase += kPostChunk) {  // workgroup-uniform
         // metadata of this wavefront's entries of the chunk, lane l = entry cbase + 8 l + wave;
@@ -353,24 +381,27 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
                 mfl = Q.of[me];
                 mnt = Q.ntried[me];
                 mt0 = Q.tried[2 * me];
-                mt1 = Q.tried[2 * me + 1];
+                mt1 = K1 ? 0ULL : Q.tried[2 * me + 1];  // (K <= 64: the upper tried word stays 0)
             }
         }
         const int nval = (int)__builtin_amdgcn_readfirstlane((int)__popcll(__ballot(mvalid)));  // lanes 0..nval-1
-        const int npair = (nval + 1) >> 1;
-        // channel rows of the first pair; later pairs' rows are prefetched one pair ahead
-        double c[4], cn[4];
-        load_row4(Q.llr + (int64_t)bcast64((uint64_t)mf, hs) * (Q.rm_E ? Q.rm_E : N), Q.rm_E, Q.rm_src, N, hl, c);
+        const int npair = (nval + EPW - 1) / EPW;
+        // channel rows of the first entries; the next iteration's rows are loaded into c as soon as
+        // the replay has copied c to LDS (one row's registers live, not two)
+        double c[EL];
+        load_rowq<HLN>(Q.llr + (int64_t)bcast64((uint64_t)mf, hs) * (Q.rm_E ? Q.rm_E : N), Q.rm_E, Q.rm_src, N, hl, c);
         for (int it = 0; it < npair; ++it) {
-            const int src = 2 * it + hs;  // this half's metadata lane
+            const int src = EPW * it + hs;  // this entry slot's metadata lane
             bool valid = src < nval;
             const int e = __shfl(me, src);
             const int64_t f = (int64_t)bcast64((uint64_t)mf, src);
-            const uint64_t b0 = bcast64(mb0, src), b1 = bcast64(mb1, src);
+            const uint64_t b0 = bcast64(mb0, src), b1 = K1 ? 0ULL : bcast64(mb1, src);
             const int nt = Q.init ? 0 : __shfl(mnt, src);
-            if (it + 1 < npair)
-                load_row4(Q.llr + (int64_t)bcast64((uint64_t)mf, src + 2 < nval ? src + 2 : 0) * (Q.rm_E ? Q.rm_E : N),
-                          Q.rm_E, Q.rm_src, N, hl, cn);
+            auto prefetch = [&]() {
+                if (it + 1 < npair)
+                    load_rowq<HLN>(Q.llr + (int64_t)bcast64((uint64_t)mf, src + EPW < nval ? src + EPW : 0) * (Q.rm_E ? Q.rm_E : N),
+                                   Q.rm_E, Q.rm_src, N, hl, c);
+            };
             bool more;
             if (Q.init) {  // baseline failing by construction (dl_compact); nothing tried yet
                 more = valid && Q.rounds > 0;
@@ -387,26 +418,27 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
                 if (valid && hl == 0) ++decodes;
                 more = valid && !(fl & PSCL_FLAG_CRC_PASS) && nt < Q.rounds;
             }
-            if (__ballot(more)) {  // (wave-uniform: both halves run the steps below; a half with
+            if (!__ballot(more)) prefetch();
+            if (__ballot(more)) {  // (wave-uniform: every slot runs the steps below; a slot with
                                    // nothing to do computes on its own buffers and writes nothing)
                 // ---- replay: the leaves of the attempt's best path, level by level
-                uint64_t u0 = 0, u1 = 0;  // the path's bits u[0..63], u[64..127] (this half's)
+                uint64_t u0 = 0, u1 = 0;  // the path's bits u[0..63], u[64..127] (this entry's)
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const int j = jpos[m];
-                    const bool bit = j >= 0 && (((j < 64 ? b0 : b1) >> (j & 63)) & 1ULL);
+                for (int m = 0; m < EL; ++m) {
+                    const int j = jpos(m);
+                    const bool bit = j >= 0 && (((K1 || j < 64 ? b0 : b1) >> (j & 63)) & 1ULL);
                     const uint64_t bm = __ballot(bit) >> hb;
-                    const uint64_t part = bm & 0xffffffffULL;
-                    if (m == 0) u0 |= part;
-                    if (m == 1) u0 |= part << 32;
-                    if (m == 2) u1 |= part;
-                    if (m == 3) u1 |= part << 32;
+                    const uint64_t part = bm & (HLN == 64 ? ~0ULL : ((1ULL << HLN) - 1ULL));
+                    const int pos = HLN * m;  // (bits hl + HLN m: positions pos .. pos + HLN - 1)
+                    if (pos < 64) u0 |= part << pos;
+                    else u1 |= part << (pos - 64);
                 }
                 double* cur = buf0;
                 double* nxt = buf1;
 #pragma unroll
-                for (int m = 0; m < 4; ++m)
-                    if (hl + 32 * m < N) cur[hl + 32 * m] = c[m];
+                for (int m = 0; m < EL; ++m)
+                    if (hl + HLN * m < N) cur[hl + HLN * m] = c[m];
+                prefetch();
                 pscl::wave_lds_fence();
                 // partial sums of level lw2 from X_lw2 = u after butterfly stages 1..2^(lw2-1)
                 // (see replay_leaves)
@@ -424,8 +456,8 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
                 for (int d = 0; d < n; ++d) {
                     const int lw2 = n - d - 1, w2 = 1 << lw2;
 #pragma unroll
-                    for (int m = 0; m < 4; ++m) {
-                        const int p2 = hl + 32 * m;
+                    for (int m = 0; m < EL; ++m) {
+                        const int p2 = hl + HLN * m;
                         if (p2 < N) {
                             const int k2 = p2 >> lw2, i = p2 & (w2 - 1);
                             const int pa = ((k2 >> 1) << (lw2 + 1)) + i;
@@ -450,29 +482,29 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
                 // (K = 64, narrow form: an fp32 copy too, in nxt's upper half -- free until the tails)
                 float* const l32 = reinterpret_cast<float*>(nxt + 64);
 #pragma unroll
-                for (int m = 0; m < 4; ++m)
-                    if (jpos[m] >= 0) {
-                        nxt[jpos[m]] = fabs(cur[hl + 32 * m]);
-                        if (KC == 64 && beta_lds == 2) l32[jpos[m]] = (float)fabs(cur[hl + 32 * m]);
+                for (int m = 0; m < EL; ++m)
+                    if (jpos(m) >= 0) {
+                        nxt[jpos(m)] = fabs(cur[hl + HLN * m]);
+                        if (KC == 64 && beta_lds == 2) l32[jpos(m)] = (float)fabs(cur[hl + HLN * m]);
                     }
                 pscl::wave_lds_fence();
                 // ---- next flip: argmin over untried (q, index), q = |L0| @ beta summed in
                 // index order (flip.py:104-108), q = |L0| without beta
-                const uint64_t t0 = Q.init ? 0ULL : bcast64(mt0, src), t1 = Q.init ? 0ULL : bcast64(mt1, src);
+                const uint64_t t0 = Q.init ? 0ULL : bcast64(mt0, src), t1 = Q.init || K1 ? 0ULL : bcast64(mt1, src);
                 uint64_t bk = ~0ULL;
                 int bj = 0x7fffffff;
-                // candidates j = hl + 32 m; their sums advance together (one |L0_k| read serves
+                // candidates j = hl + HLN m; their sums advance together (one |L0_k| read serves
                 // all, and the dependent adds of the chains interleave)
-                constexpr int MC = KC ? (KC + 31) / 32 : 4;
+                constexpr int MC = KC ? (KC + HLN - 1) / HLN : PSCL_FAST_N / HLN;
                 double qv[MC];
                 auto argmin = [&]() {  // (key, index) over the untried candidates of this half
                     bk = ~0ULL;
                     bj = 0x7fffffff;
 #pragma unroll
                     for (int m = 0; m < MC; ++m) {
-                        const int j = hl + 32 * m;
+                        const int j = hl + HLN * m;
                         if (j < K) {
-                            const bool seen = ((j < 64 ? t0 : t1) >> (j & 63)) & 1ULL;
+                            const bool seen = ((K1 || j < 64 ? t0 : t1) >> (j & 63)) & 1ULL;
                             const uint64_t key = seen ? ~0ULL : order_key(qv[m]);
                             if (key < bk) {  // lower m first: ties keep the lower index
                                 bk = key;
@@ -481,7 +513,7 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
                         }
                     }
 #pragma unroll
-                    for (int sft = 1; sft < 32; sft <<= 1) {
+                    for (int sft = 1; sft < HLN; sft <<= 1) {
                         const uint64_t ok = pscl::shfl_u64(bk, lane ^ sft);
                         const int oj = __shfl(bj, lane ^ sft);
                         if (ok < bk || (ok == bk && oj < bj)) {
@@ -496,12 +528,12 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
 #pragma unroll
                     for (int m = 0; m < MC; ++m) qv[m] = 0.0;
                     const double* bc = beta + hl;
-#pragma unroll PSCL_POST_UNROLL
+#pragma unroll kSumUnroll
                     for (int k = 0; k < K; ++k) {
                         const double ak = nxt[k];
 #pragma unroll
                         for (int m = 0; m < MC; ++m)
-                            if (hl + 32 * m < K) qv[m] = qv[m] + ak * bc[k * K + 32 * m];
+                            if (hl + HLN * m < K) qv[m] = qv[m] + ak * bc[k * K + HLN * m];
                     }
                 };
                 if (Q.beta && !(PSCL_POST_ABLATE & 4)) {
@@ -516,49 +548,58 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
                     for (int m = 0; m < MC; ++m) qv[m] = 0.0;
                     constexpr bool PK = KC == 64;  // packed fp32 sums (narrow form, K = 64; e2 below)
                     if (PK && beta_lds == 2) {
-                        // both candidates of the lane in one v_pk_fma_f32 per k: |L0| read 4 at a time
-                        // (fp32 copy), beta pairs from the pair layout; summed in fp32 and certified
+                        // the lane's candidates in pairs, one v_pk_fma_f32 per pair and k: |L0| read 4 at
+                        // a time (fp32 copy), beta from the lane layout; summed in fp32 and certified
                         // against the fp32 bound below (the exact fp64 sums when uncertified)
                         typedef float f2 __attribute__((ext_vector_type(2)));
                         typedef float f4 __attribute__((ext_vector_type(4)));
-                        const f2* bp = reinterpret_cast<const f2*>(sbeta32) + hl;
+                        constexpr int NP = MC / 2;  // candidate pairs per lane
+                        const f2* bp = reinterpret_cast<const f2*>(sbeta32) + hl * NP;
                         const f4* lp = reinterpret_cast<const f4*>(l32);
-                        f2 acc = {0.0f, 0.0f};
-#pragma unroll 4
+                        f2 acc[NP];
+#pragma unroll
+                        for (int i = 0; i < NP; ++i) acc[i] = (f2){0.0f, 0.0f};
+#pragma unroll kPkUnroll
                         for (int k4 = 0; k4 < 16; ++k4) {
                             const f4 a = lp[k4];
-                            acc = __builtin_elementwise_fma((f2){a.x, a.x}, bp[(4 * k4 + 0) * 32], acc);
-                            acc = __builtin_elementwise_fma((f2){a.y, a.y}, bp[(4 * k4 + 1) * 32], acc);
-                            acc = __builtin_elementwise_fma((f2){a.z, a.z}, bp[(4 * k4 + 2) * 32], acc);
-                            acc = __builtin_elementwise_fma((f2){a.w, a.w}, bp[(4 * k4 + 3) * 32], acc);
+#pragma unroll
+                            for (int i = 0; i < NP; ++i) {
+                                acc[i] = __builtin_elementwise_fma((f2){a.x, a.x}, bp[(4 * k4 + 0) * HLN * NP + i], acc[i]);
+                                acc[i] = __builtin_elementwise_fma((f2){a.y, a.y}, bp[(4 * k4 + 1) * HLN * NP + i], acc[i]);
+                                acc[i] = __builtin_elementwise_fma((f2){a.z, a.z}, bp[(4 * k4 + 2) * HLN * NP + i], acc[i]);
+                                acc[i] = __builtin_elementwise_fma((f2){a.w, a.w}, bp[(4 * k4 + 3) * HLN * NP + i], acc[i]);
+                            }
                         }
-                        qv[0] = (double)acc.x;  // (exact widening; MC = 2 here)
-                        qv[1] = (double)acc.y;
+#pragma unroll
+                        for (int i = 0; i < NP; ++i) {  // (exact widening; candidate m = 2 i, 2 i + 1)
+                            qv[2 * i] = (double)acc[i].x;
+                            qv[2 * i + 1] = (double)acc[i].y;
+                        }
                     } else if (beta_lds == 2) {  // (narrow form: beta staged in LDS as fp32, see e2 below)
                         const float* bc = sbeta32 + hl;
-#pragma unroll PSCL_POST_UNROLL
+#pragma unroll kSumUnroll
                         for (int k = 0; k < K; ++k) {
                             const double ak = nxt[k];
 #pragma unroll
                             for (int m = 0; m < MC; ++m)
-                                if (hl + 32 * m < K) qv[m] = __builtin_fma(ak, (double)bc[k * K + 32 * m], qv[m]);
+                                if (hl + HLN * m < K) qv[m] = __builtin_fma(ak, (double)bc[k * K + HLN * m], qv[m]);
                         }
                     } else {
                         const double* bc = beta + hl;
-#pragma unroll PSCL_POST_UNROLL
+#pragma unroll kSumUnroll
                         for (int k = 0; k < K; ++k) {
                             const double ak = nxt[k];
 #pragma unroll
                             for (int m = 0; m < MC; ++m)
-                                if (hl + 32 * m < K) qv[m] = __builtin_fma(ak, bc[k * K + 32 * m], qv[m]);
+                                if (hl + HLN * m < K) qv[m] = __builtin_fma(ak, bc[k * K + HLN * m], qv[m]);
                         }
                     }
                     argmin();
                     double as = 0.0;
 #pragma unroll
-                    for (int m = 0; m < MC; ++m) as = as + (hl + 32 * m < K ? nxt[hl + 32 * m] : 0.0);
+                    for (int m = 0; m < MC; ++m) as = as + (hl + HLN * m < K ? nxt[hl + HLN * m] : 0.0);
 #pragma unroll
-                    for (int sft = 1; sft < 32; sft <<= 1) as = as + pscl_asf64(pscl::shfl_u64(pscl_asu64(as), lane ^ sft));
+                    for (int sft = 1; sft < HLN; sft <<= 1) as = as + pscl_asf64(pscl::shfl_u64(pscl_asu64(as), lane ^ sft));
                     // 2 E = 2 (gamma_K + gamma_K+1) S <= (4 K + 2 + slack) u S, u = 2^-53 (K = 64:
                     // 264 u, 2.3 % slack; the bound grows with K, so the (128,88) and runtime-K
                     // instances get their own); fp32 beta adds |beta32 - beta| <= 2^-24 |beta| + 2^-150
@@ -585,14 +626,14 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
                                                       : as * Q.beta_absmax * gk;
                     double qmine = qv[0];
 #pragma unroll
-                    for (int m = 1; m < MC; ++m) qmine = (bj >> 5) == m ? qv[m] : qmine;
-                    const double qb = pscl_asf64(pscl::shfl_u64(pscl_asu64(qmine), hb + (bj & 31)));
+                    for (int m = 1; m < MC; ++m) qmine = (bj / HLN) == m ? qv[m] : qmine;
+                    const double qb = pscl_asf64(pscl::shfl_u64(pscl_asu64(qmine), hb + (bj % HLN)));
                     const double thr = qb + e2 * (1.0 + 0x1p-40);
                     bool near = false;
 #pragma unroll
                     for (int m = 0; m < MC; ++m) {
-                        const int j = hl + 32 * m;
-                        const bool seen = ((j < 64 ? t0 : t1) >> (j & 63)) & 1ULL;
+                        const int j = hl + HLN * m;
+                        const bool seen = ((K1 || j < 64 ? t0 : t1) >> (j & 63)) & 1ULL;
                         near = near || (j < K && j != bj && !seen && !(qv[m] > thr));
                     }
                     if (__ballot(near && more)) {
@@ -605,7 +646,7 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
 #endif
                 } else {
 #pragma unroll
-                    for (int m = 0; m < MC; ++m) qv[m] = hl + 32 * m < K ? nxt[hl + 32 * m] : 0.0;
+                    for (int m = 0; m < MC; ++m) qv[m] = hl + HLN * m < K ? nxt[hl + HLN * m] : 0.0;
                     argmin();
                 }
                 const int idx = bj;  // (half-uniform) an untried index exists: rounds <= min(retries, K)
@@ -618,8 +659,8 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
                 // the decode kernel forms them: good child metric + L, bad child metric +
                 // (|llr| + L), llr == 0: metric + LOGE2), then summed in phase order
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const int p = hl + 32 * m;
+                for (int m = 0; m < EL; ++m) {
+                    const int p = hl + HLN * m;
                     if (p < 16 * seg) {
                         const double lam = cur[p];  // (the leaves stay in cur)
                         const uint32_t bit = (uint32_t)(((p < 64 ? u0 : u1) >> (p & 63)) & 1ULL);
@@ -663,29 +704,31 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(PS
                 }
                 pscl::wave_lds_fence();  // the LDS buffers are rewritten by the next pair
             }
-#pragma unroll
-            for (int m = 0; m < 4; ++m) c[m] = cn[m];
         }
         // flush: one global atomic per non-empty bucket, then the staged entries scattered
+        // (tid opaque: the flush's thread-indexed addresses are formed here, not hoisted out of
+        // the entry loop into registers held across it)
+        int tid = (int)threadIdx.x;
+        asm volatile("" : "+v"(tid));
         __syncthreads();
-        if (threadIdx.x < PSCL_DL_NSEG) {
-            const int cc = S.lcnt[threadIdx.x];
+        if (tid < PSCL_DL_NSEG) {
+            const int cc = S.lcnt[tid];
             int g = 0;
             if (cc) {
                 if (PSCL_POST_ABLATE & 1) g = 0;
-                else g = atomicAdd(Q.out_count + threadIdx.x * PSCL_DL_CSTRIDE, cc);
+                else g = atomicAdd(Q.out_count + tid * PSCL_DL_CSTRIDE, cc);
             }
-            S.gbase[threadIdx.x] = g;
+            S.gbase[tid] = g;
         }
         __syncthreads();
         const int nst = S.nst;
-        for (int x = threadIdx.x; x < nst; x += blockDim.x) {
+        for (int x = tid; x < nst; x += (int)blockDim.x) {
             const int sg = S.st_seg[x];
             Q.out_list[(int64_t)sg * Q.cap + S.gbase[sg] + S.st_pos[x]] = S.st_e[x];
         }
         __syncthreads();
-        if (threadIdx.x < PSCL_DL_NSEG) S.lcnt[threadIdx.x] = 0;
-        if (threadIdx.x == 0) S.nst = 0;
+        if (tid < PSCL_DL_NSEG) S.lcnt[tid] = 0;
+        if (tid == 0) S.nst = 0;
         __syncthreads();
     }
     if (Q.counters && decodes)
@@ -846,12 +889,21 @@ hipError_t pscl_launch_replay(const pscl_replay_params& R, int64_t cap, hipStrea
     return hipGetLastError();
 }
 
+// entries per wavefront of the launch (the 4-entry form is instantiated for the (128,64) code: its
+// K = 64 sums fit 3 wavefronts per SIMD without spills; others run 2 entries per wavefront)
+int pscl_post_epw(const pscl_post_params& Q) {
+    if (!Q.narrow) return kPostEpwWide;
+    if (!(Q.N == 128 && Q.K == 64)) return 2;
+    return Q.epw == 2 || Q.epw == 4 ? Q.epw : kPostEpwNarrow;
+}
+
 hipError_t pscl_launch_dl_post(const pscl_post_params& Q, int64_t entries, hipStream_t s) {
     if (entries <= 0) return hipSuccess;
-    // workgroups of PW wavefronts (2 PW entries in flight), sized for `pairs` entry pairs per wavefront
+    // workgroups of PW wavefronts (EPW PW entries in flight), sized for `pairs` iterations per wavefront
     const int PW = Q.narrow ? kPostWavesNarrow : kPostWavesWide;
+    const int EPW = pscl_post_epw(Q);
     const int64_t pairs = Q.pairs >= 1 && Q.pairs <= 32 ? Q.pairs : PSCL_POST_PAIRS;
-    int64_t grid = (entries + PW * 2 * pairs - 1) / (PW * 2 * pairs);
+    int64_t grid = (entries + PW * EPW * pairs - 1) / (PW * EPW * pairs);
     const int64_t gcap = Q.grid_cap >= 16 && Q.grid_cap <= 4096 ? Q.grid_cap : PSCL_POST_GRID;  // (tuning knob)
     if (grid > gcap) grid = gcap;
     // beta in LDS: fp64 in the wide form (LDS <= 64 KB), fp32 in the narrow one (16 KB at K = 64, beside
@@ -862,19 +914,21 @@ hipError_t pscl_launch_dl_post(const pscl_post_params& Q, int64_t entries, hipSt
                          : (PSCL_POST_BETA32 && Q.narrow && (size_t)Q.K * Q.K * 4 <= 16 * 1024) ? 2 : 0;
     const size_t lds = beta_lds == 1 ? (size_t)Q.K * Q.K * 8 : beta_lds == 2 ? (size_t)Q.K * Q.K * 4 : 0;
     const dim3 g((unsigned)grid), b(PW * 64);
-    if (Q.narrow) {
+    if (Q.narrow && EPW == 4) {
+        hipLaunchKernelGGL((dl_post_kernel<128, 64, kPostWavesNarrow, 4>), g, b, lds, s, Q, beta_lds);
+    } else if (Q.narrow) {
         if (Q.N == 128 && Q.K == 64)
-            hipLaunchKernelGGL((dl_post_kernel<128, 64, kPostWavesNarrow>), g, b, lds, s, Q, beta_lds);
+            hipLaunchKernelGGL((dl_post_kernel<128, 64, kPostWavesNarrow, 2>), g, b, lds, s, Q, beta_lds);
         else if (Q.N == 128 && Q.K == 88)
-            hipLaunchKernelGGL((dl_post_kernel<128, 88, kPostWavesNarrow>), g, b, lds, s, Q, beta_lds);
+            hipLaunchKernelGGL((dl_post_kernel<128, 88, kPostWavesNarrow, 2>), g, b, lds, s, Q, beta_lds);
         else
-            hipLaunchKernelGGL((dl_post_kernel<0, 0, kPostWavesNarrow>), g, b, lds, s, Q, beta_lds);
+            hipLaunchKernelGGL((dl_post_kernel<0, 0, kPostWavesNarrow, 2>), g, b, lds, s, Q, beta_lds);
     } else if (Q.N == 128 && Q.K == 64) {
-        hipLaunchKernelGGL((dl_post_kernel<128, 64, kPostWavesWide>), g, b, lds, s, Q, beta_lds);
+        hipLaunchKernelGGL((dl_post_kernel<128, 64, kPostWavesWide, kPostEpwWide>), g, b, lds, s, Q, beta_lds);
     } else if (Q.N == 128 && Q.K == 88) {
-        hipLaunchKernelGGL((dl_post_kernel<128, 88, kPostWavesWide>), g, b, lds, s, Q, beta_lds);
+        hipLaunchKernelGGL((dl_post_kernel<128, 88, kPostWavesWide, kPostEpwWide>), g, b, lds, s, Q, beta_lds);
     } else {
-        hipLaunchKernelGGL((dl_post_kernel<0, 0, kPostWavesWide>), g, b, lds, s, Q, beta_lds);
+        hipLaunchKernelGGL((dl_post_kernel<0, 0, kPostWavesWide, kPostEpwWide>), g, b, lds, s, Q, beta_lds);
     }
     return hipGetLastError();
 }

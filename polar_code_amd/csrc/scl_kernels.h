@@ -31,6 +31,7 @@ struct pscl_post_params {
     const uint64_t* exp_table;   // glibc exp table (exact metric tails)
     int rounds;                  // min(retries, K)
     int narrow;                  // small workgroups, beta through L2 (pipelined calls, dl_post_kernel)
+    int epw;                     // narrow form: entries per wavefront (2, 4; 0: PSCL_POST_EPW_NARROW)
     int64_t grid_cap;            // 0, or the workgroup cap of a launch (tuning knob; default PSCL_POST_GRID)
     int64_t pairs;               // 0, or the entry pairs per wavefront the grid is sized for (tuning knob)
     int init;
@@ -319,6 +320,7 @@ hipError_t pscl_launch_tail_abs_scan(uint32_t lo, uint32_t hi, const uint64_t* e
 hipError_t pscl_launch_softplus_tails(const double* v, int64_t n, const uint64_t* exp_table, double* exact,
                                      double* apx, hipStream_t s);
 hipError_t pscl_launch_dl_post(const pscl_post_params& Q, int64_t entries, hipStream_t s);
+int pscl_post_epw(const pscl_post_params& Q);  // entries per wavefront the launch runs with
 hipError_t pscl_launch_dl_post_long(const pscl_post_long_params& Q, hipStream_t s);
 hipError_t pscl_launch_dl_count(const uint64_t* best, const uint8_t* flags, const uint64_t* ref, int64_t B, int W,
                                 int k_payload, int64_t* counters, hipStream_t s);

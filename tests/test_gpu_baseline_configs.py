@@ -119,15 +119,19 @@ def test_config5_nr_E256_L8_1e6_frames_vs_oracle():
     print(f"config 5: payload FER {cnt[PAY_ERR] / B:.6f}, BER {cnt[PAY_BIT] / (B * 64):.3e}, 0/{B} oracle mismatches")
 
 
-def _dl_config(L, beta_name, ebno, nb, seed, tuning=None):
+def _dl_config(L, beta_name, ebno, nb, seed, tuning=None, pipelined=False):
     """One DL-SCL batch of nb frames (8 flips, beta_<beta_name>) against the oracle's
-    decode_with_retries, frame by frame; returns (SCL counters, DL counters, oracle attempts)."""
+    decode_with_retries, frame by frame; returns (SCL counters, DL counters, oracle attempts).
+    pipelined: the call as bench.py's steps enqueue it (pscl_set_pipelined: the post pass's narrow
+    form, PSCL_TUNE_POST_EPW)."""
     K, kp, R = 64, 40, 8
     info = construct_info_set(128, K)
     beta = np.load(GOLDEN / f"beta_{beta_name}.npy")
     dec = _native.Decoder(128, info, L, POLY)
     if tuning:
         dec.set_tuning(**tuning)
+    if pipelined:
+        dec.set_pipelined(True)
     with _native.DeviceArena(dec) as mem:
         d_llr, d_msg = mem.alloc(nb * 128 * 8), mem.alloc(nb * 8)
         dec.channel_device(seed, int(ebno * 10), ebno, K / 128, kp, 0, nb, d_llr, d_msg)
@@ -137,8 +141,12 @@ def _dl_config(L, beta_name, ebno, nb, seed, tuning=None):
         mem.memset(d_cd, 0, 64)
         dec.dlscl_device(d_llr, nb, R, beta=beta, d_best=d_best, d_flags=d_flags, d_attempts=d_att, d_ref=d_msg,
                          k_payload=kp, d_counters_scl=d_cs, d_counters_dl=d_cd)
+        if pipelined:
+            dec.join()
         dec.sync()
         paths = dec.path_stats()
+        if tuning and "post_epw" in tuning:
+            assert (paths["post_epw4_launches"] > 0) == (pipelined and tuning["post_epw"] == 4), paths
         if tuning and tuning.get("dl_fused_post") == 1:  # (the schedule under test ran)
             assert paths["fused_post_rounds"] > 0 and paths["post_rounds"] == 0, paths
         if tuning and tuning.get("dl_fused_post") == 2:
@@ -183,7 +191,32 @@ def test_config4_dlscl_L4_r8_beta4_1e6_frames_vs_oracle():
 def test_dlscl_screened_retry_decodes_vs_oracle(L, beta, ebno, nb, tuning):
     """Screened DL-SCL retry rounds (forced-bit screening decodes + exact decodes of the entries
     they defer) against the oracle on every frame: bits, CRC flags, attempt counts, counters."""
-    cs, cd, att_o = _dl_config(L, beta, ebno, nb, seed=60 + L, tuning=tuning)
+    _screened_vs_oracle(L, beta, ebno, nb, tuning, False)
+
+
+@pytest.mark.parametrize("L,beta,ebno,nb,epw", [
+    (4, "M4", 5.0, 1_000_000, 4),  # config 4 as the bench runs it: the narrow post pass, 4 entries per wavefront
+    (8, "M8", 4.0, 200_000, 4),
+    (8, "M8", 4.0, 200_000, 2),    # 2 entries per wavefront
+])
+def test_dlscl_pipelined_post_forms_vs_oracle(L, beta, ebno, nb, epw):
+    """The narrow (pipelined) post pass in both forms (PSCL_TUNE_POST_EPW: 32 or 16 lanes per entry)
+    against the oracle on every frame."""
+    _screened_vs_oracle(L, beta, ebno, nb, {"post_epw": epw}, True)
+
+
+def test_post_epw_knob_validated():
+    dec = _native.Decoder(128, construct_info_set(128, 64), 4, POLY)
+    for bad in (1, 3, 5):
+        with pytest.raises(Exception):
+            dec.set_tuning(post_epw=bad)
+    dec.set_tuning(post_epw=4)
+    dec.set_tuning(post_epw=0)
+    dec.close()
+
+
+def _screened_vs_oracle(L, beta, ebno, nb, tuning, pipelined):
+    cs, cd, att_o = _dl_config(L, beta, ebno, nb, seed=60 + L, tuning=tuning, pipelined=pipelined)
     assert int(np.count_nonzero(att_o > 2)) > nb // 200  # many multi-round entries (warm starts, growth)
     print(f"L={L} {ebno} dB {tuning}: SCL FER {cs[FRAME_ERR] / nb:.5f}, DL-SCL FER {cd[FRAME_ERR] / nb:.5f}, "
           f"0/{nb} oracle mismatches")
