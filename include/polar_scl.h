@@ -333,6 +333,11 @@ int pscl_join(pscl_handle* h);
  *   PSCL_TUNE_POST_EPW      2 or 4: entries a wavefront of the DL-SCL post pass works on at once in
  *                           its narrow form (pipelined calls; 32 or 16 lanes per entry); 0 (default):
  *                           the measured faster
+ *   PSCL_TUNE_LANE_EXACT    exact decodes of the (128,64) and NR (128,88) codes at L = 4, 8 -- the
+ *                           deferred frames' re-decode and the exact DL-SCL retry rounds: 1 on the
+ *                           exact lane-per-path kernel, 2 on the two-lanes-per-path exact kernel;
+ *                           3 (tests) also every plain decode, unscreened; 0 (default): the measured
+ *                           faster
  */
 #define PSCL_TUNE_DL_SCREEN 1
 #define PSCL_TUNE_DL_CHUNKS 2
@@ -348,7 +353,8 @@ int pscl_join(pscl_handle* h);
 #define PSCL_TUNE_TX_FUSED 12
 #define PSCL_TUNE_DL_FUSED_POST 13
 #define PSCL_TUNE_POST_EPW 14
-#define PSCL_TUNE_COUNT 15
+#define PSCL_TUNE_LANE_EXACT 15
+#define PSCL_TUNE_COUNT 16
 int pscl_set_tuning(pscl_handle* h, int knob, int64_t value);
 
 /*
@@ -400,11 +406,12 @@ int pscl_host_stats(pscl_handle* h, double* call_ms, double* wait_ms, int64_t* c
  * Which schedules this handle has enqueued since it was created (tests assert the path they
  * mean to exercise ran): DL-SCL retry rounds whose post pass ran inside the screened retry
  * decode (PSCL_TUNE_DL_FUSED_POST), rounds with the separate dl_post_kernel, and pscl_simulate
- * blocks whose TX was fused into the baseline decode (PSCL_TUNE_TX_FUSED), and dl_post_kernel
- * launches in the 4-entries-per-wavefront form (PSCL_TUNE_POST_EPW).  Any pointer may be NULL.
+ * blocks whose TX was fused into the baseline decode (PSCL_TUNE_TX_FUSED), dl_post_kernel
+ * launches in the 4-entries-per-wavefront form (PSCL_TUNE_POST_EPW), and exact decodes launched on
+ * the exact lane-per-path kernel (PSCL_TUNE_LANE_EXACT).  Any pointer may be NULL.
  */
 int pscl_path_stats(pscl_handle* h, int64_t* fused_post_rounds, int64_t* post_rounds, int64_t* fused_tx_blocks,
-                    int64_t* post_epw4_launches);
+                    int64_t* post_epw4_launches, int64_t* lane_exact_launches);
 
 /*
  * The product's host (CPU) decoder: pscl_decode's contract and outputs (bit-identical) without a

@@ -48,7 +48,7 @@ EXPORTS = (
 
 # pscl_set_tuning knobs (include/polar_scl.h)
 TUNE = {"dl_screen": 1, "dl_chunks": 2, "dl_split": 3, "side_priority": 4, "post_grid": 5, "retry_wpg": 6, "dl_lane": 7, "dl_screen_min": 8, "dl_retry_lane": 9, "post_pairs": 10, "dl_streams": 11, "tx_fused": 12,
-        "dl_fused_post": 13, "post_epw": 14}
+        "dl_fused_post": 13, "post_epw": 14, "lane_exact": 15}
 
 _vp, _i32, _i64, _u64, _dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
 
@@ -114,7 +114,7 @@ def lib() -> C.CDLL:
                                       _vp, _vp, C.c_int]),
         "pscl_timing_read_split": (C.c_int, [_vp, P(_i64), P(_dbl), P(_i64), P(_dbl)]),
         "pscl_host_stats": (C.c_int, [_vp, P(_dbl), P(_dbl), P(_i64), C.c_int]),
-        "pscl_path_stats": (C.c_int, [_vp, P(_i64), P(_i64), P(_i64), P(_i64)]),
+        "pscl_path_stats": (C.c_int, [_vp, P(_i64), P(_i64), P(_i64), P(_i64), P(_i64)]),
         "pscl_device_count": (C.c_int, []),
         "pscl_create": (C.c_int, [P(_vp), C.c_int, C.c_int, P(_i32), C.c_int, C.c_int, _u64]),
         "pscl_destroy": (C.c_int, [_vp]),
@@ -463,11 +463,11 @@ class Decoder:
 
     def path_stats(self) -> dict:
         """Schedules enqueued so far (pscl_path_stats): fused-post rounds, separate-post rounds,
-        fused-TX blocks, 4-entry-form post launches."""
-        a, b, c, d = _i64(), _i64(), _i64(), _i64()
-        check(lib().pscl_path_stats(self._h, C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
+        fused-TX blocks, 4-entry-form post launches, exact lane-per-path launches."""
+        a, b, c, d, x = _i64(), _i64(), _i64(), _i64(), _i64()
+        check(lib().pscl_path_stats(self._h, C.byref(a), C.byref(b), C.byref(c), C.byref(d), C.byref(x)))
         return {"fused_post_rounds": int(a.value), "post_rounds": int(b.value), "fused_tx_blocks": int(c.value),
-                "post_epw4_launches": int(d.value)}
+                "post_epw4_launches": int(d.value), "lane_exact_launches": int(x.value)}
 
     def launch_info(self, B: int):
         w, g, lds = C.c_int(), _i64(), C.c_int()

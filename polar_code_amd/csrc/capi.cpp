@@ -183,7 +183,7 @@ struct pscl_handle {
     int64_t tune[PSCL_TUNE_COUNT] = {};  // pscl_set_tuning knobs (0 = the default schedule)
     double host_call_ms = 0.0, host_wait_ms = 0.0;  // pscl_host_stats
     int64_t host_calls = 0;
-    int64_t n_fpost_rounds = 0, n_post_rounds = 0, n_fused_tx = 0, n_post_epw4 = 0;  // pscl_path_stats
+    int64_t n_fpost_rounds = 0, n_post_rounds = 0, n_fused_tx = 0, n_post_epw4 = 0, n_lane_exact = 0;  // pscl_path_stats
 };
 
 namespace {
@@ -326,6 +326,19 @@ int with_count_slots(pscl_handle* h, pscl_decode_params& P, int hist, int slot, 
 // scr_slot: the scratch buffer of a long-code decode (decodes that may run concurrently on
 // different streams need different slots)
 // pipe: the caller is a plain pscl_decode_device on a pipelined handle (see pscl_handle)
+// exact decodes on the exact lane-per-path instance where it applies (PSCL_TUNE_LANE_EXACT): off by
+// default -- these launches are few frames, bound by one wavefront's latency, and one lane per path
+// runs each path's tree updates serially where the two-lanes-per-path kernel splits them: re-decode
+// 169 us against 99 us per 10^6-frame headline step, side-chain rounds 208 against 182 us
+// (profiles/r06r_lane_exact_ab.txt)
+#ifndef PSCL_LANE_EXACT_DEFAULT
+#define PSCL_LANE_EXACT_DEFAULT 0
+#endif
+bool lane_exact_on(const pscl_handle* h) {
+    const int64_t lx = h->tune[PSCL_TUNE_LANE_EXACT];
+    return lx == 1 || lx == 3 || (lx == 0 && PSCL_LANE_EXACT_DEFAULT);
+}
+
 int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStream_t st = nullptr, int scr_slot = 38,
                   bool pipe = false) {
     if (!st) st = h->stream;
@@ -356,7 +369,8 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
     // (long codes: the lane-per-path screening kernel, scl_lane_long.hip, N = 256..1024, L = 4, 8)
     pscl_decode_params T = P;
     T.apx = 1;
-    const bool screen = h->screen && !hist && !P.metrics && !P.cands && !P.force && !P.sc_hard && !P.fidx &&
+    const int64_t lx = h->tune[PSCL_TUNE_LANE_EXACT];  // the exact lane-per-path instance (knob 3: every frame)
+    const bool screen = h->screen && lx != 3 && !hist && !P.metrics && !P.cands && !P.force && !P.sc_hard && !P.fidx &&
                         !P.d_count &&
                         (P.fast ? (pscl_screening_available(P) != 0 || pscl_lane_long128_available(T) != 0)
                                 : pscl_lane_long_available(T) != 0);
@@ -428,6 +442,7 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
             X.fidx = (const int64_t*)d_list;
             X.d_count = (const int32_t*)d_cnt;
             X.out_by_row = 1;
+            X.lane_exact = lane_exact_on(h) ? 1 : 0;
             // few frames: one resident set of workgroups (4 waves/SIMD on 256 CUs), striding
             // over the listed frames, instead of a grid sized for the whole batch
             X.grid_cap = (int64_t)256 * 16 / (pscl_decode_wpg(X) > 0 ? pscl_decode_wpg(X) : 1);
@@ -437,6 +452,7 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
                 if (h->timing) HIP_TRY(hipEventRecord(e1, st));
                 HIP_TRY(hipEventRecord(h->ev_pscr[p], st));
                 HIP_TRY(hipStreamWaitEvent(h->pipe_stream, h->ev_pscr[p], 0));
+                if (!hist && pscl_lane_exact_available(X)) h->n_lane_exact++;
                 err = pscl_launch_decode(X, hist, h->pipe_stream);
                 if (err == hipSuccess && S.cpart)
                     err = pscl_launch_count_reduce(S.cpart, pscl_decode_count_slots(S, hist), S.counters, h->pipe_stream);
@@ -445,11 +461,14 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
                 h->px_pending[p] = true;
                 return PSCL_OK;
             }
+            if (!hist && pscl_lane_exact_available(X)) h->n_lane_exact++;
             err = pscl_launch_decode(X, hist, st);
         }
     } else {
+        if (lx == 3) P.lane_exact = 1;  // (test knob: plain decodes on the exact lane instance)
         const int rc = with_count_slots(h, P, hist, 92, st);
         if (rc) return rc;
+        if (!hist && pscl_lane_exact_available(P)) h->n_lane_exact++;
         err = pscl_launch_decode(P, hist, st);
         if (err == hipSuccess && P.cpart) err = pscl_launch_count_reduce(P.cpart, pscl_decode_count_slots(P, hist), P.counters, st);
     }
@@ -788,7 +807,7 @@ int pscl_set_pipelined(pscl_handle* h, int enable) {
 int pscl_set_tuning(pscl_handle* h, int knob, int64_t value) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
     static const int64_t lim[PSCL_TUNE_COUNT][2] = {{0, 0}, {0, 2}, {0, 64}, {0, 2}, {0, 1}, {0, 4096}, {0, PSCL_MAX_WAVES_PER_WG}, {0, 2},
-                                                    {0, (int64_t)1 << 30}, {0, 2}, {0, 32}, {0, 3}, {0, 2}, {0, 2}, {0, 4}};
+                                                    {0, (int64_t)1 << 30}, {0, 2}, {0, 32}, {0, 3}, {0, 2}, {0, 2}, {0, 4}, {0, 3}};
     if (knob < 1 || knob >= PSCL_TUNE_COUNT) return fail(PSCL_EINVAL, "unknown tuning knob %d", knob);
     if (value < lim[knob][0] || value > lim[knob][1] || (knob == PSCL_TUNE_POST_GRID && value && value < 16))
         return fail(PSCL_EINVAL, "tuning knob %d: value %lld out of range", knob, (long long)value);
@@ -976,6 +995,7 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     H.warm_metric = S.warm_metric;
     H.warm_u = S.warm_u;
     H.wpg_cap = (int)h->tune[PSCL_TUNE_RETRY_WPG];
+    H.lane_exact = lane_exact_on(h) ? 1 : 0;  // (exact retry rounds: the lane-per-path instance)
     if (pscl_decode_wpg(H) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
     int rc;
     // screening retry decodes (measured in DESIGN.md §5.4): the forced-bit screening instance
@@ -1053,6 +1073,7 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
             HIP_TRY(hipStreamWaitEvent(side, ev_s, 0));
             HX.elist = side_list(r);
             HX.bcount = side_cnt(r);
+            if (pscl_lane_exact_available(HX)) h->n_lane_exact++;
             if ((e = pscl_launch_decode(HX, 0, side)) != hipSuccess)
                 return fail(PSCL_EDEVICE, "exact retry re-decode: %s", hipGetErrorString(e));
             QD.in_list = side_list(r);
@@ -2020,8 +2041,9 @@ int pscl_host_stats(pscl_handle* h, double* call_ms, double* wait_ms, int64_t* c
 }
 
 int pscl_path_stats(pscl_handle* h, int64_t* fused_post_rounds, int64_t* post_rounds, int64_t* fused_tx_blocks,
-                    int64_t* post_epw4_launches) {
+                    int64_t* post_epw4_launches, int64_t* lane_exact_launches) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
+    if (lane_exact_launches) *lane_exact_launches = h->n_lane_exact;
     if (post_epw4_launches) *post_epw4_launches = h->n_post_epw4;
     if (fused_post_rounds) *fused_post_rounds = h->n_fpost_rounds;
     if (post_rounds) *post_rounds = h->n_post_rounds;

@@ -94,6 +94,21 @@ int pscl_lane_fs_available(const pscl_decode_params& P) {
     return spec_code(P) == 1;
 }
 
+// an exact decode of the (128,64) code (or the rate-matched NR (128,88) code) at L = 4, 8 without
+// metrics, candidates or decision LLRs runs the exact lane-per-path instance (P.lane_exact): plain
+// frames (optionally listed by P.fidx / P.d_count, outputs at their rows), or a forced-bit retry
+// round of the (128,64) code (bucket lists, warm start)
+int pscl_lane_exact_available(const pscl_decode_params& P) {
+    if (!P.lane_exact || P.apx || P.no_lane || P.sc_hard || P.tx || P.fpost || P.long_mode) return 0;
+    if (P.metrics || P.cands || P.info_llrs || P.best_info_llrs) return 0;
+    if (P.N != 128 || (P.L != 8 && P.L != 4)) return 0;
+    const int code = spec_code(P);
+    if (P.force)
+        return code == 1 && P.elist && P.fidx && P.warm_metric && P.warm_u && !P.d_count && !P.ref && !P.rm_E && !P.out_by_row;
+    if (P.elist) return 0;
+    return (code == 1 && !P.rm_E) || (code == 2 && P.rm_E);
+}
+
 int pscl_screening_available(const pscl_decode_params& P) {
     if (!P.fast || P.force || P.sc_hard || P.L != pscl_decode_lmax(P.L)) return 0;
     const int code = spec_code(P);

@@ -81,6 +81,8 @@ struct LaneLayout {
     // the fused post pass's FS instance replays the best path's 128 leaves in the frame's region
     // (208 doubles at L = 8; at L = 4 the stride grows 120 -> 152, still = 24 mod 32)
     static constexpr int FSTRIDE_FS = FSTRIDE >= 128 ? FSTRIDE : FSTRIDE + 32;
+    // the exact instance (EX) adds a frame's routing slots (16 ints: a survivor's code by list position)
+    static constexpr int FSTRIDE_EX = FSTRIDE + 8;
 };
 
 // monotone map of an fp64 to uint64 (total order of non-NaN values, -0 == +0), as dlscl.hip
@@ -167,11 +169,22 @@ __device__ __forceinline__ void tx_frame_words(const pscl_decode_params& P, uint
 // FP: the FS instance with the fused post pass (P.fpost; its own instantiation -- compiled into the
 // plain FS instance behind a runtime flag, the post's registers raised that kernel's peak too,
 // L = 8 173 -> 226 VGPRs, L = 4 240 -> 256 + 26 spilled)
-template <int LMAX, int CODE, bool FS = false, bool TXF = false, bool FP = false>
+// EX: the EXACT lane-per-path decode (pscl_launch_lane_exact): the deferred frames'
+// re-decode (plain, rows by P.fidx, outputs at their rows) and the exact forced-bit retry decodes (FS:
+// the side chain, unscreened chains).  Natural-log LLR tree, glibc-exact metric tails
+// (pscl_softplus_tail_bf), children metrics as scl128_kernel forms them, and the list kept in LIST
+// ORDER in the frame's lanes (lane p = list position p): the stable sort's (metric, 2 position + bit)
+// order decides every survivor set and position exactly (scl.py:163-174) -- in place when every
+// worse child lies above the largest better child and the better children are in order (the keep
+// tier), else by ranking the 2L children (each lane counts the keys below its two, DPP-free
+// shuffles over the frame's lanes) and routing the survivors through LDS slots; frozen phases
+// re-sort only when a metric fell below its predecessor's.  No certificates, no deferral.
+template <int LMAX, int CODE, bool FS = false, bool TXF = false, bool FP = false, bool EX = false>
 __global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(const pscl_decode_params P) {
     static_assert(LMAX == 4 || LMAX == 8, "the lane-per-path decoder is built for L = 4 and 8");
     static_assert(!TXF || (!FS && CODE == 1), "fused TX: plain decodes of the (128,64) code");
     static_assert(!FP || (FS && CODE == 1), "fused post pass: the FS instance of the (128,64) code");
+    static_assert(!EX || (!TXF && !FP), "the exact instance: plain re-decodes and forced-bit retry decodes");
     using Ly = LaneLayout<LMAX>;
     constexpr int G = Ly::G, F = Ly::F, LOG_G = Ly::LOG_G;
     constexpr int EPL = 16 / G;                 // depth-3 elements per lane at a recompute
@@ -183,7 +196,7 @@ __global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PS
     const int lane = threadIdx.x & 63;
     // frame fl of the wavefront and path index p of this lane; lane_lo / lane_hi: the frame's lanes
     // of p = 0 and p = 4 (PSCL_LANE_REMAP at L = 8), or its first lane
-    constexpr bool REMAP = PSCL_LANE_REMAP && G == 8;
+    constexpr bool REMAP = PSCL_LANE_REMAP && G == 8 && !EX;
     const int rq = (lane >> 2) & 3, inner = (rq == 1 || rq == 2) ? 1 : 0;
     const int fl = REMAP ? 2 * (lane >> 4) + inner : lane >> LOG_G;
     const int p = REMAP ? (lane & 3) + 4 * (rq & 1) : lane & (G - 1);
@@ -191,13 +204,14 @@ __global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PS
     const int lane_hi = REMAP ? (lane & ~15) + (inner ? 4 : 12) : lane_lo + 4;
     // the lane of path index q of this frame
     auto lane_of = [&](uint32_t q) -> int { return REMAP ? (q < 4u ? lane_lo + (int)q : lane_hi + (int)q - 4) : lane_lo + (int)q; };
-    double* const Af = A + fl * (FP ? Ly::FSTRIDE_FS : Ly::FSTRIDE);
+    double* const Af = A + fl * (FP ? Ly::FSTRIDE_FS : EX ? Ly::FSTRIDE_EX : Ly::FSTRIDE);
+    int* const sl = reinterpret_cast<int*>(Af + Ly::FSTRIDE);  // EX: the frame's routing slots
     const uint8_t* const GT = reinterpret_cast<const uint8_t*>(P.epi_table);   // [16][256] u-byte -> info bits
     const uint32_t* const ST = reinterpret_cast<const uint32_t*>(GT + 16 * 256);  // [K/4][16] nibble -> syndrome
     auto hiw = [](double m) { return (uint32_t)(pscl_asu64(m) >> 32); };
     // the margin-raised key hi(fma(m, 1 + 2^-40, MARGIN)) as one VOP3 fma with the factor in an SGPR
     // (left to itself the compiler emits a copy of the margin register plus v_fmac_f64)
-    constexpr bool BITS = !FS && PSCL_LANE_BITS;
+    constexpr bool BITS = !FS && !EX && PSCL_LANE_BITS;
     constexpr double MARGIN = BITS ? PSCL_TAIL2_MARGIN : PSCL_TAIL_ABS_MARGIN;
     auto hiw_up = [&](double m) {
         double r;
@@ -219,6 +233,8 @@ __global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PS
     if constexpr (FS) {
         const int64_t tot = pscl_bucket_prefix(P.bcount, P.bcap, bpre);
         Bn = tot < P.B ? tot : P.B;
+    } else if constexpr (EX) {  // (the re-decode: the first *d_count listed frames)
+        if (P.d_count) Bn = *P.d_count < P.B ? (int64_t)*P.d_count : P.B;
     }
     for (int64_t f0 = (int64_t)blockIdx.x * F; f0 < Bn; f0 += (int64_t)gridDim.x * F) {
         const int64_t fi = f0 + fl;
@@ -233,6 +249,8 @@ __global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PS
             f = pscl_elist_entry(P, fsafe, bpre);
             seg0 = pscl_bucket_of(f0, bpre);
             frow = P.fidx[f];
+        } else if constexpr (EX) {
+            if (P.fidx) frow = P.fidx[fsafe];
         }
         // CODE = 2 (the NR (128,88) code, config 5): the input rows are rate matched -- E received
         // LLRs, de-rate-matched and de-interleaved per position as the values are loaded
@@ -318,7 +336,7 @@ __global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PS
         double cs = fabs(c[0]);
 #pragma unroll
         for (int m = 1; m < 8 * EPL; ++m) cs = cs + fabs(c[m]);
-        uint64_t amb = wmask(!(cs < (BITS ? PSCL_TAIL2_CHAN_SUM : 0x1p25)));
+        uint64_t amb = EX ? 0ULL : wmask(!(cs < (BITS ? PSCL_TAIL2_CHAN_SUM : 0x1p25)));
         const uint64_t vmask = wmask(fvalid);
 
         double metric = 0.0;
@@ -511,7 +529,98 @@ __global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PS
                     for (int k = 0; k < 2; ++k) r6[k] = q6[k];
             };
             const double lam = (phi & 1) ? g_node(lab.x, lab.y, lastbit) : f_minsum(lab.x, lab.y);
-            const double Lt = BITS ? pscl_softplus_tail2(lam) : pscl_softplus_tail_abs(lam);
+            const double Lt = EX ? pscl_softplus_tail_bf(lam, P.exp_table) : BITS ? pscl_softplus_tail2(lam) : pscl_softplus_tail_abs(lam);
+            if constexpr (EX) {
+                // ---- exact: lanes 0..ncur-1 of the frame hold its live paths in list order
+                const int ncur = FS ? (1 << lcnt) : cnt;
+                const bool live = p < ncur;
+                const bool zl = lam == 0.0;
+                // the whole state of lane src's path (its metric chosen by the caller)
+                auto pull_path = [&](int src) {
+                    u0 = shfl_u64(u0, src);
+                    if constexpr (phi >= 64) u1 = shfl_u64(u1, src);
+                    tab = bperm32(tab, src);
+                    double q5[4], q6[2];
+                    carry(src, q5, q6);
+                    take(q5, q6);
+                };
+                if constexpr (!is_info) {  // bit 0 (scl.py:149-153), then the list re-sorted stably
+                    metric = zl ? metric + PSCL_LOGE2 : metric + (relu_neg(lam) + Lt);
+                    lastbit = 0;
+                    const double pm = shfl_f64(metric, p > 0 ? lane - 1 : lane);
+                    if ((wmask(live && pm > metric) & vmask) == 0) return;
+                    const double mk = live ? metric : __builtin_inf();
+                    uint32_t r = 0;
+#pragma unroll
+                    for (int sx = 1; sx < G; ++sx) {
+                        const double om = shfl_f64(mk, lane ^ sx);
+                        r += (om < mk || (om == mk && (p ^ sx) < p)) ? 1u : 0u;
+                    }
+                    if (live) sl[r] = p;
+                    wave_lds_fence();
+                    const int src = lane_lo + sl[p & (ncur - 1)];  // (lanes beyond the list: copies)
+                    wave_lds_fence();
+                    metric = shfl_f64(metric, src);
+                    pull_path(src);
+                    return;
+                }
+                // children metrics as scl128_kernel forms them (scl.py:102-105): along the LLR sign
+                // metric + L, against it metric + (|lam| + L); an exactly zero LLR both metric + ln 2
+                const bool neg = lam < 0.0;
+                const double mgd = metric + Lt, mbd = metric + (fabs(lam) + Lt);
+                double m0 = neg ? mbd : mgd, m1 = neg ? mgd : mbd;
+                if (zl) {
+                    m0 = metric + PSCL_LOGE2;
+                    m1 = m0;
+                }
+                bool forced = false;
+                uint32_t fbit = 0;
+                if constexpr (FS) {
+                    const uint64_t fmw = jb < 64 ? fm0 : fm1, fvw = jb < 64 ? fv0 : fv1;
+                    forced = ((fmw >> (jb & 63)) & 1ULL) != 0;
+                    fbit = (uint32_t)((fvw >> (jb & 63)) & 1ULL);
+                }
+                // frames decided without ranking: a forced single path takes the forced child; a
+                // full list keeps its better children in place when they stay in order and every
+                // worse child lies strictly above the largest of them (the stable sort's outcome)
+                const double top = shfl_f64(mgd, lane_lo + LMAX - 1), pg = shfl_f64(mgd, p > 0 ? lane - 1 : lane);
+                const bool badk = zl || (p > 0 && pg > mgd) || !(mbd > top);
+                const bool fast = forced ? ncur == 1 : (ncur == LMAX && frame_bits(wmask(badk)) == 0);
+                uint32_t b = forced ? fbit : sign_bit(lam);
+                if ((wmask(!fast) & vmask) != 0) {
+                    // rank the frame's valid children on (metric, 2 position + bit); the first ncnt
+                    // survive at list positions = their ranks (scl.py:163-174)
+                    const bool v0 = live && (!forced || fbit == 0u), v1 = live && (!forced || fbit == 1u);
+                    const int ncnt = forced ? ncur : (2 * ncur < LMAX ? 2 * ncur : LMAX);
+                    const double k0 = v0 ? m0 : __builtin_inf(), k1 = v1 ? m1 : __builtin_inf();
+                    uint32_t r0 = k1 < k0 ? 1u : 0u, r1 = k0 <= k1 ? 1u : 0u;
+#pragma unroll
+                    for (int sx = 1; sx < G; ++sx) {
+                        const double o0 = shfl_f64(k0, lane ^ sx), o1 = shfl_f64(k1, lane ^ sx);
+                        const bool lt = (p ^ sx) < p;
+                        r0 += ((o0 < k0 || (o0 == k0 && lt)) ? 1u : 0u) + ((o1 < k0 || (o1 == k0 && lt)) ? 1u : 0u);
+                        r1 += ((o0 < k1 || (o0 == k1 && lt)) ? 1u : 0u) + ((o1 < k1 || (o1 == k1 && lt)) ? 1u : 0u);
+                    }
+                    if (!fast) {
+                        if (v0 && r0 < (uint32_t)ncnt) sl[r0] = 2 * p;
+                        if (v1 && r1 < (uint32_t)ncnt) sl[r1] = 2 * p + 1;
+                    }
+                    wave_lds_fence();
+                    const int code = fast ? 2 * p + (int)b : sl[p & (ncnt - 1)];  // (beyond the list: copies)
+                    wave_lds_fence();
+                    const int src = lane_lo + (code >> 1);
+                    b = (uint32_t)code & 1u;
+                    const double p0 = shfl_f64(m0, src), p1 = shfl_f64(m1, src);
+                    metric = b ? p1 : p0;
+                    pull_path(src);
+                    if constexpr (FS) lcnt += (!fast && !forced && ncur < LMAX) ? 1 : 0;
+                } else {
+                    metric = b ? m1 : m0;
+                }
+                if (phi < 64) u0 |= (uint64_t)b << phi; else u1 |= (uint64_t)b << (phi - 64);
+                lastbit = b;
+                return;
+            }
             if constexpr (!is_info) {  // frozen: bit 0 (scl.py:149-153)
                 metric = metric + (relu_neg(lam) + Lt);
                 lastbit = 0;
@@ -1055,15 +1164,19 @@ __global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PS
             r += oh < kh ? 1u : 0u;
             near = near || !(ku < oh || ou < kh);
         };
-        cmp_perm(dpp32<kQX1>(kh), dpp32<kQX1>(ku));
-        cmp_perm(dpp32<kQX2>(kh), dpp32<kQX2>(ku));
-        cmp_perm(dpp32<kQX3>(kh), dpp32<kQX3>(ku));
-        if constexpr (G == 8) {
-            const uint32_t mh = dpp32<kFMIR>(kh), mu = dpp32<kFMIR>(ku);
-            cmp_perm(mh, mu);
-            cmp_perm(dpp32<kQX1>(mh), dpp32<kQX1>(mu));
-            cmp_perm(dpp32<kQX2>(mh), dpp32<kQX2>(mu));
-            cmp_perm(dpp32<kQX3>(mh), dpp32<kQX3>(mu));
+        if constexpr (EX) {
+            r = (uint32_t)p;  // (the exact instance keeps list order in its lanes)
+        } else {
+            cmp_perm(dpp32<kQX1>(kh), dpp32<kQX1>(ku));
+            cmp_perm(dpp32<kQX2>(kh), dpp32<kQX2>(ku));
+            cmp_perm(dpp32<kQX3>(kh), dpp32<kQX3>(ku));
+            if constexpr (G == 8) {
+                const uint32_t mh = dpp32<kFMIR>(kh), mu = dpp32<kFMIR>(ku);
+                cmp_perm(mh, mu);
+                cmp_perm(dpp32<kQX1>(mh), dpp32<kQX1>(mu));
+                cmp_perm(dpp32<kQX2>(mh), dpp32<kQX2>(mu));
+                cmp_perm(dpp32<kQX3>(mh), dpp32<kQX3>(mu));
+            }
         }
         amb |= wmask(near && live) & vmask;
         const bool famb = frame_bits(amb) != 0;
@@ -1085,15 +1198,16 @@ __global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PS
         if (fvalid && !famb && keyb == kbest) {
             const int best = (int)(kbest & (uint32_t)(LMAX - 1));
             const bool bpass = kbest < (uint32_t)LMAX;
+            const int64_t fo = (EX && !FS && P.out_by_row) ? frow : f;  // (the re-decode: at the frame's row)
             if (P.best) {
-                P.best[f * PW] = ib0;
-                if (PW > 1) P.best[f * PW + 1] = ib1;
+                P.best[fo * PW] = ib0;
+                if (PW > 1) P.best[fo * PW + 1] = ib1;
             }
-            if (P.flags) P.flags[f] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
-            if (P.n_paths) P.n_paths[f] = FS ? (1 << lcnt) : LMAX;
+            if (P.flags) P.flags[fo] = (uint8_t)((bpass ? PSCL_FLAG_CRC_PASS : 0u) | (uint32_t)best);
+            if (P.n_paths) P.n_paths[fo] = FS ? (1 << lcnt) : LMAX;
             if (!FS && P.ref) {
                 const uint64_t ibw[2] = {ib0, ib1};
-                tally_errors(ibw, TXF ? tm : P.ref + fi * PW, PW, P.k_payload, bpass, cfe, cbe, cpe, cpb);
+                tally_errors(ibw, TXF ? tm : P.ref + fo * PW, PW, P.k_payload, bpass, cfe, cbe, cpe, cpb);
             }
         }
         if constexpr (FS) {
@@ -1111,7 +1225,7 @@ __global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PS
     }
     if (!FS && P.ref) {
         flush_counts_p(P, blockIdx.x, cfe, cbe, cpe, cpb);
-        if (blockIdx.x == 0 && threadIdx.x == 0)
+        if (blockIdx.x == 0 && threadIdx.x == 0 && !(EX && P.out_by_row))  // (a re-decode's frames were counted)
             atomicAdd(reinterpret_cast<unsigned long long*>(P.counters) + PSCL_CNT_FRAMES, (unsigned long long)P.B);
     }
     if constexpr (FS) {
@@ -1165,6 +1279,41 @@ hipError_t pscl_launch_lane(const pscl_decode_params& P, int64_t grid, hipStream
         hipLaunchKernelGGL((scl_lane_kernel<4, 2>), dim3((unsigned)grid), dim3(64), lds4, s, P);
     else
         return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+// the exact lane-per-path launch (pscl_lane_exact_available): the deferred frames' re-decode of a
+// plain decode, or an exact forced-bit retry round (FS); grid capped by P.grid_cap
+int64_t pscl_lane_exact_grid(const pscl_decode_params& P) {
+    const int F = 64 / P.L;
+    const int64_t grid = (P.B + F - 1) / F, cap = P.grid_cap > 0 ? P.grid_cap : (1 << 20);
+    return grid < 1 ? 1 : (grid > cap ? cap : grid);
+}
+
+hipError_t pscl_launch_lane_exact(const pscl_decode_params& P, hipStream_t s) {
+    const int64_t grid = pscl_lane_exact_grid(P);
+    const int lds8 = LaneLayout<8>::F * LaneLayout<8>::FSTRIDE_EX * 8, lds4 = LaneLayout<4>::F * LaneLayout<4>::FSTRIDE_EX * 8;
+    const dim3 g((unsigned)grid), b(64);
+    if (P.force) {
+        if (P.L == 8)
+            hipLaunchKernelGGL((scl_lane_kernel<8, 1, true, false, false, true>), g, b, lds8, s, P);
+        else if (P.L == 4)
+            hipLaunchKernelGGL((scl_lane_kernel<4, 1, true, false, false, true>), g, b, lds4, s, P);
+        else
+            return hipErrorInvalidValue;
+    } else if (P.L == 8) {
+        if (P.rm_E)
+            hipLaunchKernelGGL((scl_lane_kernel<8, 2, false, false, false, true>), g, b, lds8, s, P);
+        else
+            hipLaunchKernelGGL((scl_lane_kernel<8, 1, false, false, false, true>), g, b, lds8, s, P);
+    } else if (P.L == 4) {
+        if (P.rm_E)
+            hipLaunchKernelGGL((scl_lane_kernel<4, 2, false, false, false, true>), g, b, lds4, s, P);
+        else
+            hipLaunchKernelGGL((scl_lane_kernel<4, 1, false, false, false, true>), g, b, lds4, s, P);
+    } else {
+        return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -151,6 +151,9 @@ struct pscl_decode_params {
     int fpost;
     pscl_post_params fp;
     const float* fp_beta32g;     // beta in fp32, [K][G][K / G] (lane p's candidates p + G i contiguous), or null
+    // 1: an exact decode of the compiled-in N = 128 codes at L = 4, 8 may run on the exact lane-per-path
+    // instance (pscl_lane_exact_available: the deferred frames' re-decode, exact forced-bit retry rounds)
+    int lane_exact;
 };
 
 #define PSCL_DL_NSEG 8     // 16-phase segments of N = 128: warm-start buckets
@@ -300,6 +303,9 @@ int pscl_screening_fs_available(const pscl_decode_params& P);  // forced-bit scr
 // the lane-per-path form of a screened DL-SCL retry decode (scl128_lane.hip, FS)
 int pscl_lane_fs_available(const pscl_decode_params& P);
 hipError_t pscl_launch_lane_fs(const pscl_decode_params& P, int64_t grid, hipStream_t s);
+int pscl_lane_exact_available(const pscl_decode_params& P);
+hipError_t pscl_launch_lane_exact(const pscl_decode_params& P, hipStream_t s);
+int64_t pscl_lane_exact_grid(const pscl_decode_params& P);  // its workgroups (one wavefront each)
 hipError_t pscl_launch_decode128(const pscl_decode_params& P, int hist, int wpg, int64_t grid, int lds, hipStream_t s);
 int64_t pscl_decode_grid(const pscl_decode_params& P);
 int pscl_decode_wpg(const pscl_decode_params& P);

@@ -622,6 +622,7 @@ hipError_t pscl_launch_decode(const pscl_decode_params& P, int hist, hipStream_t
         return pscl_launch_lane_fs(P, g < 1 ? 1 : (g > (1 << 20) ? (1 << 20) : g), s);
     }
     if (!hist && lane_long128(P)) return pscl_launch_lane_long(P, s);
+    if (!hist && pscl_lane_exact_available(P)) return pscl_launch_lane_exact(P, s);
     if (pscl_decode_wpg(P) < 1) return hipErrorInvalidValue;
     const int64_t grid = pscl_decode_grid(P);
     if (P.fast) return pscl_launch_decode128(P, hist, pscl_decode_wpg(P), grid, decode_lds_bytes(P, hist), s);
@@ -648,6 +649,7 @@ int64_t pscl_decode_count_slots(const pscl_decode_params& P0, int hist) {
         return g < 1 ? 1 : (g > (1 << 20) ? (1 << 20) : g);
     }
     if (lane_long128(P)) return pscl_lane_long_grid(P);
+    if (pscl_lane_exact_available(P)) return pscl_lane_exact_grid(P);
     if (!P.fast || pscl_decode_wpg(P) < 1) return 0;  // (the generic kernel adds per frame)
     return pscl_decode_grid(P) * pscl_decode_wpg(P);
 }

@@ -145,6 +145,8 @@ def _dl_config(L, beta_name, ebno, nb, seed, tuning=None, pipelined=False):
             dec.join()
         dec.sync()
         paths = dec.path_stats()
+        if tuning and "lane_exact" in tuning:  # (exact retry rounds / side chain on the lane instance)
+            assert (paths["lane_exact_launches"] > 0) == (tuning["lane_exact"] == 1), paths
         if tuning and "post_epw" in tuning:
             assert (paths["post_epw4_launches"] > 0) == (pipelined and tuning["post_epw"] == 4), paths
         if tuning and tuning.get("dl_fused_post") == 1:  # (the schedule under test ran)
@@ -187,6 +189,10 @@ def test_config4_dlscl_L4_r8_beta4_1e6_frames_vs_oracle():
     (8, "M8", 4.5, 200_000, {"dl_screen": 1, "dl_fused_post": 1}),  # the post pass fused into the retry decodes
     (4, "M4", 5.0, 1_000_000, {"dl_screen": 1, "dl_fused_post": 1}),
     (8, "M8", 4.5, 200_000, {"dl_screen": 1, "dl_fused_post": 2}),  # the separate post pass
+    (8, "M8", 4.0, 200_000, {"dl_screen": 2, "lane_exact": 1}),  # every retry round exact, lane-per-path
+    (4, "M4", 5.0, 1_000_000, {"dl_screen": 2, "lane_exact": 1}),
+    (8, "M8", 4.0, 200_000, {"dl_screen": 2, "lane_exact": 2}),  # every retry round on the exact kernel
+    (8, "M8", 4.5, 200_000, {"dl_screen": 1, "lane_exact": 2}),  # the side chain on the exact kernel
 ])
 def test_dlscl_screened_retry_decodes_vs_oracle(L, beta, ebno, nb, tuning):
     """Screened DL-SCL retry rounds (forced-bit screening decodes + exact decodes of the entries
