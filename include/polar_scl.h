@@ -338,6 +338,10 @@ int pscl_join(pscl_handle* h);
  *                           exact lane-per-path kernel, 2 on the two-lanes-per-path exact kernel;
  *                           3 (tests) also every plain decode, unscreened; 0 (default): the measured
  *                           faster
+ *   PSCL_TUNE_DL_WARM_APX   1: the screened DL-SCL chain's warm-start metrics from the screening tail
+ *                           (the post pass skips the exact tails; entries its decodes defer start
+ *                           the side chain's exact decode at phase 0), 2: exact warm-start metrics;
+ *                           0 (default): the measured faster
  */
 #define PSCL_TUNE_DL_SCREEN 1
 #define PSCL_TUNE_DL_CHUNKS 2
@@ -354,7 +358,8 @@ int pscl_join(pscl_handle* h);
 #define PSCL_TUNE_DL_FUSED_POST 13
 #define PSCL_TUNE_POST_EPW 14
 #define PSCL_TUNE_LANE_EXACT 15
-#define PSCL_TUNE_COUNT 16
+#define PSCL_TUNE_DL_WARM_APX 16
+#define PSCL_TUNE_COUNT 17
 int pscl_set_tuning(pscl_handle* h, int knob, int64_t value);
 
 /*

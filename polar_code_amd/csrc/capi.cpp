@@ -807,7 +807,7 @@ int pscl_set_pipelined(pscl_handle* h, int enable) {
 int pscl_set_tuning(pscl_handle* h, int knob, int64_t value) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
     static const int64_t lim[PSCL_TUNE_COUNT][2] = {{0, 0}, {0, 2}, {0, 64}, {0, 2}, {0, 1}, {0, 4096}, {0, PSCL_MAX_WAVES_PER_WG}, {0, 2},
-                                                    {0, (int64_t)1 << 30}, {0, 2}, {0, 32}, {0, 3}, {0, 2}, {0, 2}, {0, 4}, {0, 3}};
+                                                    {0, (int64_t)1 << 30}, {0, 2}, {0, 32}, {0, 3}, {0, 2}, {0, 2}, {0, 4}, {0, 3}, {0, 2}};
     if (knob < 1 || knob >= PSCL_TUNE_COUNT) return fail(PSCL_EINVAL, "unknown tuning knob %d", knob);
     if (value < lim[knob][0] || value > lim[knob][1] || (knob == PSCL_TUNE_POST_GRID && value && value < 16))
         return fail(PSCL_EINVAL, "tuning knob %d: value %lld out of range", knob, (long long)value);
@@ -927,6 +927,10 @@ struct DlState {
     uint8_t* of2;            //   `of` concurrently, where the deferred mark must stay)
 };
 
+#ifndef PSCL_DL_WARM_APX_DEFAULT
+#define PSCL_DL_WARM_APX_DEFAULT 1  // (measured: profiles/r06t_warm_apx_ab.txt)
+#endif
+
 hipError_t launch_post(pscl_handle* h, const pscl_post_params& Q, int64_t A, hipStream_t s) {
     if (pscl_post_epw(Q) == 4) h->n_post_epw4++;
     return pscl_launch_dl_post(Q, A, s);
@@ -975,12 +979,6 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
     Q.tried_stride = tried_stride;
     Q.counters = d_cnt_dl;
     int32_t* lists[2] = {S.list0, S.list1};
-    // first flips: replay of every baseline best path (flip.py:97-111)
-    Q.init = 1;
-    Q.in_count = nullptr;
-    Q.out_count = S.bcnt;
-    Q.out_list = lists[0];
-    if ((e = launch_post(h, Q, A, st)) != hipSuccess) return fail(PSCL_EDEVICE, "dl_post launch: %s", hipGetErrorString(e));
     // the retry decodes: entries bucket by bucket, LLR rows by indirection, forced prefixes,
     // warm-started past them (the compiled-in FS kernels; others decode from phase 0)
     pscl_decode_params H;
@@ -1048,7 +1046,22 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
         QD.ob = S.ob2;
         QD.of = S.of2;
         HIP_TRY(hipMemsetAsync(S.dcnt, 0, (size_t)(rounds + 1) * bstride * 4, st));
+        // the main chain's warm-start metrics from the screening tail (PSCL_TUNE_DL_WARM_APX): its
+        // screened decodes certify against margins that cover every increment's tail error, the
+        // prefix's too; the entries they defer go to the side chain's bucket 0 (exact from phase 0),
+        // whose own posts (QD) keep exact metrics
+        const int64_t wk = h->tune[PSCL_TUNE_DL_WARM_APX];
+        if (!fpost && (wk == 1 || (wk == 0 && PSCL_DL_WARM_APX_DEFAULT))) {
+            Q.warm_apx = 1;
+            HA.warm_apx = 1;
+        }
     }
+    // first flips: replay of every baseline best path (flip.py:97-111)
+    Q.init = 1;
+    Q.in_count = nullptr;
+    Q.out_count = S.bcnt;
+    Q.out_list = lists[0];
+    if ((e = launch_post(h, Q, A, st)) != hipSuccess) return fail(PSCL_EDEVICE, "dl_post launch: %s", hipGetErrorString(e));
     auto side_list = [&](int r) { return S.dlist + (size_t)r * PSCL_DL_NSEG * (size_t)A; };
     auto side_cnt = [&](int r) { return S.dcnt + (size_t)r * bstride; };
     Q.init = 0;

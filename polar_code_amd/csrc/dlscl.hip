@@ -658,17 +658,24 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(EP
                 // ---- exact metric increments of the forced prefix's leaves (scl.py:102-105, as
                 // the decode kernel forms them: good child metric + L, bad child metric +
                 // (|llr| + L), llr == 0: metric + LOGE2), then summed in phase order
+                // (Q.warm_apx: the screening tail, PSCL_TUNE_DL_WARM_APX -- a screened decode's own)
+                auto tails = [&](auto tailf) {
 #pragma unroll
-                for (int m = 0; m < EL; ++m) {
-                    const int p = hl + HLN * m;
-                    if (p < 16 * seg) {
-                        const double lam = cur[p];  // (the leaves stay in cur)
-                        const uint32_t bit = (uint32_t)(((p < 64 ? u0 : u1) >> (p & 63)) & 1ULL);
-                        const double Lt = pscl_softplus_tail_bf(lam, S.exp_table);
-                        const bool good = bit == (lam < 0.0 ? 1u : 0u);
-                        nxt[p] = lam == 0.0 ? PSCL_LOGE2 : (good ? Lt : fabs(lam) + Lt);
+                    for (int m = 0; m < EL; ++m) {
+                        const int p = hl + HLN * m;
+                        if (p < 16 * seg) {
+                            const double lam = cur[p];  // (the leaves stay in cur)
+                            const uint32_t bit = (uint32_t)(((p < 64 ? u0 : u1) >> (p & 63)) & 1ULL);
+                            const double Lt = tailf(lam);
+                            const bool good = bit == (lam < 0.0 ? 1u : 0u);
+                            nxt[p] = lam == 0.0 ? PSCL_LOGE2 : (good ? Lt : fabs(lam) + Lt);
+                        }
                     }
-                }
+                };
+                if (Q.warm_apx)
+                    tails([](double v) { return pscl_softplus_tail_abs(v); });
+                else
+                    tails([&](double v) { return pscl_softplus_tail_bf(v, S.exp_table); });
                 pscl::wave_lds_fence();
                 if (more && hl == 0) {
                     double mt = 0.0;

@@ -926,7 +926,7 @@ scl128_kernel(const pscl_decode_params P) {
         const bool famb = APX && ((amb >> gbase) & (G == 64 ? ~0ULL : ((1ULL << (G & 63)) - 1))) != 0;
         if (APX && !PSCL_APX_ABLATE && famb && g == 0 && fvalid) {
             if (FS && P.amb_elist) {  // DL-SCL retry round: into the entry's bucket, flagged deferred
-                const int fseg = pscl_bucket_of(fsafe, bpre);
+                const int fseg = P.warm_apx ? 0 : pscl_bucket_of(fsafe, bpre);  // (screening warm metrics: exact from phase 0)
                 const int slot = atomicAdd(P.amb_count + fseg * PSCL_DL_CSTRIDE, 1);
                 P.amb_elist[(int64_t)fseg * P.bcap + slot] = (int32_t)f;
                 P.flags[f] = PSCL_DL_DEFERRED;

@@ -1183,7 +1183,7 @@ __global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PS
         if (famb && p == 0 && fvalid) {
             if constexpr (FS) {  // DL-SCL retry round: into the entry's deferred bucket (with the
                                  // fused post pass bucket 0: its warm metric is a screening one)
-                const int fseg = FP ? 0 : pscl_bucket_of(fsafe, bpre);
+                const int fseg = (FP || P.warm_apx) ? 0 : pscl_bucket_of(fsafe, bpre);
                 const int slot = atomicAdd(P.amb_count + fseg * PSCL_DL_CSTRIDE, 1);
                 P.amb_elist[(int64_t)fseg * P.bcap + slot] = (int32_t)f;
                 P.flags[f] = PSCL_DL_DEFERRED;

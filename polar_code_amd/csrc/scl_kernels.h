@@ -32,6 +32,8 @@ struct pscl_post_params {
     int rounds;                  // min(retries, K)
     int narrow;                  // small workgroups, beta through L2 (pipelined calls, dl_post_kernel)
     int epw;                     // narrow form: entries per wavefront (2, 4; 0: PSCL_POST_EPW_NARROW)
+    int warm_apx;                // 1: warm-start metrics from the screening tail (the main chain of a
+                                 // screened chain, PSCL_TUNE_DL_WARM_APX), 0: exact
     int64_t grid_cap;            // 0, or the workgroup cap of a launch (tuning knob; default PSCL_POST_GRID)
     int64_t pairs;               // 0, or the entry pairs per wavefront the grid is sized for (tuning knob)
     int init;
@@ -154,6 +156,9 @@ struct pscl_decode_params {
     // 1: an exact decode of the compiled-in N = 128 codes at L = 4, 8 may run on the exact lane-per-path
     // instance (pscl_lane_exact_available: the deferred frames' re-decode, exact forced-bit retry rounds)
     int lane_exact;
+    // 1: a screened retry round whose warm-start metrics are screening sums (PSCL_TUNE_DL_WARM_APX):
+    // the entries it defers go to bucket 0 of the side list (their exact decode starts at phase 0)
+    int warm_apx;
 };
 
 #define PSCL_DL_NSEG 8     // 16-phase segments of N = 128: warm-start buckets

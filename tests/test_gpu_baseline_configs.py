@@ -193,6 +193,9 @@ def test_config4_dlscl_L4_r8_beta4_1e6_frames_vs_oracle():
     (4, "M4", 5.0, 1_000_000, {"dl_screen": 2, "lane_exact": 1}),
     (8, "M8", 4.0, 200_000, {"dl_screen": 2, "lane_exact": 2}),  # every retry round on the exact kernel
     (8, "M8", 4.5, 200_000, {"dl_screen": 1, "lane_exact": 2}),  # the side chain on the exact kernel
+    (8, "M8", 4.5, 200_000, {"dl_screen": 1, "dl_warm_apx": 1}),  # screening-tail warm starts (default)
+    (8, "M8", 4.5, 200_000, {"dl_screen": 1, "dl_warm_apx": 2}),  # exact warm starts, deferrals at their bucket
+    (8, "M8", 4.0, 100_000, {"dl_screen": 1, "dl_warm_apx": 1, "dl_retry_lane": 2}),  # (two-lanes-per-path screening)
 ])
 def test_dlscl_screened_retry_decodes_vs_oracle(L, beta, ebno, nb, tuning):
     """Screened DL-SCL retry rounds (forced-bit screening decodes + exact decodes of the entries
@@ -200,15 +203,18 @@ def test_dlscl_screened_retry_decodes_vs_oracle(L, beta, ebno, nb, tuning):
     _screened_vs_oracle(L, beta, ebno, nb, tuning, False)
 
 
-@pytest.mark.parametrize("L,beta,ebno,nb,epw", [
-    (4, "M4", 5.0, 1_000_000, 4),  # config 4 as the bench runs it: the narrow post pass, 4 entries per wavefront
-    (8, "M8", 4.0, 200_000, 4),
-    (8, "M8", 4.0, 200_000, 2),    # 2 entries per wavefront
+@pytest.mark.parametrize("L,beta,ebno,nb,tuning", [
+    (4, "M4", 5.0, 1_000_000, {"post_epw": 4}),  # config 4 as the bench runs it: the narrow post pass, 4 entries per wavefront
+    (8, "M8", 4.0, 200_000, {"post_epw": 4}),
+    (8, "M8", 4.0, 200_000, {"post_epw": 2}),    # 2 entries per wavefront
+    (4, "M4", 5.0, 1_000_000, {"dl_warm_apx": 1}),  # screening-tail warm starts, deferrals exact from phase 0
+    (8, "M8", 4.0, 200_000, {"dl_warm_apx": 1}),
 ])
-def test_dlscl_pipelined_post_forms_vs_oracle(L, beta, ebno, nb, epw):
+def test_dlscl_pipelined_post_forms_vs_oracle(L, beta, ebno, nb, tuning):
     """The narrow (pipelined) post pass in both forms (PSCL_TUNE_POST_EPW: 32 or 16 lanes per entry)
-    against the oracle on every frame."""
-    _screened_vs_oracle(L, beta, ebno, nb, {"post_epw": epw}, True)
+    and with screening-tail warm-start metrics (PSCL_TUNE_DL_WARM_APX) against the oracle on every
+    frame."""
+    _screened_vs_oracle(L, beta, ebno, nb, tuning, True)
 
 
 def test_post_epw_knob_validated():

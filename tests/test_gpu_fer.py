@@ -232,13 +232,16 @@ def test_device_retry_loop_split_chains(chunks, split):
     assert dev["counters"]["dl"][1] == int((~host["success"]).sum())
 
 
-@pytest.mark.parametrize("L,depth,split,epw", [(4, 2, 0, 0), (8, 2, 0, 0), (4, 4, 0, 0), (8, 3, 0, 0), (4, 3, 2, 0),
-                                               (4, 2, 0, 4), (8, 3, 0, 4), (4, 2, 0, 2)])
-def test_pipelined_dlscl_calls_equal_stream_ordered(L, depth, split, epw):
+@pytest.mark.parametrize("L,depth,split,tune", [(4, 2, 0, {}), (8, 2, 0, {}), (4, 4, 0, {}), (8, 3, 0, {}), (4, 3, 2, {}),
+                                                (4, 2, 0, {"post_epw": 4}), (8, 3, 0, {"post_epw": 4}),
+                                                (4, 2, 0, {"post_epw": 2}), (4, 3, 0, {"dl_warm_apx": 1}),
+                                                (8, 2, 0, {"dl_warm_apx": 2})])
+def test_pipelined_dlscl_calls_equal_stream_ordered(L, depth, split, tune):
     """pscl_set_pipelined on pscl_dlscl_device: each call's retry chains and DL counters stay on
     the retry streams and overlap the next call's baseline (and, in the other chain set, the
-    previous call's chains); split 0 = the pipelined default (one chain per call), 2 = two; epw:
-    the narrow post pass's entries per wavefront (PSCL_TUNE_POST_EPW).  Calls on `depth` rotating output buffers (as bench.py's steps): a
+    previous call's chains); split 0 = the pipelined default (one chain per call), 2 = two; tune:
+    the narrow post pass's entries per wavefront (PSCL_TUNE_POST_EPW), screening-tail warm starts
+    (PSCL_TUNE_DL_WARM_APX).  Calls on `depth` rotating output buffers (as bench.py's steps): a
     call's buffers are reused by the depth-th following call, which must start after that call's
     chains end.  After a join the last `depth` calls' bits, flags and attempts and the SCL/DL
     counters of all calls equal the stream-ordered calls'."""
@@ -253,8 +256,8 @@ def test_pipelined_dlscl_calls_equal_stream_ordered(L, depth, split, epw):
         dec.set_pipelined(pipe, depth=depth)
         if split:
             dec.set_tuning(dl_split=split)
-        if epw:
-            dec.set_tuning(post_epw=epw)
+        if tune:
+            dec.set_tuning(**tune)
         with _native.DeviceArena(dec) as mem:
             d_llr = [mem.alloc(B * 128 * 8) for _ in range(nb)]
             d_msg = [mem.alloc(B * 8) for _ in range(nb)]
@@ -268,8 +271,8 @@ def test_pipelined_dlscl_calls_equal_stream_ordered(L, depth, split, epw):
                 dec.dlscl_device(d_llr[i], B, 8, beta=beta, d_best=o[0], d_flags=o[1], d_attempts=o[2],
                                  d_ref=d_msg[i], k_payload=40, d_counters_scl=d_cnt, d_counters_dl=d_cnt + nc * 8)
             dec.join()
-            if epw:
-                assert (dec.path_stats()["post_epw4_launches"] > 0) == (pipe and epw == 4)
+            if "post_epw" in tune:
+                assert (dec.path_stats()["post_epw4_launches"] > 0) == (pipe and tune["post_epw"] == 4)
             res[pipe] = ([(mem.download(b, B * 8, np.uint64), mem.download(f, B, np.uint8),
                            mem.download(a, B * 4, np.int32)) for b, f, a in d_out],
                          mem.download(d_cnt, 2 * nc * 8, np.int64).reshape(2, nc))
