@@ -677,13 +677,32 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(EP
                 else
                     tails([&](double v) { return pscl_softplus_tail_bf(v, S.exp_table); });
                 pscl::wave_lds_fence();
+                if (Q.warm_apx) {
+                    // screening warm metrics (any summation order: the screened decode's relative
+                    // slack covers it): the 16-phase blocks summed in parallel, lane b block b,
+                    // into cur (its leaves are read)
+                    if (hl < seg) {
+                        double bsum = 0.0;
+#pragma unroll
+                        for (int qq = 0; qq < 16; ++qq) bsum = bsum + nxt[16 * hl + qq];
+                        cur[hl] = bsum;
+                    }
+                    pscl::wave_lds_fence();
+                }
                 if (more && hl == 0) {
                     double mt = 0.0;
                     double* wm = Q.warm_metric + (int64_t)e * PSCL_DL_NSEG;
-                    for (int k = 0; k <= seg; ++k) {
-                        wm[k] = mt;
-                        if (k < seg && !(PSCL_POST_ABLATE & 8))
-                            for (int qq = 0; qq < 16; ++qq) mt = mt + nxt[16 * k + qq];
+                    if (Q.warm_apx) {
+                        for (int k = 0; k <= seg; ++k) {
+                            wm[k] = mt;
+                            if (k < seg) mt = mt + cur[k];
+                        }
+                    } else {  // exact: in phase order, as the exact decode accumulates them
+                        for (int k = 0; k <= seg; ++k) {
+                            wm[k] = mt;
+                            if (k < seg && !(PSCL_POST_ABLATE & 8))
+                                for (int qq = 0; qq < 16; ++qq) mt = mt + nxt[16 * k + qq];
+                        }
                     }
                     Q.warm_u[2 * e] = u0;
                     Q.warm_u[2 * e + 1] = u1;
