@@ -189,7 +189,8 @@ __global__ void __launch_bounds__(256) replay_kernel(const pscl_replay_params R,
 
 // Timing-only ablations of dl_post_kernel (tools/build_variant.py --unit dlscl
 // -DPSCL_POST_ABLATE=m; 0 in the product, results invalid otherwise): 1 no bucket atomics,
-// 2 no warm-start tails, 4 no flip metric (q = |L0|), 8 no serial prefix sums
+// 2 no warm-start tails, 4 no flip metric (q = |L0|), 8 no serial prefix sums, 64 no exact
+// fallback of uncertified packed flip sums
 #ifndef PSCL_POST_ABLATE
 #define PSCL_POST_ABLATE 0
 #endif
@@ -238,6 +239,15 @@ __global__ void __launch_bounds__(256) replay_kernel(const pscl_replay_params R,
 #endif
 // the flip metric's sums with fused multiply-adds, certified against the exact sums' bound (1), or
 // the exact index-order sums throughout (0)
+// the packed fp32 flip sums of the 2-entry narrow form on the matrix cores (1: v_mfma_f32_16x16x4_f32,
+// bit for bit the same k-ordered fp32 fma chains, MI355X_MICROARCH.md, leaving the VALU to the decode
+// beside it), or as v_pk_fma_f32 on the VALU (0).  Measured (profiles/r06v_post_mfma_ab.txt): bit-
+// identical, config 4 2.27 against 2.19 ms -- a post wavefront's 64 MFMAs (16 columns, 2 used) hold
+// its slot and LDS ~2,000 cycles longer per entry pair, and that costs the decode more than the
+// VALU cycles it gives back: off
+#ifndef PSCL_POST_MFMA
+#define PSCL_POST_MFMA 0
+#endif
 #ifndef PSCL_POST_FMA
 #define PSCL_POST_FMA 1
 #endif
@@ -299,6 +309,7 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(EP
     constexpr bool K1 = KC > 0 && KC <= 64;                 // one word of information bits
     // (sums unrolled less in the 4-entry form: its twice as many candidates per lane hold the loads)
     constexpr int kSumUnroll = EPW == 4 ? 2 : PSCL_POST_UNROLL, kPkUnroll = EPW == 4 ? 2 : 4;
+    constexpr bool MF = PSCL_POST_MFMA && KC == 64 && EPW == 2;  // (flip sums on the matrix cores)
     __shared__ PostShared<PW, EPW> S;
     extern __shared__ double sbeta[];  // [K][K]: fp64 when beta_lds == 1, fp32 when 2
     float* const sbeta32 = reinterpret_cast<float*>(sbeta);
@@ -309,8 +320,14 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(EP
     if (beta_lds == 1)
         for (int i = threadIdx.x; i < K * K; i += blockDim.x) sbeta[i] = Q.beta[i];
     else if (beta_lds == 2) {
-        if constexpr (KC == 64) {  // lane layout [k][hl][m] = beta[k][hl + HLN m]: one 8- (16-) byte read
-                                   // gives a lane all of its 2 (4) candidates (the packed sums below)
+        if constexpr (MF) {  // [k][j ^ 16 (k & 3)]: the MFMA's A operand rows k = 4 s + kl, columns
+                             // 16 t + jl read without bank conflicts (each kl group on its own 16 banks)
+            for (int i = threadIdx.x; i < K * K; i += blockDim.x) {
+                const int k = i >> 6, j = i & 63;
+                sbeta32[k * 64 + (j ^ (16 * (k & 3)))] = (float)Q.beta[i];
+            }
+        } else if constexpr (KC == 64) {  // lane layout [k][hl][m] = beta[k][hl + HLN m]: one 8- (16-) byte
+                                          // read gives a lane all of its 2 (4) candidates (the packed sums below)
             for (int i = threadIdx.x; i < K * K; i += blockDim.x) {
                 const int k = i >> 6, j = i & 63;
                 sbeta32[(k * HLN + (j % HLN)) * (64 / HLN) + (j / HLN)] = (float)Q.beta[i];
@@ -547,7 +564,41 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(EP
 #pragma unroll
                     for (int m = 0; m < MC; ++m) qv[m] = 0.0;
                     constexpr bool PK = KC == 64;  // packed fp32 sums (narrow form, K = 64; e2 below)
-                    if (PK && beta_lds == 2) {
+                    if (MF && beta_lds == 2) {
+                        // D[i][j] = sum_k beta[k][16 t + i] |L0_k| of entry slot j (j < 2), tile t = 0..3,
+                        // on v_mfma_f32_16x16x4_f32: lane l gives A[l & 15][l >> 4] (a beta row) and
+                        // B[l >> 4][l & 15] (the |L0| of slot l & 15, 0 for l & 15 >= 2); each output is
+                        // the k-ordered fp32 fma chain of the packed path below, bit for bit
+                        typedef float f4m __attribute__((ext_vector_type(4)));
+                        const int jl = lane & 15, kl = lane >> 4;
+                        // entry slot jl's fp32 |L0| (the same buffer parity as this lane's nxt)
+                        const float* lj = reinterpret_cast<const float*>(S.lvl[wave][jl < 2 ? jl : 0][nxt == buf0 ? 0 : 1] + 64);
+                        f4m acc[4];
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) acc[t] = (f4m){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 2
+                        for (int s4 = 0; s4 < 16; ++s4) {
+                            const int k = 4 * s4 + kl;
+                            const float bv = jl < 2 ? lj[k] : 0.0f;
+#pragma unroll
+                            for (int t = 0; t < 4; ++t)
+                                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(sbeta32[k * 64 + ((16 * t + jl) ^ (16 * kl))], bv, acc[t], 0, 0, 0);
+                        }
+                        // D row 4 kl + r, column jl: candidate 16 t + 4 kl + r of slot jl, to LDS (doubles
+                        // 96..127 of the slot's nxt: free until the tails), then each lane its own two
+                        pscl::wave_lds_fence();  // (every lane's reads of the |L0| copies are done)
+                        float* qj = reinterpret_cast<float*>(S.lvl[wave][jl < 2 ? jl : 0][nxt == buf0 ? 0 : 1] + 96);
+                        if (jl < 2) {
+#pragma unroll
+                            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) qj[16 * t + 4 * kl + r] = acc[t][r];
+                        }
+                        pscl::wave_lds_fence();
+                        const float* qm = reinterpret_cast<const float*>(nxt + 96);
+#pragma unroll
+                        for (int m = 0; m < MC; ++m) qv[m] = (double)qm[hl + HLN * m];  // (exact widening)
+                    } else if (PK && beta_lds == 2) {
                         // the lane's candidates in pairs, one v_pk_fma_f32 per pair and k: |L0| read 4 at
                         // a time (fp32 copy), beta from the lane layout; summed in fp32 and certified
                         // against the fp32 bound below (the exact fp64 sums when uncertified)
@@ -636,7 +687,7 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(EP
                         const bool seen = ((K1 || j < 64 ? t0 : t1) >> (j & 63)) & 1ULL;
                         near = near || (j < K && j != bj && !seen && !(qv[m] > thr));
                     }
-                    if (__ballot(near && more)) {
+                    if (__ballot(near && more) && !(PSCL_POST_ABLATE & 64)) {
                         sums_exact();
                         argmin();
                     }
