@@ -45,6 +45,20 @@ using pscl::f_minsum;
 using pscl::g_node;
 using pscl::polar_transform64;
 
+// cross-lane steps of the post pass's per-entry reductions: DPP within a 16-lane row (quad_perm xor 1,
+// xor 2, the half-row mirror i <-> 7 - i, the row mirror i <-> 15 - i: after the four every lane
+// holds its row's reduction), then one swizzle-free exchange between the two rows of a 32-lane entry
+// -- VALU-latency steps where ds_bpermute round trips had been
+template <int CTRL>
+__device__ __forceinline__ uint32_t post_dpp32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t post_dpp64(uint64_t v) {
+    return ((uint64_t)post_dpp32<CTRL>((uint32_t)(v >> 32)) << 32) | post_dpp32<CTRL>((uint32_t)v);
+}
+// (steps: quad_perm [1,0,3,2] = 0xB1, [2,3,0,1] = 0x4E, row_half_mirror 0x141, row_mirror 0x140)
+
 // monotone map of an fp64 to uint64 (total order of non-NaN values, -0 == +0)
 __device__ __forceinline__ uint64_t order_key(double q) {
     if (q == 0.0) q = 0.0;
@@ -452,11 +466,6 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(EP
                 }
                 double* cur = buf0;
                 double* nxt = buf1;
-#pragma unroll
-                for (int m = 0; m < EL; ++m)
-                    if (hl + HLN * m < N) cur[hl + HLN * m] = c[m];
-                prefetch();
-                pscl::wave_lds_fence();
                 // partial sums of level lw2 from X_lw2 = u after butterfly stages 1..2^(lw2-1)
                 // (see replay_leaves)
                 auto stage = [](uint64_t x, int st) {
@@ -470,7 +479,29 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(EP
                     X0 = stage(X0, 1 << (mm - 1));
                     X1 = stage(X1, 1 << (mm - 1));
                 }
-                for (int d = 0; d < n; ++d) {
+                int d0 = 0;  // first level through LDS
+                if constexpr (NC == 128 && EPW == 2) {
+                    // levels w = 64 and 32 pair a lane's own four positions hl + 32 m: in registers
+                    auto xb = [&](int q) { return (uint32_t)(((q >> 6) ? X1 : X0) >> (q & 63)) & 1u; };
+                    const double v0 = f_minsum(c[0], c[2]), v1 = f_minsum(c[1], c[3]);
+                    const double v2 = g_node(c[0], c[2], xb(hl)), v3 = g_node(c[1], c[3], xb(hl + 32));
+                    X0 = stage(X0, 32);
+                    X1 = stage(X1, 32);
+                    cur[hl] = f_minsum(v0, v1);
+                    cur[hl + 32] = g_node(v0, v1, xb(hl));
+                    cur[hl + 64] = f_minsum(v2, v3);
+                    cur[hl + 96] = g_node(v2, v3, xb(hl + 64));
+                    X0 = stage(X0, 16);
+                    X1 = stage(X1, 16);
+                    d0 = 2;
+                } else {
+#pragma unroll
+                    for (int m = 0; m < EL; ++m)
+                        if (hl + HLN * m < N) cur[hl + HLN * m] = c[m];
+                }
+                prefetch();
+                pscl::wave_lds_fence();
+                for (int d = d0; d < n; ++d) {
                     const int lw2 = n - d - 1, w2 = 1 << lw2;
 #pragma unroll
                     for (int m = 0; m < EL; ++m) {
@@ -529,15 +560,17 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(EP
                             }
                         }
                     }
-#pragma unroll
-                    for (int sft = 1; sft < HLN; sft <<= 1) {
-                        const uint64_t ok = pscl::shfl_u64(bk, lane ^ sft);
-                        const int oj = __shfl(bj, lane ^ sft);
+                    auto take = [&](uint64_t ok, int oj) {
                         if (ok < bk || (ok == bk && oj < bj)) {
                             bk = ok;
                             bj = oj;
                         }
-                    }
+                    };
+                    take(post_dpp64<0xB1>(bk), (int)post_dpp32<0xB1>((uint32_t)bj));
+                    take(post_dpp64<0x4E>(bk), (int)post_dpp32<0x4E>((uint32_t)bj));
+                    take(post_dpp64<0x141>(bk), (int)post_dpp32<0x141>((uint32_t)bj));
+                    take(post_dpp64<0x140>(bk), (int)post_dpp32<0x140>((uint32_t)bj));
+                    if constexpr (HLN == 32) take(pscl::shfl_u64(bk, lane ^ 16), __shfl(bj, lane ^ 16));
                 };
                 // exact sums: index order, each product and sum rounded (the oracle's restatement
                 // of numpy's abs_l0 @ beta)
@@ -649,8 +682,11 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(EP
                     double as = 0.0;
 #pragma unroll
                     for (int m = 0; m < MC; ++m) as = as + (hl + HLN * m < K ? nxt[hl + HLN * m] : 0.0);
-#pragma unroll
-                    for (int sft = 1; sft < HLN; sft <<= 1) as = as + pscl_asf64(pscl::shfl_u64(pscl_asu64(as), lane ^ sft));
+                    as = as + pscl_asf64(post_dpp64<0xB1>(pscl_asu64(as)));
+                    as = as + pscl_asf64(post_dpp64<0x4E>(pscl_asu64(as)));
+                    as = as + pscl_asf64(post_dpp64<0x141>(pscl_asu64(as)));
+                    as = as + pscl_asf64(post_dpp64<0x140>(pscl_asu64(as)));
+                    if constexpr (HLN == 32) as = as + pscl_asf64(pscl::shfl_u64(pscl_asu64(as), lane ^ 16));
                     // 2 E = 2 (gamma_K + gamma_K+1) S <= (4 K + 2 + slack) u S, u = 2^-53 (K = 64:
                     // 264 u, 2.3 % slack; the bound grows with K, so the (128,88) and runtime-K
                     // instances get their own); fp32 beta adds |beta32 - beta| <= 2^-24 |beta| + 2^-150
