@@ -306,9 +306,21 @@ __device__ __forceinline__ void load_rowq(const double* row, int rm_E, const int
     }
 }
 
-// per-entry broadcast of lane l's value (ds_bpermute; l differs between the entry slots)
-__device__ __forceinline__ uint64_t bcast64(uint64_t v, int l) {
-    return ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), l) << 32) | (uint32_t)__shfl((int)(uint32_t)v, l);
+// per-entry broadcast of lane base + hs's value to entry slot hs (base wave-uniform): one scalar read
+// per slot and a select, not a ds_bpermute round trip
+template <int EPW>
+__device__ __forceinline__ uint32_t slot_bcast32(uint32_t v, int base, int hs) {
+    uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)v, base);
+#pragma unroll
+    for (int k = 1; k < EPW; ++k) {
+        const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)v, base + k);
+        r = hs == k ? x : r;
+    }
+    return r;
+}
+template <int EPW>
+__device__ __forceinline__ uint64_t slot_bcast64(uint64_t v, int base, int hs) {
+    return ((uint64_t)slot_bcast32<EPW>((uint32_t)(v >> 32), base, hs) << 32) | slot_bcast32<EPW>((uint32_t)v, base, hs);
 }
 
 // NC, KC: N and K compiled in (128 and 64 / 88: the BASELINE codes) or 0 (from Q).  EPW: entries a
@@ -355,6 +367,16 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(EP
     const double* beta = beta_lds == 1 ? sbeta : Q.beta;  // (the exact sums: fp64 beta)
     const uint64_t info0 = Q.info_mask[0], info1 = Q.info_mask[1];
     const int ninfo0 = __popcll(info0);
+    // information bits in the 16-phase blocks 0..b (b < 7), for the flip's warm-start segment
+    int icum[PSCL_DL_NSEG - 1];
+    {
+        int acc = 0;
+#pragma unroll
+        for (int b = 0; b < PSCL_DL_NSEG - 1; ++b) {
+            acc += __popcll(((b < 4 ? info0 : info1) >> (16 * (b & 3))) & 0xffffULL);
+            icum[b] = acc;
+        }
+    }
     int pre[PSCL_DL_NSEG + 1];
     int64_t n_in;
     if (Q.init) {
@@ -420,24 +442,26 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(EP
         // channel rows of the first entries; the next iteration's rows are loaded into c as soon as
         // the replay has copied c to LDS (one row's registers live, not two)
         double c[EL];
-        load_rowq<HLN>(Q.llr + (int64_t)bcast64((uint64_t)mf, hs) * (Q.rm_E ? Q.rm_E : N), Q.rm_E, Q.rm_src, N, hl, c);
+        auto bc32 = [&](uint32_t v, int base) { return slot_bcast32<EPW>(v, base, hs); };
+        auto bc64 = [&](uint64_t v, int base) { return slot_bcast64<EPW>(v, base, hs); };
+        load_rowq<HLN>(Q.llr + (int64_t)bc64((uint64_t)mf, 0) * (Q.rm_E ? Q.rm_E : N), Q.rm_E, Q.rm_src, N, hl, c);
         for (int it = 0; it < npair; ++it) {
-            const int src = EPW * it + hs;  // this entry slot's metadata lane
+            const int sb = EPW * it, src = sb + hs;  // this entry slot's metadata lane
             bool valid = src < nval;
-            const int e = __shfl(me, src);
-            const int64_t f = (int64_t)bcast64((uint64_t)mf, src);
-            const uint64_t b0 = bcast64(mb0, src), b1 = K1 ? 0ULL : bcast64(mb1, src);
-            const int nt = Q.init ? 0 : __shfl(mnt, src);
-            auto prefetch = [&]() {
+            const int e = (int)bc32((uint32_t)me, sb);
+            const int64_t f = (int64_t)bc64((uint64_t)mf, sb);
+            const uint64_t b0 = bc64(mb0, sb), b1 = K1 ? 0ULL : bc64(mb1, sb);
+            const int nt = Q.init ? 0 : (int)bc32((uint32_t)mnt, sb);
+            auto prefetch = [&]() {  // (metadata lanes past nval hold entry 0's: a valid row)
                 if (it + 1 < npair)
-                    load_rowq<HLN>(Q.llr + (int64_t)bcast64((uint64_t)mf, src + EPW < nval ? src + EPW : 0) * (Q.rm_E ? Q.rm_E : N),
+                    load_rowq<HLN>(Q.llr + (int64_t)bc64((uint64_t)mf, sb + EPW) * (Q.rm_E ? Q.rm_E : N),
                                    Q.rm_E, Q.rm_src, N, hl, c);
             };
             bool more;
             if (Q.init) {  // baseline failing by construction (dl_compact); nothing tried yet
                 more = valid && Q.rounds > 0;
             } else {       // the attempt just decoded is the frame's latest (flip.py:123-136)
-                const uint32_t fl = (uint32_t)__shfl((int)mfl, src);
+                const uint32_t fl = bc32(mfl, sb);
                 // (deferred by the screening retry decode: its exact decode and post pass follow)
                 if (fl == PSCL_DL_DEFERRED) valid = false;
                 if (valid && hl == 0) {
@@ -538,7 +562,7 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(EP
                 pscl::wave_lds_fence();
                 // ---- next flip: argmin over untried (q, index), q = |L0| @ beta summed in
                 // index order (flip.py:104-108), q = |L0| without beta
-                const uint64_t t0 = Q.init ? 0ULL : bcast64(mt0, src), t1 = Q.init || K1 ? 0ULL : bcast64(mt1, src);
+                const uint64_t t0 = Q.init ? 0ULL : bc64(mt0, sb), t1 = Q.init || K1 ? 0ULL : bc64(mt1, sb);
                 uint64_t bk = ~0ULL;
                 int bj = 0x7fffffff;
                 // candidates j = hl + HLN m; their sums advance together (one |L0_k| read serves
@@ -737,9 +761,11 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(EP
                     argmin();
                 }
                 const int idx = bj;  // (half-uniform) an untried index exists: rounds <= min(retries, K)
-                const int phis = Q.info_set[idx < K ? idx : 0];
-                int seg = phis >> 4;
-                if (seg > PSCL_DL_NSEG - 1) seg = PSCL_DL_NSEG - 1;
+                // the 16-phase block of its position (info_set[idx] >> 4): blocks whose cumulative
+                // information-bit count is at most idx (no memory read)
+                int seg = 0;
+#pragma unroll
+                for (int b = 0; b < PSCL_DL_NSEG - 1; ++b) seg += (idx < K && icum[b] <= idx) ? 1 : 0;
                 if (PSCL_POST_ABLATE & 2) seg = 0;
                 pscl::wave_lds_fence();  // (the select's reads of nxt before the tails overwrite it)
                 // ---- exact metric increments of the forced prefix's leaves (scl.py:102-105, as
