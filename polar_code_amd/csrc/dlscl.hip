@@ -59,6 +59,17 @@ __device__ __forceinline__ uint64_t post_dpp64(uint64_t v) {
 }
 // (steps: quad_perm [1,0,3,2] = 0xB1, [2,3,0,1] = 0x4E, row_half_mirror 0x141, row_mirror 0x140)
 
+// the value of lane (lane ^ W) within a 32-lane entry half (W = 1..16): quad_perm xor 1 / xor 2,
+// xor 4 as the half-row mirror then quad_perm xor 3, xor 8 as row_ror:8, xor 16 across the two rows
+template <int W>
+__device__ __forceinline__ uint64_t post_xor64(uint64_t v, int lane) {
+    if constexpr (W == 1) return post_dpp64<0xB1>(v);
+    else if constexpr (W == 2) return post_dpp64<0x4E>(v);
+    else if constexpr (W == 4) return post_dpp64<0x1B>(post_dpp64<0x141>(v));
+    else if constexpr (W == 8) return post_dpp64<0x128>(v);
+    else return pscl::shfl_u64(v, lane ^ 16);
+}
+
 // monotone map of an fp64 to uint64 (total order of non-NaN values, -0 == +0)
 __device__ __forceinline__ uint64_t order_key(double q) {
     if (q == 0.0) q = 0.0;
@@ -504,20 +515,44 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(EP
                     X1 = stage(X1, 1 << (mm - 1));
                 }
                 int d0 = 0;  // first level through LDS
-                if constexpr (NC == 128 && EPW == 2) {
-                    // levels w = 64 and 32 pair a lane's own four positions hl + 32 m: in registers
+                // RR (N = 128, 32-lane entries): the whole replay in the lane's registers -- levels
+                // w = 64 and 32 pair its own four positions hl + 32 m, levels w = 16 .. 1 pair
+                // position p with p ^ w in lane hl ^ w (post_xor64); the leaves stay in lv[]
+                constexpr bool RR = NC == 128 && EPW == 2;
+                double lv[EL];
+                if constexpr (RR) {
                     auto xb = [&](int q) { return (uint32_t)(((q >> 6) ? X1 : X0) >> (q & 63)) & 1u; };
                     const double v0 = f_minsum(c[0], c[2]), v1 = f_minsum(c[1], c[3]);
                     const double v2 = g_node(c[0], c[2], xb(hl)), v3 = g_node(c[1], c[3], xb(hl + 32));
                     X0 = stage(X0, 32);
                     X1 = stage(X1, 32);
-                    cur[hl] = f_minsum(v0, v1);
-                    cur[hl + 32] = g_node(v0, v1, xb(hl));
-                    cur[hl + 64] = f_minsum(v2, v3);
-                    cur[hl + 96] = g_node(v2, v3, xb(hl + 64));
+                    lv[0] = f_minsum(v0, v1);
+                    lv[1] = g_node(v0, v1, xb(hl));
+                    lv[2] = f_minsum(v2, v3);
+                    lv[3] = g_node(v2, v3, xb(hl + 64));
                     X0 = stage(X0, 16);
                     X1 = stage(X1, 16);
-                    d0 = 2;
+                    auto level = [&](auto WC) {
+                        constexpr int w = decltype(WC)::value;
+                        const bool hi = (hl & w) != 0;  // (the pair's second position: g, else f)
+#pragma unroll
+                        for (int m = 0; m < EL; ++m) {
+                            const double oth = pscl_asf64(post_xor64<w>(pscl_asu64(lv[m]), lane));
+                            const double a = hi ? oth : lv[m], bb = hi ? lv[m] : oth;
+                            const double gv = g_node(a, bb, xb((hl ^ w) + 32 * m)), fv = f_minsum(a, bb);
+                            lv[m] = hi ? gv : fv;
+                        }
+                        if constexpr (w > 1) {
+                            X0 = stage(X0, w >> 1);
+                            X1 = stage(X1, w >> 1);
+                        }
+                    };
+                    level(std::integral_constant<int, 16>{});
+                    level(std::integral_constant<int, 8>{});
+                    level(std::integral_constant<int, 4>{});
+                    level(std::integral_constant<int, 2>{});
+                    level(std::integral_constant<int, 1>{});
+                    d0 = n;
                 } else {
 #pragma unroll
                     for (int m = 0; m < EL; ++m)
@@ -556,8 +591,9 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(EP
 #pragma unroll
                 for (int m = 0; m < EL; ++m)
                     if (jpos(m) >= 0) {
-                        nxt[jpos(m)] = fabs(cur[hl + HLN * m]);
-                        if (KC == 64 && beta_lds == 2) l32[jpos(m)] = (float)fabs(cur[hl + HLN * m]);
+                        const double leaf = RR ? lv[m] : cur[hl + HLN * m];
+                        nxt[jpos(m)] = fabs(leaf);
+                        if (KC == 64 && beta_lds == 2) l32[jpos(m)] = (float)fabs(leaf);
                     }
                 pscl::wave_lds_fence();
                 // ---- next flip: argmin over untried (q, index), q = |L0| @ beta summed in
@@ -777,7 +813,7 @@ __global__ void __launch_bounds__(PW * 64) __attribute__((amdgpu_waves_per_eu(EP
                     for (int m = 0; m < EL; ++m) {
                         const int p = hl + HLN * m;
                         if (p < 16 * seg) {
-                            const double lam = cur[p];  // (the leaves stay in cur)
+                            const double lam = RR ? lv[m] : cur[p];  // (the leaves: lv[], or in cur)
                             const uint32_t bit = (uint32_t)(((p < 64 ? u0 : u1) >> (p & 63)) & 1ULL);
                             const double Lt = tailf(lam);
                             const bool good = bit == (lam < 0.0 ? 1u : 0u);
