@@ -342,6 +342,9 @@ int pscl_join(pscl_handle* h);
  *                           (the post pass skips the exact tails; entries its decodes defer start
  *                           the side chain's exact decode at phase 0), 2: exact warm-start metrics;
  *                           0 (default): the measured faster
+ *   PSCL_TUNE_DL_TAIL       1: a pipelined DL-SCL call's baseline tail (the re-decode of its deferred
+ *                           frames, the compaction of the failing ones) on the handle's stream, before
+ *                           the next call's baseline; 0 (default): on a stream of its own beside it
  */
 #define PSCL_TUNE_DL_SCREEN 1
 #define PSCL_TUNE_DL_CHUNKS 2
@@ -359,7 +362,8 @@ int pscl_join(pscl_handle* h);
 #define PSCL_TUNE_POST_EPW 14
 #define PSCL_TUNE_LANE_EXACT 15
 #define PSCL_TUNE_DL_WARM_APX 16
-#define PSCL_TUNE_COUNT 17
+#define PSCL_TUNE_DL_TAIL 17
+#define PSCL_TUNE_COUNT 18
 int pscl_set_tuning(pscl_handle* h, int knob, int64_t value);
 
 /*

@@ -48,7 +48,7 @@ EXPORTS = (
 
 # pscl_set_tuning knobs (include/polar_scl.h)
 TUNE = {"dl_screen": 1, "dl_chunks": 2, "dl_split": 3, "side_priority": 4, "post_grid": 5, "retry_wpg": 6, "dl_lane": 7, "dl_screen_min": 8, "dl_retry_lane": 9, "post_pairs": 10, "dl_streams": 11, "tx_fused": 12,
-        "dl_fused_post": 13, "post_epw": 14, "lane_exact": 15, "dl_warm_apx": 16}
+        "dl_fused_post": 13, "post_epw": 14, "lane_exact": 15, "dl_warm_apx": 16, "dl_tail": 17}
 
 _vp, _i32, _i64, _u64, _dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
 

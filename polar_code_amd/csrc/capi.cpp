@@ -165,6 +165,13 @@ struct pscl_handle {
     hipEvent_t ev_pscr[2] = {nullptr, nullptr}, ev_px[2] = {nullptr, nullptr};
     bool px_pending[2] = {false, false};
     int pipe_par = 0;
+    // pipelined pscl_dlscl_device: the baseline's tail (the exact re-decode of its deferred frames,
+    // the compaction of the failing frames and their count for the host) runs on tail_stream, so the
+    // next call's baseline starts right after this call's screening pass; two parities of deferred-
+    // frame scratch (slots 124/125, 126/127), ev_tail[q] marks the end of parity q's tail
+    hipStream_t tail_stream = nullptr;
+    hipEvent_t ev_tscr[2] = {nullptr, nullptr}, ev_tail[2] = {nullptr, nullptr};
+    bool tail_pending[2] = {false, false};
     // pipelined pscl_dlscl_device: a call's retry chains (and its DL counters) stay on the retry
     // streams and overlap the next call's baseline decode; the calls alternate the compaction
     // parity (act/cnt), ev_dl[p] marks the end of parity p's chains
@@ -222,6 +229,11 @@ int join_pipe(pscl_handle* h, int what = 3) {
         const int rc = dl_enqueue_deferred(h);
         if (rc) return rc;
     }
+    for (int p = 0; p < 2; ++p)
+        if ((what & 2) && h->tail_pending[p]) {
+            HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_tail[p], 0));
+            h->tail_pending[p] = false;
+        }
     for (int p = 0; p < kDlPar; ++p) {
         if ((what & 1) && p < 2 && h->px_pending[p]) {
             HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_px[p], 0));
@@ -239,6 +251,7 @@ int join_pipe(pscl_handle* h, int what = 3) {
 // freed and regrown)
 void quiesce(pscl_handle* h) {
     if (h->pipe_stream) hipStreamSynchronize(h->pipe_stream);
+    if (h->tail_stream) hipStreamSynchronize(h->tail_stream);
     for (int i = 0; i < kChainStreams; ++i) {
         if (h->retry_stream[i]) hipStreamSynchronize(h->retry_stream[i]);
         if (h->side_stream[i]) hipStreamSynchronize(h->side_stream[i]);
@@ -258,6 +271,8 @@ void drop_side_streams(pscl_handle* h) {
     }
     if (h->pipe_stream) hipStreamDestroy(h->pipe_stream);
     h->pipe_stream = nullptr;
+    if (h->tail_stream) hipStreamDestroy(h->tail_stream);
+    h->tail_stream = nullptr;
     for (int i = 0; i < kChainStreams; ++i) {
         if (h->retry_stream[i]) hipStreamDestroy(h->retry_stream[i]);
         if (h->side_stream[i]) hipStreamDestroy(h->side_stream[i]);
@@ -339,8 +354,11 @@ bool lane_exact_on(const pscl_handle* h) {
     return lx == 1 || lx == 3 || (lx == 0 && PSCL_LANE_EXACT_DEFAULT);
 }
 
+// tail (a pipelined DL-SCL baseline, tail_par its scratch parity): the re-decode of the deferred
+// frames goes to tail after the screening pass, and the call returns; the caller queues the rest of
+// the baseline's tail there and marks it with ev_tail[tail_par]
 int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStream_t st = nullptr, int scr_slot = 38,
-                  bool pipe = false) {
+                  bool pipe = false, hipStream_t tail = nullptr, int tail_par = 0) {
     if (!st) st = h->stream;
     pscl_decode_params P = P0;
     if (P.long_mode) {  // global scratch of every workgroup in flight (scl_long.hip)
@@ -384,7 +402,13 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
         int rc;
         // pipelined: parity p's list may still be read by the re-decode two calls back
         const int p = pipe ? h->pipe_par : 0;
-        const int s_cnt = p ? 64 : 36, s_list = p ? 65 : 37;
+        const bool tl = tail && !pipe;
+        const int s_cnt = tl ? (tail_par ? 126 : 124) : (p ? 64 : 36), s_list = tl ? (tail_par ? 127 : 125) : (p ? 65 : 37);
+        if (tl && h->tail_pending[tail_par]) {  // (the parity's previous tail still reads its list)
+            if (h->scratch[s_list].n < (size_t)P.B * 8) HIP_TRY(hipEventSynchronize(h->ev_tail[tail_par]));  // (regrown)
+            HIP_TRY(hipStreamWaitEvent(st, h->ev_tail[tail_par], 0));
+            h->tail_pending[tail_par] = false;
+        }
         if (pipe) {
             if (!h->pipe_stream) {
                 HIP_TRY(create_priority_stream(h, &h->pipe_stream));
@@ -446,6 +470,15 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
             // few frames: one resident set of workgroups (4 waves/SIMD on 256 CUs), striding
             // over the listed frames, instead of a grid sized for the whole batch
             X.grid_cap = (int64_t)256 * 16 / (pscl_decode_wpg(X) > 0 ? pscl_decode_wpg(X) : 1);
+            if (tl) {  // (the caller's tail stream: this call's baseline tail, off the handle's stream)
+                if (h->timing) HIP_TRY(hipEventRecord(e1, st));
+                HIP_TRY(hipEventRecord(h->ev_tscr[tail_par], st));
+                HIP_TRY(hipStreamWaitEvent(tail, h->ev_tscr[tail_par], 0));
+                if (!hist && pscl_lane_exact_available(X)) h->n_lane_exact++;
+                err = pscl_launch_decode(X, hist, tail);
+                if (err != hipSuccess) return fail(PSCL_EDEVICE, "decode kernel launch: %s", hipGetErrorString(err));
+                return PSCL_OK;
+            }
             if (pipe) {
                 // the re-decode overlaps the caller's next decode; the timed interval is the
                 // screening launch alone
@@ -471,6 +504,10 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
         if (!hist && pscl_lane_exact_available(P)) h->n_lane_exact++;
         err = pscl_launch_decode(P, hist, st);
         if (err == hipSuccess && P.cpart) err = pscl_launch_count_reduce(P.cpart, pscl_decode_count_slots(P, hist), P.counters, st);
+        if (err == hipSuccess && tail && !pipe) {  // (no screening pass: the caller's tail follows the decode)
+            HIP_TRY(hipEventRecord(h->ev_tscr[tail_par], st));
+            HIP_TRY(hipStreamWaitEvent(tail, h->ev_tscr[tail_par], 0));
+        }
     }
     if (err != hipSuccess) return fail(PSCL_EDEVICE, "decode kernel launch: %s", hipGetErrorString(err));
     if (h->timing) HIP_TRY(hipEventRecord(e1, st));
@@ -714,8 +751,11 @@ int pscl_destroy(pscl_handle* h) {
     for (int i = 0; i < 2; ++i) {
         if (h->ev_pscr[i]) hipEventDestroy(h->ev_pscr[i]);
         if (h->ev_px[i]) hipEventDestroy(h->ev_px[i]);
+        if (h->ev_tscr[i]) hipEventDestroy(h->ev_tscr[i]);
+        if (h->ev_tail[i]) hipEventDestroy(h->ev_tail[i]);
     }
     if (h->pipe_stream) hipStreamDestroy(h->pipe_stream);
+    if (h->tail_stream) hipStreamDestroy(h->tail_stream);
     if (h->stash_pipe) hipStreamDestroy(h->stash_pipe);
     for (int i = 0; i < kChainStreams; ++i) {
         if (h->stash_retry[i]) hipStreamDestroy(h->stash_retry[i]);
@@ -807,7 +847,7 @@ int pscl_set_pipelined(pscl_handle* h, int enable) {
 int pscl_set_tuning(pscl_handle* h, int knob, int64_t value) {
     if (!h) return fail(PSCL_EINVAL, "NULL handle");
     static const int64_t lim[PSCL_TUNE_COUNT][2] = {{0, 0}, {0, 2}, {0, 64}, {0, 2}, {0, 1}, {0, 4096}, {0, PSCL_MAX_WAVES_PER_WG}, {0, 2},
-                                                    {0, (int64_t)1 << 30}, {0, 2}, {0, 32}, {0, 3}, {0, 2}, {0, 2}, {0, 4}, {0, 3}, {0, 2}};
+                                                    {0, (int64_t)1 << 30}, {0, 2}, {0, 32}, {0, 3}, {0, 2}, {0, 2}, {0, 4}, {0, 3}, {0, 2}, {0, 1}};
     if (knob < 1 || knob >= PSCL_TUNE_COUNT) return fail(PSCL_EINVAL, "unknown tuning knob %d", knob);
     if (value < lim[knob][0] || value > lim[knob][1] || (knob == PSCL_TUNE_POST_GRID && value && value < 16))
         return fail(PSCL_EINVAL, "tuning knob %d: value %lld out of range", knob, (long long)value);
@@ -1399,6 +1439,10 @@ int dlscl_impl(pscl_handle* h, const double* d_llr, int64_t B, int retries, uint
                int64_t* d_counters_scl, int64_t* d_counters_dl, const TxSpec* tx);
 }  // namespace
 
+#ifndef PSCL_DL_TAIL_STREAM
+#define PSCL_DL_TAIL_STREAM 1
+#endif
+
 int pscl_dlscl_device(pscl_handle* h, const double* d_llr, int64_t B, int retries, uint64_t* d_best, uint8_t* d_flags,
                       int32_t* d_attempts, int32_t* d_tried, int tried_stride, const uint64_t* d_ref, int k_payload,
                       int64_t* d_counters_scl, int64_t* d_counters_dl) {
@@ -1535,19 +1579,41 @@ int dlscl_impl(pscl_handle* h, const double* d_llr, int64_t B, int retries, uint
             P.tx_unc_counters = tx->unc;
         }
         if (pscl_decode_wpg(P) < 1) return fail(PSCL_EUNSUP, "LDS budget exceeded (L=%d, K=%d)", h->L, h->K);
-        if ((rc = launch_decode(h, P, 0))) return rc;
+        // a pipelined call's baseline tail (re-decode, compaction, count) on tail_stream: the next
+        // call's baseline follows this one's screening pass directly
+        hipStream_t ts = s;
+        const int tpar = a.pbase & 1;
+        if (a.pipe && PSCL_DL_TAIL_STREAM && !h->tune[PSCL_TUNE_DL_TAIL]) {
+            if (!h->tail_stream) {
+                HIP_TRY(create_priority_stream(h, &h->tail_stream));
+                for (int i = 0; i < 2; ++i) {
+                    HIP_TRY(hipEventCreateWithFlags(&h->ev_tscr[i], hipEventDisableTiming));
+                    HIP_TRY(hipEventCreateWithFlags(&h->ev_tail[i], hipEventDisableTiming));
+                }
+            }
+            ts = h->tail_stream;
+        }
+        if ((rc = launch_decode(h, P, 0, s, 38, false, ts != s ? ts : nullptr, tpar))) return rc;
+        if (ts != s && rounds <= 0) {  // (no compaction: the tail ends with the re-decode)
+            HIP_TRY(hipEventRecord(h->ev_tail[tpar], ts));
+            h->tail_pending[tpar] = true;
+        }
         if (rounds > 0) {
             const int p = dl_parity(a, c);
-            if (c >= 2) HIP_TRY(hipStreamWaitEvent(s, h->ev_retry[p], 0));  // the parity's indices free again
-            HIP_TRY(hipMemsetAsync(bufs.cnt[p], 0, 4, s));
-            if ((e = pscl_launch_dl_compact(d_flags + c0, nc, c0, bufs.act[p], nullptr, bufs.cnt[p], s)) != hipSuccess)
+            if (c >= 2) HIP_TRY(hipStreamWaitEvent(ts, h->ev_retry[p], 0));  // the parity's indices free again
+            HIP_TRY(hipMemsetAsync(bufs.cnt[p], 0, 4, ts));
+            if ((e = pscl_launch_dl_compact(d_flags + c0, nc, c0, bufs.act[p], nullptr, bufs.cnt[p], ts)) != hipSuccess)
                 return fail(PSCL_EDEVICE, "dl_compact launch: %s", hipGetErrorString(e));
             // fused TX: the failing frames' rows, read by the retry chain (entries hold call-level frame
             // indices c0 + f)
-            if (tx && (e = pscl_launch_tx_rows(P, bufs.act[p], bufs.cnt[p], nc, tx->rows, tx->frame0, s)) != hipSuccess)
+            if (tx && (e = pscl_launch_tx_rows(P, bufs.act[p], bufs.cnt[p], nc, tx->rows, tx->frame0, ts)) != hipSuccess)
                 return fail(PSCL_EDEVICE, "tx_rows launch: %s", hipGetErrorString(e));
-            HIP_TRY(hipMemcpyAsync(h->h_count + p, bufs.cnt[p], 4, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipEventRecord(h->ev_base[p], s));
+            HIP_TRY(hipMemcpyAsync(h->h_count + p, bufs.cnt[p], 4, hipMemcpyDeviceToHost, ts));
+            HIP_TRY(hipEventRecord(h->ev_base[p], ts));
+            if (ts != s) {
+                HIP_TRY(hipEventRecord(h->ev_tail[tpar], ts));
+                h->tail_pending[tpar] = true;
+            }
             if (c >= 1 && (rc = dl_chain(h, a, bufs, c - 1, true))) return rc;
         }
     }

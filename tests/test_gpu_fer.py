@@ -235,13 +235,15 @@ def test_device_retry_loop_split_chains(chunks, split):
 @pytest.mark.parametrize("L,depth,split,tune", [(4, 2, 0, {}), (8, 2, 0, {}), (4, 4, 0, {}), (8, 3, 0, {}), (4, 3, 2, {}),
                                                 (4, 2, 0, {"post_epw": 4}), (8, 3, 0, {"post_epw": 4}),
                                                 (4, 2, 0, {"post_epw": 2}), (4, 3, 0, {"dl_warm_apx": 1}),
-                                                (8, 2, 0, {"dl_warm_apx": 2})])
+                                                (8, 2, 0, {"dl_warm_apx": 2}), (4, 2, 0, {"dl_tail": 1}),
+                                                (8, 4, 0, {"dl_tail": 1})])
 def test_pipelined_dlscl_calls_equal_stream_ordered(L, depth, split, tune):
     """pscl_set_pipelined on pscl_dlscl_device: each call's retry chains and DL counters stay on
     the retry streams and overlap the next call's baseline (and, in the other chain set, the
     previous call's chains); split 0 = the pipelined default (one chain per call), 2 = two; tune:
     the narrow post pass's entries per wavefront (PSCL_TUNE_POST_EPW), screening-tail warm starts
-    (PSCL_TUNE_DL_WARM_APX).  Calls on `depth` rotating output buffers (as bench.py's steps): a
+    (PSCL_TUNE_DL_WARM_APX), the baseline tail on the handle's stream (PSCL_TUNE_DL_TAIL; by default
+    it runs on a stream of its own beside the next call's baseline).  Calls on `depth` rotating output buffers (as bench.py's steps): a
     call's buffers are reused by the depth-th following call, which must start after that call's
     chains end.  After a join the last `depth` calls' bits, flags and attempts and the SCL/DL
     counters of all calls equal the stream-ordered calls'."""
