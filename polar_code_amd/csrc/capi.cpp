@@ -168,7 +168,8 @@ struct pscl_handle {
     // pipelined pscl_dlscl_device: the baseline's tail (the exact re-decode of its deferred frames,
     // the compaction of the failing frames and their count for the host) runs on tail_stream, so the
     // next call's baseline starts right after this call's screening pass; two parities of deferred-
-    // frame scratch (slots 124/125, 126/127), ev_tail[q] marks the end of parity q's tail
+    // frame scratch (slots 124/125, 126/127) and of count partials (70, 71), ev_tail[q] marks the end of
+    // parity q's tail
     hipStream_t tail_stream = nullptr;
     hipEvent_t ev_tscr[2] = {nullptr, nullptr}, ev_tail[2] = {nullptr, nullptr};
     bool tail_pending[2] = {false, false};
@@ -434,7 +435,7 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
         S.amb_count = (int32_t*)d_cnt;
         // (pipelined: the count buffers alternate with the call parity, and the reduce runs on the
         // side stream after the re-decode, off the handle's stream)
-        if ((rc = with_count_slots(h, S, hist, pipe ? 92 + p : 92, st))) return rc;
+        if ((rc = with_count_slots(h, S, hist, tl ? 70 + tail_par : (pipe ? 92 + p : 92), st))) return rc;
         S.tx_upart = nullptr;
         if (S.tx && S.tx_unc_counters) {  // fused TX: the uncoded baseline's per-wavefront partials
             const int64_t slots = pscl_decode_count_slots(S, hist);
@@ -458,7 +459,7 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
 #else
         constexpr bool screen_only = false;  // the shipped library always re-decodes deferred frames
 #endif
-        if (err == hipSuccess && S.cpart && (!pipe || screen_only))
+        if (err == hipSuccess && S.cpart && ((!pipe && !tl) || screen_only))
             err = pscl_launch_count_reduce(S.cpart, pscl_decode_count_slots(S, hist), S.counters, st);
         if (err == hipSuccess && !screen_only) {
             pscl_decode_params X = P;  // exact decode of the listed frames, outputs at their rows
@@ -476,6 +477,8 @@ int launch_decode(pscl_handle* h, const pscl_decode_params& P0, int hist, hipStr
                 HIP_TRY(hipStreamWaitEvent(tail, h->ev_tscr[tail_par], 0));
                 if (!hist && pscl_lane_exact_available(X)) h->n_lane_exact++;
                 err = pscl_launch_decode(X, hist, tail);
+                if (err == hipSuccess && S.cpart)  // (the screening's count partials, parity slot 70 + tail_par)
+                    err = pscl_launch_count_reduce(S.cpart, pscl_decode_count_slots(S, hist), S.counters, tail);
                 if (err != hipSuccess) return fail(PSCL_EDEVICE, "decode kernel launch: %s", hipGetErrorString(err));
                 return PSCL_OK;
             }
