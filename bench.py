@@ -88,7 +88,7 @@ def parse():
                          "dl_chunks, dl_split, side_priority, post_grid, retry_wpg, dl_lane); A/B tools only")
     ap.add_argument("--extra", choices=["auto", "none"], default="auto",
                     help="auto: also time BASELINE configs 2, 4, 5 (extra_configs) after the headline")
-    ap.add_argument("--extra-steps", type=int, default=10)
+    ap.add_argument("--extra-steps", type=int, default=20)
     ap.add_argument("--extra-parity", type=int, default=50_000, help="oracle parity frames per extra config")
     return ap.parse_args()
 
