@@ -150,6 +150,11 @@ __device__ __forceinline__ void tx_frame_words(const pscl_decode_params& P, uint
     }
 }
 
+// occupancy hint of the L = 8 forced-bit (FS) retry instance: 3 waves per SIMD (168 VGPRs), the plain
+// kernel's occupancy; left to the default (2) it took 173
+#ifndef PSCL_FS_WAVES
+#define PSCL_FS_WAVES 3
+#endif
 // occupancy hint of the fused TX instance at L = 8: 3 waves per SIMD (168 VGPRs), the plain kernel's
 // occupancy (its LDS allows no more); its draws would otherwise take it to ~177 VGPRs and 2 waves
 #ifndef PSCL_TX_WAVES
@@ -180,7 +185,9 @@ __device__ __forceinline__ void tx_frame_words(const pscl_decode_params& P, uint
 // shuffles over the frame's lanes) and routing the survivors through LDS slots; frozen phases
 // re-sort only when a metric fell below its predecessor's.  No certificates, no deferral.
 template <int LMAX, int CODE, bool FS = false, bool TXF = false, bool FP = false, bool EX = false>
-__global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2) : PSCL_LANE_WAVES_PER_EU) scl_lane_kernel(const pscl_decode_params P) {
+__global__ void __launch_bounds__(64, TXF ? (LMAX == 8 ? PSCL_TX_WAVES : 2)
+                                           : (FS && !FP && !EX && LMAX == 8) ? PSCL_FS_WAVES : PSCL_LANE_WAVES_PER_EU)
+scl_lane_kernel(const pscl_decode_params P) {
     static_assert(LMAX == 4 || LMAX == 8, "the lane-per-path decoder is built for L = 4 and 8");
     static_assert(!TXF || (!FS && CODE == 1), "fused TX: plain decodes of the (128,64) code");
     static_assert(!FP || (FS && CODE == 1), "fused post pass: the FS instance of the (128,64) code");
