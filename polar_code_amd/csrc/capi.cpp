@@ -1093,8 +1093,10 @@ int dl_retry_chunk(pscl_handle* h, const DlState& S, int A, int rounds, const do
         // screened decodes certify against margins that cover every increment's tail error, the
         // prefix's too; the entries they defer go to the side chain's bucket 0 (exact from phase 0),
         // whose own posts (QD) keep exact metrics
+        // (default: for chains beside a later baseline decode, which are throughput-bound; a chain
+        // running alone is latency-bound, and its side chain -- the longer one -- keeps warm starts)
         const int64_t wk = h->tune[PSCL_TUNE_DL_WARM_APX];
-        if (!fpost && (wk == 1 || (wk == 0 && PSCL_DL_WARM_APX_DEFAULT))) {
+        if (!fpost && (wk == 1 || (wk == 0 && PSCL_DL_WARM_APX_DEFAULT && beside))) {
             Q.warm_apx = 1;
             HA.warm_apx = 1;
         }
