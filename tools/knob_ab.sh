@@ -18,8 +18,8 @@ for r in $(seq 1 $rounds); do
       p5) cmd="python3 tools/config3_run.py 1000000 5.0 5.0 $t" ;;
       c4|head)
         arg=""; [ "$t" != "-" ] && arg="--tune $t"
-        if [ $wl = c4 ]; then cmd="python3 bench.py --list 4 --retries 8 --steps 10 --warmup 2 --no-cpu-baseline --extra none $arg"
-        else cmd="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --extra none $arg"; fi ;;
+        if [ $wl = c4 ]; then cmd="python3 bench.py --list 4 --retries 8 --steps 10 --warmup 2 --no-cpu-baseline --extra none $arg ${KNOB_AB_EXTRA:-}"
+        else cmd="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --extra none $arg ${KNOB_AB_EXTRA:-}"; fi ;;
       *) echo "unknown workload $wl"; exit 2 ;;
     esac
     timeout -k 10 200 $cmd > $log 2>&1 || { echo "$wl $t failed"; tail -5 $log; exit 1; }
