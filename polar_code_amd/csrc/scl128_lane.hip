@@ -58,6 +58,14 @@ namespace {
 #define PSCL_LANE_REG56 1
 #endif
 
+// frame stride residues (doubles mod 32; see FSTRIDE below): L = 8 8 (stride 200), L = 4 24 (120)
+#ifndef PSCL_LANE_FRES8
+#define PSCL_LANE_FRES8 8
+#endif
+#ifndef PSCL_LANE_FRES4
+#define PSCL_LANE_FRES4 24
+#endif
+
 template <int LMAX>
 struct LaneLayout {
     static constexpr int G = LMAX;
@@ -71,12 +79,14 @@ struct LaneLayout {
     // 5 and 6 live in registers (depth 4 is rewritten after the recompute has read them)
     static constexpr int OFFX = PSCL_LANE_REG56 ? OFF4 : OFF6;
     static constexpr int RAW = PSCL_LANE_REG56 ? OFF5 : OFF6 + 2 * LMAX;
-    // frame stride in doubles: = 16 (mod 32) at L = 8 (240, or 208 with REG56): frames start
-    // alternately on the two 128-byte halves of the 256-byte bank row and a ds_read_b128 lane group
-    // (lanes of 4 frames) touching one pair index of its paths' slots covers 4 distinct 64-byte
-    // quarters; = 24 (mod 32) at L = 4 (120 either way; 112 = 16 mod 32 measured 46 % bank
+    // frame stride in doubles: = 8 (mod 32) at L = 8 (200 with REG56; round 6): frames start at
+    // 64-byte steps of the 256-byte bank row.  The = 16 stride (208: frames alternate the two
+    // 128-byte halves, so a ds_read_b128 lane group's four frames pair up per half) measured 15.6 %
+    // LDS bank conflicts against 29 % here, yet the launch is 3-4 % slower (profiles/
+    // r06an_frame_stride_ab.txt: strides 192 196 200 204 208 timed) -- the conflict counter is not
+    // what bounds this kernel.  = 24 (mod 32) at L = 4 (120; 112 = 16 mod 32 measured 46 % bank
     // conflicts against 4.5 %: the L = 4 kernel's occupancy is bound by its VGPRs, not its LDS)
-    static constexpr int FRES = LMAX == 8 ? 16 : 24;
+    static constexpr int FRES = LMAX == 8 ? PSCL_LANE_FRES8 : PSCL_LANE_FRES4;
     static constexpr int FSTRIDE = RAW + (((FRES - RAW) % 32) + 32) % 32;
     // the fused post pass's FS instance replays the best path's 128 leaves in the frame's region
     // (208 doubles at L = 8; at L = 4 the stride grows 120 -> 152, still = 24 mod 32)
